@@ -1,0 +1,238 @@
+"""ctypes wrapper of the CPU parity oracle (oracle/coup_oracle.c).
+
+TEST INFRASTRUCTURE ONLY.  Importable from tests/, __graft_entry__.smoke()
+and bench.py's cpu_baseline leg; the product package never imports it.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+
+OBS_SIZE = 98
+INFO_SIZE = 2492
+MAX_HIST = 136
+
+
+class _OcCard(ctypes.Structure):
+    _fields_ = [("value", ctypes.c_int), ("state", ctypes.c_int)]
+
+
+class _OcPlayer(ctypes.Structure):
+    _fields_ = [("cards", _OcCard * 4), ("ncards", ctypes.c_int),
+                ("coins", ctypes.c_int), ("last_action", ctypes.c_int),
+                ("lost_challenge", ctypes.c_int)]
+
+
+class _OcState(ctypes.Structure):
+    _fields_ = [("deck", ctypes.c_int * 5), ("pl", _OcPlayer * 2),
+                ("queue", ctypes.c_int * 8), ("qlen", ctypes.c_int),
+                ("turn_player", ctypes.c_int), ("move_player", ctypes.c_int),
+                ("opp_player", ctypes.c_int), ("turn_begin", ctypes.c_int),
+                ("turn_number", ctypes.c_int), ("is_chance", ctypes.c_int),
+                ("rewards", ctypes.c_int * 2), ("move_number", ctypes.c_int),
+                ("hist_len", ctypes.c_int),
+                ("hist_player", ctypes.c_int * MAX_HIST),
+                ("hist_action", ctypes.c_int * MAX_HIST),
+                ("hist_deal_to", ctypes.c_int * MAX_HIST),
+                ("error", ctypes.c_int)]
+
+
+class _RolloutArgs(ctypes.Structure):
+    _fields_ = [("seed", ctypes.c_uint64), ("env_id_base", ctypes.c_uint32),
+                ("n", ctypes.c_int64), ("steps", ctypes.c_int64),
+                ("auto_reset", ctypes.c_int), ("obs_last_only", ctypes.c_int),
+                ("actions", ctypes.c_void_p), ("rewards", ctypes.c_void_p),
+                ("step_type", ctypes.c_void_p), ("legal", ctypes.c_void_p),
+                ("obs", ctypes.c_void_p), ("final_state", ctypes.c_void_p),
+                ("decisions", ctypes.c_void_p), ("episodes_done", ctypes.c_void_p),
+                ("return_sum_p0", ctypes.c_void_p)]
+
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH) or (
+                os.path.getmtime(_LIB_PATH) < os.path.getmtime(os.path.join(_HERE, "coup_oracle.c"))):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        P = ctypes.POINTER(_OcState)
+        L.oc_init.argtypes = [P]
+        L.oc_is_terminal.argtypes = [P]
+        L.oc_current_player.argtypes = [P]
+        L.oc_legal_actions.argtypes = [P, ctypes.POINTER(ctypes.c_int)]
+        L.oc_legal_mask.argtypes = [P]
+        L.oc_legal_mask.restype = ctypes.c_uint32
+        L.oc_apply_action.argtypes = [P, ctypes.c_int]
+        L.oc_returns.argtypes = [P, ctypes.POINTER(ctypes.c_int)]
+        L.oc_rewards.argtypes = [P, ctypes.POINTER(ctypes.c_int)]
+        L.oc_chance_outcomes.argtypes = [P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_double)]
+        L.oc_observation_tensor.argtypes = [P, ctypes.c_int, ctypes.POINTER(ctypes.c_float)]
+        L.oc_info_state_tensor.argtypes = [P, ctypes.c_int, ctypes.POINTER(ctypes.c_float)]
+        for f in (L.oc_observation_string, L.oc_info_state_string):
+            f.argtypes = [P, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+        L.oc_to_string.argtypes = [P, ctypes.c_char_p, ctypes.c_int]
+        L.oc_pack.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
+        L.oc_draw.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
+        L.oc_draw.restype = ctypes.c_uint32
+        L.oc_philox4x32_10.argtypes = [ctypes.POINTER(ctypes.c_uint32)] * 2 + [ctypes.POINTER(ctypes.c_uint32)]
+        L.oc_rollout.argtypes = [ctypes.POINTER(_RolloutArgs)]
+        _lib = L
+    return _lib
+
+
+class OracleState:
+    """One reference-semantics Coup game (pyspiel.State-like surface)."""
+
+    def __init__(self):
+        self._s = _OcState()
+        lib().oc_init(ctypes.byref(self._s))
+
+    def clone(self):
+        c = OracleState.__new__(OracleState)
+        c._s = _OcState()
+        ctypes.memmove(ctypes.byref(c._s), ctypes.byref(self._s), ctypes.sizeof(_OcState))
+        return c
+
+    @property
+    def raw(self):
+        return self._s
+
+    def is_terminal(self):
+        return bool(lib().oc_is_terminal(ctypes.byref(self._s)))
+
+    def current_player(self):
+        return lib().oc_current_player(ctypes.byref(self._s))
+
+    def is_chance_node(self):
+        return self.current_player() == -1
+
+    def legal_actions(self):
+        buf = (ctypes.c_int * 18)()
+        n = lib().oc_legal_actions(ctypes.byref(self._s), buf)
+        return list(buf[:n])
+
+    def legal_mask(self):
+        return lib().oc_legal_mask(ctypes.byref(self._s))
+
+    def apply_action(self, a):
+        err = lib().oc_apply_action(ctypes.byref(self._s), int(a))
+        if err:
+            raise RuntimeError(f"oracle apply_action({a}) failed with code {err}")
+
+    def returns(self):
+        buf = (ctypes.c_int * 2)()
+        lib().oc_returns(ctypes.byref(self._s), buf)
+        return list(buf)
+
+    def rewards(self):
+        buf = (ctypes.c_int * 2)()
+        lib().oc_rewards(ctypes.byref(self._s), buf)
+        return list(buf)
+
+    def chance_outcomes(self):
+        acts = (ctypes.c_int * 5)()
+        probs = (ctypes.c_double * 5)()
+        n = lib().oc_chance_outcomes(ctypes.byref(self._s), acts, probs)
+        return [(acts[i], probs[i]) for i in range(n)]
+
+    def observation_tensor(self, player):
+        out = np.zeros(OBS_SIZE, np.float32)
+        lib().oc_observation_tensor(ctypes.byref(self._s), player,
+                                    out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+        return out
+
+    def information_state_tensor(self, player):
+        out = np.zeros(INFO_SIZE, np.float32)
+        lib().oc_info_state_tensor(ctypes.byref(self._s), player,
+                                   out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+        return out
+
+    def _string(self, fn, *args):
+        buf = ctypes.create_string_buffer(8192)
+        n = fn(ctypes.byref(self._s), *args, buf, 8192)
+        assert n < 8192
+        return buf.value.decode()
+
+    def observation_string(self, player):
+        return self._string(lib().oc_observation_string, player)
+
+    def information_state_string(self, player):
+        return self._string(lib().oc_info_state_string, player)
+
+    def to_string(self):
+        return self._string(lib().oc_to_string)
+
+    def pack(self, episode=0, err=0):
+        out = (ctypes.c_uint32 * 4)()
+        lib().oc_pack(ctypes.byref(self._s), episode, err, out)
+        return list(out)
+
+    def history(self):
+        return list(self._s.hist_action[:self._s.hist_len])
+
+    def coins(self, p):
+        return self._s.pl[p].coins
+
+    def cards(self, p):
+        pl = self._s.pl[p]
+        return [(pl.cards[i].value, pl.cards[i].state) for i in range(pl.ncards)]
+
+    def deck(self):
+        return list(self._s.deck)
+
+    def last_action(self, p):
+        return self._s.pl[p].last_action
+
+
+def draw(seed, env_id, episode, draw_idx):
+    return lib().oc_draw(seed, env_id, episode, draw_idx)
+
+
+def philox(ctr, key):
+    c = (ctypes.c_uint32 * 4)(*ctr)
+    k = (ctypes.c_uint32 * 2)(*key)
+    o = (ctypes.c_uint32 * 4)()
+    lib().oc_philox4x32_10(c, k, o)
+    return list(o)
+
+
+def rollout(seed, n, steps, env_id_base=0, auto_reset=True, want_obs=False,
+            obs_last_only=False, want_trajectory=True):
+    """Uniform-random batched rollout under the sampling contract.
+
+    Returns a dict of numpy arrays (step-major: [steps][n]...)."""
+    out = {}
+    a = _RolloutArgs()
+    a.seed, a.env_id_base, a.n, a.steps = seed, env_id_base, n, steps
+    a.auto_reset, a.obs_last_only = int(auto_reset), int(obs_last_only)
+
+    def buf(name, shape, dtype):
+        arr = np.zeros(shape, dtype)
+        out[name] = arr
+        return arr.ctypes.data
+
+    if want_trajectory:
+        a.actions = buf("actions", (steps, n), np.int8)
+        a.rewards = buf("rewards", (steps, n, 2), np.int8)
+        a.step_type = buf("step_type", (steps, n), np.uint8)
+        a.legal = buf("legal", (steps, n), np.uint32)
+    if want_obs:
+        shape = (n, 2, OBS_SIZE) if obs_last_only else (steps, n, 2, OBS_SIZE)
+        a.obs = buf("obs", shape, np.float32)
+    a.final_state = buf("final_state", (n, 4), np.uint32)
+    a.decisions = buf("decisions", (1,), np.int64)
+    a.episodes_done = buf("episodes_done", (1,), np.int64)
+    a.return_sum_p0 = buf("return_sum_p0", (1,), np.int64)
+    lib().oc_rollout(ctypes.byref(a))
+    return out
