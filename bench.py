@@ -1,0 +1,163 @@
+"""Coup env-steps/sec on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4r]
+
+Workload (default, configs[2] of BASELINE.json, the batch-2^20 config the
+metric is quoted on): 2-player Coup, B = 2^20 lanes per GPU, uniform-random
+policy drawn in-kernel, one env step per lane per launch, with the
+ObservationTensor of both players written out (fp32 [B][2][98]) every step
+plus actions, rewards, step types and legal masks -- the batched
+rl_environment/SyncVectorEnv step.  Synthetic data: the games themselves.
+
+A "step" is one batched env step over all B lanes; value = env-steps/s of
+the whole job (N x B x K / max-over-ranks wall time).  Multi-GPU: one
+process per GPU (torchrun), global env ids sharded by rank, no collective
+inside the step loop; the timed region ends with one RCCL all-gather of
+the ranks' final per-lane rewards/step types (trajectory collation).
+
+roofline: algorithmic bytes per launch (824 B x B)
+over the step kernel's average duration from HIP events on the launch
+stream; traffic: HBM bytes per launch from the rocprofv3 PMC pass recorded
+in profiles/ (null if absent).  cpu_baseline: the C oracle (a scalar port
+of the reference rules) on one host core, same workload per lane.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+BYTES_PER_STEP = {"c3": 824, "c2": 40}
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="c3", choices=["c3", "c2"])
+    ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="target duration of the bounded CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(target_s, with_obs):
+    """Bounded sample of the same per-lane workload on the oracle (1 core)."""
+    from oracle import oracle
+    n = 4096
+    t0 = time.perf_counter()
+    oracle.rollout(seed=7, n=n, steps=16, want_obs=with_obs, obs_overwrite=True, want_trajectory=False)
+    per_step = (time.perf_counter() - t0) / (n * 16)
+    steps = max(16, int(target_s / per_step / n))
+    t0 = time.perf_counter()
+    oracle.rollout(seed=7, n=n, steps=steps, want_obs=with_obs, obs_overwrite=True, want_trajectory=False)
+    dt = time.perf_counter() - t0
+    return {"value": n * steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{n} lanes x {steps} uniform-random steps"
+                      + (" with ObservationTensor x2 written per step" if with_obs else "")
+                      + f", {dt:.1f} s, oracle/coup_oracle.c -O2"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from open_spiel_coup_amd import BatchedCoupEnv
+
+    cfg = args.config
+    B = args.batch or (1 << 20 if cfg == "c3" else 65536)
+    with_obs = cfg == "c3"
+    env = BatchedCoupEnv(B, seed=args.seed, env_id_base=rank * B, auto_reset=True, obs=with_obs, device=dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        env.step()
+    barrier()
+
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    gathered = None
+    barrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        env.step()
+        ev[k][1].record(stream)
+    if world > 1:
+        # collate the final step's per-lane outcome over xGMI (RCCL)
+        payload = torch.cat([env.rewards.view(torch.uint8).reshape(-1), env.step_type], 0)
+        gathered = [torch.empty_like(payload) for _ in range(world)]
+        dist.all_gather(gathered, payload)
+    barrier()
+    elapsed = time.perf_counter() - t0
+
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    errors = env.error_count()
+
+    if rank == 0:
+        bytes_per_launch = BYTES_PER_STEP[cfg] * B
+        achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+        traffic = None
+        if os.path.exists(TRAFFIC_FILE):
+            with open(TRAFFIC_FILE) as f:
+                tr = json.load(f)
+            if tr.get("config") == cfg and tr.get("batch") == B:
+                traffic = tr.get("hbm_bytes_per_launch")
+        line = {
+            "metric": "Coup env-steps/sec at batch 2^20, 1/2/4/8 MI355X; HBM GB/s vs peak",
+            "value": world * B * args.steps / elapsed,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic (uniform-random self-play games)",
+            "config": {"workload": "coup-2p-uniform-b2^20-obs" if cfg == "c3" else "coup-2p-uniform-b65536",
+                       "batch_per_gpu": B, "global_batch": world * B, "players": 2,
+                       "obs": "ObservationTensor fp32 [B][2][98] per step" if with_obs else "none",
+                       "auto_reset": True, "parallelism": f"dp{world} (env-id sharding)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "k_step<true,%s>" % ("true" if with_obs else "false"),
+                         "kernel_ms": kern_ms, "bytes_per_launch": bytes_per_launch},
+            "lane_errors": errors,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, with_obs)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

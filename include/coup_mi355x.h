@@ -1,0 +1,148 @@
+/*
+ * coup_mi355x.h -- C ABI of the MI355X-native batched Coup environment.
+ *
+ * One env handle = B independent 2-player Coup games ("lanes") whose state
+ * lives in HBM as one 16-byte record per lane (layout: DESIGN.md section 3).
+ * Every compute entry point runs on the GPU (gfx950 HIP kernels, one lane
+ * per thread); there is no CPU fallback.  All array arguments are DEVICE
+ * pointers owned by the caller (e.g. torch tensors' data_ptr()), laid out
+ * lane-major ([B] or [B][...]).  Any output pointer may be NULL to skip it.
+ * Work is enqueued on the env's HIP stream (coup_set_stream); calls are
+ * asynchronous unless stated otherwise.  Return value: 0 on success,
+ * otherwise a COUP_E_* code with a message in coup_last_error().
+ *
+ * Reference interfaces replaced (BStarcheus/open_spiel_coup):
+ *   open_spiel::Game / State virtual API     open_spiel/spiel.h:210-1035
+ *   CoupGame / CoupState                     open_spiel/games/coup.h:111-231
+ *   pure C ABI pattern for Game/State        open_spiel/rust/src/rust_open_spiel.h:24-84
+ *   rl_environment.Environment reset/step    open_spiel/python/rl_environment.py:282-367
+ *   SyncVectorEnv step(reset_if_done)        open_spiel/python/vector_env.py:40-78
+ */
+#ifndef COUP_MI355X_H_
+#define COUP_MI355X_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define COUP_ABI_VERSION 1
+
+#define COUP_NUM_PLAYERS 2          /* coup.h:42 */
+#define COUP_NUM_ACTIONS 18         /* coup.h:203 NumDistinctActions */
+#define COUP_NUM_CARD_TYPES 5       /* coup.h:44, MaxChanceOutcomes */
+#define COUP_OBS_SIZE 98            /* coup.cc:1118-1130 ObservationTensorShape */
+#define COUP_INFO_STATE_SIZE 2492   /* coup.cc:1104-1116 InformationStateTensorShape */
+#define COUP_MAX_GAME_LENGTH 90     /* coup.h:219 */
+#define COUP_STATE_BYTES 16         /* packed lane record */
+
+/* rl_environment.StepType (rl_environment.py:96-103) */
+#define COUP_STEP_FIRST 0
+#define COUP_STEP_MID 1
+#define COUP_STEP_LAST 2
+
+/* open_spiel player ids (spiel_globals.h:28,34) */
+#define COUP_CHANCE_PLAYER (-1)
+#define COUP_TERMINAL_PLAYER (-4)
+
+/* Bit set in coup_query's legal mask at chance nodes: bits 0..4 are then the
+ * card types with a non-zero deck count (LegalActionsMask(kChancePlayerId),
+ * spiel.cc:371-377). */
+#define COUP_MASK_CHANCE_FLAG (1u << 31)
+
+/* error codes */
+#define COUP_OK 0
+#define COUP_E_INVALID 1    /* bad argument (null env, bad batch, ...) */
+#define COUP_E_HIP 2        /* HIP runtime error */
+#define COUP_E_LANES 3      /* one or more lanes rejected an action (see coup_error_count) */
+
+typedef struct coup_env coup_env;
+
+/* Outputs of one batched env step; every pointer optional (NULL = skip). */
+typedef struct {
+  int8_t* actions;      /* [B]  decision action applied this step (-1: lane was reset) */
+  int8_t* rewards;      /* [B][2] Rewards() after the step (coup.cc:1012) */
+  uint8_t* step_type;   /* [B]  COUP_STEP_* */
+  uint32_t* legal_mask; /* [B]  bit a set iff a in LegalActions() of the current player */
+  int8_t* cur_player;   /* [B]  CurrentPlayer() of the (post-reset) state */
+  float* obs;           /* [B][2][98] ObservationTensor(p) for p = 0, 1 */
+} coup_step_outputs;
+
+/* Per-lane query of the current state (State accessors); all optional. */
+typedef struct {
+  uint32_t* legal_mask; /* [B] decision mask, or chance mask | COUP_MASK_CHANCE_FLAG */
+  int8_t* cur_player;   /* [B] CurrentPlayer() (coup.cc:458-466) */
+  uint8_t* terminal;    /* [B] IsTerminal() (coup.cc:989-1010) */
+  int8_t* rewards;      /* [B][2] Rewards() (coup.cc:1012-1014) */
+  int8_t* returns;      /* [B][2] Returns() (coup.cc:1016-1032) */
+  float* obs;           /* [B][2][98] ObservationTensor (coup.cc:1051-1056) */
+} coup_query_outputs;
+
+/* Per-lane rollout statistics accumulated by coup_rollout (device, [B]). */
+typedef struct {
+  int32_t* episodes;    /* [B] episodes finished */
+  int32_t* return_sum;  /* [B] sum over finished episodes of player 0's return */
+  int32_t* length_sum;  /* [B] sum over finished episodes of decisions taken */
+} coup_rollout_stats;
+
+/* ABI version of the loaded library (== COUP_ABI_VERSION). */
+int coup_abi_version(void);
+/* Message of the last failing call on this thread ("" if none). */
+const char* coup_last_error(void);
+
+/* Create an env of `batch` lanes on the current HIP device.  Lane i uses the
+ * global env id env_id_base + i for its random streams, so a batch split over
+ * ranks by id range reproduces the single-GPU trajectories bit for bit.
+ * auto_reset=1: SyncVectorEnv(reset_if_done=True) semantics (a finished lane
+ * restarts inside the same step); 0: rl_environment semantics (LAST, then the
+ * next step resets).  The env starts with every lane reset and dealt
+ * (rl_environment.reset, rl_environment.py:324-367).  Synchronous. */
+int coup_create(int64_t batch, uint64_t seed, uint32_t env_id_base, int auto_reset, coup_env** out);
+int coup_destroy(coup_env* env);
+/* Use this HIP stream (hipStream_t, may be NULL = default) for later calls. */
+int coup_set_stream(coup_env* env, void* hip_stream);
+int64_t coup_batch(const coup_env* env);
+
+/* Reset lanes (all if lane_mask == NULL, else lanes with lane_mask[i] != 0):
+ * next episode, fresh CoupState, chance deals resolved (FIRST step). */
+int coup_reset(coup_env* env, const uint8_t* lane_mask);
+
+/* One batched rl_environment step.  actions: [B] decision actions (int8),
+ * or NULL to draw each lane's action uniformly from its legal set under the
+ * sampling contract (random_agent.py:29-42).  Per lane: apply the action
+ * (State::ApplyAction, spiel.cc:322-331), resolve the chance deals that
+ * follow (rl_environment.py:369-382), report rewards / step type, reset a
+ * finished lane (see auto_reset) and write the post-step legal mask and
+ * observations.  An illegal action leaves the lane unchanged and counts in
+ * coup_error_count. */
+int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out);
+
+/* `steps` uniform-random env steps per lane in one launch, state kept in
+ * registers (auto-reset always on); per-lane statistics are accumulated
+ * into `stats` (optional). */
+int coup_rollout(coup_env* env, int64_t steps, const coup_rollout_stats* stats);
+
+/* --- open_spiel::State surface, one action per lane -------------------- */
+
+/* Put lanes (mask as in coup_reset) in NewInitialState() (coup.cc:393-428):
+ * a chance node with four deals pending, episode counter advanced. */
+int coup_new_initial_state(coup_env* env, const uint8_t* lane_mask);
+/* State::ApplyAction (spiel.cc:322-331) per lane, decision or chance outcome;
+ * actions[i] < 0 leaves lane i untouched.  No chance auto-resolution. */
+int coup_apply_action(coup_env* env, const int8_t* actions);
+/* Per-lane accessors of the current state. */
+int coup_query(coup_env* env, const coup_query_outputs* out);
+
+/* Copy the packed lane records ([B][4] uint32, device) out of / into the env. */
+int coup_export_state(coup_env* env, uint32_t* dst);
+int coup_import_state(coup_env* env, const uint32_t* src);
+
+/* Number of lanes that rejected an action since the last call (resets the
+ * counter).  Synchronises the env's stream. */
+int coup_error_count(coup_env* env, int64_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* COUP_MI355X_H_ */

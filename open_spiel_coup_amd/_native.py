@@ -1,0 +1,90 @@
+"""Loader for the C-ABI library libcoup_mi355x.so (include/coup_mi355x.h).
+
+The library is built in-tree by open_spiel_coup_amd.build (hipcc, gfx950).
+There is no fallback: if the library is missing or cannot be loaded, every
+entry point raises.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libcoup_mi355x.so")
+ABI_VERSION = 1
+
+COUP_OK, COUP_E_INVALID, COUP_E_HIP, COUP_E_LANES = 0, 1, 2, 3
+
+# Every symbol declared in include/coup_mi355x.h
+SYMBOLS = (
+    "coup_abi_version", "coup_last_error", "coup_create", "coup_destroy",
+    "coup_set_stream", "coup_batch", "coup_reset", "coup_step", "coup_rollout",
+    "coup_new_initial_state", "coup_apply_action", "coup_query",
+    "coup_export_state", "coup_import_state", "coup_error_count",
+)
+
+
+class StepOutputs(ctypes.Structure):
+    _fields_ = [("actions", ctypes.c_void_p), ("rewards", ctypes.c_void_p),
+                ("step_type", ctypes.c_void_p), ("legal_mask", ctypes.c_void_p),
+                ("cur_player", ctypes.c_void_p), ("obs", ctypes.c_void_p)]
+
+
+class QueryOutputs(ctypes.Structure):
+    _fields_ = [("legal_mask", ctypes.c_void_p), ("cur_player", ctypes.c_void_p),
+                ("terminal", ctypes.c_void_p), ("rewards", ctypes.c_void_p),
+                ("returns", ctypes.c_void_p), ("obs", ctypes.c_void_p)]
+
+
+class RolloutStats(ctypes.Structure):
+    _fields_ = [("episodes", ctypes.c_void_p), ("return_sum", ctypes.c_void_p),
+                ("length_sum", ctypes.c_void_p)]
+
+
+class CoupError(RuntimeError):
+    """Raised for a failing C-ABI call (mirrors pyspiel.SpielError)."""
+
+
+_lib = None
+
+
+def load():
+    """Load libcoup_mi355x.so once.  torch is imported first so the process
+    uses torch's HIP runtime (same soname) for both torch and our kernels."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    import torch  # noqa: F401  (HIP runtime first)
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not built; run `python -m open_spiel_coup_amd.build`")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+    sig = {
+        "coup_abi_version": ([], i32),
+        "coup_last_error": ([], ctypes.c_char_p),
+        "coup_create": ([i64, ctypes.c_uint64, ctypes.c_uint32, i32, ctypes.POINTER(vp)], i32),
+        "coup_destroy": ([vp], i32),
+        "coup_set_stream": ([vp, vp], i32),
+        "coup_batch": ([vp], i64),
+        "coup_reset": ([vp, vp], i32),
+        "coup_step": ([vp, vp, ctypes.POINTER(StepOutputs)], i32),
+        "coup_rollout": ([vp, i64, ctypes.POINTER(RolloutStats)], i32),
+        "coup_new_initial_state": ([vp, vp], i32),
+        "coup_apply_action": ([vp, vp], i32),
+        "coup_query": ([vp, ctypes.POINTER(QueryOutputs)], i32),
+        "coup_export_state": ([vp, vp], i32),
+        "coup_import_state": ([vp, vp], i32),
+        "coup_error_count": ([vp, ctypes.POINTER(i64)], i32),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    if L.coup_abi_version() != ABI_VERSION:
+        raise ImportError(f"libcoup_mi355x ABI {L.coup_abi_version()} != {ABI_VERSION}")
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != COUP_OK:
+        msg = load().coup_last_error().decode(errors="replace")
+        raise CoupError(f"coup C-ABI error {rc}: {msg}")

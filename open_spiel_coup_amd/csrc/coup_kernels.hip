@@ -1,0 +1,498 @@
+// coup_kernels.hip -- gfx950 kernels of the batched Coup environment and the
+// C ABI declared in include/coup_mi355x.h.
+//
+// One thread = one lane (game).  A lane's 16-byte record is loaded with one
+// dwordx4 per thread (1 KiB contiguous per wave instruction), the step runs
+// in registers (coup_lane.h), and the record is stored back the same way.
+// Integer/branching work only: no MFMA, no LDS.  The HBM-heavy output is
+// the optional ObservationTensor write-out (784 B per lane and step).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "coup_lane.h"
+#include "coup_mi355x.h"
+
+namespace coup {
+
+constexpr int kThreads = 256;
+constexpr int kObsSize = COUP_OBS_SIZE;
+
+// ------------------------------------------------------- observation tensor
+
+// CoupObserver::WriteTensor with kDefaultObsType (coup.cc:248-287,
+// observer.h:287-290) through ContiguousAllocator (zero-filled, blocks laid
+// out back to back, observer.h:173-176):
+//   [0:2] observer one-hot          [2:22] P1 cards [4][5]   [22:42] P2 cards
+//   [42:44] cur_move_player one-hot (zeros when terminal)
+//   [44:60] cards_state [2][4][2]   [60:62] coins           [62:98] last_action [2][18]
+// A card's type is visible for the owner's face-down cards and for every
+// face-up card.  `f` is a compile-time constant after unrolling, so every
+// element folds to one or two compares on a nibble.
+template <int P>
+__device__ __forceinline__ float obs_at(const Lane& L, bool term, const int f) {
+  if (f < 2) return f == P ? 1.0f : 0.0f;
+  if (f < 42) {
+    const int q = (f - 2) / 20, i = ((f - 2) % 20) / 5, t = (f - 2) % 5;
+    const uint32_t n = nib(q ? L.h1 : L.h0, (uint32_t)i);
+    const bool v = (n == (uint32_t)(2 * t + 1)) || (q == P && n == (uint32_t)(2 * t));
+    return v ? 1.0f : 0.0f;
+  }
+  if (f < 44) return (!term && L.M == (uint32_t)(f - 42)) ? 1.0f : 0.0f;
+  if (f < 60) {
+    const int q = (f - 44) / 8, i = ((f - 44) % 8) / 2, s = (f - 44) % 2;
+    const uint32_t n = nib(q ? L.h1 : L.h0, (uint32_t)i);
+    return (n != 0xFu && (n & 1u) == (uint32_t)s) ? 1.0f : 0.0f;
+  }
+  if (f < 62) return (float)(f == 60 ? L.c0 : L.c1);
+  const int q = (f - 62) / 18, a = (f - 62) % 18;
+  return ((q ? L.l1 : L.l0) == (uint32_t)a) ? 1.0f : 0.0f;
+}
+
+__device__ __forceinline__ float obs_pair_at(const Lane& L, bool term, const int g) {
+  return g < kObsSize ? obs_at<0>(L, term, g) : obs_at<1>(L, term, g - kObsSize);
+}
+
+// Both players' 98-float rows of one lane: 784 contiguous bytes = 49 float4.
+__device__ __forceinline__ void write_obs_pair(float* __restrict__ dst, const Lane& L) {
+  const bool term = is_terminal(L);
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  v4f* d4 = reinterpret_cast<v4f*>(dst);
+#pragma unroll
+  for (int j = 0; j < 2 * kObsSize / 4; ++j) {
+    v4f v;
+    v.x = obs_pair_at(L, term, 4 * j + 0);
+    v.y = obs_pair_at(L, term, 4 * j + 1);
+    v.z = obs_pair_at(L, term, 4 * j + 2);
+    v.w = obs_pair_at(L, term, 4 * j + 3);
+    __builtin_nontemporal_store(v, d4 + j);
+  }
+}
+
+__device__ __forceinline__ int32_t return0(const Lane& L) {
+  // Returns (coup.cc:1016-1032): face-up(P2) - face-up(P1)
+  return (int32_t)face_up_count(L.h1) - (int32_t)face_up_count(L.h0);
+}
+
+__device__ __forceinline__ void count_error(uint32_t* err_count) { atomicAdd(err_count, 1u); }
+
+// ------------------------------------------------------------------ kernels
+
+struct StepArgs {
+  uint4* state;
+  int64_t n;
+  uint32_t seed_lo, seed_hi, env_id_base;
+  int auto_reset;
+  const int8_t* actions_in;
+  int8_t* actions;
+  int8_t* rewards;
+  uint8_t* step_type;
+  uint32_t* legal;
+  int8_t* cur_player;
+  float* obs;
+  uint32_t* err_count;
+};
+
+// One rl_environment step per lane (rl_environment.py:282-322), optionally
+// with SyncVectorEnv auto-reset (vector_env.py:40-67).
+template <bool UNIFORM, bool OBS>
+__global__ __launch_bounds__(kThreads) void k_step(StepArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= a.n) return;
+  Lane L = unpack(a.state[i]);
+  Rng rng{a.seed_lo, a.seed_hi, a.env_id_base + (uint32_t)i, 0u, make_uint4(0, 0, 0, 0)};
+  int act = -1;
+  uint32_t st;
+  int32_t rew = 0;
+  if (is_terminal(L)) {
+    // step() after LAST starts a new episode (rl_environment.py:310-311)
+    L = initial_lane(L.episode + 1u);
+    resolve_chance(L, rng);
+    st = COUP_STEP_FIRST;
+  } else {
+    resolve_chance(L, rng);  // no-op unless the lane was left at a chance node
+    const uint32_t m = decision_mask(L);
+    uint32_t x;
+    if (UNIFORM) {
+      x = m ? sample_action(m, rng.draw(L.episode, L.move)) : 32u;
+    } else {
+      x = (uint32_t)(uint8_t)a.actions_in[i];
+    }
+    st = COUP_STEP_MID;
+    if (x > 17u || ((m >> x) & 1u) == 0u || is_terminal(L)) {
+      count_error(a.err_count);
+    } else {
+      const uint32_t err_before = L.err;
+      apply_decision(L, x);
+      L.move += 1u;
+      resolve_chance(L, rng);
+      if (L.err && !err_before) count_error(a.err_count);
+      act = (int)x;
+      rew = L.r0;
+      if (is_terminal(L)) {
+        st = COUP_STEP_LAST;
+        if (a.auto_reset) {
+          L = initial_lane(L.episode + 1u);
+          resolve_chance(L, rng);
+        }
+      }
+    }
+  }
+  a.state[i] = pack(L);
+  if (a.actions) a.actions[i] = (int8_t)act;
+  if (a.rewards) {
+    a.rewards[2 * i] = (int8_t)rew;
+    a.rewards[2 * i + 1] = (int8_t)(-rew);
+  }
+  if (a.step_type) a.step_type[i] = (uint8_t)st;
+  if (a.legal) a.legal[i] = legal_mask(L);
+  if (a.cur_player) a.cur_player[i] = (int8_t)current_player(L);
+  if (OBS) write_obs_pair(a.obs + i * (2 * kObsSize), L);
+}
+
+struct RolloutArgs {
+  uint4* state;
+  int64_t n;
+  uint32_t seed_lo, seed_hi, env_id_base;
+  int64_t steps;
+  int32_t* episodes;
+  int32_t* return_sum;
+  int32_t* length_sum;
+  uint32_t* err_count;
+};
+
+// `steps` uniform-random env steps per lane with auto-reset, state held in
+// registers for the whole launch.
+__global__ __launch_bounds__(kThreads) void k_rollout(RolloutArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= a.n) return;
+  Lane L = unpack(a.state[i]);
+  Rng rng{a.seed_lo, a.seed_hi, a.env_id_base + (uint32_t)i, 0u, make_uint4(0, 0, 0, 0)};
+  int32_t eps = 0, ret = 0, len = 0, cur = 0;
+  uint32_t errs = 0;
+  for (int64_t s = 0; s < a.steps; ++s) {
+    if (is_terminal(L)) {
+      L = initial_lane(L.episode + 1u);
+    }
+    resolve_chance(L, rng);
+    const uint32_t m = decision_mask(L);
+    if (m == 0u) {
+      errs += 1u;
+      break;
+    }
+    const uint32_t err_before = L.err;
+    apply_decision(L, sample_action(m, rng.draw(L.episode, L.move)));
+    L.move += 1u;
+    resolve_chance(L, rng);
+    errs += (L.err && !err_before) ? 1u : 0u;
+    cur += 1;
+    if (is_terminal(L)) {
+      eps += 1;
+      ret += return0(L);
+      len += cur;
+      cur = 0;
+      L = initial_lane(L.episode + 1u);
+      resolve_chance(L, rng);
+    }
+  }
+  a.state[i] = pack(L);
+  if (a.episodes) a.episodes[i] += eps;
+  if (a.return_sum) a.return_sum[i] += ret;
+  if (a.length_sum) a.length_sum[i] += len;
+  if (errs) atomicAdd(a.err_count, errs);
+}
+
+// NewInitialState / reset of selected lanes.  mode 0: fresh env (episode 0);
+// mode 1: next episode.  deal: resolve the four initial deals.
+__global__ __launch_bounds__(kThreads) void k_reset(uint4* state, int64_t n, const uint8_t* mask, int mode, int deal,
+                                                  uint32_t seed_lo, uint32_t seed_hi, uint32_t env_id_base) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  if (mask && mask[i] == 0) return;
+  const uint32_t ep = mode == 0 ? 0u : unpack(state[i]).episode + 1u;
+  Lane L = initial_lane(ep);
+  if (deal) {
+    Rng rng{seed_lo, seed_hi, env_id_base + (uint32_t)i, 0u, make_uint4(0, 0, 0, 0)};
+    resolve_chance(L, rng);
+  }
+  state[i] = pack(L);
+}
+
+// State::ApplyAction per lane (decision or chance outcome).
+__global__ __launch_bounds__(kThreads) void k_apply(uint4* state, int64_t n, const int8_t* actions,
+                                                  uint32_t* err_count) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  const int x = actions[i];
+  if (x < 0) return;
+  Lane L = unpack(state[i]);
+  const uint32_t err_before = L.err;
+  if (!apply_action(L, (uint32_t)x)) {
+    count_error(err_count);
+    return;
+  }
+  if (L.err && !err_before) count_error(err_count);
+  state[i] = pack(L);
+}
+
+struct QueryArgs {
+  const uint4* state;
+  int64_t n;
+  uint32_t* legal;
+  int8_t* cur_player;
+  uint8_t* terminal;
+  int8_t* rewards;
+  int8_t* returns;
+  float* obs;
+};
+
+__global__ __launch_bounds__(kThreads) void k_query(QueryArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= a.n) return;
+  const Lane L = unpack(a.state[i]);
+  if (a.legal) a.legal[i] = legal_mask(L);
+  if (a.cur_player) a.cur_player[i] = (int8_t)current_player(L);
+  if (a.terminal) a.terminal[i] = is_terminal(L) ? 1 : 0;
+  if (a.rewards) {
+    a.rewards[2 * i] = (int8_t)L.r0;
+    a.rewards[2 * i + 1] = (int8_t)(-L.r0);
+  }
+  if (a.returns) {
+    const int32_t r = return0(L);
+    a.returns[2 * i] = (int8_t)r;
+    a.returns[2 * i + 1] = (int8_t)(-r);
+  }
+  if (a.obs) write_obs_pair(a.obs + i * (2 * kObsSize), L);
+}
+
+}  // namespace coup
+
+// ====================================================================== C ABI
+
+struct coup_env {
+  int64_t batch;
+  uint64_t seed;
+  uint32_t env_id_base;
+  int auto_reset;
+  uint4* state;
+  uint32_t* err_count;
+  hipStream_t stream;
+};
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define COUP_HIP_TRY(expr)                                                                    \
+  do {                                                                                        \
+    hipError_t _e = (expr);                                                                   \
+    if (_e != hipSuccess) return fail(COUP_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+#define COUP_CHECK_ENV(env) \
+  if (!(env)) return fail(COUP_E_INVALID, "null coup_env")
+
+unsigned grid_for(int64_t n) { return (unsigned)((n + coup::kThreads - 1) / coup::kThreads); }
+
+int launch_reset(coup_env* env, const uint8_t* mask, int mode, int deal) {
+  if (env->batch == 0) return COUP_OK;
+  coup::k_reset<<<grid_for(env->batch), coup::kThreads, 0, env->stream>>>(
+      env->state, env->batch, mask, mode, deal, (uint32_t)env->seed, (uint32_t)(env->seed >> 32), env->env_id_base);
+  COUP_HIP_TRY(hipGetLastError());
+  return COUP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int coup_abi_version(void) { return COUP_ABI_VERSION; }
+
+const char* coup_last_error(void) { return g_last_error.c_str(); }
+
+int coup_create(int64_t batch, uint64_t seed, uint32_t env_id_base, int auto_reset, coup_env** out) {
+  if (!out) return fail(COUP_E_INVALID, "coup_create: out is null");
+  *out = nullptr;
+  if (batch < 0 || batch > (int64_t(1) << 32)) return fail(COUP_E_INVALID, "coup_create: batch out of range");
+  coup_env* env = new coup_env();
+  env->batch = batch;
+  env->seed = seed;
+  env->env_id_base = env_id_base;
+  env->auto_reset = auto_reset ? 1 : 0;
+  env->stream = nullptr;
+  env->state = nullptr;
+  env->err_count = nullptr;
+  hipError_t e = hipMalloc(&env->state, (size_t)(batch > 0 ? batch : 1) * sizeof(uint4));
+  if (e == hipSuccess) e = hipMalloc(&env->err_count, sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemset(env->err_count, 0, sizeof(uint32_t));
+  if (e != hipSuccess) {
+    (void)hipFree(env->state);
+    (void)hipFree(env->err_count);
+    delete env;
+    return fail(COUP_E_HIP, std::string("coup_create: ") + hipGetErrorString(e));
+  }
+  int rc = launch_reset(env, nullptr, /*mode=*/0, /*deal=*/1);
+  if (rc == COUP_OK) {
+    e = hipStreamSynchronize(env->stream);
+    if (e != hipSuccess) rc = fail(COUP_E_HIP, std::string("coup_create: ") + hipGetErrorString(e));
+  }
+  if (rc != COUP_OK) {
+    (void)hipFree(env->state);
+    (void)hipFree(env->err_count);
+    delete env;
+    return rc;
+  }
+  *out = env;
+  return COUP_OK;
+}
+
+int coup_destroy(coup_env* env) {
+  COUP_CHECK_ENV(env);
+  hipError_t e1 = hipStreamSynchronize(env->stream);
+  hipError_t e2 = hipFree(env->state);
+  hipError_t e3 = hipFree(env->err_count);
+  delete env;
+  if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess)
+    return fail(COUP_E_HIP, "coup_destroy: HIP error while releasing the env");
+  return COUP_OK;
+}
+
+int coup_set_stream(coup_env* env, void* hip_stream) {
+  COUP_CHECK_ENV(env);
+  env->stream = (hipStream_t)hip_stream;
+  return COUP_OK;
+}
+
+int64_t coup_batch(const coup_env* env) { return env ? env->batch : -1; }
+
+int coup_reset(coup_env* env, const uint8_t* lane_mask) {
+  COUP_CHECK_ENV(env);
+  return launch_reset(env, lane_mask, /*mode=*/1, /*deal=*/1);
+}
+
+int coup_new_initial_state(coup_env* env, const uint8_t* lane_mask) {
+  COUP_CHECK_ENV(env);
+  return launch_reset(env, lane_mask, /*mode=*/1, /*deal=*/0);
+}
+
+int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out) {
+  COUP_CHECK_ENV(env);
+  if (env->batch == 0) return COUP_OK;
+  coup::StepArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.state = env->state;
+  a.n = env->batch;
+  a.seed_lo = (uint32_t)env->seed;
+  a.seed_hi = (uint32_t)(env->seed >> 32);
+  a.env_id_base = env->env_id_base;
+  a.auto_reset = env->auto_reset;
+  a.actions_in = actions;
+  a.err_count = env->err_count;
+  if (out) {
+    a.actions = out->actions;
+    a.rewards = out->rewards;
+    a.step_type = out->step_type;
+    a.legal = out->legal_mask;
+    a.cur_player = out->cur_player;
+    a.obs = out->obs;
+  }
+  const unsigned g = grid_for(env->batch);
+  const bool uniform = actions == nullptr, obs = a.obs != nullptr;
+  if (uniform && obs)
+    coup::k_step<true, true><<<g, coup::kThreads, 0, env->stream>>>(a);
+  else if (uniform)
+    coup::k_step<true, false><<<g, coup::kThreads, 0, env->stream>>>(a);
+  else if (obs)
+    coup::k_step<false, true><<<g, coup::kThreads, 0, env->stream>>>(a);
+  else
+    coup::k_step<false, false><<<g, coup::kThreads, 0, env->stream>>>(a);
+  COUP_HIP_TRY(hipGetLastError());
+  return COUP_OK;
+}
+
+int coup_rollout(coup_env* env, int64_t steps, const coup_rollout_stats* stats) {
+  COUP_CHECK_ENV(env);
+  if (steps < 0) return fail(COUP_E_INVALID, "coup_rollout: negative steps");
+  if (env->batch == 0 || steps == 0) return COUP_OK;
+  coup::RolloutArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.state = env->state;
+  a.n = env->batch;
+  a.seed_lo = (uint32_t)env->seed;
+  a.seed_hi = (uint32_t)(env->seed >> 32);
+  a.env_id_base = env->env_id_base;
+  a.steps = steps;
+  a.err_count = env->err_count;
+  if (stats) {
+    a.episodes = stats->episodes;
+    a.return_sum = stats->return_sum;
+    a.length_sum = stats->length_sum;
+  }
+  coup::k_rollout<<<grid_for(env->batch), coup::kThreads, 0, env->stream>>>(a);
+  COUP_HIP_TRY(hipGetLastError());
+  return COUP_OK;
+}
+
+int coup_apply_action(coup_env* env, const int8_t* actions) {
+  COUP_CHECK_ENV(env);
+  if (!actions) return fail(COUP_E_INVALID, "coup_apply_action: actions is null");
+  if (env->batch == 0) return COUP_OK;
+  coup::k_apply<<<grid_for(env->batch), coup::kThreads, 0, env->stream>>>(env->state, env->batch, actions,
+                                                                          env->err_count);
+  COUP_HIP_TRY(hipGetLastError());
+  return COUP_OK;
+}
+
+int coup_query(coup_env* env, const coup_query_outputs* out) {
+  COUP_CHECK_ENV(env);
+  if (!out) return fail(COUP_E_INVALID, "coup_query: out is null");
+  if (env->batch == 0) return COUP_OK;
+  coup::QueryArgs a;
+  a.state = env->state;
+  a.n = env->batch;
+  a.legal = out->legal_mask;
+  a.cur_player = out->cur_player;
+  a.terminal = out->terminal;
+  a.rewards = out->rewards;
+  a.returns = out->returns;
+  a.obs = out->obs;
+  coup::k_query<<<grid_for(env->batch), coup::kThreads, 0, env->stream>>>(a);
+  COUP_HIP_TRY(hipGetLastError());
+  return COUP_OK;
+}
+
+int coup_export_state(coup_env* env, uint32_t* dst) {
+  COUP_CHECK_ENV(env);
+  if (!dst) return fail(COUP_E_INVALID, "coup_export_state: dst is null");
+  COUP_HIP_TRY(hipMemcpyAsync(dst, env->state, (size_t)env->batch * sizeof(uint4), hipMemcpyDeviceToDevice,
+                              env->stream));
+  return COUP_OK;
+}
+
+int coup_import_state(coup_env* env, const uint32_t* src) {
+  COUP_CHECK_ENV(env);
+  if (!src) return fail(COUP_E_INVALID, "coup_import_state: src is null");
+  COUP_HIP_TRY(hipMemcpyAsync(env->state, src, (size_t)env->batch * sizeof(uint4), hipMemcpyDeviceToDevice,
+                              env->stream));
+  return COUP_OK;
+}
+
+int coup_error_count(coup_env* env, int64_t* out) {
+  COUP_CHECK_ENV(env);
+  if (!out) return fail(COUP_E_INVALID, "coup_error_count: out is null");
+  uint32_t h = 0;
+  COUP_HIP_TRY(hipMemcpyAsync(&h, env->err_count, sizeof(uint32_t), hipMemcpyDeviceToHost, env->stream));
+  COUP_HIP_TRY(hipMemsetAsync(env->err_count, 0, sizeof(uint32_t), env->stream));
+  COUP_HIP_TRY(hipStreamSynchronize(env->stream));
+  *out = (int64_t)h;
+  return COUP_OK;
+}
+
+}  // extern "C"

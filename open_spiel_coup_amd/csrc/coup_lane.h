@@ -1,0 +1,598 @@
+// coup_lane.h -- Coup rules on a register-resident lane (gfx950 device code).
+//
+// One lane = one independent 2-player game.  In HBM a lane is a 16-byte
+// record (4 x u32); a kernel unpacks it into the Lane
+// struct below (scalars only: no per-player arrays, so nothing spills to
+// scratch through dynamic indexing), runs the step, and packs it back.
+//
+// Hands are 16-bit words of four nibbles, one per hand slot, holding the
+// card "kind" = 2*type + face (0 = down, 1 = up); empty slots are 0xF.
+// Because the reference keeps every hand sorted by (type, face)
+// (coup.cc:389-391, coup.h:91-94), a hand is a sorted nibble string with
+// the empties on top: inserting, removing and flipping cards are shifts and
+// masks, and "slot i" in action ids (LoseCard1/2, ExchangeReturnXY) is
+// nibble i.
+//
+// Every transition cites the reference line it reproduces.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace coup {
+
+// ActionType (coup.h:65-85)
+enum : uint32_t {
+  kIncome = 0, kForeignAid = 1, kCoup = 2, kTax = 3, kAssassinate = 4,
+  kExchange = 5, kSteal = 6, kLoseCard1 = 7, kLoseCard2 = 8, kPass = 9,
+  kBlock = 10, kChallenge = 11, kExchangeReturn12 = 12, kExchangeReturn34 = 17,
+  kNoAction = 31  // ActionType::kNone in the packed record
+};
+// CardType (coup.h:50-57)
+enum : uint32_t { kAssassin = 0, kAmbassador = 1, kCaptain = 2, kContessa = 3, kDuke = 4 };
+
+constexpr uint32_t kEmptyHand = 0xFFFFu;
+constexpr uint32_t kInitialDeck = 0x33333u;  // kNumEachCardInDeck = 3 of each type
+constexpr uint32_t kMaxGameLength = 90;      // coup.h:219
+constexpr uint32_t kChanceFlag = 1u << 31;
+constexpr uint32_t kEpisodeMask = 0x1FFFFFFu;  // 25-bit episode counter
+
+struct Lane {
+  uint32_t h0, h1;      // hands of P1 / P2 (16-bit nibble strings)
+  uint32_t deck;        // 5 x 4-bit counts (can exceed 3: coup.cc:794 quirk)
+  uint32_t c0, c1;      // coins
+  int32_t r0;           // cur_rewards_[0]; cur_rewards_[1] == -r0 always
+  uint32_t err;         // set where the reference would SpielFatalError
+  uint32_t l0, l1;      // last_action (kNoAction = None)
+  uint32_t lost0, lost1;
+  uint32_t qlen, qids;  // deal_card_to_ FIFO: length, entry j = bit j
+  uint32_t T, M, begin; // cur_player_turn_, cur_player_move_, is_turn_begin_
+  uint32_t move, turn;  // move_number_, turn_number_
+  uint32_t episode;
+};
+
+// ---------------------------------------------------------------- packing
+
+__device__ __forceinline__ Lane unpack(uint4 w) {
+  Lane L;
+  L.h0 = w.x & 0xFFFFu;
+  L.h1 = w.x >> 16;
+  L.deck = w.y & 0xFFFFFu;
+  L.c0 = (w.y >> 20) & 0xFu;
+  L.c1 = (w.y >> 24) & 0xFu;
+  L.r0 = (int32_t)((w.y >> 28) & 0x7u) - 2;
+  L.err = w.y >> 31;
+  L.l0 = w.z & 0x1Fu;
+  L.l1 = (w.z >> 5) & 0x1Fu;
+  L.lost0 = (w.z >> 10) & 1u;
+  L.lost1 = (w.z >> 11) & 1u;
+  L.qlen = (w.z >> 12) & 0x7u;
+  L.qids = (w.z >> 15) & 0xFu;
+  L.T = (w.z >> 19) & 1u;
+  L.M = (w.z >> 20) & 1u;
+  L.begin = (w.z >> 21) & 1u;
+  L.move = (w.z >> 22) & 0x7Fu;
+  L.turn = w.w & 0x7Fu;
+  L.episode = w.w >> 7;
+  return L;
+}
+
+__device__ __forceinline__ uint4 pack(const Lane& L) {
+  uint4 w;
+  w.x = L.h0 | (L.h1 << 16);
+  w.y = L.deck | (L.c0 << 20) | (L.c1 << 24) | ((uint32_t)(L.r0 + 2) << 28) | (L.err << 31);
+  w.z = L.l0 | (L.l1 << 5) | (L.lost0 << 10) | (L.lost1 << 11) | (L.qlen << 12) | (L.qids << 15) |
+        (L.T << 19) | (L.M << 20) | (L.begin << 21) | (L.move << 22);
+  w.w = L.turn | ((L.episode & kEpisodeMask) << 7);
+  return w;
+}
+
+// CoupState::CoupState (coup.cc:393-428): deck 3 of each, P1 1 coin, P2 2
+// coins, no last actions, deal queue [P1, P2, P1, P2], P1 to move.
+__device__ __forceinline__ Lane initial_lane(uint32_t episode) {
+  Lane L;
+  L.h0 = kEmptyHand;
+  L.h1 = kEmptyHand;
+  L.deck = kInitialDeck;
+  L.c0 = 1;
+  L.c1 = 2;
+  L.r0 = 0;
+  L.err = 0;
+  L.l0 = kNoAction;
+  L.l1 = kNoAction;
+  L.lost0 = 0;
+  L.lost1 = 0;
+  L.qlen = 4;
+  L.qids = 0xAu;  // entries 0..3 = 0, 1, 0, 1
+  L.T = 0;
+  L.M = 0;
+  L.begin = 1;
+  L.move = 0;
+  L.turn = 0;
+  L.episode = episode & kEpisodeMask;
+  return L;
+}
+
+// --------------------------------------------------------- hand nibbles
+
+__device__ __forceinline__ uint32_t nib(uint32_t h, uint32_t i) { return (h >> (4u * i)) & 0xFu; }
+
+// bit 4i set where nibble i == k (k in 0..15)
+__device__ __forceinline__ uint32_t nib_eq(uint32_t h, uint32_t k) {
+  uint32_t x = (h ^ (k * 0x1111u)) & 0xFFFFu;
+  return ~(x | (x >> 1) | (x >> 2) | (x >> 3)) & 0x1111u;
+}
+
+// HasFaceDownCard (coup.cc:379-387): some slot holds kind 2*type
+__device__ __forceinline__ bool has_face_down(uint32_t h, uint32_t type) { return nib_eq(h, 2u * type) != 0; }
+
+// hand holds a face-down card (kinds are even when face down; 0xF is odd)
+__device__ __forceinline__ bool any_face_down(uint32_t h) { return (~h & 0x1111u) != 0; }
+
+// IsTerminal's per-player test (coup.cc:994-1006): fewer than two cards
+// (mid-deal) or any face-down card
+__device__ __forceinline__ bool alive(uint32_t h) { return nib(h, 1) == 0xFu || any_face_down(h); }
+
+__device__ __forceinline__ uint32_t hand_size(uint32_t h) {
+  return (nib(h, 0) != 0xFu) + (nib(h, 1) != 0xFu) + (nib(h, 2) != 0xFu) + (nib(h, 3) != 0xFu);
+}
+
+__device__ __forceinline__ uint32_t face_up_count(uint32_t h) {
+  uint32_t empty = h & (h >> 1) & (h >> 2) & (h >> 3) & 0x1111u;
+  return __popc(h & 0x1111u) - __popc(empty);
+}
+
+// Insert kind k keeping the nibble string sorted (push_back + SortCards,
+// coup.cc:508-510).  The hand has an empty slot.
+__device__ __forceinline__ uint32_t hand_insert(uint32_t h, uint32_t k) {
+  uint32_t pos = (nib(h, 0) <= k) + (nib(h, 1) <= k) + (nib(h, 2) <= k) + (nib(h, 3) <= k);
+  uint32_t sh = 4u * pos;
+  uint32_t keep = (1u << sh) - 1u;
+  uint32_t above = ~((1u << (sh + 4u)) - 1u);
+  return (h & keep) | (k << sh) | ((h << 4) & 0xFFFFu & above);
+}
+
+// Erase slot p (vector::erase, coup.cc:477, 793)
+__device__ __forceinline__ uint32_t hand_remove(uint32_t h, uint32_t p) {
+  uint32_t keep = (1u << (4u * p)) - 1u;
+  return (h & keep) | ((h >> 4) & ~keep & 0x0FFFu) | 0xF000u;
+}
+
+// ----------------------------------------------------- per-player access
+
+#define COUP_PGET(L, f, p) ((p) ? (L).f##1 : (L).f##0)
+#define COUP_PSET(L, f, p, v)          \
+  do {                                 \
+    uint32_t _v = (v);                 \
+    bool _p = (p) != 0;                \
+    (L).f##0 = _p ? (L).f##0 : _v;     \
+    (L).f##1 = _p ? _v : (L).f##1;     \
+  } while (0)
+
+__device__ __forceinline__ uint32_t deck_count(uint32_t deck, uint32_t t) { return (deck >> (4u * t)) & 0xFu; }
+
+__device__ __forceinline__ bool is_terminal(const Lane& L) {
+  // IsTerminal (coup.cc:989-1010): move_number_ > MaxGameLength, or at most
+  // one player alive
+  return L.move > kMaxGameLength || !(alive(L.h0) && alive(L.h1));
+}
+
+__device__ __forceinline__ bool is_chance(const Lane& L) { return L.qlen != 0; }
+
+// CurrentPlayer (coup.cc:458-466)
+__device__ __forceinline__ int current_player(const Lane& L) {
+  return is_terminal(L) ? -4 : (is_chance(L) ? -1 : (int)L.M);
+}
+
+// ------------------------------------------------------------ legal mask
+
+// LegalLoseCardActions (coup.cc:811-822): only slots 0 and 1 are offered
+__device__ __forceinline__ uint32_t lose_card_mask(uint32_t h) {
+  return ((nib(h, 0) & 1u) ? 0u : (1u << kLoseCard1)) | ((nib(h, 1) & 1u) ? 0u : (1u << kLoseCard2));
+}
+
+// Chance-node legal actions (coup.cc:828-836): card types still in the deck
+__device__ __forceinline__ uint32_t chance_mask(uint32_t deck) {
+  uint32_t m = 0;
+#pragma unroll
+  for (uint32_t t = 0; t < 5; ++t) m |= (deck_count(deck, t) != 0) << t;
+  return m;
+}
+
+// Decision-node LegalActions (coup.cc:838-937) as an 18-bit mask.  Returns 0
+// where the reference raises "Invalid action progression".
+__device__ __forceinline__ uint32_t decision_mask(const Lane& L) {
+  const uint32_t M = L.M, O = M ^ 1u;
+  const uint32_t cp_coins = COUP_PGET(L, c, M), op_coins = COUP_PGET(L, c, O);
+  const uint32_t cp_last = COUP_PGET(L, l, M), op_last = COUP_PGET(L, l, O);
+  const uint32_t cp_hand = COUP_PGET(L, h, M);
+  if (L.begin) {
+    if (cp_coins >= 10) return 1u << kCoup;
+    uint32_t m = (1u << kIncome) | (1u << kForeignAid) | (1u << kTax) | (1u << kExchange);
+    m |= (cp_coins >= 7) ? (1u << kCoup) : 0u;
+    m |= (cp_coins >= 3) ? (1u << kAssassinate) : 0u;
+    m |= (op_coins > 0) ? (1u << kSteal) : 0u;
+    return m;
+  }
+  if (COUP_PGET(L, lost, M)) return lose_card_mask(cp_hand);
+  if (M != L.T) {
+    // responses to the turn player's claim (coup.cc:860-887)
+    switch (op_last) {
+      case kForeignAid: return (1u << kPass) | (1u << kBlock);
+      case kTax:
+      case kExchange: return (1u << kPass) | (1u << kChallenge);
+      case kSteal: return (1u << kPass) | (1u << kBlock) | (1u << kChallenge);
+      case kAssassinate: return lose_card_mask(cp_hand) | (1u << kBlock) | (1u << kChallenge);
+      case kCoup: return lose_card_mask(cp_hand);
+      default: return 0u;
+    }
+  }
+  if (cp_last == kExchange) {
+    // coup.cc:889-928: all pairs of returned slots, minus pairs containing
+    // the first face-up slot.  Table: for face-up slot s, the 6-bit set of
+    // ExchangeReturn ids (relative to 12) that contain s.
+    if (nib(cp_hand, 3) == 0xFu) return 0u;  // fewer than 4 cards
+    uint32_t up = cp_hand & 0x1111u;
+    if (up == 0) return 0x3Fu << kExchangeReturn12;
+    uint32_t s = (uint32_t)__builtin_ctz(up) >> 2;
+    uint32_t excl = (0x07u | (0x19u << 6) | (0x2Au << 12) | (0x34u << 18)) >> (6u * s);
+    return ((~excl) & 0x3Fu) << kExchangeReturn12;
+  }
+  if (op_last == kBlock) return (1u << kPass) | (1u << kChallenge);
+  return 0u;
+}
+
+// LegalActionsMask of the current player: decision mask, chance mask with
+// kChanceFlag, or 0 when terminal.
+__device__ __forceinline__ uint32_t legal_mask(const Lane& L) {
+  if (is_terminal(L)) return 0u;
+  if (is_chance(L)) return chance_mask(L.deck) | kChanceFlag;
+  return decision_mask(L);
+}
+
+// ----------------------------------------------------------- transitions
+
+__device__ __forceinline__ void next_turn(Lane& L) {
+  // NextPlayerTurn (coup.cc:1079-1086)
+  L.T ^= 1u;
+  L.M = L.T;
+  L.turn += 1u;
+  L.begin = 1u;
+}
+
+__device__ __forceinline__ void next_move(Lane& L) {
+  // NextPlayerMove (coup.cc:1088-1092)
+  L.M ^= 1u;
+  L.begin = 0u;
+}
+
+// +d to cur_rewards_[M], -d to cur_rewards_[O]
+__device__ __forceinline__ void reward_mover(Lane& L, int32_t d) { L.r0 += L.M ? -d : d; }
+
+__device__ __forceinline__ void queue_push(Lane& L, uint32_t p) {
+  L.qids |= p << L.qlen;
+  L.qlen += 1u;
+}
+
+// ChallengeFailReplaceCard (coup.cc:468-486): the opponent reveals the
+// claimed card, it goes back to the deck and a replacement deal is queued.
+__device__ __forceinline__ void replace_card(Lane& L, uint32_t type) {
+  const uint32_t O = L.M ^ 1u;
+  const uint32_t h = COUP_PGET(L, h, O);
+  const uint32_t hit = nib_eq(h, 2u * type);
+  if (hit == 0) {
+    L.err = 1u;
+    return;
+  }
+  L.deck += 1u << (4u * type);
+  COUP_PSET(L, h, O, hand_remove(h, (uint32_t)__builtin_ctz(hit) >> 2));
+  queue_push(L, O);
+}
+
+// Flip slots 0 and 1 of player p face up (no re-sort), +/-1 reward per
+// flipped card to the mover: coup.cc:660-669 (p = O, d = +1) and
+// coup.cc:733-742 (p = M, d = -1).
+__device__ __forceinline__ void flip_two(Lane& L, uint32_t p, int32_t d) {
+  uint32_t h = COUP_PGET(L, h, p);
+#pragma unroll
+  for (uint32_t i = 0; i < 2; ++i) {
+    if ((nib(h, i) & 1u) == 0) {
+      h |= 1u << (4u * i);
+      reward_mover(L, d);
+    }
+  }
+  COUP_PSET(L, h, p, h);
+}
+
+// Second half of FA / Tax / Exchange / Steal, entered through the Pass
+// recursion (coup.cc:628) or the lost Exchange challenge (coup.cc:718); the
+// mover is the original actor and is_turn_begin_ is false here.
+__device__ __forceinline__ void complete_claim(Lane& L, uint32_t a) {
+  const uint32_t M = L.M, O = M ^ 1u;
+  switch (a) {
+    case kForeignAid:  // coup.cc:542-546
+      COUP_PSET(L, c, M, COUP_PGET(L, c, M) + 2u);
+      next_turn(L);
+      break;
+    case kTax:  // coup.cc:561-565
+      COUP_PSET(L, c, M, COUP_PGET(L, c, M) + 3u);
+      next_turn(L);
+      break;
+    case kExchange:  // coup.cc:581-587: draw two cards
+      queue_push(L, M);
+      queue_push(L, M);
+      break;
+    case kSteal: {  // coup.cc:597-603
+      const uint32_t oc = COUP_PGET(L, c, O);
+      const uint32_t k = oc > 1u ? 2u : 1u;
+      COUP_PSET(L, c, M, COUP_PGET(L, c, M) + k);
+      COUP_PSET(L, c, O, oc - k);
+      next_turn(L);
+      break;
+    }
+    default:
+      L.err = 1u;
+  }
+}
+
+// Challenge (coup.cc:635-771)
+__device__ __forceinline__ void apply_challenge(Lane& L) {
+  const uint32_t M = L.M, O = M ^ 1u;
+  const uint32_t op_last = COUP_PGET(L, l, O);
+  const uint32_t cp_last = COUP_PGET(L, l, M);
+  const uint32_t op_hand = COUP_PGET(L, h, O);
+  COUP_PSET(L, l, M, kChallenge);
+  if (op_last == kBlock) {
+    // the turn player challenges the block of its own claim (coup.cc:636-693)
+    if (cp_last == kForeignAid) {
+      if (has_face_down(op_hand, kDuke)) {
+        COUP_PSET(L, lost, M, 1u);
+        replace_card(L, kDuke);
+      } else {
+        COUP_PSET(L, lost, O, 1u);
+        COUP_PSET(L, c, M, COUP_PGET(L, c, M) + 2u);
+        next_move(L);
+      }
+    } else if (cp_last == kAssassinate) {
+      if (has_face_down(op_hand, kContessa)) {
+        COUP_PSET(L, lost, M, 1u);
+        replace_card(L, kContessa);
+      } else {
+        flip_two(L, O, +1);
+      }
+    } else if (cp_last == kSteal) {
+      if (has_face_down(op_hand, kCaptain)) {
+        COUP_PSET(L, lost, M, 1u);
+        replace_card(L, kCaptain);
+      } else if (has_face_down(op_hand, kAmbassador)) {
+        COUP_PSET(L, lost, M, 1u);
+        replace_card(L, kAmbassador);
+      } else {
+        COUP_PSET(L, lost, O, 1u);
+        const uint32_t oc = COUP_PGET(L, c, O);
+        const uint32_t k = oc > 1u ? 2u : 1u;
+        COUP_PSET(L, c, M, COUP_PGET(L, c, M) + k);
+        COUP_PSET(L, c, O, oc - k);
+        next_move(L);
+      }
+    } else {
+      COUP_PSET(L, l, M, cp_last);  // the reference aborts before touching state
+      L.err = 1u;
+    }
+    return;
+  }
+  switch (op_last) {
+    case kTax:  // coup.cc:694-706
+      if (has_face_down(op_hand, kDuke)) {
+        COUP_PSET(L, lost, M, 1u);
+        replace_card(L, kDuke);
+        COUP_PSET(L, c, O, COUP_PGET(L, c, O) + 3u);
+      } else {
+        COUP_PSET(L, lost, O, 1u);
+        next_move(L);
+      }
+      break;
+    case kExchange:  // coup.cc:708-725
+      if (has_face_down(op_hand, kAmbassador)) {
+        COUP_PSET(L, lost, M, 1u);
+        replace_card(L, kAmbassador);
+        next_move(L);
+        complete_claim(L, kExchange);  // queue: exchanger x3
+      } else {
+        COUP_PSET(L, lost, O, 1u);
+        next_move(L);
+      }
+      break;
+    case kAssassinate:  // coup.cc:727-749
+      if (has_face_down(op_hand, kAssassin)) {
+        flip_two(L, M, -1);
+      } else {
+        COUP_PSET(L, lost, O, 1u);
+        COUP_PSET(L, c, O, COUP_PGET(L, c, O) + 3u);  // refund
+        next_move(L);
+      }
+      break;
+    case kSteal:  // coup.cc:751-767 (the Ambassador does not count here)
+      if (has_face_down(op_hand, kCaptain)) {
+        COUP_PSET(L, lost, M, 1u);
+        replace_card(L, kCaptain);
+        const uint32_t mc = COUP_PGET(L, c, M);
+        const uint32_t k = mc > 1u ? 2u : 1u;
+        COUP_PSET(L, c, O, COUP_PGET(L, c, O) + k);
+        COUP_PSET(L, c, M, mc - k);
+      } else {
+        COUP_PSET(L, lost, O, 1u);
+        next_move(L);
+      }
+      break;
+    default:
+      COUP_PSET(L, l, M, cp_last);
+      L.err = 1u;
+  }
+}
+
+// Decision branch of DoApplyAction (coup.cc:522-808) for a LEGAL action.
+// Claims (FA / Tax / Exchange / Steal) are only legal at turn begin, so the
+// direct call always takes their "announce" half.
+__device__ __forceinline__ void apply_decision(Lane& L, uint32_t a) {
+  const uint32_t M = L.M, O = M ^ 1u;
+  L.r0 = 0;  // cur_rewards_ = {0, 0} (coup.cc:527)
+  if (a == kChallenge) {
+    apply_challenge(L);
+    return;
+  }
+  if (a >= kExchangeReturn12) {
+    // coup.cc:773-804: erase the higher slot, then the lower; each erased
+    // slot INDEX is credited to the deck (coup.cc:794 reference quirk)
+    const uint32_t k = a - kExchangeReturn12;
+    const uint32_t lo = (0x211000u >> (4u * k)) & 0xFu;  // {0,0,0,1,1,2}
+    const uint32_t hi = (0x332321u >> (4u * k)) & 0xFu;  // {1,2,3,2,3,3}
+    const uint32_t h = COUP_PGET(L, h, M);
+    COUP_PSET(L, h, M, hand_remove(hand_remove(h, hi), lo));
+    L.deck += (1u << (4u * hi)) + (1u << (4u * lo));
+    COUP_PSET(L, l, M, a);
+    if (COUP_PGET(L, lost, O))
+      next_move(L);
+    else
+      next_turn(L);
+    return;
+  }
+  if (a == kLoseCard1 || a == kLoseCard2) {
+    // coup.cc:605-616: flip the slot face up, re-sort, -1/+1 reward
+    const uint32_t slot = a - kLoseCard1;
+    const uint32_t h = COUP_PGET(L, h, M);
+    const uint32_t kind = nib(h, slot) | 1u;
+    COUP_PSET(L, h, M, hand_insert(hand_remove(h, slot), kind));
+    COUP_PSET(L, l, M, a);
+    COUP_PSET(L, lost, M, 0u);
+    reward_mover(L, -1);
+    next_turn(L);
+    return;
+  }
+  if (a == kPass) {
+    // coup.cc:618-629
+    const uint32_t pending = COUP_PGET(L, l, O);
+    COUP_PSET(L, l, M, kPass);
+    if (pending == kBlock) {
+      next_turn(L);
+    } else {
+      next_move(L);
+      complete_claim(L, pending);
+    }
+    return;
+  }
+  COUP_PSET(L, l, M, a);
+  switch (a) {
+    case kIncome:  // coup.cc:531-534
+      COUP_PSET(L, c, M, COUP_PGET(L, c, M) + 1u);
+      next_turn(L);
+      break;
+    case kCoup:  // coup.cc:548-553
+      COUP_PSET(L, c, M, COUP_PGET(L, c, M) - 7u);
+      next_move(L);
+      break;
+    case kAssassinate:  // coup.cc:567-573: paid even if blocked/challenged
+      COUP_PSET(L, c, M, COUP_PGET(L, c, M) - 3u);
+      next_move(L);
+      break;
+    default:  // FA, Tax, Exchange, Steal announce; Block (coup.cc:631-633)
+      next_move(L);
+      break;
+  }
+}
+
+// Chance branch of DoApplyAction (coup.cc:491-520): deal card `type` to the
+// queue front, keep the hand sorted.
+__device__ __forceinline__ void apply_deal(Lane& L, uint32_t type) {
+  const uint32_t p = L.qids & 1u;
+  L.qids >>= 1;
+  L.qlen -= 1u;
+  L.deck -= 1u << (4u * type);
+  COUP_PSET(L, h, p, hand_insert(COUP_PGET(L, h, p), 2u * type));
+}
+
+// State::ApplyAction (spiel.cc:322-331) with a legality check.  Returns false
+// (lane untouched) for an illegal action.
+__device__ __forceinline__ bool apply_action(Lane& L, uint32_t a) {
+  if (a > 17u) return false;
+  const uint32_t m = legal_mask(L);
+  if (((m >> a) & 1u) == 0u) return false;
+  if (m & kChanceFlag)
+    apply_deal(L, a);
+  else
+    apply_decision(L, a);
+  L.move += 1u;
+  return true;
+}
+
+// --------------------------------------------------- sampling contract
+
+// Philox4x32-10 (Salmon et al., SC'11), Random123 constants.
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// One 32-bit draw per history slot `idx` of episode `ep` of env `env_id`:
+// key = (env_id, seed lo), counter = (idx / 4, ep, seed hi, 'Coup'),
+// word idx % 4.  The Rng keeps the last Philox block so consecutive slots
+// of one block cost one evaluation.
+struct Rng {
+  uint32_t seed_lo, seed_hi, env_id;
+  uint32_t blk_tag;  // (episode << 5 | block) + 1 of the cached block, 0 = none
+  uint4 blk;
+
+  __device__ __forceinline__ uint32_t draw(uint32_t ep, uint32_t idx) {
+    const uint32_t tag = ((ep << 5) | (idx >> 2)) + 1u;
+    if (tag != blk_tag) {
+      blk = philox4x32_10(make_uint4(idx >> 2, ep, seed_hi, 0x436F7570u), env_id, seed_lo);
+      blk_tag = tag;
+    }
+    const uint32_t j = idx & 3u;
+    return j == 0 ? blk.x : (j == 1 ? blk.y : (j == 2 ? blk.z : blk.w));
+  }
+};
+
+// Chance draw: r = floor(u * sum(deck) / 2^32), first type whose cumulative
+// count exceeds r.
+__device__ __forceinline__ uint32_t sample_card(uint32_t deck, uint32_t u) {
+  uint32_t total = 0;
+#pragma unroll
+  for (uint32_t t = 0; t < 5; ++t) total += deck_count(deck, t);
+  const uint32_t r = __umulhi(u, total);
+  // r < total, so if no type below the Duke qualifies the Duke does
+  uint32_t cum = 0, pick = 4u;
+#pragma unroll
+  for (uint32_t t = 0; t < 4; ++t) {
+    cum += deck_count(deck, t);
+    pick = (pick == 4u && cum > r) ? t : pick;
+  }
+  return pick;
+}
+
+// Policy draw: idx = floor(u * popc(mask) / 2^32); the idx-th set bit of the
+// ascending mask (== LegalActions()[idx], coup.cc:824-938).
+__device__ __forceinline__ uint32_t sample_action(uint32_t mask, uint32_t u) {
+  const uint32_t idx = __umulhi(u, (uint32_t)__popc(mask));
+  for (uint32_t i = 0; i < idx; ++i) mask &= mask - 1u;
+  return (uint32_t)__builtin_ctz(mask);
+}
+
+// rl_environment._sample_external_events (rl_environment.py:369-382):
+// deal until a decision node or a terminal state.
+__device__ __forceinline__ void resolve_chance(Lane& L, Rng& rng) {
+  while (L.qlen != 0u && !is_terminal(L)) {
+    const uint32_t u = rng.draw(L.episode, L.move);
+    apply_deal(L, sample_card(L.deck, u));
+    L.move += 1u;
+  }
+}
+
+}  // namespace coup

@@ -1,0 +1,175 @@
+"""Batched Coup environment on one MI355X: torch tensors over the C ABI.
+
+`BatchedCoupEnv` is the vectorised replacement of the reference's per-game
+Python loop (rl_environment.Environment + SyncVectorEnv,
+open_spiel/python/rl_environment.py:143-470, vector_env.py:17-78): one call
+steps every lane on the GPU.  Buffers are caller-visible torch tensors on
+the env's device; kernels run on torch's current stream.
+"""
+import ctypes
+
+import torch
+
+from . import _native
+
+FIRST, MID, LAST = 0, 1, 2
+NUM_ACTIONS = 18
+OBS_SIZE = 98
+INFO_STATE_SIZE = 2492
+CHANCE_FLAG = 1 << 31
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class BatchedCoupEnv:
+    """B independent 2-player Coup games stepped together.
+
+    Args:
+      batch: number of lanes B.
+      seed: 64-bit seed of the sampling contract.
+      env_id_base: global id of lane 0 (lane i uses env_id_base + i); ranks
+        of a multi-GPU job pass disjoint ranges.
+      auto_reset: SyncVectorEnv(reset_if_done=True) semantics if True,
+        rl_environment semantics (LAST, then reset on the next step) if False.
+      obs: write ObservationTensor of both players on every step.
+      device: CUDA (HIP) device.
+    """
+
+    def __init__(self, batch, seed=0, env_id_base=0, auto_reset=True, obs=True, device=None):
+        self.lib = _native.load()
+        self.device = torch.device(device if device is not None else "cuda")
+        if self.device.type != "cuda":
+            raise ValueError("BatchedCoupEnv runs on a HIP device only")
+        self.batch = int(batch)
+        self.seed = int(seed)
+        self.env_id_base = int(env_id_base)
+        self.auto_reset = bool(auto_reset)
+        self._h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _native.check(self.lib.coup_create(self.batch, self.seed, self.env_id_base,
+                                               int(self.auto_reset), ctypes.byref(self._h)))
+        B, dev = self.batch, self.device
+        self.actions = torch.empty(B, dtype=torch.int8, device=dev)
+        self.rewards = torch.zeros(B, 2, dtype=torch.int8, device=dev)
+        self.step_type = torch.zeros(B, dtype=torch.uint8, device=dev)
+        self.legal_mask = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.cur_player = torch.zeros(B, dtype=torch.int8, device=dev)
+        self.obs = torch.zeros(B, 2, OBS_SIZE, dtype=torch.float32, device=dev) if obs else None
+        self._out = _native.StepOutputs(
+            _ptr(self.actions).value, _ptr(self.rewards).value, _ptr(self.step_type).value,
+            _ptr(self.legal_mask).value, _ptr(self.cur_player).value,
+            _ptr(self.obs).value if self.obs is not None else None)
+
+    # ------------------------------------------------------------ plumbing
+    def _bind_stream(self):
+        s = torch.cuda.current_stream(self.device).cuda_stream
+        _native.check(self.lib.coup_set_stream(self._h, ctypes.c_void_p(s)))
+
+    def close(self):
+        if self._h:
+            self.lib.coup_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _mask_ptr(self, mask):
+        if mask is None:
+            return None
+        mask = mask.to(device=self.device, dtype=torch.uint8).contiguous()
+        self._keep = mask
+        return _ptr(mask)
+
+    # ------------------------------------------------------------ batched API
+    def reset(self, mask=None):
+        """rl_environment.reset for all lanes (or lanes where mask != 0)."""
+        self._bind_stream()
+        _native.check(self.lib.coup_reset(self._h, self._mask_ptr(mask)))
+        return self.query()
+
+    def step(self, actions=None):
+        """One batched env step.  actions: int8/long tensor [B] of decision
+        actions, or None for the in-kernel uniform random policy.  Returns a
+        dict of tensors (views of the env's output buffers)."""
+        self._bind_stream()
+        a = None
+        if actions is not None:
+            actions = actions.to(device=self.device, dtype=torch.int8).contiguous()
+            if actions.numel() != self.batch:
+                raise ValueError("actions must have one entry per lane")
+            self._keep_actions = actions
+            a = _ptr(actions)
+        _native.check(self.lib.coup_step(self._h, a, ctypes.byref(self._out)))
+        out = {"actions": self.actions, "rewards": self.rewards, "step_type": self.step_type,
+               "legal_mask": self.legal_mask, "current_player": self.cur_player}
+        if self.obs is not None:
+            out["obs"] = self.obs
+        return out
+
+    def rollout(self, steps, stats=None):
+        """`steps` uniform-random steps per lane in one launch.  stats: optional
+        dict with int32 [B] tensors 'episodes', 'return_sum', 'length_sum'
+        (accumulated)."""
+        self._bind_stream()
+        s = None
+        if stats is not None:
+            s = _native.RolloutStats(_ptr(stats["episodes"]).value, _ptr(stats["return_sum"]).value,
+                                     _ptr(stats["length_sum"]).value)
+        _native.check(self.lib.coup_rollout(self._h, int(steps), ctypes.byref(s) if s else None))
+
+    def new_stats(self):
+        z = lambda: torch.zeros(self.batch, dtype=torch.int32, device=self.device)  # noqa: E731
+        return {"episodes": z(), "return_sum": z(), "length_sum": z()}
+
+    # ------------------------------------------------- State surface per lane
+    def new_initial_state(self, mask=None):
+        self._bind_stream()
+        _native.check(self.lib.coup_new_initial_state(self._h, self._mask_ptr(mask)))
+
+    def apply_action(self, actions):
+        """State::ApplyAction per lane (decision or chance outcome; <0 = skip)."""
+        self._bind_stream()
+        actions = actions.to(device=self.device, dtype=torch.int8).contiguous()
+        self._keep_actions = actions
+        _native.check(self.lib.coup_apply_action(self._h, _ptr(actions)))
+
+    def query(self, obs=True):
+        self._bind_stream()
+        B, dev = self.batch, self.device
+        q = {"legal_mask": torch.empty(B, dtype=torch.int32, device=dev),
+             "current_player": torch.empty(B, dtype=torch.int8, device=dev),
+             "terminal": torch.empty(B, dtype=torch.uint8, device=dev),
+             "rewards": torch.empty(B, 2, dtype=torch.int8, device=dev),
+             "returns": torch.empty(B, 2, dtype=torch.int8, device=dev)}
+        if obs:
+            q["obs"] = torch.empty(B, 2, OBS_SIZE, dtype=torch.float32, device=dev)
+        qo = _native.QueryOutputs(*[_ptr(q[k]).value if k in q else None for k in
+                                    ("legal_mask", "current_player", "terminal", "rewards", "returns", "obs")])
+        _native.check(self.lib.coup_query(self._h, ctypes.byref(qo)))
+        return q
+
+    def export_state(self):
+        self._bind_stream()
+        out = torch.empty(self.batch, 4, dtype=torch.int32, device=self.device)
+        _native.check(self.lib.coup_export_state(self._h, _ptr(out)))
+        return out
+
+    def import_state(self, packed):
+        self._bind_stream()
+        packed = packed.to(device=self.device, dtype=torch.int32).contiguous()
+        if packed.shape != (self.batch, 4):
+            raise ValueError("packed state must be [B, 4] int32")
+        self._keep_state = packed
+        _native.check(self.lib.coup_import_state(self._h, _ptr(packed)))
+
+    def error_count(self):
+        """Lanes that rejected an action since the last call (synchronises)."""
+        self._bind_stream()
+        n = ctypes.c_int64()
+        _native.check(self.lib.coup_error_count(self._h, ctypes.byref(n)))
+        return n.value

@@ -892,8 +892,8 @@ int oc_rollout(const oc_rollout_args* a) {
       }
       if (a->step_type) a->step_type[o] = st;
       if (a->legal) a->legal[o] = oc_legal_mask(&s);
-      if (a->obs && (!a->obs_last_only || t == a->steps - 1)) {
-        float* dst = a->obs + (a->obs_last_only ? lane : o) * 2 * OC_OBS_SIZE;
+      if (a->obs) {
+        float* dst = a->obs + (a->obs_overwrite ? lane : o) * 2 * OC_OBS_SIZE;
         oc_observation_tensor(&s, 0, dst);
         oc_observation_tensor(&s, 1, dst + OC_OBS_SIZE);
       }

@@ -119,7 +119,8 @@ uint32_t oc_draw(uint64_t seed, uint32_t env_id, uint32_t episode, uint32_t draw
  * restart finished episodes.  Any output pointer may be NULL.
  *   actions[steps][n], rewards[steps][n][2], step_type[steps][n],
  *   legal[steps][n], obs[steps][n][2][98], final_state[n][4]
- * obs_last_only: write obs only for the final step, into obs[n][2][98].
+ * obs_overwrite: write obs at every step into the same obs[n][2][98] buffer
+ * (the GPU env overwrites its obs buffer the same way).
  */
 typedef struct {
   uint64_t seed;
@@ -127,7 +128,7 @@ typedef struct {
   int64_t n;
   int64_t steps;
   int auto_reset;
-  int obs_last_only;
+  int obs_overwrite;
   int8_t* actions;
   int8_t* rewards;
   uint8_t* step_type;

@@ -44,7 +44,7 @@ class _OcState(ctypes.Structure):
 class _RolloutArgs(ctypes.Structure):
     _fields_ = [("seed", ctypes.c_uint64), ("env_id_base", ctypes.c_uint32),
                 ("n", ctypes.c_int64), ("steps", ctypes.c_int64),
-                ("auto_reset", ctypes.c_int), ("obs_last_only", ctypes.c_int),
+                ("auto_reset", ctypes.c_int), ("obs_overwrite", ctypes.c_int),
                 ("actions", ctypes.c_void_p), ("rewards", ctypes.c_void_p),
                 ("step_type", ctypes.c_void_p), ("legal", ctypes.c_void_p),
                 ("obs", ctypes.c_void_p), ("final_state", ctypes.c_void_p),
@@ -208,14 +208,14 @@ def philox(ctr, key):
 
 
 def rollout(seed, n, steps, env_id_base=0, auto_reset=True, want_obs=False,
-            obs_last_only=False, want_trajectory=True):
+            obs_overwrite=False, want_trajectory=True):
     """Uniform-random batched rollout under the sampling contract.
 
     Returns a dict of numpy arrays (step-major: [steps][n]...)."""
     out = {}
     a = _RolloutArgs()
     a.seed, a.env_id_base, a.n, a.steps = seed, env_id_base, n, steps
-    a.auto_reset, a.obs_last_only = int(auto_reset), int(obs_last_only)
+    a.auto_reset, a.obs_overwrite = int(auto_reset), int(obs_overwrite)
 
     def buf(name, shape, dtype):
         arr = np.zeros(shape, dtype)
@@ -228,7 +228,7 @@ def rollout(seed, n, steps, env_id_base=0, auto_reset=True, want_obs=False,
         a.step_type = buf("step_type", (steps, n), np.uint8)
         a.legal = buf("legal", (steps, n), np.uint32)
     if want_obs:
-        shape = (n, 2, OBS_SIZE) if obs_last_only else (steps, n, 2, OBS_SIZE)
+        shape = (n, 2, OBS_SIZE) if obs_overwrite else (steps, n, 2, OBS_SIZE)
         a.obs = buf("obs", shape, np.float32)
     a.final_state = buf("final_state", (n, 4), np.uint32)
     a.decisions = buf("decisions", (1,), np.int64)

@@ -1,0 +1,202 @@
+"""Parity of the HIP path (through the C ABI) with the oracle and with the
+reference's golden vectors.  Bit-exact everywhere: integer state, legal
+masks, rewards, step types and the fp32 observation tensors (whose values
+are exact small integers)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle
+from tests import golden_util as G
+
+pytestmark = pytest.mark.gpu
+
+from open_spiel_coup_amd import BatchedCoupEnv, packed  # noqa: E402
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+def _mask_to_list(m):
+    m = int(m) & 0x3FFFF
+    return [a for a in range(18) if (m >> a) & 1]
+
+
+# ------------------------------------------------------------------ goldens
+
+def test_kat_scenarios_batched():
+    """All 14 coup_test.cc scenarios at once, one lane each, through
+    coup_apply_action / coup_query / coup_export_state."""
+    kats = G.load_kats()
+    B = len(kats)
+    env = BatchedCoupEnv(B, seed=0, obs=False)
+    env.new_initial_state()
+    maxlen = max(len(s["actions"]) for s in kats)
+    checks = {(i, c["after"]): c for i, s in enumerate(kats) for c in s["checks"]}
+    for k in range(maxlen + 1):
+        if k > 0:
+            acts = torch.tensor([s["actions"][k - 1] if k - 1 < len(s["actions"]) else -1 for s in kats],
+                                dtype=torch.int8)
+            env.apply_action(acts)
+        q = env.query(obs=False)
+        words = _np(env.export_state())
+        legal, cur, term = _np(q["legal_mask"]), _np(q["current_player"]), _np(q["terminal"])
+        rew, ret = _np(q["rewards"]), _np(q["returns"])
+        for i in range(B):
+            c = checks.get((i, k))
+            if c is None:
+                continue
+            r = packed.lane(words, i)
+            G.check_kat(c, lambda p: r["cards"][p], lambda p: r["coins"][p], lambda p: r["last_action"][p],
+                        lambda: int(cur[i]), lambda: _mask_to_list(legal[i]), lambda: bool(term[i]),
+                        lambda: rew[i].tolist(), lambda: ret[i].tolist())
+    assert env.error_count() == 0
+
+
+def test_playthrough_transcript():
+    """Replay coup.txt's history; compare every recorded field (legal sets,
+    chance probabilities, current player, rewards, returns, obs tensors)."""
+    pt = G.load_playthrough()["states"]
+    env = BatchedCoupEnv(1, seed=0, obs=False)
+    env.new_initial_state()
+    hist = pt[-1]["history"]
+    for k in range(len(hist) + 1):
+        if k > 0:
+            env.apply_action(torch.tensor([hist[k - 1]], dtype=torch.int8))
+        rec = pt[k]
+        assert rec["history"] == hist[:k]
+        q = env.query()
+        r = packed.lane(_np(env.export_state()), 0)
+        assert r["move_number"] == k
+        if "current_player" not in rec:
+            continue
+        cur, term = int(_np(q["current_player"])[0]), bool(_np(q["terminal"])[0])
+        assert cur == rec["current_player"] and term == rec["is_terminal"]
+        mask = int(_np(q["legal_mask"])[0]) & 0xFFFFFFFF
+        if rec["is_chance"]:
+            assert mask & (1 << 31)
+            assert _mask_to_list(mask & 0x1F) == rec["legal_actions"]
+            total = float(sum(r["deck"]))
+            got = [(t, r["deck"][t] / total) for t in range(5) if r["deck"][t] > 0]
+            assert got == [tuple(x) for x in rec["chance_outcomes"]]
+        else:
+            if not term:
+                assert _mask_to_list(mask) == rec["legal_actions"]
+            assert _np(q["rewards"])[0].tolist() == [int(x) for x in rec["rewards"]]
+            assert _np(q["returns"])[0].tolist() == [int(x) for x in rec["returns"]]
+        obs = _np(q["obs"])[0]
+        for p in (0, 1):
+            np.testing.assert_array_equal(obs[p], G.dense(rec["ObservationTensor"][str(p)], 98))
+
+
+# --------------------------------------------------------- oracle rollouts
+
+@pytest.mark.parametrize("auto_reset", [True, False])
+def test_uniform_rollout_matches_oracle(auto_reset):
+    """coup_step with the in-kernel uniform policy == the oracle's rollout
+    under the same sampling contract: actions, rewards, step types, legal
+    masks and obs at every step, final packed state bit for bit."""
+    n, steps, seed, base = 2048, 160, 11, 1000
+    ref = oracle.rollout(seed=seed, n=n, steps=steps, env_id_base=base, auto_reset=auto_reset, want_obs=True)
+    env = BatchedCoupEnv(n, seed=seed, env_id_base=base, auto_reset=auto_reset, obs=True)
+    for t in range(steps):
+        o = env.step()
+        np.testing.assert_array_equal(_np(o["actions"]), ref["actions"][t], err_msg=f"step {t}")
+        np.testing.assert_array_equal(_np(o["rewards"]), ref["rewards"][t], err_msg=f"step {t}")
+        np.testing.assert_array_equal(_np(o["step_type"]), ref["step_type"][t], err_msg=f"step {t}")
+        np.testing.assert_array_equal(_np(o["legal_mask"]).astype(np.uint32), ref["legal"][t],
+                                      err_msg=f"step {t}")
+        np.testing.assert_array_equal(_np(o["obs"]), ref["obs"][t], err_msg=f"step {t}")
+    np.testing.assert_array_equal(_np(env.export_state()).astype(np.uint32), ref["final_state"])
+    assert env.error_count() == 0
+
+
+def test_external_actions_replay():
+    """Feeding the oracle's chosen actions back through coup_step(actions)
+    reproduces the same trajectory (chance deals depend only on the env's
+    stream, not on who chose the decision)."""
+    n, steps, seed = 1024, 120, 5
+    ref = oracle.rollout(seed=seed, n=n, steps=steps, auto_reset=True)
+    env = BatchedCoupEnv(n, seed=seed, auto_reset=True, obs=False)
+    for t in range(steps):
+        o = env.step(torch.from_numpy(ref["actions"][t]).cuda())
+        np.testing.assert_array_equal(_np(o["rewards"]), ref["rewards"][t])
+        np.testing.assert_array_equal(_np(o["legal_mask"]).astype(np.uint32), ref["legal"][t])
+    np.testing.assert_array_equal(_np(env.export_state()).astype(np.uint32), ref["final_state"])
+    assert env.error_count() == 0
+
+
+def test_fused_rollout_matches_oracle():
+    """coup_rollout (K steps per launch, registers only) lands on the same
+    states and episode statistics as the oracle."""
+    n, steps, seed = 4096, 300, 21
+    ref = oracle.rollout(seed=seed, n=n, steps=steps, auto_reset=True, want_trajectory=False)
+    env = BatchedCoupEnv(n, seed=seed, auto_reset=True, obs=False)
+    stats = env.new_stats()
+    env.rollout(100, stats)
+    env.rollout(200, stats)
+    np.testing.assert_array_equal(_np(env.export_state()).astype(np.uint32), ref["final_state"])
+    assert int(stats["episodes"].sum()) == int(ref["episodes_done"][0])
+    assert int(stats["return_sum"].sum()) == int(ref["return_sum_p0"][0])
+    assert env.error_count() == 0
+
+
+def test_illegal_action_rejected():
+    env = BatchedCoupEnv(4, seed=0, obs=False)
+    before = _np(env.export_state()).copy()
+    # at the first decision P1 may not Pass / Block / LoseCard
+    env.step(torch.tensor([9, 10, 7, 18], dtype=torch.int8))
+    assert env.error_count() == 4
+    np.testing.assert_array_equal(_np(env.export_state()), before)
+
+
+def test_shard_invariance():
+    """Lanes [k, k+m) of one env == an env of m lanes with env_id_base=k:
+    the basis of id-range sharding over GPUs."""
+    seed, steps = 99, 64
+    big = BatchedCoupEnv(1024, seed=seed, obs=False)
+    part = BatchedCoupEnv(256, seed=seed, env_id_base=512, obs=False)
+    big.rollout(steps)
+    part.rollout(steps)
+    np.testing.assert_array_equal(_np(big.export_state())[512:768], _np(part.export_state()))
+
+
+# ------------------------------------------------------ full-size properties
+
+def test_full_batch_properties():
+    """At the benchmark batch (2^20 lanes): per-lane invariants after many
+    steps.  Deck + hands always hold 15 cards, at most one face-up card per
+    live player's 2-card hand, legal masks non-empty and well-formed, obs
+    one-hots valid and coins mirrored, rewards zero-sum."""
+    B = 1 << 20
+    env = BatchedCoupEnv(B, seed=1, obs=True)
+    for _ in range(40):
+        o = env.step()
+    d = packed.decode(_np(env.export_state()))
+    cards = np.zeros(B, np.int64)
+    for p in (0, 1):
+        h = d["hand"][:, p]
+        for i in range(4):
+            cards += ((h >> (4 * i)) & 0xF) != 0xF
+    assert np.all(d["deck"].sum(1) + cards == 15)
+    assert np.all(d["queue_len"] == 0) and np.all(d["error"] == 0)
+    legal = _np(o["legal_mask"]).astype(np.uint32)
+    assert np.all(legal != 0) and np.all(legal < (1 << 18))
+    obs = _np(o["obs"])
+    assert np.all(obs[:, 0, 0] == 1) and np.all(obs[:, 1, 1] == 1)
+    assert np.all(obs[:, :, 42:44].sum(-1) == 1)
+    assert np.all(obs[:, 0, 60:62] == d["coins"]) and np.all(obs[:, 1, 60:62] == d["coins"])
+    rw = _np(o["rewards"]).astype(np.int32)
+    assert np.all(rw[:, 0] == -rw[:, 1]) and np.all(np.abs(rw) <= 2)
+    assert env.error_count() == 0
+
+
+def test_determinism_full_batch():
+    B = 1 << 20
+    a = BatchedCoupEnv(B, seed=3, obs=False)
+    b = BatchedCoupEnv(B, seed=3, obs=False)
+    a.rollout(50)
+    for _ in range(50):
+        b.step()
+    assert torch.equal(a.export_state(), b.export_state())
