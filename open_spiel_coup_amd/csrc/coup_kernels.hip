@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -71,6 +72,128 @@ __device__ __forceinline__ void write_obs_pair(float* __restrict__ dst, const La
   }
 }
 
+// ---- wave-cooperative write-out ------------------------------------------
+//
+// A wave's 64 lanes own 64 consecutive rows of 196 floats = 3136 float4
+// (50,176 contiguous bytes).  Iteration j of 49 stores float4 number
+// 64*j + lane of that chunk, so every store instruction writes 1 KiB
+// contiguous.  The float4 belongs to lane o = x / 49 (x = 64*j + lane), at
+// float offset 4*(x % 49) of o's row; its four values are decoded from o's
+// observation KEY (3 u32 fetched with ds_bpermute) through a per-offset
+// DESCRIPTOR table held in LDS.
+//
+// Key words (per lane; only K0 depends on the observer P):
+//   K0_P: [0] P, [1+3k .. 3+3k] visible type of card slot k = 4*owner+slot
+//         (7 = hidden or empty), [25:26] mover (3 when terminal),
+//         [27+2k .. 28+2k] face of slot k < 2 (0 down, 1 up, 3 empty)
+//   K1:   [2(k-2) ..] face of slots k = 2..7, [12:15] P1 coins,
+//         [16:19] P2 coins, [20:24] P1 last action, [25:29] P2 last action
+// Descriptor of float g in [0,196): [4:0] bit offset, [12:8] width,
+//   [20:16] value compared against, [24] raw (coins: the field itself),
+//   [25] field in K1, [26] observer P = g >= 98.
+constexpr int kRowF4 = 2 * kObsSize / 4;  // 49 float4 per lane row
+
+__device__ __forceinline__ uint32_t obs_desc(int g) {
+  const uint32_t P = g >= kObsSize;
+  const int f = g - (int)P * kObsSize;
+  uint32_t off, width, cmp = 0, raw = 0, k1 = 0;
+  if (f < 2) {
+    off = 0, width = 1, cmp = f;
+  } else if (f < 42) {
+    const int k = (f - 2) / 5;  // 4*owner + slot
+    off = 1 + 3 * k, width = 3, cmp = (f - 2) % 5;
+  } else if (f < 44) {
+    off = 25, width = 2, cmp = f - 42;
+  } else if (f < 60) {
+    const int k = (f - 44) / 2;
+    width = 2, cmp = (f - 44) % 2;
+    if (k < 2) {
+      off = 27 + 2 * k;
+    } else {
+      off = 2 * (k - 2), k1 = 1;
+    }
+  } else if (f < 62) {
+    off = 12 + 4 * (f - 60), width = 4, raw = 1, k1 = 1;
+  } else {
+    const int q = (f - 62) / 18;
+    off = 20 + 5 * q, width = 5, cmp = (f - 62) % 18, k1 = 1;
+  }
+  return off | (width << 8) | (cmp << 16) | (raw << 24) | (k1 << 25) | (P << 26);
+}
+
+struct ObsKey {
+  uint32_t k0p0, k0p1, k1;
+};
+
+__device__ __forceinline__ ObsKey obs_key(const Lane& L) {
+  const bool term = is_terminal(L);
+  uint32_t vis0 = 0, vis1 = 0, face_lo = 0, k1 = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 8; ++k) {
+    const uint32_t n = nib(k < 4 ? L.h0 : L.h1, k & 3u);
+    const uint32_t up = n & 1u;
+    const uint32_t own = n == 0xFu ? 7u : (n >> 1);          // owner sees every card
+    const uint32_t pub = (n == 0xFu || !up) ? 7u : (n >> 1); // others see face-up cards
+    vis0 |= (k < 4 ? own : pub) << (1u + 3u * k);
+    vis1 |= (k < 4 ? pub : own) << (1u + 3u * k);
+    const uint32_t face = n == 0xFu ? 3u : up;
+    if (k < 2)
+      face_lo |= face << (27u + 2u * k);
+    else
+      k1 |= face << (2u * (k - 2u));
+  }
+  const uint32_t cur = (term ? 3u : L.M) << 25;
+  ObsKey K;
+  K.k0p0 = vis0 | cur | face_lo;
+  K.k0p1 = 1u | vis1 | cur | face_lo;
+  K.k1 = k1 | (L.c0 << 12) | (L.c1 << 16) | (L.l0 << 20) | (L.l1 << 25);
+  return K;
+}
+
+__device__ __forceinline__ float obs_decode(uint32_t d, uint32_t k0p0, uint32_t k0p1, uint32_t k1) {
+  const uint32_t w = (d & (1u << 25)) ? k1 : ((d & (1u << 26)) ? k0p1 : k0p0);
+  const uint32_t v = __builtin_amdgcn_ubfe(w, d & 31u, (d >> 8) & 31u);
+  const uint32_t c = (d >> 16) & 31u;
+  return (d & (1u << 24)) ? (float)v : (v == c ? 1.0f : 0.0f);
+}
+
+// All 64 lanes of the wave must call this (no lane may have exited).
+// wave_obs: the wave's first row; n_valid: rows of this wave that exist.
+template <bool NT>
+__device__ __forceinline__ void write_obs_wave(float* __restrict__ wave_obs, const ObsKey& K, uint32_t n_valid,
+                                               const uint4* __restrict__ desc_lds) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  v4f* dst = reinterpret_cast<v4f*>(wave_obs);
+  const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll 7
+  for (uint32_t j = 0; j < (uint32_t)kRowF4; ++j) {
+    const uint32_t x = 64u * j + lane;
+    const uint32_t o = x / (uint32_t)kRowF4;
+    const uint32_t c = x - o * (uint32_t)kRowF4;
+    const uint32_t a0 = (uint32_t)__shfl((int)K.k0p0, (int)o);
+    const uint32_t a1 = (uint32_t)__shfl((int)K.k0p1, (int)o);
+    const uint32_t b = (uint32_t)__shfl((int)K.k1, (int)o);
+    const uint4 d = desc_lds[c];
+    v4f v;
+    v.x = obs_decode(d.x, a0, a1, b);
+    v.y = obs_decode(d.y, a0, a1, b);
+    v.z = obs_decode(d.z, a0, a1, b);
+    v.w = obs_decode(d.w, a0, a1, b);
+    if (o < n_valid) {
+      if (NT)
+        __builtin_nontemporal_store(v, dst + x);
+      else
+        dst[x] = v;
+    }
+  }
+}
+
+// Fill the block's LDS copy of the 196-entry descriptor table (as 49 uint4).
+__device__ __forceinline__ void load_obs_desc(uint32_t* desc_lds) {
+  for (int g = threadIdx.x; g < 2 * kObsSize; g += blockDim.x) desc_lds[g] = obs_desc(g);
+  __syncthreads();
+}
+
 __device__ __forceinline__ int32_t return0(const Lane& L) {
   // Returns (coup.cc:1016-1032): face-up(P2) - face-up(P1)
   return (int32_t)face_up_count(L.h1) - (int32_t)face_up_count(L.h0);
@@ -97,59 +220,89 @@ struct StepArgs {
 
 // One rl_environment step per lane (rl_environment.py:282-322), optionally
 // with SyncVectorEnv auto-reset (vector_env.py:40-67).
-template <bool UNIFORM, bool OBS>
-__global__ __launch_bounds__(kThreads) void k_step(StepArgs a) {
-  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (i >= a.n) return;
-  Lane L = unpack(a.state[i]);
+// Observation write-out variants (COUP_OBS_MODE selects one at run time for
+// A/B measurements; kObsWave is the default).
+enum ObsMode : int { kObsNone = 0, kObsLaneRows = 1, kObsWave = 2, kObsWaveNT = 3 };
+
+// The per-lane part of one env step: returns the decision applied (-1 if
+// none), the step type and player 0's reward; L is updated in place.
+template <bool UNIFORM>
+__device__ __forceinline__ void step_lane(const StepArgs& a, int64_t i, Lane& L, int& act, uint32_t& st,
+                                          int32_t& rew) {
   Rng rng{a.seed_lo, a.seed_hi, a.env_id_base + (uint32_t)i, 0u, make_uint4(0, 0, 0, 0)};
-  int act = -1;
-  uint32_t st;
-  int32_t rew = 0;
+  act = -1;
+  rew = 0;
   if (is_terminal(L)) {
     // step() after LAST starts a new episode (rl_environment.py:310-311)
     L = initial_lane(L.episode + 1u);
     resolve_chance(L, rng);
     st = COUP_STEP_FIRST;
+    return;
+  }
+  resolve_chance(L, rng);  // no-op unless the lane was left at a chance node
+  const uint32_t m = decision_mask(L);
+  uint32_t x;
+  if (UNIFORM) {
+    x = m ? sample_action(m, rng.draw(L.episode, L.move)) : 32u;
   } else {
-    resolve_chance(L, rng);  // no-op unless the lane was left at a chance node
-    const uint32_t m = decision_mask(L);
-    uint32_t x;
-    if (UNIFORM) {
-      x = m ? sample_action(m, rng.draw(L.episode, L.move)) : 32u;
-    } else {
-      x = (uint32_t)(uint8_t)a.actions_in[i];
-    }
-    st = COUP_STEP_MID;
-    if (x > 17u || ((m >> x) & 1u) == 0u || is_terminal(L)) {
-      count_error(a.err_count);
-    } else {
-      const uint32_t err_before = L.err;
-      apply_decision(L, x);
-      L.move += 1u;
+    x = (uint32_t)(uint8_t)a.actions_in[i];
+  }
+  st = COUP_STEP_MID;
+  if (x > 17u || ((m >> x) & 1u) == 0u || is_terminal(L)) {
+    count_error(a.err_count);
+    return;
+  }
+  const uint32_t err_before = L.err;
+  apply_decision(L, x);
+  L.move += 1u;
+  resolve_chance(L, rng);
+  if (L.err && !err_before) count_error(a.err_count);
+  act = (int)x;
+  rew = L.r0;
+  if (is_terminal(L)) {
+    st = COUP_STEP_LAST;
+    if (a.auto_reset) {
+      // SyncVectorEnv.step(reset_if_done=True) (vector_env.py:62-65)
+      L = initial_lane(L.episode + 1u);
       resolve_chance(L, rng);
-      if (L.err && !err_before) count_error(a.err_count);
-      act = (int)x;
-      rew = L.r0;
-      if (is_terminal(L)) {
-        st = COUP_STEP_LAST;
-        if (a.auto_reset) {
-          L = initial_lane(L.episode + 1u);
-          resolve_chance(L, rng);
-        }
-      }
     }
   }
-  a.state[i] = pack(L);
-  if (a.actions) a.actions[i] = (int8_t)act;
-  if (a.rewards) {
-    a.rewards[2 * i] = (int8_t)rew;
-    a.rewards[2 * i + 1] = (int8_t)(-rew);
+}
+
+// One rl_environment step per lane (rl_environment.py:282-322), optionally
+// with SyncVectorEnv auto-reset (vector_env.py:40-67).  No early exit: the
+// wave-cooperative obs writer needs every lane of the wave.
+template <bool UNIFORM, int OBS>
+__global__ __launch_bounds__(kThreads) void k_step(StepArgs a) {
+  __shared__ uint4 desc_lds[kRowF4];
+  if (OBS == kObsWave || OBS == kObsWaveNT) load_obs_desc(reinterpret_cast<uint32_t*>(desc_lds));
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  const bool active = i < a.n;
+  Lane L = initial_lane(0);
+  if (active) {
+    L = unpack(a.state[i]);
+    int act;
+    uint32_t st;
+    int32_t rew;
+    step_lane<UNIFORM>(a, i, L, act, st, rew);
+    a.state[i] = pack(L);
+    if (a.actions) a.actions[i] = (int8_t)act;
+    if (a.rewards) {
+      a.rewards[2 * i] = (int8_t)rew;
+      a.rewards[2 * i + 1] = (int8_t)(-rew);
+    }
+    if (a.step_type) a.step_type[i] = (uint8_t)st;
+    if (a.legal) a.legal[i] = legal_mask(L);
+    if (a.cur_player) a.cur_player[i] = (int8_t)current_player(L);
+    if (OBS == kObsLaneRows) write_obs_pair(a.obs + i * (2 * kObsSize), L);
   }
-  if (a.step_type) a.step_type[i] = (uint8_t)st;
-  if (a.legal) a.legal[i] = legal_mask(L);
-  if (a.cur_player) a.cur_player[i] = (int8_t)current_player(L);
-  if (OBS) write_obs_pair(a.obs + i * (2 * kObsSize), L);
+  if (OBS == kObsWave || OBS == kObsWaveNT) {
+    const int64_t wave0 = i - (int64_t)(threadIdx.x & 63u);
+    const int64_t left = a.n - wave0;
+    const uint32_t n_valid = left >= 64 ? 64u : (left > 0 ? (uint32_t)left : 0u);
+    if (n_valid > 0)  // wave-uniform
+      write_obs_wave<OBS == kObsWaveNT>(a.obs + wave0 * (2 * kObsSize), obs_key(L), n_valid, desc_lds);
+  }
 }
 
 struct RolloutArgs {
@@ -299,6 +452,13 @@ int fail(int code, const std::string& msg) {
 #define COUP_CHECK_ENV(env) \
   if (!(env)) return fail(COUP_E_INVALID, "null coup_env")
 
+// COUP_OBS_MODE=1|2|3 overrides the observation writer (A/B measurements).
+int obs_mode() {
+  const char* e = std::getenv("COUP_OBS_MODE");
+  const int m = e ? std::atoi(e) : (int)coup::kObsWave;
+  return (m >= 1 && m <= 3) ? m : (int)coup::kObsWave;
+}
+
 unsigned grid_for(int64_t n) { return (unsigned)((n + coup::kThreads - 1) / coup::kThreads); }
 
 int launch_reset(coup_env* env, const uint8_t* mask, int mode, int deal) {
@@ -404,15 +564,21 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
     a.obs = out->obs;
   }
   const unsigned g = grid_for(env->batch);
-  const bool uniform = actions == nullptr, obs = a.obs != nullptr;
-  if (uniform && obs)
-    coup::k_step<true, true><<<g, coup::kThreads, 0, env->stream>>>(a);
-  else if (uniform)
-    coup::k_step<true, false><<<g, coup::kThreads, 0, env->stream>>>(a);
-  else if (obs)
-    coup::k_step<false, true><<<g, coup::kThreads, 0, env->stream>>>(a);
-  else
-    coup::k_step<false, false><<<g, coup::kThreads, 0, env->stream>>>(a);
+  const bool uniform = actions == nullptr;
+  const int mode = a.obs == nullptr ? coup::kObsNone : obs_mode();
+  hipStream_t s = env->stream;
+#define COUP_LAUNCH_STEP(U, M) coup::k_step<U, M><<<g, coup::kThreads, 0, s>>>(a)
+  switch ((uniform ? 4 : 0) + mode) {
+    case 0: COUP_LAUNCH_STEP(false, coup::kObsNone); break;
+    case 1: COUP_LAUNCH_STEP(false, coup::kObsLaneRows); break;
+    case 2: COUP_LAUNCH_STEP(false, coup::kObsWave); break;
+    case 3: COUP_LAUNCH_STEP(false, coup::kObsWaveNT); break;
+    case 4: COUP_LAUNCH_STEP(true, coup::kObsNone); break;
+    case 5: COUP_LAUNCH_STEP(true, coup::kObsLaneRows); break;
+    case 6: COUP_LAUNCH_STEP(true, coup::kObsWave); break;
+    default: COUP_LAUNCH_STEP(true, coup::kObsWaveNT); break;
+  }
+#undef COUP_LAUNCH_STEP
   COUP_HIP_TRY(hipGetLastError());
   return COUP_OK;
 }

@@ -112,6 +112,24 @@ def test_uniform_rollout_matches_oracle(auto_reset):
     assert env.error_count() == 0
 
 
+@pytest.mark.parametrize("mode", ["1", "2", "3"])
+def test_obs_writers_match_oracle(mode, monkeypatch):
+    """Every observation writer (per-lane rows, wave-cooperative, wave +
+    non-temporal) gives the oracle's tensors, including a ragged last wave
+    (1000 lanes = 15 full waves + 40)."""
+    monkeypatch.setenv("COUP_OBS_MODE", mode)
+    n, steps, seed = 1000, 40, 17
+    ref = oracle.rollout(seed=seed, n=n, steps=steps, want_obs=True)
+    env = BatchedCoupEnv(n, seed=seed, obs=True)
+    guard = torch.full((n + 64, 2, 98), -7.0, device="cuda")
+    env.obs = guard[:n]
+    env._out.obs = env.obs.data_ptr()
+    for t in range(steps):
+        o = env.step()
+        np.testing.assert_array_equal(_np(o["obs"]), ref["obs"][t], err_msg=f"mode {mode} step {t}")
+    assert torch.all(guard[n:] == -7.0), "writer touched memory past the last lane"
+
+
 def test_external_actions_replay():
     """Feeding the oracle's chosen actions back through coup_step(actions)
     reproduces the same trajectory (chance deals depend only on the env's
