@@ -148,7 +148,7 @@ def main():
                        "auto_reset": True, "parallelism": f"dp{world} (env-id sharding)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_step<true,%s>" % ("true" if with_obs else "false"),
+                         "kernel": "coup::k_step<true, %d>" % (3 if with_obs else 0),
                          "kernel_ms": kern_ms, "bytes_per_launch": bytes_per_launch},
             "lane_errors": errors,
         }

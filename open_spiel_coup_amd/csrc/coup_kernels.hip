@@ -221,7 +221,7 @@ struct StepArgs {
 // One rl_environment step per lane (rl_environment.py:282-322), optionally
 // with SyncVectorEnv auto-reset (vector_env.py:40-67).
 // Observation write-out variants (COUP_OBS_MODE selects one at run time for
-// A/B measurements; kObsWave is the default).
+// A/B measurements; kObsWaveNT is the default).
 enum ObsMode : int { kObsNone = 0, kObsLaneRows = 1, kObsWave = 2, kObsWaveNT = 3 };
 
 // The per-lane part of one env step: returns the decision applied (-1 if
@@ -455,8 +455,8 @@ int fail(int code, const std::string& msg) {
 // COUP_OBS_MODE=1|2|3 overrides the observation writer (A/B measurements).
 int obs_mode() {
   const char* e = std::getenv("COUP_OBS_MODE");
-  const int m = e ? std::atoi(e) : (int)coup::kObsWave;
-  return (m >= 1 && m <= 3) ? m : (int)coup::kObsWave;
+  const int m = e ? std::atoi(e) : (int)coup::kObsWaveNT;
+  return (m >= 1 && m <= 3) ? m : (int)coup::kObsWaveNT;
 }
 
 unsigned grid_for(int64_t n) { return (unsigned)((n + coup::kThreads - 1) / coup::kThreads); }

@@ -1,0 +1,73 @@
+// hbm_probe.hip -- measured HBM ceilings for the roofline discussion
+// (DESIGN.md section 5): a pure streaming write of the obs buffer size, the
+// same with non-temporal stores, and a float4 copy.  Measurement tool only.
+//   hipcc --offload-arch=gfx950 -O3 -o tools/hbm_probe tools/hbm_probe.hip
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+template <bool NT>
+__global__ __launch_bounds__(256) void k_write(v4f* __restrict__ dst, size_t n) {
+  const v4f z = {0.f, 1.f, 0.f, 0.f};
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    if (NT)
+      __builtin_nontemporal_store(z, dst + i);
+    else
+      dst[i] = z;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_copy(v4f* __restrict__ dst, const v4f* __restrict__ src, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) dst[i] = src[i];
+}
+
+#define CK(x)                                                              \
+  do {                                                                     \
+    hipError_t e = (x);                                                    \
+    if (e != hipSuccess) {                                                 \
+      std::printf("%s: %s\n", #x, hipGetErrorString(e));                   \
+      return 1;                                                            \
+    }                                                                      \
+  } while (0)
+
+int main() {
+  const size_t bytes = (size_t)784 << 20;  // 2^20 lanes x 784 B
+  const size_t n = bytes / 16;
+  v4f *a, *b;
+  CK(hipMalloc(&a, bytes));
+  CK(hipMalloc(&b, bytes));
+  CK(hipMemset(a, 0, bytes));
+  CK(hipMemset(b, 0, bytes));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const int reps = 20;
+  for (int grid : {2048, 4096, 16384}) {
+    for (int kind = 0; kind < 3; ++kind) {
+      for (int w = 0; w < 3; ++w) {
+        if (kind == 0) k_write<false><<<grid, 256>>>(a, n);
+        if (kind == 1) k_write<true><<<grid, 256>>>(a, n);
+        if (kind == 2) k_copy<<<grid, 256>>>(a, b, n);
+      }
+      CK(hipEventRecord(e0));
+      for (int r = 0; r < reps; ++r) {
+        if (kind == 0) k_write<false><<<grid, 256>>>(a, n);
+        if (kind == 1) k_write<true><<<grid, 256>>>(a, n);
+        if (kind == 2) k_copy<<<grid, 256>>>(a, b, n);
+      }
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      const double moved = (kind == 2 ? 2.0 : 1.0) * (double)bytes;
+      const char* names[3] = {"write", "write_nt", "copy"};
+      std::printf("{\"kernel\": \"%s\", \"grid\": %d, \"bytes\": %.0f, \"us\": %.2f, \"GBps\": %.1f}\n", names[kind],
+                  grid, moved, ms * 1e3 / reps, moved / (ms * 1e-3 / reps) / 1e9);
+    }
+  }
+  CK(hipFree(a));
+  CK(hipFree(b));
+  return 0;
+}

@@ -1,0 +1,100 @@
+"""Condense rocprofv3 output (tools/profile_gpu.sh) into committed evidence.
+
+    python tools/traffic.py gpurun_out/prof/<tag> [bench.py args]
+
+Writes profiles/<tag>/kernel_stats.csv (the --stats summary as produced),
+profiles/<tag>/summary.json, and profiles/traffic.json, which bench.py
+reads for roofline.traffic.
+
+HBM bytes per launch follow MI355X_MICROARCH.md (HBM section): FETCH_SIZE and
+WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide
+coalesced streaming read (16 B/lane), so it is doubled; WRITE_SIZE is exact
+for 16-B-per-lane streaming stores.
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def rows(pattern):
+    out = []
+    for path in sorted(glob.glob(pattern, recursive=True)):
+        with open(path, newline="") as f:
+            out.extend(csv.DictReader(f))
+    return out
+
+
+def col(row, *needles):
+    for k in row:
+        lk = k.lower()
+        if all(n in lk for n in needles):
+            return k
+    raise KeyError(needles)
+
+
+def main():
+    src = sys.argv[1]
+    args = sys.argv[2:]
+    tag = os.path.basename(os.path.normpath(src))
+    cfg = "c3"
+    batch = None
+    for i, a in enumerate(args):
+        if a == "--config":
+            cfg = args[i + 1]
+        if a == "--batch":
+            batch = int(args[i + 1])
+    batch = batch or (1 << 20 if cfg == "c3" else 65536)
+    step_kernel = "k_step<true, 3>" if cfg == "c3" else "k_step<true, 0>"
+
+    dst = os.path.join(ROOT, "profiles", tag)
+    os.makedirs(dst, exist_ok=True)
+    summary = {"tag": tag, "config": cfg, "batch": batch}
+
+    stats = glob.glob(os.path.join(src, "trace", "**", "*kernel_stats.csv"), recursive=True)
+    if stats:
+        shutil.copy(stats[0], os.path.join(dst, "kernel_stats.csv"))
+        for r in rows(stats[0]):
+            name = r[col(r, "name")]
+            if "k_step" in name:
+                summary.setdefault("kernels", {})[name] = {
+                    "calls": int(r[col(r, "calls")]),
+                    "avg_ns": float(r[col(r, "average")]),
+                }
+
+    def counter(kind, cname):
+        vals = []
+        for r in rows(os.path.join(src, kind, "**", "*counter_collection.csv")):
+            kn = r[col(r, "kernel", "name")]
+            mode = "3" if cfg == "c3" else "0"
+            if f"k_step<true, {mode}>" not in kn and f"k_stepILb1ELi{mode}E" not in kn:
+                continue
+            if r[col(r, "counter", "name")] != cname:
+                continue
+            vals.append(float(r[col(r, "counter", "value")]))
+        return sum(vals) / len(vals) if vals else None
+
+    fetch_kb = counter("fetch", "FETCH_SIZE")
+    write_kb = counter("write", "WRITE_SIZE")
+    summary["fetch_size_kb_avg"] = fetch_kb
+    summary["write_size_kb_avg"] = write_kb
+    traffic = None
+    if fetch_kb is not None and write_kb is not None:
+        traffic = (2.0 * fetch_kb + write_kb) * 1024.0
+    summary["hbm_bytes_per_launch"] = traffic
+    summary["correction"] = "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE halving)"
+    summary["step_kernel"] = step_kernel
+    with open(os.path.join(dst, "summary.json"), "w") as f:
+        json.dump(summary, f, indent=1)
+    with open(os.path.join(ROOT, "profiles", "traffic.json"), "w") as f:
+        json.dump({"config": cfg, "batch": batch, "hbm_bytes_per_launch": traffic,
+                   "source": f"profiles/{tag}/summary.json"}, f, indent=1)
+    print(json.dumps(summary, indent=1))
+
+
+if __name__ == "__main__":
+    main()
