@@ -188,6 +188,90 @@ __device__ __forceinline__ void write_obs_wave(float* __restrict__ wave_obs, con
   }
 }
 
+// ---- bitmap variant -------------------------------------------------------
+//
+// Every element of the two observation rows is 0 or 1 except the four coin
+// counts, so a lane's 196 floats are a 196-bit string plus two coin values.
+// Each lane builds that string once (one row as a 98-bit (lo, hi) pair per
+// observer, concatenated), stores it with the coins as 8 words in LDS, and
+// the coalesced store loop turns nibble c of the owner's string into the
+// float4 at offset 4c.  Coins sit at row offsets 60-61: float4 15 (.x, .y)
+// of the P1 row and float4 39 (.z, .w) of the P2 row.
+
+// One observer's 98-bit row (bit f = element f of ObservationTensor(P)).
+template <int P>
+__device__ __forceinline__ void obs_row_bits(const Lane& L, bool term, uint64_t& lo, uint64_t& hi) {
+  lo = 1ull << P;  // observer one-hot
+#pragma unroll
+  for (uint32_t k = 0; k < 8; ++k) {
+    const uint32_t q = k >> 2, i = k & 3u;
+    const uint32_t n = nib(q ? L.h1 : L.h0, i);
+    const bool exists = n != 0xFu;
+    const bool visible = exists && (q == (uint32_t)P || (n & 1u));
+    lo |= (uint64_t)visible << (2u + 20u * q + 5u * i + (n >> 1));
+    lo |= (uint64_t)exists << (44u + 8u * q + 2u * i + (n & 1u));
+  }
+  lo |= (uint64_t)(!term) << (42u + L.M);
+  hi = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < 2; ++q) {
+    const uint32_t a = q ? L.l1 : L.l0;
+    const uint32_t p = 62u + 18u * q + a;
+    const bool has = a != kNoAction;
+    lo |= (uint64_t)(has && p < 64u) << (p & 63u);
+    hi |= (uint64_t)(has && p >= 64u) << ((p - 64u) & 63u);
+  }
+}
+
+// 8 LDS words of a lane: the 196-bit string (row P1 at bits 0..97, row P2
+// at 98..195) in words 0..6, coins (P1 | P2 << 8) in word 7.
+__device__ __forceinline__ void obs_bits_to_lds(const Lane& L, uint32_t* __restrict__ w) {
+  const bool term = is_terminal(L);
+  uint64_t a_lo, a_hi, b_lo, b_hi;
+  obs_row_bits<0>(L, term, a_lo, a_hi);
+  obs_row_bits<1>(L, term, b_lo, b_hi);
+  uint4 x, y;
+  x.x = (uint32_t)a_lo;
+  x.y = (uint32_t)(a_lo >> 32);
+  x.z = (uint32_t)a_hi;
+  x.w = (uint32_t)((a_hi >> 32) & 3u) | (uint32_t)(b_lo << 2);
+  y.x = (uint32_t)(b_lo >> 30);
+  y.y = (uint32_t)(b_lo >> 62) | (uint32_t)(b_hi << 2);
+  y.z = (uint32_t)(b_hi >> 30) & 0xFu;
+  y.w = L.c0 | (L.c1 << 8);
+  reinterpret_cast<uint4*>(w)[0] = x;
+  reinterpret_cast<uint4*>(w)[1] = y;
+}
+
+// wave_bits: this wave's 64 x 8 LDS words, written by obs_bits_to_lds and
+// made visible by a barrier before the call.
+__device__ __forceinline__ void write_obs_wave_bits(float* __restrict__ wave_obs, const uint32_t* __restrict__ wave_bits,
+                                                    uint32_t n_valid) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  v4f* dst = reinterpret_cast<v4f*>(wave_obs);
+  const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll 7
+  for (uint32_t j = 0; j < (uint32_t)kRowF4; ++j) {
+    const uint32_t x = 64u * j + lane;
+    const uint32_t o = x / (uint32_t)kRowF4;
+    const uint32_t c = x - o * (uint32_t)kRowF4;
+    const uint32_t word = wave_bits[8u * o + (c >> 3)];
+    const uint32_t coins = wave_bits[8u * o + 7u];
+    const uint32_t nb = word >> (4u * (c & 7u));
+    v4f v;
+    v.x = (float)(nb & 1u);
+    v.y = (float)((nb >> 1) & 1u);
+    v.z = (float)((nb >> 2) & 1u);
+    v.w = (float)((nb >> 3) & 1u);
+    const float c0 = (float)(coins & 0xFFu), c1 = (float)(coins >> 8);
+    v.x = c == 15u ? c0 : v.x;
+    v.y = c == 15u ? c1 : v.y;
+    v.z = c == 39u ? c0 : v.z;
+    v.w = c == 39u ? c1 : v.w;
+    if (o < n_valid) __builtin_nontemporal_store(v, dst + x);
+  }
+}
+
 // Fill the block's LDS copy of the 196-entry descriptor table (as 49 uint4).
 __device__ __forceinline__ void load_obs_desc(uint32_t* desc_lds) {
   for (int g = threadIdx.x; g < 2 * kObsSize; g += blockDim.x) desc_lds[g] = obs_desc(g);
@@ -222,7 +306,7 @@ struct StepArgs {
 // with SyncVectorEnv auto-reset (vector_env.py:40-67).
 // Observation write-out variants (COUP_OBS_MODE selects one at run time for
 // A/B measurements; kObsWaveNT is the default).
-enum ObsMode : int { kObsNone = 0, kObsLaneRows = 1, kObsWave = 2, kObsWaveNT = 3 };
+enum ObsMode : int { kObsNone = 0, kObsLaneRows = 1, kObsWave = 2, kObsWaveNT = 3, kObsWaveBits = 4 };
 
 // The per-lane part of one env step: returns the decision applied (-1 if
 // none), the step type and player 0's reward; L is updated in place.
@@ -296,12 +380,19 @@ __global__ __launch_bounds__(kThreads) void k_step(StepArgs a) {
     if (a.cur_player) a.cur_player[i] = (int8_t)current_player(L);
     if (OBS == kObsLaneRows) write_obs_pair(a.obs + i * (2 * kObsSize), L);
   }
-  if (OBS == kObsWave || OBS == kObsWaveNT) {
+  if (OBS == kObsWave || OBS == kObsWaveNT || OBS == kObsWaveBits) {
     const int64_t wave0 = i - (int64_t)(threadIdx.x & 63u);
     const int64_t left = a.n - wave0;
     const uint32_t n_valid = left >= 64 ? 64u : (left > 0 ? (uint32_t)left : 0u);
-    if (n_valid > 0)  // wave-uniform
+    if (OBS == kObsWaveBits) {
+      __shared__ uint32_t bits_lds[kThreads * 8];
+      obs_bits_to_lds(L, bits_lds + threadIdx.x * 8u);
+      __syncthreads();
+      if (n_valid > 0)  // wave-uniform
+        write_obs_wave_bits(a.obs + wave0 * (2 * kObsSize), bits_lds + (threadIdx.x & ~63u) * 8u, n_valid);
+    } else if (n_valid > 0) {
       write_obs_wave<OBS == kObsWaveNT>(a.obs + wave0 * (2 * kObsSize), obs_key(L), n_valid, desc_lds);
+    }
   }
 }
 
@@ -456,7 +547,7 @@ int fail(int code, const std::string& msg) {
 int obs_mode() {
   const char* e = std::getenv("COUP_OBS_MODE");
   const int m = e ? std::atoi(e) : (int)coup::kObsWaveNT;
-  return (m >= 1 && m <= 3) ? m : (int)coup::kObsWaveNT;
+  return (m >= 1 && m <= 4) ? m : (int)coup::kObsWaveNT;
 }
 
 unsigned grid_for(int64_t n) { return (unsigned)((n + coup::kThreads - 1) / coup::kThreads); }
@@ -568,15 +659,17 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
   const int mode = a.obs == nullptr ? coup::kObsNone : obs_mode();
   hipStream_t s = env->stream;
 #define COUP_LAUNCH_STEP(U, M) coup::k_step<U, M><<<g, coup::kThreads, 0, s>>>(a)
-  switch ((uniform ? 4 : 0) + mode) {
+  switch ((uniform ? 8 : 0) + mode) {
     case 0: COUP_LAUNCH_STEP(false, coup::kObsNone); break;
     case 1: COUP_LAUNCH_STEP(false, coup::kObsLaneRows); break;
     case 2: COUP_LAUNCH_STEP(false, coup::kObsWave); break;
     case 3: COUP_LAUNCH_STEP(false, coup::kObsWaveNT); break;
-    case 4: COUP_LAUNCH_STEP(true, coup::kObsNone); break;
-    case 5: COUP_LAUNCH_STEP(true, coup::kObsLaneRows); break;
-    case 6: COUP_LAUNCH_STEP(true, coup::kObsWave); break;
-    default: COUP_LAUNCH_STEP(true, coup::kObsWaveNT); break;
+    case 4: COUP_LAUNCH_STEP(false, coup::kObsWaveBits); break;
+    case 8: COUP_LAUNCH_STEP(true, coup::kObsNone); break;
+    case 9: COUP_LAUNCH_STEP(true, coup::kObsLaneRows); break;
+    case 10: COUP_LAUNCH_STEP(true, coup::kObsWave); break;
+    case 11: COUP_LAUNCH_STEP(true, coup::kObsWaveNT); break;
+    default: COUP_LAUNCH_STEP(true, coup::kObsWaveBits); break;
   }
 #undef COUP_LAUNCH_STEP
   COUP_HIP_TRY(hipGetLastError());

@@ -19,6 +19,17 @@ __global__ __launch_bounds__(256) void k_write(v4f* __restrict__ dst, size_t n) 
   }
 }
 
+// The step kernel's store pattern with no compute: every wave writes its own
+// 50,176-byte chunk as 49 consecutive 1 KiB store instructions.
+__global__ __launch_bounds__(256) void k_write_chunks(v4f* __restrict__ dst, size_t n) {
+  const v4f z = {0.f, 1.f, 0.f, 0.f};
+  const size_t wave = ((size_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  const size_t lane = threadIdx.x & 63;
+  v4f* base = dst + wave * 3136;
+  if ((wave + 1) * 3136 > n) return;
+  for (int j = 0; j < 49; ++j) __builtin_nontemporal_store(z, base + 64 * j + lane);
+}
+
 __global__ __launch_bounds__(256) void k_copy(v4f* __restrict__ dst, const v4f* __restrict__ src, size_t n) {
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) dst[i] = src[i];
 }
@@ -66,6 +77,18 @@ int main() {
       std::printf("{\"kernel\": \"%s\", \"grid\": %d, \"bytes\": %.0f, \"us\": %.2f, \"GBps\": %.1f}\n", names[kind],
                   grid, moved, ms * 1e3 / reps, moved / (ms * 1e-3 / reps) / 1e9);
     }
+  }
+  {
+    const int grid = (int)(n / 3136 / 4);  // 4 waves per block, one chunk per wave
+    for (int w = 0; w < 3; ++w) k_write_chunks<<<grid, 256>>>(a, n);
+    CK(hipEventRecord(e0));
+    for (int r = 0; r < reps; ++r) k_write_chunks<<<grid, 256>>>(a, n);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    std::printf("{\"kernel\": \"write_chunks_nt\", \"grid\": %d, \"bytes\": %.0f, \"us\": %.2f, \"GBps\": %.1f}\n", grid,
+                (double)bytes, ms * 1e3 / reps, (double)bytes / (ms * 1e-3 / reps) / 1e9);
   }
   CK(hipFree(a));
   CK(hipFree(b));
