@@ -35,6 +35,13 @@ BYTES_PER_STEP = {"c3": 824, "c2": 40}
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
 
 
+def _writer(mode_env):
+    """(ObsMode template value, block size) of the step kernel that
+    coup_step launches for COUP_OBS_MODE (default 6; csrc/coup_kernels.hip)."""
+    m = int(mode_env) if mode_env and mode_env.isdigit() and 1 <= int(mode_env) <= 7 else 6
+    return {1: (1, 256), 2: (2, 256), 3: (3, 256), 4: (4, 256), 5: (5, 256), 6: (5, 1024), 7: (7, 1024)}[m]
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -148,7 +155,8 @@ def main():
                        "auto_reset": True, "parallelism": f"dp{world} (env-id sharding)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "coup::k_step<true, %d>" % (3 if with_obs else 0),
+                         "kernel": "coup::k_step<true, %s>" % (
+                             ("%d, %d" % _writer(os.environ.get("COUP_OBS_MODE"))) if with_obs else "0, 256"),
                          "kernel_ms": kern_ms, "bytes_per_launch": bytes_per_launch},
             "lane_errors": errors,
         }

@@ -272,6 +272,43 @@ __device__ __forceinline__ void write_obs_wave_bits(float* __restrict__ wave_obs
   }
 }
 
+// Block-cooperative form: the T lanes of a block own T consecutive rows
+// (T x 784 B contiguous) and iteration j stores float4 T*j + t, so each
+// iteration of the block writes T x 16 contiguous bytes (16 KiB at T=1024).
+// Measured with no compute (tools/hbm_probe.hip), this order streams ~8%
+// faster than per-wave chunks.
+template <int T, bool NT>
+__device__ __forceinline__ void write_obs_block_bits(float* __restrict__ block_obs, const uint32_t* __restrict__ bits,
+                                                     uint32_t n_valid) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  v4f* dst = reinterpret_cast<v4f*>(block_obs);
+#pragma unroll 7
+  for (uint32_t j = 0; j < (uint32_t)kRowF4; ++j) {
+    const uint32_t x = (uint32_t)T * j + threadIdx.x;
+    const uint32_t o = x / (uint32_t)kRowF4;
+    const uint32_t c = x - o * (uint32_t)kRowF4;
+    const uint32_t word = bits[8u * o + (c >> 3)];
+    const uint32_t coins = bits[8u * o + 7u];
+    const uint32_t nb = word >> (4u * (c & 7u));
+    v4f v;
+    v.x = (float)(nb & 1u);
+    v.y = (float)((nb >> 1) & 1u);
+    v.z = (float)((nb >> 2) & 1u);
+    v.w = (float)((nb >> 3) & 1u);
+    const float c0 = (float)(coins & 0xFFu), c1 = (float)(coins >> 8);
+    v.x = c == 15u ? c0 : v.x;
+    v.y = c == 15u ? c1 : v.y;
+    v.z = c == 39u ? c0 : v.z;
+    v.w = c == 39u ? c1 : v.w;
+    if (o < n_valid) {
+      if (NT)
+        __builtin_nontemporal_store(v, dst + x);
+      else
+        dst[x] = v;
+    }
+  }
+}
+
 // Fill the block's LDS copy of the 196-entry descriptor table (as 49 uint4).
 __device__ __forceinline__ void load_obs_desc(uint32_t* desc_lds) {
   for (int g = threadIdx.x; g < 2 * kObsSize; g += blockDim.x) desc_lds[g] = obs_desc(g);
@@ -302,11 +339,17 @@ struct StepArgs {
   uint32_t* err_count;
 };
 
-// One rl_environment step per lane (rl_environment.py:282-322), optionally
-// with SyncVectorEnv auto-reset (vector_env.py:40-67).
 // Observation write-out variants (COUP_OBS_MODE selects one at run time for
-// A/B measurements; kObsWaveNT is the default).
-enum ObsMode : int { kObsNone = 0, kObsLaneRows = 1, kObsWave = 2, kObsWaveNT = 3, kObsWaveBits = 4 };
+// A/B measurements; kObsBlockBits at 1024 threads is the default):
+//   1 per-lane rows (each lane stores its own 784 B; uncoalesced)
+//   2/3 wave-cooperative, ds_bpermute keys + descriptor table (plain / nt)
+//   4 wave-cooperative from the LDS bitmap, nt stores
+//   5/6 block-cooperative from the LDS bitmap, 256 / 1024 threads, plain stores
+//   7 block-cooperative, 1024 threads, nt stores
+enum ObsMode : int {
+  kObsNone = 0, kObsLaneRows = 1, kObsWave = 2, kObsWaveNT = 3, kObsWaveBits = 4,
+  kObsBlockBits = 5, kObsBlockBitsNT = 7
+};
 
 // The per-lane part of one env step: returns the decision applied (-1 if
 // none), the step type and player 0's reward; L is updated in place.
@@ -354,13 +397,17 @@ __device__ __forceinline__ void step_lane(const StepArgs& a, int64_t i, Lane& L,
 }
 
 // One rl_environment step per lane (rl_environment.py:282-322), optionally
-// with SyncVectorEnv auto-reset (vector_env.py:40-67).  No early exit: the
-// wave-cooperative obs writer needs every lane of the wave.
-template <bool UNIFORM, int OBS>
-__global__ __launch_bounds__(kThreads) void k_step(StepArgs a) {
-  __shared__ uint4 desc_lds[kRowF4];
-  if (OBS == kObsWave || OBS == kObsWaveNT) load_obs_desc(reinterpret_cast<uint32_t*>(desc_lds));
-  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+// with SyncVectorEnv auto-reset (vector_env.py:40-67).  T threads per block.
+// No early exit: the cooperative obs writers need every lane of the wave /
+// block.
+template <bool UNIFORM, int OBS, int T>
+__global__ __launch_bounds__(T) void k_step(StepArgs a) {
+  constexpr bool kDesc = OBS == kObsWave || OBS == kObsWaveNT;
+  constexpr bool kBits = OBS == kObsWaveBits || OBS == kObsBlockBits || OBS == kObsBlockBitsNT;
+  __shared__ uint4 desc_lds[kDesc ? kRowF4 : 1];
+  __shared__ uint32_t bits_lds[kBits ? T * 8 : 1];
+  if (kDesc) load_obs_desc(reinterpret_cast<uint32_t*>(desc_lds));
+  const int64_t i = (int64_t)blockIdx.x * T + threadIdx.x;
   const bool active = i < a.n;
   Lane L = initial_lane(0);
   if (active) {
@@ -380,18 +427,24 @@ __global__ __launch_bounds__(kThreads) void k_step(StepArgs a) {
     if (a.cur_player) a.cur_player[i] = (int8_t)current_player(L);
     if (OBS == kObsLaneRows) write_obs_pair(a.obs + i * (2 * kObsSize), L);
   }
-  if (OBS == kObsWave || OBS == kObsWaveNT || OBS == kObsWaveBits) {
+  if (kBits) {
+    obs_bits_to_lds(L, bits_lds + threadIdx.x * 8u);
+    __syncthreads();
+  }
+  if (OBS == kObsBlockBits || OBS == kObsBlockBitsNT) {
+    const int64_t block0 = (int64_t)blockIdx.x * T;
+    const int64_t left = a.n - block0;
+    const uint32_t n_valid = left >= T ? (uint32_t)T : (uint32_t)left;  // block-uniform, > 0
+    write_obs_block_bits<T, OBS == kObsBlockBitsNT>(a.obs + block0 * (2 * kObsSize), bits_lds, n_valid);
+  } else if (kDesc || OBS == kObsWaveBits) {
     const int64_t wave0 = i - (int64_t)(threadIdx.x & 63u);
     const int64_t left = a.n - wave0;
     const uint32_t n_valid = left >= 64 ? 64u : (left > 0 ? (uint32_t)left : 0u);
-    if (OBS == kObsWaveBits) {
-      __shared__ uint32_t bits_lds[kThreads * 8];
-      obs_bits_to_lds(L, bits_lds + threadIdx.x * 8u);
-      __syncthreads();
-      if (n_valid > 0)  // wave-uniform
+    if (n_valid > 0) {  // wave-uniform
+      if (OBS == kObsWaveBits)
         write_obs_wave_bits(a.obs + wave0 * (2 * kObsSize), bits_lds + (threadIdx.x & ~63u) * 8u, n_valid);
-    } else if (n_valid > 0) {
-      write_obs_wave<OBS == kObsWaveNT>(a.obs + wave0 * (2 * kObsSize), obs_key(L), n_valid, desc_lds);
+      else
+        write_obs_wave<OBS == kObsWaveNT>(a.obs + wave0 * (2 * kObsSize), obs_key(L), n_valid, desc_lds);
     }
   }
 }
@@ -543,11 +596,14 @@ int fail(int code, const std::string& msg) {
 #define COUP_CHECK_ENV(env) \
   if (!(env)) return fail(COUP_E_INVALID, "null coup_env")
 
-// COUP_OBS_MODE=1|2|3 overrides the observation writer (A/B measurements).
+// COUP_OBS_MODE=1..7 overrides the observation writer (A/B measurements;
+// the modes are listed at coup::ObsMode).  6 = block-cooperative, 1024
+// threads, plain stores.
+constexpr int kDefaultObsMode = 6;
 int obs_mode() {
   const char* e = std::getenv("COUP_OBS_MODE");
-  const int m = e ? std::atoi(e) : (int)coup::kObsWaveNT;
-  return (m >= 1 && m <= 4) ? m : (int)coup::kObsWaveNT;
+  const int m = e ? std::atoi(e) : kDefaultObsMode;
+  return (m >= 1 && m <= 7) ? m : kDefaultObsMode;
 }
 
 unsigned grid_for(int64_t n) { return (unsigned)((n + coup::kThreads - 1) / coup::kThreads); }
@@ -654,23 +710,29 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
     a.cur_player = out->cur_player;
     a.obs = out->obs;
   }
-  const unsigned g = grid_for(env->batch);
   const bool uniform = actions == nullptr;
   const int mode = a.obs == nullptr ? coup::kObsNone : obs_mode();
   hipStream_t s = env->stream;
-#define COUP_LAUNCH_STEP(U, M) coup::k_step<U, M><<<g, coup::kThreads, 0, s>>>(a)
-  switch ((uniform ? 8 : 0) + mode) {
-    case 0: COUP_LAUNCH_STEP(false, coup::kObsNone); break;
-    case 1: COUP_LAUNCH_STEP(false, coup::kObsLaneRows); break;
-    case 2: COUP_LAUNCH_STEP(false, coup::kObsWave); break;
-    case 3: COUP_LAUNCH_STEP(false, coup::kObsWaveNT); break;
-    case 4: COUP_LAUNCH_STEP(false, coup::kObsWaveBits); break;
-    case 8: COUP_LAUNCH_STEP(true, coup::kObsNone); break;
-    case 9: COUP_LAUNCH_STEP(true, coup::kObsLaneRows); break;
-    case 10: COUP_LAUNCH_STEP(true, coup::kObsWave); break;
-    case 11: COUP_LAUNCH_STEP(true, coup::kObsWaveNT); break;
-    default: COUP_LAUNCH_STEP(true, coup::kObsWaveBits); break;
+  const int64_t n = env->batch;
+#define COUP_LAUNCH_STEP(U, M, T) \
+  coup::k_step<U, M, T><<<(unsigned)((n + (T)-1) / (T)), T, 0, s>>>(a)
+#define COUP_LAUNCH_MODES(U)                                                 \
+  switch (mode) {                                                            \
+    case 0: COUP_LAUNCH_STEP(U, coup::kObsNone, 256); break;                 \
+    case 1: COUP_LAUNCH_STEP(U, coup::kObsLaneRows, 256); break;             \
+    case 2: COUP_LAUNCH_STEP(U, coup::kObsWave, 256); break;                 \
+    case 3: COUP_LAUNCH_STEP(U, coup::kObsWaveNT, 256); break;               \
+    case 4: COUP_LAUNCH_STEP(U, coup::kObsWaveBits, 256); break;             \
+    case 5: COUP_LAUNCH_STEP(U, coup::kObsBlockBits, 256); break;            \
+    case 6: COUP_LAUNCH_STEP(U, coup::kObsBlockBits, 1024); break;           \
+    default: COUP_LAUNCH_STEP(U, coup::kObsBlockBitsNT, 1024); break;        \
   }
+  if (uniform) {
+    COUP_LAUNCH_MODES(true)
+  } else {
+    COUP_LAUNCH_MODES(false)
+  }
+#undef COUP_LAUNCH_MODES
 #undef COUP_LAUNCH_STEP
   COUP_HIP_TRY(hipGetLastError());
   return COUP_OK;

@@ -112,7 +112,7 @@ def test_uniform_rollout_matches_oracle(auto_reset):
     assert env.error_count() == 0
 
 
-@pytest.mark.parametrize("mode", ["1", "2", "3", "4"])
+@pytest.mark.parametrize("mode", ["1", "2", "3", "4", "5", "6", "7"])
 def test_obs_writers_match_oracle(mode, monkeypatch):
     """Every observation writer (per-lane rows, wave-cooperative, wave +
     non-temporal) gives the oracle's tensors, including a ragged last wave

@@ -30,6 +30,21 @@ __global__ __launch_bounds__(256) void k_write_chunks(v4f* __restrict__ dst, siz
   for (int j = 0; j < 49; ++j) __builtin_nontemporal_store(z, base + 64 * j + lane);
 }
 
+// Block-cooperative chunks: a block of T threads owns T rows (T x 784 B) and
+// iteration j writes T consecutive float4 (T x 16 B contiguous).
+template <int T, bool NT>
+__global__ __launch_bounds__(T) void k_write_block_chunks(v4f* __restrict__ dst, size_t n) {
+  const v4f z = {0.f, 1.f, 0.f, 0.f};
+  v4f* base = dst + (size_t)blockIdx.x * T * 49;
+  if (((size_t)blockIdx.x + 1) * T * 49 > n) return;
+  for (int j = 0; j < 49; ++j) {
+    if (NT)
+      __builtin_nontemporal_store(z, base + T * j + threadIdx.x);
+    else
+      base[T * j + threadIdx.x] = z;
+  }
+}
+
 __global__ __launch_bounds__(256) void k_copy(v4f* __restrict__ dst, const v4f* __restrict__ src, size_t n) {
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) dst[i] = src[i];
 }
@@ -89,6 +104,26 @@ int main() {
     CK(hipEventElapsedTime(&ms, e0, e1));
     std::printf("{\"kernel\": \"write_chunks_nt\", \"grid\": %d, \"bytes\": %.0f, \"us\": %.2f, \"GBps\": %.1f}\n", grid,
                 (double)bytes, ms * 1e3 / reps, (double)bytes / (ms * 1e-3 / reps) / 1e9);
+  }
+  auto timed = [&](const char* name, int grid, auto launch) -> int {
+    for (int w = 0; w < 3; ++w) launch();
+    CK(hipEventRecord(e0));
+    for (int r = 0; r < reps; ++r) launch();
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    std::printf("{\"kernel\": \"%s\", \"grid\": %d, \"bytes\": %.0f, \"us\": %.2f, \"GBps\": %.1f}\n", name, grid,
+                (double)bytes, ms * 1e3 / reps, (double)bytes / (ms * 1e-3 / reps) / 1e9);
+    return 0;
+  };
+  {
+    const int g256 = (int)(n / (256 * 49)), g512 = (int)(n / (512 * 49)), g1024 = (int)(n / (1024 * 49));
+    timed("block256_chunks_nt", g256, [&] { k_write_block_chunks<256, true><<<g256, 256>>>(a, n); });
+    timed("block256_chunks", g256, [&] { k_write_block_chunks<256, false><<<g256, 256>>>(a, n); });
+    timed("block512_chunks_nt", g512, [&] { k_write_block_chunks<512, true><<<g512, 512>>>(a, n); });
+    timed("block1024_chunks_nt", g1024, [&] { k_write_block_chunks<1024, true><<<g1024, 1024>>>(a, n); });
+    timed("block1024_chunks", g1024, [&] { k_write_block_chunks<1024, false><<<g1024, 1024>>>(a, n); });
   }
   CK(hipFree(a));
   CK(hipFree(b));

@@ -15,6 +15,7 @@ import csv
 import glob
 import json
 import os
+import re
 import shutil
 import sys
 
@@ -49,7 +50,7 @@ def main():
         if a == "--batch":
             batch = int(args[i + 1])
     batch = batch or (1 << 20 if cfg == "c3" else 65536)
-    step_kernel = "k_step<true, 3>" if cfg == "c3" else "k_step<true, 0>"
+    step_kernel = os.environ.get("COUP_STEP_KERNEL", "coup::k_step<true, OBS, T> (uniform policy)")
 
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
@@ -70,8 +71,8 @@ def main():
         vals = []
         for r in rows(os.path.join(src, kind, "**", "*counter_collection.csv")):
             kn = r[col(r, "kernel", "name")]
-            mode = "3" if cfg == "c3" else "0"
-            if f"k_step<true, {mode}>" not in kn and f"k_stepILb1ELi{mode}E" not in kn:
+            m = re.search(r"k_step<true, (\d+), \d+>", kn) or re.search(r"k_stepILb1ELi(\d+)ELi\d+E", kn)
+            if not m or (m.group(1) == "0") != (cfg != "c3"):
                 continue
             if r[col(r, "counter", "name")] != cname:
                 continue
