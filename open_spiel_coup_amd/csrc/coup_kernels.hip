@@ -400,6 +400,16 @@ __device__ __forceinline__ void step_lane(const StepArgs& a, int64_t i, Lane& L,
 // with SyncVectorEnv auto-reset (vector_env.py:40-67).  T threads per block.
 // No early exit: the cooperative obs writers need every lane of the wave /
 // block.
+// Wave-scope hand-off of LDS data between lanes of one wave.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <bool UNIFORM, int OBS, int T>
+__device__ __forceinline__ void step_group(const StepArgs& a, int64_t grp, const uint4* desc_lds,
+                                           uint32_t* bits_lds);
+
 template <bool UNIFORM, int OBS, int T>
 __global__ __launch_bounds__(T) void k_step(StepArgs a) {
   constexpr bool kDesc = OBS == kObsWave || OBS == kObsWaveNT;
@@ -407,7 +417,19 @@ __global__ __launch_bounds__(T) void k_step(StepArgs a) {
   __shared__ uint4 desc_lds[kDesc ? kRowF4 : 1];
   __shared__ uint32_t bits_lds[kBits ? T * 8 : 1];
   if (kDesc) load_obs_desc(reinterpret_cast<uint32_t*>(desc_lds));
-  const int64_t i = (int64_t)blockIdx.x * T + threadIdx.x;
+  // Grid-stride over groups of T lanes: with a grid smaller than the group
+  // count, a wave's stores for one group drain while it steps the next.
+  for (int64_t grp = blockIdx.x; grp * T < a.n; grp += gridDim.x) {
+    step_group<UNIFORM, OBS, T>(a, grp, desc_lds, bits_lds);
+  }
+}
+
+template <bool UNIFORM, int OBS, int T>
+__device__ __forceinline__ void step_group(const StepArgs& a, int64_t grp, const uint4* desc_lds,
+                                           uint32_t* bits_lds) {
+  constexpr bool kDesc = OBS == kObsWave || OBS == kObsWaveNT;
+  constexpr bool kBits = OBS == kObsWaveBits || OBS == kObsBlockBits || OBS == kObsBlockBitsNT;
+  const int64_t i = grp * T + threadIdx.x;
   const bool active = i < a.n;
   Lane L = initial_lane(0);
   if (active) {
@@ -427,12 +449,17 @@ __global__ __launch_bounds__(T) void k_step(StepArgs a) {
     if (a.cur_player) a.cur_player[i] = (int8_t)current_player(L);
     if (OBS == kObsLaneRows) write_obs_pair(a.obs + i * (2 * kObsSize), L);
   }
-  if (kBits) {
+  if (OBS == kObsWaveBits) {
+    // each wave reads only its own lanes' words: a wave-scope hand-off
+    obs_bits_to_lds(L, bits_lds + threadIdx.x * 8u);
+    wave_sync();
+  } else if (kBits) {
+    __syncthreads();  // previous group's words fully read by every wave
     obs_bits_to_lds(L, bits_lds + threadIdx.x * 8u);
     __syncthreads();
   }
   if (OBS == kObsBlockBits || OBS == kObsBlockBitsNT) {
-    const int64_t block0 = (int64_t)blockIdx.x * T;
+    const int64_t block0 = grp * T;
     const int64_t left = a.n - block0;
     const uint32_t n_valid = left >= T ? (uint32_t)T : (uint32_t)left;  // block-uniform, > 0
     write_obs_block_bits<T, OBS == kObsBlockBitsNT>(a.obs + block0 * (2 * kObsSize), bits_lds, n_valid);
@@ -446,6 +473,7 @@ __global__ __launch_bounds__(T) void k_step(StepArgs a) {
       else
         write_obs_wave<OBS == kObsWaveNT>(a.obs + wave0 * (2 * kObsSize), obs_key(L), n_valid, desc_lds);
     }
+    if (OBS == kObsWaveBits) wave_sync();  // words read before the next group overwrites them
   }
 }
 
@@ -599,11 +627,23 @@ int fail(int code, const std::string& msg) {
 // COUP_OBS_MODE=1..7 overrides the observation writer (A/B measurements;
 // the modes are listed at coup::ObsMode).  6 = block-cooperative, 1024
 // threads, plain stores.
-constexpr int kDefaultObsMode = 6;
+constexpr int kDefaultObsMode = 4;
 int obs_mode() {
   const char* e = std::getenv("COUP_OBS_MODE");
   const int m = e ? std::atoi(e) : kDefaultObsMode;
   return (m >= 1 && m <= 7) ? m : kDefaultObsMode;
+}
+
+// Blocks of the step kernel: one per group of T lanes, or at most
+// COUP_STEP_WAVES_PER_CU x 256 CUs worth of waves (grid-stride) when set.
+unsigned step_grid(int64_t groups, int T) {
+  const char* e = std::getenv("COUP_STEP_WAVES_PER_CU");
+  int64_t g = groups;
+  if (e && std::atoi(e) > 0) {
+    const int64_t cap = (int64_t)std::atoi(e) * 256 * 64 / T;
+    g = groups < cap ? groups : cap;
+  }
+  return (unsigned)(g > 0 ? g : 1);
 }
 
 unsigned grid_for(int64_t n) { return (unsigned)((n + coup::kThreads - 1) / coup::kThreads); }
@@ -715,7 +755,7 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
   hipStream_t s = env->stream;
   const int64_t n = env->batch;
 #define COUP_LAUNCH_STEP(U, M, T) \
-  coup::k_step<U, M, T><<<(unsigned)((n + (T)-1) / (T)), T, 0, s>>>(a)
+  coup::k_step<U, M, T><<<step_grid((n + (T)-1) / (T), T), T, 0, s>>>(a)
 #define COUP_LAUNCH_MODES(U)                                                 \
   switch (mode) {                                                            \
     case 0: COUP_LAUNCH_STEP(U, coup::kObsNone, 256); break;                 \
