@@ -78,21 +78,17 @@ def main():
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-
     from open_spiel_coup_amd import BatchedCoupEnv
+    from open_spiel_coup_amd import distributed as D
+
+    rank, world, _ = D.world_info()
+    dev = D.init("nccl")  # RCCL over xGMI when world > 1
 
     cfg = args.config
     B = args.batch or (1 << 20 if cfg == "c3" else 65536)
     with_obs = cfg == "c3"
-    env = BatchedCoupEnv(B, seed=args.seed, env_id_base=rank * B, auto_reset=True, obs=with_obs, device=dev)
+    env = BatchedCoupEnv(B, seed=args.seed, env_id_base=D.env_id_base(rank, B), auto_reset=True, obs=with_obs,
+                         device=dev)
 
     def barrier():
         if world > 1:
@@ -105,7 +101,6 @@ def main():
 
     stream = torch.cuda.current_stream(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    gathered = None
     barrier()
     t0 = time.perf_counter()
     for k in range(args.steps):
@@ -113,18 +108,13 @@ def main():
         env.step()
         ev[k][1].record(stream)
     if world > 1:
-        # collate the final step's per-lane outcome over xGMI (RCCL)
-        payload = torch.cat([env.rewards.view(torch.uint8).reshape(-1), env.step_type], 0)
-        gathered = [torch.empty_like(payload) for _ in range(world)]
-        dist.all_gather(gathered, payload)
+        # collate the final step's per-lane outcome over xGMI (RCCL all-gather)
+        D.collate(torch.cat([env.rewards.view(torch.uint8), env.step_type.view(-1, 1)], 1))
     barrier()
     elapsed = time.perf_counter() - t0
 
     kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed = D.max_over_ranks(elapsed, dev)
     errors = env.error_count()
 
     if rank == 0:

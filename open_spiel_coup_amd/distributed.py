@@ -1,0 +1,57 @@
+"""Multi-GPU plumbing: one process per GPU, games sharded by global env id.
+
+Games never interact, so the step loop has no collective.  Rank r of a
+world of W owns global env ids [r*B, (r+1)*B) (B lanes per rank); because
+every lane's random stream is keyed by its global id,
+the union of the ranks' trajectories equals a single-process run over W*B
+lanes.  `collate` gathers per-lane results over RCCL (xGMI) -- or gloo on
+CPU tensors in tests -- outside the step loop.
+"""
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def world_info():
+    """(rank, world_size, local_rank) from the torchrun environment."""
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def env_id_base(rank, lanes_per_rank):
+    """First global env id of a rank's shard."""
+    return rank * lanes_per_rank
+
+
+def init(backend="nccl"):
+    """Initialise the process group for a torchrun launch (no-op for one
+    process).  Returns the torch device of this rank."""
+    rank, world, local = world_info()
+    if backend == "nccl":
+        dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+    else:
+        dev = torch.device("cpu")
+    if world > 1 and not dist.is_initialized():
+        kw = {"device_id": dev} if backend == "nccl" else {}
+        dist.init_process_group(backend, **kw)
+    return dev
+
+
+def collate(t):
+    """All-gather a per-lane tensor ([B, ...]) from every rank; returns the
+    [W*B, ...] concatenation in rank (= global env id) order."""
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return t
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t.contiguous())
+    return torch.cat(parts, 0)
+
+
+def max_over_ranks(x, device):
+    """Max of a host float over ranks (the bench's timing rule)."""
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())

@@ -91,9 +91,10 @@ def main():
     summary["step_kernel"] = step_kernel
     with open(os.path.join(dst, "summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
-    with open(os.path.join(ROOT, "profiles", "traffic.json"), "w") as f:
-        json.dump({"config": cfg, "batch": batch, "hbm_bytes_per_launch": traffic,
-                   "source": f"profiles/{tag}/summary.json"}, f, indent=1)
+    if traffic is not None:
+        with open(os.path.join(ROOT, "profiles", "traffic.json"), "w") as f:
+            json.dump({"config": cfg, "batch": batch, "hbm_bytes_per_launch": traffic,
+                       "source": f"profiles/{tag}/summary.json"}, f, indent=1)
     print(json.dumps(summary, indent=1))
 
 
