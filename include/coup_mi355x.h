@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define COUP_ABI_VERSION 1
+#define COUP_ABI_VERSION 2
 
 #define COUP_NUM_PLAYERS 2          /* coup.h:42 */
 #define COUP_NUM_ACTIONS 18         /* coup.h:203 NumDistinctActions */
@@ -36,6 +36,11 @@ extern "C" {
 #define COUP_INFO_STATE_SIZE 2492   /* coup.cc:1104-1116 InformationStateTensorShape */
 #define COUP_MAX_GAME_LENGTH 90     /* coup.h:219 */
 #define COUP_STATE_BYTES 16         /* packed lane record */
+#define COUP_HISTORY_BYTES 96       /* per-lane history: one byte per history index */
+
+/* coup_create flags */
+#define COUP_FLAG_AUTO_RESET 1      /* SyncVectorEnv(reset_if_done=True) semantics */
+#define COUP_FLAG_HISTORY 2         /* keep per-lane histories (InformationStateTensor, strings) */
 
 /* rl_environment.StepType (rl_environment.py:96-103) */
 #define COUP_STEP_FIRST 0
@@ -67,6 +72,7 @@ typedef struct {
   uint32_t* legal_mask; /* [B]  bit a set iff a in LegalActions() of the current player */
   int8_t* cur_player;   /* [B]  CurrentPlayer() of the (post-reset) state */
   float* obs;           /* [B][2][98] ObservationTensor(p) for p = 0, 1 */
+  float* info_state;    /* [B][2][2492] InformationStateTensor(p) (needs COUP_FLAG_HISTORY) */
 } coup_step_outputs;
 
 /* Per-lane query of the current state (State accessors); all optional. */
@@ -77,6 +83,7 @@ typedef struct {
   int8_t* rewards;      /* [B][2] Rewards() (coup.cc:1012-1014) */
   int8_t* returns;      /* [B][2] Returns() (coup.cc:1016-1032) */
   float* obs;           /* [B][2][98] ObservationTensor (coup.cc:1051-1056) */
+  float* info_state;    /* [B][2][2492] InformationStateTensor (coup.cc:1044-1049); needs COUP_FLAG_HISTORY */
 } coup_query_outputs;
 
 /* Per-lane rollout statistics accumulated by coup_rollout (device, [B]). */
@@ -94,11 +101,14 @@ const char* coup_last_error(void);
 /* Create an env of `batch` lanes on the current HIP device.  Lane i uses the
  * global env id env_id_base + i for its random streams, so a batch split over
  * ranks by id range reproduces the single-GPU trajectories bit for bit.
- * auto_reset=1: SyncVectorEnv(reset_if_done=True) semantics (a finished lane
- * restarts inside the same step); 0: rl_environment semantics (LAST, then the
- * next step resets).  The env starts with every lane reset and dealt
+ * flags: COUP_FLAG_AUTO_RESET -- SyncVectorEnv(reset_if_done=True) semantics
+ * (a finished lane restarts inside the same step); without it rl_environment
+ * semantics (LAST, then the next step resets).  COUP_FLAG_HISTORY -- keep a
+ * [B][96]-byte history (entry i = history index i: bits [4:0] action or card
+ * type, [5] chance deal, [6] acting / receiving player), needed for the
+ * InformationStateTensor.  The env starts with every lane reset and dealt
  * (rl_environment.reset, rl_environment.py:324-367).  Synchronous. */
-int coup_create(int64_t batch, uint64_t seed, uint32_t env_id_base, int auto_reset, coup_env** out);
+int coup_create(int64_t batch, uint64_t seed, uint32_t env_id_base, int flags, coup_env** out);
 int coup_destroy(coup_env* env);
 /* Use this HIP stream (hipStream_t, may be NULL = default) for later calls. */
 int coup_set_stream(coup_env* env, void* hip_stream);
@@ -120,7 +130,7 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
 
 /* `steps` uniform-random env steps per lane in one launch, state kept in
  * registers (auto-reset always on); per-lane statistics are accumulated
- * into `stats` (optional). */
+ * into `stats` (optional).  Not available with COUP_FLAG_HISTORY. */
 int coup_rollout(coup_env* env, int64_t steps, const coup_rollout_stats* stats);
 
 /* --- open_spiel::State surface, one action per lane -------------------- */
@@ -137,6 +147,9 @@ int coup_query(coup_env* env, const coup_query_outputs* out);
 /* Copy the packed lane records ([B][4] uint32, device) out of / into the env. */
 int coup_export_state(coup_env* env, uint32_t* dst);
 int coup_import_state(coup_env* env, const uint32_t* src);
+/* Copy the per-lane histories ([B][96] bytes, device; COUP_FLAG_HISTORY). */
+int coup_export_history(coup_env* env, uint8_t* dst);
+int coup_import_history(coup_env* env, const uint8_t* src);
 
 /* Number of lanes that rejected an action since the last call (resets the
  * counter).  Synchronises the env's stream. */

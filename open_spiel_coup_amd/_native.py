@@ -9,7 +9,9 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libcoup_mi355x.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
+FLAG_AUTO_RESET, FLAG_HISTORY = 1, 2
+HISTORY_BYTES = 96
 
 COUP_OK, COUP_E_INVALID, COUP_E_HIP, COUP_E_LANES = 0, 1, 2, 3
 
@@ -18,20 +20,23 @@ SYMBOLS = (
     "coup_abi_version", "coup_last_error", "coup_create", "coup_destroy",
     "coup_set_stream", "coup_batch", "coup_reset", "coup_step", "coup_rollout",
     "coup_new_initial_state", "coup_apply_action", "coup_query",
-    "coup_export_state", "coup_import_state", "coup_error_count",
+    "coup_export_state", "coup_import_state", "coup_export_history",
+    "coup_import_history", "coup_error_count",
 )
 
 
 class StepOutputs(ctypes.Structure):
     _fields_ = [("actions", ctypes.c_void_p), ("rewards", ctypes.c_void_p),
                 ("step_type", ctypes.c_void_p), ("legal_mask", ctypes.c_void_p),
-                ("cur_player", ctypes.c_void_p), ("obs", ctypes.c_void_p)]
+                ("cur_player", ctypes.c_void_p), ("obs", ctypes.c_void_p),
+                ("info_state", ctypes.c_void_p)]
 
 
 class QueryOutputs(ctypes.Structure):
     _fields_ = [("legal_mask", ctypes.c_void_p), ("cur_player", ctypes.c_void_p),
                 ("terminal", ctypes.c_void_p), ("rewards", ctypes.c_void_p),
-                ("returns", ctypes.c_void_p), ("obs", ctypes.c_void_p)]
+                ("returns", ctypes.c_void_p), ("obs", ctypes.c_void_p),
+                ("info_state", ctypes.c_void_p)]
 
 
 class RolloutStats(ctypes.Structure):
@@ -72,6 +77,8 @@ def load():
         "coup_query": ([vp, ctypes.POINTER(QueryOutputs)], i32),
         "coup_export_state": ([vp, vp], i32),
         "coup_import_state": ([vp, vp], i32),
+        "coup_export_history": ([vp, vp], i32),
+        "coup_import_history": ([vp, vp], i32),
         "coup_error_count": ([vp, ctypes.POINTER(i64)], i32),
     }
     for name, (args, res) in sig.items():

@@ -309,6 +309,106 @@ __device__ __forceinline__ void write_obs_block_bits(float* __restrict__ block_o
   }
 }
 
+// ---- InformationStateTensor ----------------------------------------------
+//
+// CoupObserver::WriteTensor with kInfoStateObsType (perfect recall,
+// coup.cc:248-287, 230-245; observer.h:294-297): the first 62 elements are
+// the observation's (observer, cards, mover, card faces, coins), then the
+// history block [135][18] with row i = history index i, one-hot at the
+// action id for player actions and at the card type for chance deals to the
+// observer only.  2492 floats per player, both players per lane = 1246
+// float4 (19,936 B).  Written wave-cooperatively like the observation: the
+// wave's 64 lanes own 1.27 MB contiguous, iteration j stores float4 64*j+lane.
+//
+// Per-lane LDS inputs: the 96-byte history (hist_lds, the lane's bytes of
+// the global history buffer) and 6 words of prefix (pre_lds): [0..1] the
+// P1-view prefix bits (element f of 0..61 at bit f), [2..3] the P2 view,
+// [4] coins (P1 | P2 << 8) | move_number << 16.
+constexpr int kInfoSize = COUP_INFO_STATE_SIZE;  // 2492
+constexpr int kInfoHalfF4 = kInfoSize / 4;       // 623 float4 per player
+constexpr int kInfoF4 = 2 * kInfoHalfF4;         // 1246 float4 per lane
+constexpr int kPreWords = 6;
+constexpr int kHist = (int)kHistoryBytes;
+
+__device__ __forceinline__ void info_prefix_to_lds(const Lane& L, uint32_t* __restrict__ pre) {
+  const bool term = is_terminal(L);
+  uint64_t a_lo, a_hi, b_lo, b_hi;
+  obs_row_bits<0>(L, term, a_lo, a_hi);
+  obs_row_bits<1>(L, term, b_lo, b_hi);
+  const uint64_t m62 = (1ull << 62) - 1ull;  // drop the observation's last_action bits
+  reinterpret_cast<uint2*>(pre)[0] = make_uint2((uint32_t)a_lo, (uint32_t)((a_lo & m62) >> 32));
+  reinterpret_cast<uint2*>(pre)[1] = make_uint2((uint32_t)b_lo, (uint32_t)((b_lo & m62) >> 32));
+  pre[4] = L.c0 | (L.c1 << 8) | (L.move << 16);
+  pre[5] = 0;
+}
+
+// All 64 lanes of the wave must call this.
+__device__ __forceinline__ void write_info_wave(float* __restrict__ wave_info, const uint8_t* __restrict__ hist,
+                                                const uint32_t* __restrict__ pre, uint32_t n_valid) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  v4f* dst = reinterpret_cast<v4f*>(wave_info);
+  const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll 2
+  for (uint32_t j = 0; j < (uint32_t)kInfoF4; ++j) {
+    const uint32_t x = 64u * j + lane;
+    const uint32_t o = x / (uint32_t)kInfoF4;
+    const uint32_t c = x - o * (uint32_t)kInfoF4;
+    const uint32_t p = c >= (uint32_t)kInfoHalfF4;
+    const int f0 = 4 * (int)(c - p * (uint32_t)kInfoHalfF4);
+    const uint32_t* po = pre + kPreWords * o;
+    const uint2 pw = reinterpret_cast<const uint2*>(po)[p];
+    const uint64_t prefix = (uint64_t)pw.x | ((uint64_t)pw.y << 32);
+    const uint32_t meta = po[4];
+    const uint32_t len = meta >> 16;
+    // history rows touched by elements f0..f0+3 (t = f - 62; two rows at most)
+    const int t0 = f0 - 62;
+    const uint32_t r0 = t0 < 0 ? 0u : (uint32_t)t0 / 18u;
+    const int col0 = t0 - 18 * (int)r0;
+    uint32_t va[2];
+#pragma unroll
+    for (uint32_t k = 0; k < 2; ++k) {
+      const uint32_t r = r0 + k;
+      const uint32_t e = hist[kHist * o + (r < (uint32_t)kHist ? r : 0u)];
+      const bool seen = (e & 0x20u) == 0u || ((e >> 6) & 1u) == p;  // deals: observer's only
+      va[k] = (r < len && seen) ? (e & 0x1Fu) : 31u;
+    }
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int f = f0 + e;
+      const int col = col0 + e;
+      const uint32_t row_act = col >= 18 ? va[1] : va[0];
+      const float h = (row_act == (uint32_t)(col >= 18 ? col - 18 : col)) ? 1.0f : 0.0f;
+      const float pb = (float)((uint32_t)(prefix >> (f & 63)) & 1u);
+      const float coin = (float)(f == 60 ? (meta & 0xFFu) : ((meta >> 8) & 0xFFu));
+      v[e] = f < 60 ? pb : (f < 62 ? coin : h);
+    }
+    if (o < n_valid) {
+      v4f w = {v[0], v[1], v[2], v[3]};
+      __builtin_nontemporal_store(w, dst + x);
+    }
+  }
+}
+
+// Cooperative copy of a wave's 64 x 96 history bytes between global memory
+// and LDS (6 x 1 KiB per direction; bytes past the last lane are skipped).
+template <bool TO_LDS>
+__device__ __forceinline__ void wave_hist_copy(uint8_t* __restrict__ global_wave, uint8_t* __restrict__ lds_wave,
+                                               uint32_t n_valid) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t limit = n_valid * (uint32_t)kHist;
+#pragma unroll
+  for (uint32_t j = 0; j < 6u; ++j) {
+    const uint32_t off = 1024u * j + 16u * lane;
+    if (off < limit) {
+      if (TO_LDS)
+        *reinterpret_cast<uint4*>(lds_wave + off) = *reinterpret_cast<const uint4*>(global_wave + off);
+      else
+        *reinterpret_cast<uint4*>(global_wave + off) = *reinterpret_cast<const uint4*>(lds_wave + off);
+    }
+  }
+}
+
 // Fill the block's LDS copy of the 196-entry descriptor table (as 49 uint4).
 __device__ __forceinline__ void load_obs_desc(uint32_t* desc_lds) {
   for (int g = threadIdx.x; g < 2 * kObsSize; g += blockDim.x) desc_lds[g] = obs_desc(g);
@@ -336,6 +436,8 @@ struct StepArgs {
   uint32_t* legal;
   int8_t* cur_player;
   float* obs;
+  uint8_t* hist;   // [B][96] history bytes (INFO != kInfoNone)
+  float* info;     // [B][2][2492] (INFO == kInfoWrite)
   uint32_t* err_count;
 };
 
@@ -352,21 +454,22 @@ enum ObsMode : int {
 };
 
 // The per-lane part of one env step: returns the decision applied (-1 if
-// none), the step type and player 0's reward; L is updated in place.
-template <bool UNIFORM>
+// none), the step type and player 0's reward; L is updated in place and
+// every applied action is recorded in `hist`.
+template <bool UNIFORM, class H>
 __device__ __forceinline__ void step_lane(const StepArgs& a, int64_t i, Lane& L, int& act, uint32_t& st,
-                                          int32_t& rew) {
+                                          int32_t& rew, const H& hist) {
   Rng rng{a.seed_lo, a.seed_hi, a.env_id_base + (uint32_t)i, 0u, make_uint4(0, 0, 0, 0)};
   act = -1;
   rew = 0;
   if (is_terminal(L)) {
     // step() after LAST starts a new episode (rl_environment.py:310-311)
     L = initial_lane(L.episode + 1u);
-    resolve_chance(L, rng);
+    resolve_chance(L, rng, hist);
     st = COUP_STEP_FIRST;
     return;
   }
-  resolve_chance(L, rng);  // no-op unless the lane was left at a chance node
+  resolve_chance(L, rng, hist);  // no-op unless the lane was left at a chance node
   const uint32_t m = decision_mask(L);
   uint32_t x;
   if (UNIFORM) {
@@ -380,9 +483,10 @@ __device__ __forceinline__ void step_lane(const StepArgs& a, int64_t i, Lane& L,
     return;
   }
   const uint32_t err_before = L.err;
+  hist.record(L.move, hist_decision(x, L.M));
   apply_decision(L, x);
   L.move += 1u;
-  resolve_chance(L, rng);
+  resolve_chance(L, rng, hist);
   if (L.err && !err_before) count_error(a.err_count);
   act = (int)x;
   rew = L.r0;
@@ -391,53 +495,75 @@ __device__ __forceinline__ void step_lane(const StepArgs& a, int64_t i, Lane& L,
     if (a.auto_reset) {
       // SyncVectorEnv.step(reset_if_done=True) (vector_env.py:62-65)
       L = initial_lane(L.episode + 1u);
-      resolve_chance(L, rng);
+      resolve_chance(L, rng, hist);
     }
   }
 }
 
-// One rl_environment step per lane (rl_environment.py:282-322), optionally
-// with SyncVectorEnv auto-reset (vector_env.py:40-67).  T threads per block.
-// No early exit: the cooperative obs writers need every lane of the wave /
-// block.
 // Wave-scope hand-off of LDS data between lanes of one wave.
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
 }
 
-template <bool UNIFORM, int OBS, int T>
-__device__ __forceinline__ void step_group(const StepArgs& a, int64_t grp, const uint4* desc_lds,
-                                           uint32_t* bits_lds);
+// History handling of the step kernel.
+enum InfoMode : int { kInfoNone = 0, kInfoHistory = 1, kInfoWrite = 2 };
 
-template <bool UNIFORM, int OBS, int T>
-__global__ __launch_bounds__(T) void k_step(StepArgs a) {
-  constexpr bool kDesc = OBS == kObsWave || OBS == kObsWaveNT;
-  constexpr bool kBits = OBS == kObsWaveBits || OBS == kObsBlockBits || OBS == kObsBlockBitsNT;
-  __shared__ uint4 desc_lds[kDesc ? kRowF4 : 1];
-  __shared__ uint32_t bits_lds[kBits ? T * 8 : 1];
-  if (kDesc) load_obs_desc(reinterpret_cast<uint32_t*>(desc_lds));
-  // Grid-stride over groups of T lanes: with a grid smaller than the group
-  // count, a wave's stores for one group drain while it steps the next.
-  for (int64_t grp = blockIdx.x; grp * T < a.n; grp += gridDim.x) {
-    step_group<UNIFORM, OBS, T>(a, grp, desc_lds, bits_lds);
-  }
+template <int OBS, int T, int INFO>
+struct StepLds {
+  static constexpr bool kDesc = OBS == kObsWave || OBS == kObsWaveNT;
+  static constexpr bool kBits = OBS == kObsWaveBits || OBS == kObsBlockBits || OBS == kObsBlockBitsNT;
+  uint4 desc[kDesc ? kRowF4 : 1];
+  uint32_t bits[kBits ? T * 8 : 1];
+  uint8_t hist[INFO != kInfoNone ? T * kHist : 16];
+  uint32_t pre[INFO == kInfoWrite ? T * kPreWords : 1];
+};
+
+template <bool UNIFORM, int OBS, int T, int INFO>
+__device__ __forceinline__ void step_group(const StepArgs& a, int64_t grp, StepLds<OBS, T, INFO>& lds);
+
+// One rl_environment step per lane (rl_environment.py:282-322), optionally
+// with SyncVectorEnv auto-reset (vector_env.py:40-67).  T threads per block.
+// No early exit: the cooperative writers need every lane of the wave /
+// block.  INFO: maintain the per-lane history, and write the
+// InformationStateTensor of both players.
+template <bool UNIFORM, int OBS, int T, int INFO>
+__global__ __launch_bounds__(T, INFO == kInfoNone ? 8 : 4) void k_step(StepArgs a) {
+  __shared__ StepLds<OBS, T, INFO> lds;
+  if (StepLds<OBS, T, INFO>::kDesc) load_obs_desc(reinterpret_cast<uint32_t*>(lds.desc));
+  // One group of T lanes per block.  (A grid-stride "persistent" variant,
+  // where a wave's stores for one group drain while it steps the next, was
+  // measured no faster and raised register pressure)
+  step_group<UNIFORM, OBS, T, INFO>(a, blockIdx.x, lds);
 }
 
-template <bool UNIFORM, int OBS, int T>
-__device__ __forceinline__ void step_group(const StepArgs& a, int64_t grp, const uint4* desc_lds,
-                                           uint32_t* bits_lds) {
-  constexpr bool kDesc = OBS == kObsWave || OBS == kObsWaveNT;
-  constexpr bool kBits = OBS == kObsWaveBits || OBS == kObsBlockBits || OBS == kObsBlockBitsNT;
+template <bool UNIFORM, int OBS, int T, int INFO>
+__device__ __forceinline__ void step_group(const StepArgs& a, int64_t grp, StepLds<OBS, T, INFO>& lds) {
+  constexpr bool kDesc = StepLds<OBS, T, INFO>::kDesc;
+  constexpr bool kBits = StepLds<OBS, T, INFO>::kBits;
   const int64_t i = grp * T + threadIdx.x;
   const bool active = i < a.n;
+  // first thread of this wave; readfirstlane keeps the wave-uniform values
+  // below in SGPRs across the step
+  const uint32_t wl = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x & ~63u));
+  const int64_t wave0 = grp * T + wl;
+  const int64_t wleft = a.n - wave0;
+  const uint32_t wave_valid = wleft >= 64 ? 64u : (wleft > 0 ? (uint32_t)wleft : 0u);  // wave-uniform
+  uint8_t* hist_wave = lds.hist + wl * kHist;
+  if (INFO != kInfoNone) {
+    if (wave_valid) wave_hist_copy<true>(a.hist + wave0 * kHist, hist_wave, wave_valid);
+    wave_sync();
+  }
   Lane L = initial_lane(0);
   if (active) {
     L = unpack(a.state[i]);
     int act;
     uint32_t st;
     int32_t rew;
-    step_lane<UNIFORM>(a, i, L, act, st, rew);
+    if (INFO != kInfoNone)
+      step_lane<UNIFORM>(a, i, L, act, st, rew, ByteHistory{lds.hist + threadIdx.x * kHist});
+    else
+      step_lane<UNIFORM>(a, i, L, act, st, rew, NoHistory{});
     a.state[i] = pack(L);
     if (a.actions) a.actions[i] = (int8_t)act;
     if (a.rewards) {
@@ -449,29 +575,34 @@ __device__ __forceinline__ void step_group(const StepArgs& a, int64_t grp, const
     if (a.cur_player) a.cur_player[i] = (int8_t)current_player(L);
     if (OBS == kObsLaneRows) write_obs_pair(a.obs + i * (2 * kObsSize), L);
   }
+  if (INFO != kInfoNone) {
+    if (INFO == kInfoWrite) info_prefix_to_lds(L, lds.pre + threadIdx.x * kPreWords);
+    wave_sync();
+    if (wave_valid) wave_hist_copy<false>(a.hist + wave0 * kHist, hist_wave, wave_valid);
+    if (INFO == kInfoWrite && wave_valid)
+      write_info_wave(a.info + wave0 * (2 * kInfoSize), hist_wave, lds.pre + wl * kPreWords, wave_valid);
+    wave_sync();  // this group's LDS words read before the next group reuses them
+  }
   if (OBS == kObsWaveBits) {
     // each wave reads only its own lanes' words: a wave-scope hand-off
-    obs_bits_to_lds(L, bits_lds + threadIdx.x * 8u);
+    obs_bits_to_lds(L, lds.bits + threadIdx.x * 8u);
     wave_sync();
   } else if (kBits) {
     __syncthreads();  // previous group's words fully read by every wave
-    obs_bits_to_lds(L, bits_lds + threadIdx.x * 8u);
+    obs_bits_to_lds(L, lds.bits + threadIdx.x * 8u);
     __syncthreads();
   }
   if (OBS == kObsBlockBits || OBS == kObsBlockBitsNT) {
     const int64_t block0 = grp * T;
     const int64_t left = a.n - block0;
     const uint32_t n_valid = left >= T ? (uint32_t)T : (uint32_t)left;  // block-uniform, > 0
-    write_obs_block_bits<T, OBS == kObsBlockBitsNT>(a.obs + block0 * (2 * kObsSize), bits_lds, n_valid);
+    write_obs_block_bits<T, OBS == kObsBlockBitsNT>(a.obs + block0 * (2 * kObsSize), lds.bits, n_valid);
   } else if (kDesc || OBS == kObsWaveBits) {
-    const int64_t wave0 = i - (int64_t)(threadIdx.x & 63u);
-    const int64_t left = a.n - wave0;
-    const uint32_t n_valid = left >= 64 ? 64u : (left > 0 ? (uint32_t)left : 0u);
-    if (n_valid > 0) {  // wave-uniform
+    if (wave_valid > 0) {
       if (OBS == kObsWaveBits)
-        write_obs_wave_bits(a.obs + wave0 * (2 * kObsSize), bits_lds + (threadIdx.x & ~63u) * 8u, n_valid);
+        write_obs_wave_bits(a.obs + wave0 * (2 * kObsSize), lds.bits + wl * 8u, wave_valid);
       else
-        write_obs_wave<OBS == kObsWaveNT>(a.obs + wave0 * (2 * kObsSize), obs_key(L), n_valid, desc_lds);
+        write_obs_wave<OBS == kObsWaveNT>(a.obs + wave0 * (2 * kObsSize), obs_key(L), wave_valid, lds.desc);
     }
     if (OBS == kObsWaveBits) wave_sync();  // words read before the next group overwrites them
   }
@@ -532,7 +663,8 @@ __global__ __launch_bounds__(kThreads) void k_rollout(RolloutArgs a) {
 // NewInitialState / reset of selected lanes.  mode 0: fresh env (episode 0);
 // mode 1: next episode.  deal: resolve the four initial deals.
 __global__ __launch_bounds__(kThreads) void k_reset(uint4* state, int64_t n, const uint8_t* mask, int mode, int deal,
-                                                  uint32_t seed_lo, uint32_t seed_hi, uint32_t env_id_base) {
+                                                  uint32_t seed_lo, uint32_t seed_hi, uint32_t env_id_base,
+                                                  uint8_t* hist) {
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= n) return;
   if (mask && mask[i] == 0) return;
@@ -540,21 +672,27 @@ __global__ __launch_bounds__(kThreads) void k_reset(uint4* state, int64_t n, con
   Lane L = initial_lane(ep);
   if (deal) {
     Rng rng{seed_lo, seed_hi, env_id_base + (uint32_t)i, 0u, make_uint4(0, 0, 0, 0)};
-    resolve_chance(L, rng);
+    if (hist)
+      resolve_chance(L, rng, ByteHistory{hist + i * kHist});
+    else
+      resolve_chance(L, rng);
   }
   state[i] = pack(L);
 }
 
-// State::ApplyAction per lane (decision or chance outcome).
+// State::ApplyAction per lane (decision or chance outcome); the entry goes
+// to the lane's history bytes when the env keeps a history.
 __global__ __launch_bounds__(kThreads) void k_apply(uint4* state, int64_t n, const int8_t* actions,
-                                                  uint32_t* err_count) {
+                                                  uint8_t* hist, uint32_t* err_count) {
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= n) return;
   const int x = actions[i];
   if (x < 0) return;
   Lane L = unpack(state[i]);
   const uint32_t err_before = L.err;
-  if (!apply_action(L, (uint32_t)x)) {
+  const bool ok = hist ? apply_action(L, (uint32_t)x, ByteHistory{hist + i * kHist})
+                       : apply_action(L, (uint32_t)x, NoHistory{});
+  if (!ok) {
     count_error(err_count);
     return;
   }
@@ -571,25 +709,52 @@ struct QueryArgs {
   int8_t* rewards;
   int8_t* returns;
   float* obs;
+  const uint8_t* hist;
+  float* info;
 };
 
+// Per-lane accessors of the current state (State::LegalActionsMask,
+// CurrentPlayer, IsTerminal, Rewards, Returns, ObservationTensor,
+// InformationStateTensor).  No early exit: the tensor writers are
+// wave-cooperative.
+template <bool OBS, bool INFO>
 __global__ __launch_bounds__(kThreads) void k_query(QueryArgs a) {
+  __shared__ uint32_t bits[OBS ? kThreads * 8 : 1];
+  __shared__ uint8_t hist[INFO ? kThreads * kHist : 16];
+  __shared__ uint32_t pre[INFO ? kThreads * kPreWords : 1];
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (i >= a.n) return;
-  const Lane L = unpack(a.state[i]);
-  if (a.legal) a.legal[i] = legal_mask(L);
-  if (a.cur_player) a.cur_player[i] = (int8_t)current_player(L);
-  if (a.terminal) a.terminal[i] = is_terminal(L) ? 1 : 0;
-  if (a.rewards) {
-    a.rewards[2 * i] = (int8_t)L.r0;
-    a.rewards[2 * i + 1] = (int8_t)(-L.r0);
+  const bool active = i < a.n;
+  const uint32_t wl = threadIdx.x & ~63u;
+  const int64_t wave0 = (int64_t)blockIdx.x * kThreads + wl;
+  const int64_t wleft = a.n - wave0;
+  const uint32_t wave_valid = wleft >= 64 ? 64u : (wleft > 0 ? (uint32_t)wleft : 0u);
+  const Lane L = active ? unpack(a.state[i]) : initial_lane(0);
+  if (active) {
+    if (a.legal) a.legal[i] = legal_mask(L);
+    if (a.cur_player) a.cur_player[i] = (int8_t)current_player(L);
+    if (a.terminal) a.terminal[i] = is_terminal(L) ? 1 : 0;
+    if (a.rewards) {
+      a.rewards[2 * i] = (int8_t)L.r0;
+      a.rewards[2 * i + 1] = (int8_t)(-L.r0);
+    }
+    if (a.returns) {
+      const int32_t r = return0(L);
+      a.returns[2 * i] = (int8_t)r;
+      a.returns[2 * i + 1] = (int8_t)(-r);
+    }
   }
-  if (a.returns) {
-    const int32_t r = return0(L);
-    a.returns[2 * i] = (int8_t)r;
-    a.returns[2 * i + 1] = (int8_t)(-r);
+  if (OBS) {
+    obs_bits_to_lds(L, bits + threadIdx.x * 8u);
+    wave_sync();
+    if (wave_valid) write_obs_wave_bits(a.obs + wave0 * (2 * kObsSize), bits + wl * 8u, wave_valid);
   }
-  if (a.obs) write_obs_pair(a.obs + i * (2 * kObsSize), L);
+  if (INFO) {
+    if (wave_valid)
+      wave_hist_copy<true>(const_cast<uint8_t*>(a.hist) + wave0 * kHist, hist + wl * kHist, wave_valid);
+    info_prefix_to_lds(L, pre + threadIdx.x * kPreWords);
+    wave_sync();
+    if (wave_valid) write_info_wave(a.info + wave0 * (2 * kInfoSize), hist + wl * kHist, pre + wl * kPreWords, wave_valid);
+  }
 }
 
 }  // namespace coup
@@ -600,8 +765,9 @@ struct coup_env {
   int64_t batch;
   uint64_t seed;
   uint32_t env_id_base;
-  int auto_reset;
+  int flags;
   uint4* state;
+  uint8_t* hist;  // [B][96] when COUP_FLAG_HISTORY
   uint32_t* err_count;
   hipStream_t stream;
 };
@@ -625,8 +791,8 @@ int fail(int code, const std::string& msg) {
   if (!(env)) return fail(COUP_E_INVALID, "null coup_env")
 
 // COUP_OBS_MODE=1..7 overrides the observation writer (A/B measurements;
-// the modes are listed at coup::ObsMode).  6 = block-cooperative, 1024
-// threads, plain stores.
+// the modes are listed at coup::ObsMode).  4 = wave-cooperative bitmap,
+// non-temporal stores.
 constexpr int kDefaultObsMode = 4;
 int obs_mode() {
   const char* e = std::getenv("COUP_OBS_MODE");
@@ -651,9 +817,17 @@ unsigned grid_for(int64_t n) { return (unsigned)((n + coup::kThreads - 1) / coup
 int launch_reset(coup_env* env, const uint8_t* mask, int mode, int deal) {
   if (env->batch == 0) return COUP_OK;
   coup::k_reset<<<grid_for(env->batch), coup::kThreads, 0, env->stream>>>(
-      env->state, env->batch, mask, mode, deal, (uint32_t)env->seed, (uint32_t)(env->seed >> 32), env->env_id_base);
+      env->state, env->batch, mask, mode, deal, (uint32_t)env->seed, (uint32_t)(env->seed >> 32), env->env_id_base,
+      env->hist);
   COUP_HIP_TRY(hipGetLastError());
   return COUP_OK;
+}
+
+void release(coup_env* env) {
+  (void)hipFree(env->state);
+  (void)hipFree(env->hist);
+  (void)hipFree(env->err_count);
+  delete env;
 }
 
 }  // namespace
@@ -664,25 +838,30 @@ int coup_abi_version(void) { return COUP_ABI_VERSION; }
 
 const char* coup_last_error(void) { return g_last_error.c_str(); }
 
-int coup_create(int64_t batch, uint64_t seed, uint32_t env_id_base, int auto_reset, coup_env** out) {
+int coup_create(int64_t batch, uint64_t seed, uint32_t env_id_base, int flags, coup_env** out) {
   if (!out) return fail(COUP_E_INVALID, "coup_create: out is null");
   *out = nullptr;
   if (batch < 0 || batch > (int64_t(1) << 32)) return fail(COUP_E_INVALID, "coup_create: batch out of range");
+  if (flags & ~(COUP_FLAG_AUTO_RESET | COUP_FLAG_HISTORY)) return fail(COUP_E_INVALID, "coup_create: unknown flags");
   coup_env* env = new coup_env();
   env->batch = batch;
   env->seed = seed;
   env->env_id_base = env_id_base;
-  env->auto_reset = auto_reset ? 1 : 0;
+  env->flags = flags;
   env->stream = nullptr;
   env->state = nullptr;
+  env->hist = nullptr;
   env->err_count = nullptr;
-  hipError_t e = hipMalloc(&env->state, (size_t)(batch > 0 ? batch : 1) * sizeof(uint4));
+  const size_t lanes = (size_t)(batch > 0 ? batch : 1);
+  hipError_t e = hipMalloc(&env->state, lanes * sizeof(uint4));
   if (e == hipSuccess) e = hipMalloc(&env->err_count, sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemset(env->err_count, 0, sizeof(uint32_t));
+  if (e == hipSuccess && (flags & COUP_FLAG_HISTORY)) {
+    e = hipMalloc(&env->hist, lanes * COUP_HISTORY_BYTES);
+    if (e == hipSuccess) e = hipMemset(env->hist, 0xFF, lanes * COUP_HISTORY_BYTES);
+  }
   if (e != hipSuccess) {
-    (void)hipFree(env->state);
-    (void)hipFree(env->err_count);
-    delete env;
+    release(env);
     return fail(COUP_E_HIP, std::string("coup_create: ") + hipGetErrorString(e));
   }
   int rc = launch_reset(env, nullptr, /*mode=*/0, /*deal=*/1);
@@ -691,9 +870,7 @@ int coup_create(int64_t batch, uint64_t seed, uint32_t env_id_base, int auto_res
     if (e != hipSuccess) rc = fail(COUP_E_HIP, std::string("coup_create: ") + hipGetErrorString(e));
   }
   if (rc != COUP_OK) {
-    (void)hipFree(env->state);
-    (void)hipFree(env->err_count);
-    delete env;
+    release(env);
     return rc;
   }
   *out = env;
@@ -703,11 +880,8 @@ int coup_create(int64_t batch, uint64_t seed, uint32_t env_id_base, int auto_res
 int coup_destroy(coup_env* env) {
   COUP_CHECK_ENV(env);
   hipError_t e1 = hipStreamSynchronize(env->stream);
-  hipError_t e2 = hipFree(env->state);
-  hipError_t e3 = hipFree(env->err_count);
-  delete env;
-  if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess)
-    return fail(COUP_E_HIP, "coup_destroy: HIP error while releasing the env");
+  release(env);
+  if (e1 != hipSuccess) return fail(COUP_E_HIP, "coup_destroy: HIP error while releasing the env");
   return COUP_OK;
 }
 
@@ -739,9 +913,10 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
   a.seed_lo = (uint32_t)env->seed;
   a.seed_hi = (uint32_t)(env->seed >> 32);
   a.env_id_base = env->env_id_base;
-  a.auto_reset = env->auto_reset;
+  a.auto_reset = (env->flags & COUP_FLAG_AUTO_RESET) ? 1 : 0;
   a.actions_in = actions;
   a.err_count = env->err_count;
+  a.hist = env->hist;
   if (out) {
     a.actions = out->actions;
     a.rewards = out->rewards;
@@ -749,23 +924,36 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
     a.legal = out->legal_mask;
     a.cur_player = out->cur_player;
     a.obs = out->obs;
+    a.info = out->info_state;
   }
+  if (a.info && !a.hist)
+    return fail(COUP_E_INVALID, "coup_step: info_state needs an env created with COUP_FLAG_HISTORY");
   const bool uniform = actions == nullptr;
-  const int mode = a.obs == nullptr ? coup::kObsNone : obs_mode();
+  const int info = a.info ? coup::kInfoWrite : (a.hist ? coup::kInfoHistory : coup::kInfoNone);
+  int mode = a.obs == nullptr ? coup::kObsNone : obs_mode();
+  if (info != coup::kInfoNone && mode != coup::kObsNone) mode = coup::kObsWaveBits;
   hipStream_t s = env->stream;
   const int64_t n = env->batch;
-#define COUP_LAUNCH_STEP(U, M, T) \
-  coup::k_step<U, M, T><<<step_grid((n + (T)-1) / (T), T), T, 0, s>>>(a)
-#define COUP_LAUNCH_MODES(U)                                                 \
-  switch (mode) {                                                            \
-    case 0: COUP_LAUNCH_STEP(U, coup::kObsNone, 256); break;                 \
-    case 1: COUP_LAUNCH_STEP(U, coup::kObsLaneRows, 256); break;             \
-    case 2: COUP_LAUNCH_STEP(U, coup::kObsWave, 256); break;                 \
-    case 3: COUP_LAUNCH_STEP(U, coup::kObsWaveNT, 256); break;               \
-    case 4: COUP_LAUNCH_STEP(U, coup::kObsWaveBits, 256); break;             \
-    case 5: COUP_LAUNCH_STEP(U, coup::kObsBlockBits, 256); break;            \
-    case 6: COUP_LAUNCH_STEP(U, coup::kObsBlockBits, 1024); break;           \
-    default: COUP_LAUNCH_STEP(U, coup::kObsBlockBitsNT, 1024); break;        \
+#define COUP_LAUNCH_STEP(U, M, T, I) \
+  coup::k_step<U, M, T, I><<<step_grid((n + (T)-1) / (T), T), T, 0, s>>>(a)
+#define COUP_LAUNCH_MODES(U)                                                                         \
+  if (info == coup::kInfoNone) {                                                                     \
+    switch (mode) {                                                                                  \
+      case 0: COUP_LAUNCH_STEP(U, coup::kObsNone, 256, coup::kInfoNone); break;                      \
+      case 1: COUP_LAUNCH_STEP(U, coup::kObsLaneRows, 256, coup::kInfoNone); break;                  \
+      case 2: COUP_LAUNCH_STEP(U, coup::kObsWave, 256, coup::kInfoNone); break;                      \
+      case 3: COUP_LAUNCH_STEP(U, coup::kObsWaveNT, 256, coup::kInfoNone); break;                    \
+      case 4: COUP_LAUNCH_STEP(U, coup::kObsWaveBits, 256, coup::kInfoNone); break;                  \
+      case 5: COUP_LAUNCH_STEP(U, coup::kObsBlockBits, 256, coup::kInfoNone); break;                 \
+      case 6: COUP_LAUNCH_STEP(U, coup::kObsBlockBits, 1024, coup::kInfoNone); break;                \
+      default: COUP_LAUNCH_STEP(U, coup::kObsBlockBitsNT, 1024, coup::kInfoNone); break;             \
+    }                                                                                                \
+  } else if (info == coup::kInfoHistory) {                                                           \
+    if (mode == 0) COUP_LAUNCH_STEP(U, coup::kObsNone, 256, coup::kInfoHistory);                     \
+    else COUP_LAUNCH_STEP(U, coup::kObsWaveBits, 256, coup::kInfoHistory);                           \
+  } else {                                                                                           \
+    if (mode == 0) COUP_LAUNCH_STEP(U, coup::kObsNone, 256, coup::kInfoWrite);                       \
+    else COUP_LAUNCH_STEP(U, coup::kObsWaveBits, 256, coup::kInfoWrite);                             \
   }
   if (uniform) {
     COUP_LAUNCH_MODES(true)
@@ -781,6 +969,7 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
 int coup_rollout(coup_env* env, int64_t steps, const coup_rollout_stats* stats) {
   COUP_CHECK_ENV(env);
   if (steps < 0) return fail(COUP_E_INVALID, "coup_rollout: negative steps");
+  if (env->hist) return fail(COUP_E_INVALID, "coup_rollout: not available on an env with COUP_FLAG_HISTORY");
   if (env->batch == 0 || steps == 0) return COUP_OK;
   coup::RolloutArgs a;
   std::memset(&a, 0, sizeof(a));
@@ -806,7 +995,7 @@ int coup_apply_action(coup_env* env, const int8_t* actions) {
   if (!actions) return fail(COUP_E_INVALID, "coup_apply_action: actions is null");
   if (env->batch == 0) return COUP_OK;
   coup::k_apply<<<grid_for(env->batch), coup::kThreads, 0, env->stream>>>(env->state, env->batch, actions,
-                                                                          env->err_count);
+                                                                          env->hist, env->err_count);
   COUP_HIP_TRY(hipGetLastError());
   return COUP_OK;
 }
@@ -814,6 +1003,8 @@ int coup_apply_action(coup_env* env, const int8_t* actions) {
 int coup_query(coup_env* env, const coup_query_outputs* out) {
   COUP_CHECK_ENV(env);
   if (!out) return fail(COUP_E_INVALID, "coup_query: out is null");
+  if (out->info_state && !env->hist)
+    return fail(COUP_E_INVALID, "coup_query: info_state needs an env created with COUP_FLAG_HISTORY");
   if (env->batch == 0) return COUP_OK;
   coup::QueryArgs a;
   a.state = env->state;
@@ -824,7 +1015,18 @@ int coup_query(coup_env* env, const coup_query_outputs* out) {
   a.rewards = out->rewards;
   a.returns = out->returns;
   a.obs = out->obs;
-  coup::k_query<<<grid_for(env->batch), coup::kThreads, 0, env->stream>>>(a);
+  a.hist = env->hist;
+  a.info = out->info_state;
+  const unsigned g = grid_for(env->batch);
+  hipStream_t s = env->stream;
+  if (a.obs && a.info)
+    coup::k_query<true, true><<<g, coup::kThreads, 0, s>>>(a);
+  else if (a.obs)
+    coup::k_query<true, false><<<g, coup::kThreads, 0, s>>>(a);
+  else if (a.info)
+    coup::k_query<false, true><<<g, coup::kThreads, 0, s>>>(a);
+  else
+    coup::k_query<false, false><<<g, coup::kThreads, 0, s>>>(a);
   COUP_HIP_TRY(hipGetLastError());
   return COUP_OK;
 }
@@ -841,6 +1043,24 @@ int coup_import_state(coup_env* env, const uint32_t* src) {
   COUP_CHECK_ENV(env);
   if (!src) return fail(COUP_E_INVALID, "coup_import_state: src is null");
   COUP_HIP_TRY(hipMemcpyAsync(env->state, src, (size_t)env->batch * sizeof(uint4), hipMemcpyDeviceToDevice,
+                              env->stream));
+  return COUP_OK;
+}
+
+int coup_export_history(coup_env* env, uint8_t* dst) {
+  COUP_CHECK_ENV(env);
+  if (!dst) return fail(COUP_E_INVALID, "coup_export_history: dst is null");
+  if (!env->hist) return fail(COUP_E_INVALID, "coup_export_history: env has no history (COUP_FLAG_HISTORY)");
+  COUP_HIP_TRY(hipMemcpyAsync(dst, env->hist, (size_t)env->batch * COUP_HISTORY_BYTES, hipMemcpyDeviceToDevice,
+                              env->stream));
+  return COUP_OK;
+}
+
+int coup_import_history(coup_env* env, const uint8_t* src) {
+  COUP_CHECK_ENV(env);
+  if (!src) return fail(COUP_E_INVALID, "coup_import_history: src is null");
+  if (!env->hist) return fail(COUP_E_INVALID, "coup_import_history: env has no history (COUP_FLAG_HISTORY)");
+  COUP_HIP_TRY(hipMemcpyAsync(env->hist, src, (size_t)env->batch * COUP_HISTORY_BYTES, hipMemcpyDeviceToDevice,
                               env->stream));
   return COUP_OK;
 }

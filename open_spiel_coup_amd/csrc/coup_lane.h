@@ -511,16 +511,45 @@ __device__ __forceinline__ void apply_deal(Lane& L, uint32_t type) {
   COUP_PSET(L, h, p, hand_insert(COUP_PGET(L, h, p), 2u * type));
 }
 
+// ---------------------------------------------------------------- history
+//
+// Optional per-lane action history (State::history_ + the chance-deal
+// owner map history_chance_deal_player_, spiel.h:733, coup.h:182), one byte
+// per history index: [4:0] action id or card type, [5] chance deal,
+// [6] acting player (decision) or receiving player (deal).  Needed by the
+// InformationStateTensor (coup.cc:230-245) and the strings.
+constexpr uint32_t kHistoryBytes = 96;  // >= MaxGameLength + 1 = 91 entries
+
+__device__ __forceinline__ uint32_t hist_decision(uint32_t a, uint32_t player) { return a | (player << 6); }
+__device__ __forceinline__ uint32_t hist_deal(uint32_t type, uint32_t to) { return type | 0x20u | (to << 6); }
+
+struct NoHistory {
+  __device__ __forceinline__ void record(uint32_t, uint32_t) const {}
+};
+
+// Records into a byte array (a lane's slot in LDS or in global memory).
+struct ByteHistory {
+  uint8_t* p;
+  __device__ __forceinline__ void record(uint32_t idx, uint32_t entry) const {
+    if (idx < kHistoryBytes) p[idx] = (uint8_t)entry;
+  }
+};
+
 // State::ApplyAction (spiel.cc:322-331) with a legality check.  Returns false
-// (lane untouched) for an illegal action.
-__device__ __forceinline__ bool apply_action(Lane& L, uint32_t a) {
+// (lane untouched) for an illegal action.  The history entry is recorded at
+// index move_number_, like history_.push_back.
+template <class H>
+__device__ __forceinline__ bool apply_action(Lane& L, uint32_t a, const H& hist) {
   if (a > 17u) return false;
   const uint32_t m = legal_mask(L);
   if (((m >> a) & 1u) == 0u) return false;
-  if (m & kChanceFlag)
+  if (m & kChanceFlag) {
+    hist.record(L.move, hist_deal(a, L.qids & 1u));
     apply_deal(L, a);
-  else
+  } else {
+    hist.record(L.move, hist_decision(a, L.M));
     apply_decision(L, a);
+  }
   L.move += 1u;
   return true;
 }
@@ -587,12 +616,17 @@ __device__ __forceinline__ uint32_t sample_action(uint32_t mask, uint32_t u) {
 
 // rl_environment._sample_external_events (rl_environment.py:369-382):
 // deal until a decision node or a terminal state.
-__device__ __forceinline__ void resolve_chance(Lane& L, Rng& rng) {
+template <class H>
+__device__ __forceinline__ void resolve_chance(Lane& L, Rng& rng, const H& hist) {
   while (L.qlen != 0u && !is_terminal(L)) {
     const uint32_t u = rng.draw(L.episode, L.move);
-    apply_deal(L, sample_card(L.deck, u));
+    const uint32_t t = sample_card(L.deck, u);
+    hist.record(L.move, hist_deal(t, L.qids & 1u));
+    apply_deal(L, t);
     L.move += 1u;
   }
 }
+
+__device__ __forceinline__ void resolve_chance(Lane& L, Rng& rng) { resolve_chance(L, rng, NoHistory{}); }
 
 }  // namespace coup

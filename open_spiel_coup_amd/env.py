@@ -16,11 +16,16 @@ FIRST, MID, LAST = 0, 1, 2
 NUM_ACTIONS = 18
 OBS_SIZE = 98
 INFO_STATE_SIZE = 2492
+HISTORY_BYTES = _native.HISTORY_BYTES
 CHANCE_FLAG = 1 << 31
 
 
 def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _addr(t):
+    return t.data_ptr() if t is not None else None
 
 
 class BatchedCoupEnv:
@@ -34,10 +39,14 @@ class BatchedCoupEnv:
       auto_reset: SyncVectorEnv(reset_if_done=True) semantics if True,
         rl_environment semantics (LAST, then reset on the next step) if False.
       obs: write ObservationTensor of both players on every step.
+      info_state: write InformationStateTensor of both players on every step
+        (implies history).
+      history: keep per-lane histories (InformationStateTensor, strings).
       device: CUDA (HIP) device.
     """
 
-    def __init__(self, batch, seed=0, env_id_base=0, auto_reset=True, obs=True, device=None):
+    def __init__(self, batch, seed=0, env_id_base=0, auto_reset=True, obs=True, info_state=False,
+                 history=False, device=None):
         self.lib = _native.load()
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
@@ -46,10 +55,11 @@ class BatchedCoupEnv:
         self.seed = int(seed)
         self.env_id_base = int(env_id_base)
         self.auto_reset = bool(auto_reset)
+        self.history = bool(history or info_state)
+        flags = (_native.FLAG_AUTO_RESET if self.auto_reset else 0) | (_native.FLAG_HISTORY if self.history else 0)
         self._h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
-            _native.check(self.lib.coup_create(self.batch, self.seed, self.env_id_base,
-                                               int(self.auto_reset), ctypes.byref(self._h)))
+            _native.check(self.lib.coup_create(self.batch, self.seed, self.env_id_base, flags, ctypes.byref(self._h)))
         B, dev = self.batch, self.device
         self.actions = torch.empty(B, dtype=torch.int8, device=dev)
         self.rewards = torch.zeros(B, 2, dtype=torch.int8, device=dev)
@@ -57,10 +67,11 @@ class BatchedCoupEnv:
         self.legal_mask = torch.zeros(B, dtype=torch.int32, device=dev)
         self.cur_player = torch.zeros(B, dtype=torch.int8, device=dev)
         self.obs = torch.zeros(B, 2, OBS_SIZE, dtype=torch.float32, device=dev) if obs else None
+        self.info_state = (torch.zeros(B, 2, INFO_STATE_SIZE, dtype=torch.float32, device=dev)
+                           if info_state else None)
         self._out = _native.StepOutputs(
-            _ptr(self.actions).value, _ptr(self.rewards).value, _ptr(self.step_type).value,
-            _ptr(self.legal_mask).value, _ptr(self.cur_player).value,
-            _ptr(self.obs).value if self.obs is not None else None)
+            _addr(self.actions), _addr(self.rewards), _addr(self.step_type), _addr(self.legal_mask),
+            _addr(self.cur_player), _addr(self.obs), _addr(self.info_state))
 
     # ------------------------------------------------------------ plumbing
     def _bind_stream(self):
@@ -85,12 +96,17 @@ class BatchedCoupEnv:
         self._keep = mask
         return _ptr(mask)
 
+    def set_output(self, name, tensor):
+        """Point one step output (e.g. 'obs') at a caller-owned tensor."""
+        setattr(self, name, tensor)
+        setattr(self._out, name, _addr(tensor))
+
     # ------------------------------------------------------------ batched API
     def reset(self, mask=None):
         """rl_environment.reset for all lanes (or lanes where mask != 0)."""
         self._bind_stream()
         _native.check(self.lib.coup_reset(self._h, self._mask_ptr(mask)))
-        return self.query()
+        return self.query(obs=self.obs is not None, info_state=self.info_state is not None)
 
     def step(self, actions=None):
         """One batched env step.  actions: int8/long tensor [B] of decision
@@ -109,6 +125,8 @@ class BatchedCoupEnv:
                "legal_mask": self.legal_mask, "current_player": self.cur_player}
         if self.obs is not None:
             out["obs"] = self.obs
+        if self.info_state is not None:
+            out["info_state"] = self.info_state
         return out
 
     def rollout(self, steps, stats=None):
@@ -118,8 +136,8 @@ class BatchedCoupEnv:
         self._bind_stream()
         s = None
         if stats is not None:
-            s = _native.RolloutStats(_ptr(stats["episodes"]).value, _ptr(stats["return_sum"]).value,
-                                     _ptr(stats["length_sum"]).value)
+            s = _native.RolloutStats(_addr(stats["episodes"]), _addr(stats["return_sum"]),
+                                     _addr(stats["length_sum"]))
         _native.check(self.lib.coup_rollout(self._h, int(steps), ctypes.byref(s) if s else None))
 
     def new_stats(self):
@@ -138,7 +156,7 @@ class BatchedCoupEnv:
         self._keep_actions = actions
         _native.check(self.lib.coup_apply_action(self._h, _ptr(actions)))
 
-    def query(self, obs=True):
+    def query(self, obs=True, info_state=False):
         self._bind_stream()
         B, dev = self.batch, self.device
         q = {"legal_mask": torch.empty(B, dtype=torch.int32, device=dev),
@@ -148,8 +166,11 @@ class BatchedCoupEnv:
              "returns": torch.empty(B, 2, dtype=torch.int8, device=dev)}
         if obs:
             q["obs"] = torch.empty(B, 2, OBS_SIZE, dtype=torch.float32, device=dev)
-        qo = _native.QueryOutputs(*[_ptr(q[k]).value if k in q else None for k in
-                                    ("legal_mask", "current_player", "terminal", "rewards", "returns", "obs")])
+        if info_state:
+            q["info_state"] = torch.empty(B, 2, INFO_STATE_SIZE, dtype=torch.float32, device=dev)
+        qo = _native.QueryOutputs(*[_addr(q.get(k)) for k in
+                                    ("legal_mask", "current_player", "terminal", "rewards", "returns", "obs",
+                                     "info_state")])
         _native.check(self.lib.coup_query(self._h, ctypes.byref(qo)))
         return q
 
@@ -166,6 +187,20 @@ class BatchedCoupEnv:
             raise ValueError("packed state must be [B, 4] int32")
         self._keep_state = packed
         _native.check(self.lib.coup_import_state(self._h, _ptr(packed)))
+
+    def export_history(self):
+        self._bind_stream()
+        out = torch.empty(self.batch, HISTORY_BYTES, dtype=torch.uint8, device=self.device)
+        _native.check(self.lib.coup_export_history(self._h, _ptr(out)))
+        return out
+
+    def import_history(self, hist):
+        self._bind_stream()
+        hist = hist.to(device=self.device, dtype=torch.uint8).contiguous()
+        if hist.shape != (self.batch, HISTORY_BYTES):
+            raise ValueError(f"history must be [B, {HISTORY_BYTES}] uint8")
+        self._keep_hist = hist
+        _native.check(self.lib.coup_import_history(self._h, _ptr(hist)))
 
     def error_count(self):
         """Lanes that rejected an action since the last call (synchronises)."""

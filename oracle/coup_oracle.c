@@ -773,6 +773,15 @@ void oc_pack(const oc_state* s, uint32_t episode, uint32_t err, uint32_t* w) {
   w[3] = (uint32_t)s->turn_number | ((episode & 0x1FFFFFFu) << 7);
 }
 
+void oc_history_bytes(const oc_state* s, uint8_t* out) {
+  memset(out, 0xFF, 96);
+  for (int i = 0; i < s->hist_len && i < 96; ++i) {
+    int chance = s->hist_player[i] == -1;
+    int who = chance ? s->hist_deal_to[i] : s->hist_player[i];
+    out[i] = (uint8_t)(s->hist_action[i] | (chance << 5) | (who << 6));
+  }
+}
+
 /* ------------------------------------------------------ sampling contract */
 
 void oc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
@@ -897,8 +906,14 @@ int oc_rollout(const oc_rollout_args* a) {
         oc_observation_tensor(&s, 0, dst);
         oc_observation_tensor(&s, 1, dst + OC_OBS_SIZE);
       }
+      if (a->info) {
+        float* dst = a->info + o * 2 * OC_INFO_SIZE;
+        oc_info_state_tensor(&s, 0, dst);
+        oc_info_state_tensor(&s, 1, dst + OC_INFO_SIZE);
+      }
     }
     if (a->final_state) oc_pack(&s, episode, s.error ? 1u : 0u, a->final_state + 4 * lane);
+    if (a->final_hist) oc_history_bytes(&s, a->final_hist + 96 * lane);
   }
   if (a->decisions) *a->decisions = decisions;
   if (a->episodes_done) *a->episodes_done = done_eps;

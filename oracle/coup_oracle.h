@@ -108,6 +108,9 @@ int oc_info_state_string(const oc_state* s, int player, char* buf, int cap);
 int oc_to_string(const oc_state* s, char* buf, int cap);
 /* canonical 16-byte packed record, layout in DESIGN.md section 3 */
 void oc_pack(const oc_state* s, uint32_t episode, uint32_t err, uint32_t* out4);
+/* history as the product's 96 history bytes (entry i: [4:0] action / card,
+ * [5] chance deal, [6] acting / receiving player; 0xFF past the end) */
+void oc_history_bytes(const oc_state* s, uint8_t* out96);
 
 /* --- Sampling contract --------------------------------------------------- */
 void oc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
@@ -134,7 +137,9 @@ typedef struct {
   uint8_t* step_type;
   uint32_t* legal;
   float* obs;
+  float* info;             /* InformationStateTensor x2: [steps][n][2][2492] */
   uint32_t* final_state;
+  uint8_t* final_hist;     /* [n][96] */
   int64_t* decisions;      /* total decisions applied (scalar) */
   int64_t* episodes_done;  /* total finished episodes (scalar) */
   int64_t* return_sum_p0;  /* sum of final returns of player 0 */

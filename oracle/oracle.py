@@ -47,7 +47,8 @@ class _RolloutArgs(ctypes.Structure):
                 ("auto_reset", ctypes.c_int), ("obs_overwrite", ctypes.c_int),
                 ("actions", ctypes.c_void_p), ("rewards", ctypes.c_void_p),
                 ("step_type", ctypes.c_void_p), ("legal", ctypes.c_void_p),
-                ("obs", ctypes.c_void_p), ("final_state", ctypes.c_void_p),
+                ("obs", ctypes.c_void_p), ("info", ctypes.c_void_p),
+                ("final_state", ctypes.c_void_p), ("final_hist", ctypes.c_void_p),
                 ("decisions", ctypes.c_void_p), ("episodes_done", ctypes.c_void_p),
                 ("return_sum_p0", ctypes.c_void_p)]
 
@@ -83,6 +84,7 @@ def lib():
             f.argtypes = [P, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
         L.oc_to_string.argtypes = [P, ctypes.c_char_p, ctypes.c_int]
         L.oc_pack.argtypes = [P, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
+        L.oc_history_bytes.argtypes = [P, ctypes.POINTER(ctypes.c_uint8)]
         L.oc_draw.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
         L.oc_draw.restype = ctypes.c_uint32
         L.oc_philox4x32_10.argtypes = [ctypes.POINTER(ctypes.c_uint32)] * 2 + [ctypes.POINTER(ctypes.c_uint32)]
@@ -181,6 +183,11 @@ class OracleState:
     def history(self):
         return list(self._s.hist_action[:self._s.hist_len])
 
+    def history_bytes(self):
+        out = (ctypes.c_uint8 * 96)()
+        lib().oc_history_bytes(ctypes.byref(self._s), out)
+        return bytes(out)
+
     def coins(self, p):
         return self._s.pl[p].coins
 
@@ -208,7 +215,7 @@ def philox(ctr, key):
 
 
 def rollout(seed, n, steps, env_id_base=0, auto_reset=True, want_obs=False,
-            obs_overwrite=False, want_trajectory=True):
+            obs_overwrite=False, want_trajectory=True, want_info=False):
     """Uniform-random batched rollout under the sampling contract.
 
     Returns a dict of numpy arrays (step-major: [steps][n]...)."""
@@ -230,7 +237,10 @@ def rollout(seed, n, steps, env_id_base=0, auto_reset=True, want_obs=False,
     if want_obs:
         shape = (n, 2, OBS_SIZE) if obs_overwrite else (steps, n, 2, OBS_SIZE)
         a.obs = buf("obs", shape, np.float32)
+    if want_info:
+        a.info = buf("info", (steps, n, 2, INFO_SIZE), np.float32)
     a.final_state = buf("final_state", (n, 4), np.uint32)
+    a.final_hist = buf("final_hist", (n, 96), np.uint8)
     a.decisions = buf("decisions", (1,), np.int64)
     a.episodes_done = buf("episodes_done", (1,), np.int64)
     a.return_sum_p0 = buf("return_sum_p0", (1,), np.int64)

@@ -122,12 +122,71 @@ def test_obs_writers_match_oracle(mode, monkeypatch):
     ref = oracle.rollout(seed=seed, n=n, steps=steps, want_obs=True)
     env = BatchedCoupEnv(n, seed=seed, obs=True)
     guard = torch.full((n + 64, 2, 98), -7.0, device="cuda")
-    env.obs = guard[:n]
-    env._out.obs = env.obs.data_ptr()
+    env.set_output("obs", guard[:n])
     for t in range(steps):
         o = env.step()
         np.testing.assert_array_equal(_np(o["obs"]), ref["obs"][t], err_msg=f"mode {mode} step {t}")
     assert torch.all(guard[n:] == -7.0), "writer touched memory past the last lane"
+
+
+def test_playthrough_information_state():
+    """InformationStateTensor (perfect recall, history block) of both players
+    at every recorded state of coup.txt, via coup_query on an env keeping
+    histories."""
+    pt = G.load_playthrough()["states"]
+    env = BatchedCoupEnv(1, seed=0, obs=False, history=True)
+    env.new_initial_state()
+    hist = pt[-1]["history"]
+    for k in range(len(hist) + 1):
+        if k > 0:
+            env.apply_action(torch.tensor([hist[k - 1]], dtype=torch.int8))
+        rec = pt[k]
+        if "InformationStateTensor" not in rec:
+            continue
+        info = _np(env.query(obs=False, info_state=True)["info_state"])[0]
+        for p in (0, 1):
+            np.testing.assert_array_equal(info[p], G.dense(rec["InformationStateTensor"][str(p)], 2492),
+                                          err_msg=f"state {k} player {p}")
+
+
+@pytest.mark.parametrize("auto_reset", [True, False])
+def test_info_state_rollout_matches_oracle(auto_reset):
+    """coup_step writing InformationStateTensor x2 every step (ragged batch of
+    200 lanes) == the oracle; histories match byte for byte."""
+    n, steps, seed = 200, 48, 31
+    ref = oracle.rollout(seed=seed, n=n, steps=steps, auto_reset=auto_reset, want_obs=True, want_info=True)
+    env = BatchedCoupEnv(n, seed=seed, auto_reset=auto_reset, obs=True, info_state=True)
+    for t in range(steps):
+        o = env.step()
+        np.testing.assert_array_equal(_np(o["actions"]), ref["actions"][t], err_msg=f"step {t}")
+        np.testing.assert_array_equal(_np(o["obs"]), ref["obs"][t], err_msg=f"step {t}")
+        np.testing.assert_array_equal(_np(o["info_state"]), ref["info"][t], err_msg=f"step {t}")
+    np.testing.assert_array_equal(_np(env.export_state()).astype(np.uint32), ref["final_state"])
+    h = _np(env.export_history())
+    moves = packed.decode(ref["final_state"])["move_number"]
+    for lane in range(n):
+        m = int(moves[lane])
+        assert bytes(h[lane, :m]) == bytes(ref["final_hist"][lane, :m]), lane
+    assert env.error_count() == 0
+
+
+def test_history_kept_by_apply_and_step():
+    """History bytes recorded by coup_apply_action (State API) equal the
+    oracle's for the KAT action sequences."""
+    kats = G.load_kats()
+    env = BatchedCoupEnv(len(kats), seed=0, obs=False, history=True)
+    env.new_initial_state()
+    maxlen = max(len(s["actions"]) for s in kats)
+    for k in range(maxlen):
+        env.apply_action(torch.tensor([s["actions"][k] if k < len(s["actions"]) else -1 for s in kats],
+                                      dtype=torch.int8))
+    h = _np(env.export_history())
+    for i, s in enumerate(kats):
+        st = oracle.OracleState()
+        for a in s["actions"]:
+            st.apply_action(a)
+        m = len(s["actions"])
+        assert bytes(h[i, :m]) == st.history_bytes()[:m], s["name"]
 
 
 def test_external_actions_replay():
