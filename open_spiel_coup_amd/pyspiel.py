@@ -1,0 +1,422 @@
+"""`pyspiel`-shaped per-game facade over the GPU engine.
+
+The reference's callers (Deep CFR, MCCFR, agent_cmp, human_game) use
+`pyspiel.load_game("coup")` and per-game `State` objects
+(open_spiel/python/pybind11/pyspiel.cc:263-375).  This module gives them the
+same surface with only an import swap:
+
+    from open_spiel_coup_amd import pyspiel
+    game = pyspiel.load_game("coup")
+    state = game.new_initial_state()
+
+A `CoupState` holds its 16-byte lane record and its history bytes on the
+host; every rules operation (apply_action, legal actions, tensors, ...)
+runs the HIP kernels on a one-lane scratch env through the C ABI -- there
+is no CPU rules engine in the product.  Query results are cached until the
+state changes.  Strings are formatted on the host (strings.py).
+This is the compatibility path; batched learners use BatchedCoupEnv.
+"""
+import enum
+
+import numpy as np
+import torch
+
+from . import packed, strings
+from ._native import CoupError
+from .env import BatchedCoupEnv, HISTORY_BYTES, INFO_STATE_SIZE, OBS_SIZE
+
+SpielError = CoupError
+
+
+class PlayerId(enum.IntEnum):
+    """open_spiel/spiel_globals.h:28-36"""
+    DEFAULT = -1
+    CHANCE = -1
+    SIMULTANEOUS = -2
+    INVALID = -3
+    TERMINAL = -4
+    MEAN_FIELD = -5
+
+
+class GameType:
+    """The fields of open_spiel::GameType (spiel.h:42-153) Coup defines
+    (coup.cc:38-52)."""
+
+    class Dynamics(enum.Enum):
+        SIMULTANEOUS = 0
+        SEQUENTIAL = 1
+        MEAN_FIELD = 2
+
+    class ChanceMode(enum.Enum):
+        DETERMINISTIC = 0
+        EXPLICIT_STOCHASTIC = 1
+        SAMPLED_STOCHASTIC = 2
+
+    class Information(enum.Enum):
+        ONE_SHOT = 0
+        PERFECT_INFORMATION = 1
+        IMPERFECT_INFORMATION = 2
+
+    class Utility(enum.Enum):
+        ZERO_SUM = 0
+        CONSTANT_SUM = 1
+        GENERAL_SUM = 2
+        IDENTICAL = 3
+
+    class RewardModel(enum.Enum):
+        REWARDS = 0
+        TERMINAL = 1
+
+    def __init__(self):
+        self.short_name = "coup"
+        self.long_name = "Coup"
+        self.dynamics = GameType.Dynamics.SEQUENTIAL
+        self.chance_mode = GameType.ChanceMode.EXPLICIT_STOCHASTIC
+        self.information = GameType.Information.IMPERFECT_INFORMATION
+        self.utility = GameType.Utility.ZERO_SUM
+        self.reward_model = GameType.RewardModel.REWARDS
+        self.max_num_players = 2
+        self.min_num_players = 2
+        self.provides_information_state_string = True
+        self.provides_information_state_tensor = True
+        self.provides_observation_string = True
+        self.provides_observation_tensor = True
+        self.provides_factored_observation_string = False
+        self.parameter_specification = {}
+
+
+class _Engine:
+    """One-lane scratch env (history kept) that runs single-state ops."""
+
+    def __init__(self, device):
+        self.env = BatchedCoupEnv(1, seed=0, auto_reset=False, obs=False, history=True, device=device)
+        self.device = self.env.device
+
+    def _load(self, rec, hist):
+        self.env.import_state(torch.from_numpy(rec.view(np.int32).reshape(1, 4)))
+        self.env.import_history(torch.from_numpy(hist.reshape(1, HISTORY_BYTES)))
+
+    def new_initial(self):
+        self.env.new_initial_state()
+        return (self.env.export_state().cpu().numpy().view(np.uint32).reshape(4).copy(),
+                np.full(HISTORY_BYTES, 0xFF, np.uint8))
+
+    def apply(self, rec, hist, action):
+        self._load(rec, hist)
+        self.env.apply_action(torch.tensor([int(action)], dtype=torch.int8))
+        if self.env.error_count():
+            raise SpielError(f"illegal action {action}")
+        return (self.env.export_state().cpu().numpy().view(np.uint32).reshape(4).copy(),
+                self.env.export_history().cpu().numpy().reshape(HISTORY_BYTES).copy())
+
+    def query(self, rec, hist, obs, info):
+        self._load(rec, hist)
+        q = self.env.query(obs=obs, info_state=info)
+        return {k: v.cpu().numpy()[0] for k, v in q.items()}
+
+
+_engines = {}
+
+
+def _engine(device=None):
+    dev = torch.device(device if device is not None else "cuda")
+    key = (dev.type, dev.index)
+    if key not in _engines:
+        _engines[key] = _Engine(dev)
+    return _engines[key]
+
+
+class CoupGame:
+    """open_spiel::coup::CoupGame (coup.h:199-231)."""
+
+    def __init__(self, params=None, device=None):
+        if params:
+            raise SpielError("coup takes no parameters (coup.cc:51-52)")
+        self._type = GameType()
+        self._device = device
+
+    # --- metadata (coup.h:203-220, spiel.h:888-890)
+    def get_type(self):
+        return self._type
+
+    def num_distinct_actions(self):
+        return 18
+
+    def max_chance_outcomes(self):
+        return 5
+
+    def num_players(self):
+        return 2
+
+    def min_utility(self):
+        return -2.0
+
+    def max_utility(self):
+        return 2.0
+
+    def utility_sum(self):
+        return 0.0
+
+    def max_game_length(self):
+        return 90
+
+    def max_chance_nodes_in_history(self):
+        return 45
+
+    def max_move_number(self):
+        return 135
+
+    def max_history_length(self):
+        return 135
+
+    def information_state_tensor_shape(self):
+        return [INFO_STATE_SIZE]
+
+    def information_state_tensor_size(self):
+        return INFO_STATE_SIZE
+
+    def observation_tensor_shape(self):
+        return [OBS_SIZE]
+
+    def observation_tensor_size(self):
+        return OBS_SIZE
+
+    def policy_tensor_shape(self):
+        return [18]
+
+    def get_parameters(self):
+        return {}
+
+    def action_to_string(self, player, action):
+        return strings.action_to_string(player, action)
+
+    def __str__(self):
+        return "coup()"
+
+    def serialize(self):
+        return "coup()"
+
+    def __eq__(self, other):
+        return isinstance(other, CoupGame)
+
+    def __hash__(self):
+        return hash("coup()")
+
+    def new_initial_state(self):
+        return CoupState(self)
+
+    def deserialize_state(self, text):
+        """Game::DeserializeState (spiel.cc:393-425): replay the history."""
+        st = self.new_initial_state()
+        for line in text.split("\n"):
+            if line:
+                st.apply_action(int(line))
+        return st
+
+
+class CoupState:
+    """open_spiel::coup::CoupState (coup.h:111-197) over the GPU engine."""
+
+    def __init__(self, game, _rec=None, _hist=None, _history=None):
+        self._game = game
+        self._eng = _engine(game._device)
+        if _rec is None:
+            _rec, _hist = self._eng.new_initial()
+            _history = []
+        self._rec, self._hist, self._history = _rec, _hist, _history
+        self._q = None
+
+    # ------------------------------------------------------------- internals
+    def _query(self, obs=False, info=False):
+        if self._q is None or (obs and "obs" not in self._q) or (info and "info_state" not in self._q):
+            self._q = self._eng.query(self._rec, self._hist, obs, info)
+        return self._q
+
+    def _words(self):
+        return self._rec.reshape(1, 4)
+
+    # ------------------------------------------------------------- State API
+    def get_game(self):
+        return self._game
+
+    def num_players(self):
+        return 2
+
+    def num_distinct_actions(self):
+        return 18
+
+    def current_player(self):
+        return int(self._query()["current_player"])
+
+    def is_terminal(self):
+        return bool(self._query()["terminal"])
+
+    def is_chance_node(self):
+        return self.current_player() == PlayerId.CHANCE
+
+    def is_player_node(self):
+        return self.current_player() >= 0
+
+    def is_simultaneous_node(self):
+        return False
+
+    def is_mean_field_node(self):
+        return False
+
+    def _mask(self):
+        return int(self._query()["legal_mask"]) & 0xFFFFFFFF
+
+    def legal_actions(self, player=None):
+        """LegalActions() / LegalActions(player) (spiel.h:255-261)."""
+        cur = self.current_player()
+        if player is not None and player != cur:
+            return []
+        if cur == PlayerId.TERMINAL:
+            return []
+        m = self._mask() & 0x3FFFF
+        return [a for a in range(18) if (m >> a) & 1]
+
+    def legal_actions_mask(self, player=None):
+        """LegalActionsMask (spiel.cc:371-377): length 5 at chance nodes."""
+        cur = self.current_player()
+        p = cur if player is None else player
+        length = 5 if p == PlayerId.CHANCE else 18
+        mask = [0] * length
+        for a in self.legal_actions(p):
+            mask[a] = 1
+        return mask
+
+    def chance_outcomes(self):
+        """ChanceOutcomes (coup.cc:1062-1077): exact count/total doubles."""
+        if not self.is_chance_node():
+            raise SpielError("chance_outcomes() at a non-chance node")
+        deck = packed.lane(self._words())["deck"]
+        total = float(sum(deck))
+        return [(t, deck[t] / total) for t in range(5) if deck[t] > 0]
+
+    def legal_chance_outcomes(self):
+        return [a for a, _ in self.chance_outcomes()]
+
+    def apply_action(self, action):
+        """State::ApplyAction (spiel.cc:322-331) on the GPU; raises SpielError
+        for an illegal action."""
+        player = self.current_player()
+        self._rec, self._hist = self._eng.apply(self._rec, self._hist, action)
+        self._history = self._history + [(player, int(action))]
+        self._q = None
+
+    def apply_action_with_legality_check(self, action):
+        self.apply_action(action)
+
+    def child(self, action):
+        c = self.clone()
+        c.apply_action(action)
+        return c
+
+    def clone(self):
+        c = CoupState(self._game, self._rec.copy(), self._hist.copy(), list(self._history))
+        c._q = self._q
+        return c
+
+    def __copy__(self):
+        return self.clone()
+
+    def __deepcopy__(self, memo):
+        return self.clone()
+
+    def rewards(self):
+        return [float(x) for x in self._query()["rewards"]]
+
+    def returns(self):
+        return [float(x) for x in self._query()["returns"]]
+
+    def player_reward(self, player):
+        return self.rewards()[player]
+
+    def player_return(self, player):
+        return self.returns()[player]
+
+    def observation_tensor(self, player=None):
+        p = self.current_player() if player is None else player
+        return self._query(obs=True)["obs"][p].tolist()
+
+    def information_state_tensor(self, player=None):
+        p = self.current_player() if player is None else player
+        return self._query(info=True)["info_state"][p].tolist()
+
+    def observation_string(self, player=None):
+        p = self.current_player() if player is None else player
+        return strings.observation_string(self._words(), self._hist, p)
+
+    def information_state_string(self, player=None):
+        p = self.current_player() if player is None else player
+        return strings.information_state_string(self._words(), self._hist, p)
+
+    def action_to_string(self, player, action=None):
+        if action is None:  # action_to_string(action) for the current player
+            player, action = self.current_player(), player
+        return strings.action_to_string(player, action)
+
+    def history(self):
+        return [a for _, a in self._history]
+
+    def full_history(self):
+        return list(self._history)
+
+    def history_str(self):
+        return ", ".join(str(a) for a in self.history())
+
+    def move_number(self):
+        return packed.lane(self._words())["move_number"]
+
+    def serialize(self):
+        """State::Serialize (spiel.cc:297-311)."""
+        return "".join(f"{a}\n" for a in self.history())
+
+    def __str__(self):
+        return strings.to_string(self._words(), self._hist)
+
+    def to_string(self):
+        return str(self)
+
+    # packed access for callers that batch states themselves
+    def packed_record(self):
+        return self._rec.copy()
+
+    def history_bytes(self):
+        return self._hist.copy()
+
+
+def load_game(name, params=None):
+    """LoadGame (spiel.h:1081-1090) for the one game this build provides."""
+    short = name.split("(")[0] if isinstance(name, str) else name
+    if short != "coup":
+        raise SpielError(f"unknown game '{name}': this build provides only 'coup'")
+    return CoupGame(params or None)
+
+
+def registered_names():
+    return ["coup"]
+
+
+def serialize_game_and_state(game, state):
+    """SerializeGameAndState (spiel.cc:428-448)."""
+    return ("# Automatically generated by OpenSpiel SerializeGameAndState\n[Meta]\nVersion: 1\n\n"
+            f"[Game]\n{game.serialize()}\n[State]\n{state.serialize()}\n")
+
+
+def deserialize_game_and_state(text):
+    """DeserializeGameAndState (spiel.cc:450-493)."""
+    section, game_s, state_lines = None, "", []
+    for line in text.split("\n"):
+        if line.startswith("#"):
+            continue
+        if line in ("[Meta]", "[Game]", "[State]"):
+            section = line
+            continue
+        if section == "[Game]" and line:
+            game_s = line
+        elif section == "[State]":
+            state_lines.append(line)
+    game = load_game(game_s)
+    return game, game.deserialize_state("\n".join(state_lines))

@@ -1,0 +1,277 @@
+"""`rl_environment`-shaped facade (open_spiel/python/rl_environment.py) over
+the GPU engine.
+
+    from open_spiel_coup_amd import rl_environment
+    env = rl_environment.Environment("coup")
+    ts = env.reset()
+    while not ts.last():
+        ts = env.step([agent_action(ts)])
+
+Semantics follow the reference line for line: observation type defaults to
+INFORMATION_STATE (rl_environment.py:195-200), chance events are sampled
+until a decision node (:369-382), every time step carries both players'
+tensors and legal actions (:219-268), discounts are 0 at LAST (:252-254),
+and step() after LAST resets (:310-311).  One Environment drives one lane of
+a BatchedCoupEnv; batched learners should use BatchedCoupEnv directly.
+
+Chance sampling: by default the deals come from the build's Philox contract
+ inside the kernel, keyed by `seed`.  Passing a
+`chance_event_sampler` (an object called with the state, like the
+reference's ChanceEventSampler, :119-131) switches to the State API path:
+decisions and deals are applied one at a time and the sampler picks each
+deal.
+"""
+import collections
+import enum
+
+import numpy as np
+import torch
+
+from . import pyspiel
+from .env import BatchedCoupEnv, HISTORY_BYTES
+
+
+class StepType(enum.Enum):
+    """rl_environment.py:96-112"""
+    FIRST = 0
+    MID = 1
+    LAST = 2
+
+    def first(self):
+        return self is StepType.FIRST
+
+    def mid(self):
+        return self is StepType.MID
+
+    def last(self):
+        return self is StepType.LAST
+
+
+class TimeStep(collections.namedtuple("TimeStep", ["observations", "rewards", "discounts", "step_type"])):
+    """rl_environment.py:47-93"""
+    __slots__ = ()
+
+    def first(self):
+        return self.step_type == StepType.FIRST
+
+    def mid(self):
+        return self.step_type == StepType.MID
+
+    def last(self):
+        return self.step_type == StepType.LAST
+
+    def is_simultaneous_move(self):
+        return self.observations["current_player"] == pyspiel.PlayerId.SIMULTANEOUS
+
+    def current_player(self):
+        return self.observations["current_player"]
+
+
+class ObservationType(enum.Enum):
+    """rl_environment.py:134-137"""
+    OBSERVATION = 0
+    INFORMATION_STATE = 1
+
+
+class ChanceEventSampler:
+    """rl_environment.py:119-131: numpy-sampled chance events (used only when
+    passed explicitly to Environment)."""
+
+    def __init__(self, seed=None):
+        self.seed(seed)
+
+    def seed(self, seed=None):
+        self._rng = np.random.RandomState(seed)
+
+    def __call__(self, state):
+        actions, probs = zip(*state.chance_outcomes())
+        return self._rng.choice(actions, p=probs)
+
+
+def registered_games():
+    return pyspiel.registered_names()
+
+
+class Environment:
+    """rl_environment.Environment for Coup on the GPU (one lane)."""
+
+    def __init__(self, game="coup", discount=1.0, chance_event_sampler=None, observation_type=None,
+                 include_full_state=False, mfg_distribution=None, mfg_population=None,
+                 enable_legality_check=False, seed=0, device=None, **kwargs):
+        if isinstance(game, str):
+            self._game = pyspiel.load_game(game, kwargs or None)
+        else:
+            self._game = game
+        if mfg_distribution is not None or mfg_population is not None:
+            raise ValueError("coup is not a mean-field game")
+        self._sampler = chance_event_sampler
+        self._include_full_state = include_full_state
+        self._enable_legality_check = enable_legality_check
+        self._num_players = self._game.num_players()
+        self._discounts = [discount] * self._num_players
+        if observation_type is None:
+            observation_type = ObservationType.INFORMATION_STATE
+        self._use_observation = observation_type == ObservationType.OBSERVATION
+        self._device = device
+        self._seed = int(seed or 0)
+        self._make_env()
+        self._should_reset = True
+        self._last = None
+
+    # ------------------------------------------------------------ plumbing
+    def _make_env(self):
+        self._env = BatchedCoupEnv(1, seed=self._seed, auto_reset=False, obs=self._use_observation,
+                                   info_state=not self._use_observation, history=True, device=self._device)
+
+    def _state_view(self):
+        words = self._env.export_state().cpu().numpy().view(np.uint32).reshape(4).copy()
+        hist = self._env.export_history().cpu().numpy().reshape(HISTORY_BYTES).copy()
+        return words, hist
+
+    def _history_list(self, words, hist):
+        from .packed import lane
+        n = lane(words.reshape(1, 4))["move_number"]
+        out = []
+        for i in range(n):
+            e = int(hist[i])
+            out.append((-1 if e & 0x20 else (e >> 6) & 1, e & 0x1F))
+        return out
+
+    def _time_step(self, q, step_type, rewards):
+        cur = int(q["current_player"])
+        mask = int(q["legal_mask"]) & 0x3FFFF
+        legal_cur = [a for a in range(18) if (mask >> a) & 1] if cur >= 0 else []
+        key = "obs" if self._use_observation else "info_state"
+        tensors = q[key]
+        obs = {"info_state": [tensors[p].tolist() for p in range(self._num_players)],
+               "legal_actions": [legal_cur if p == cur else [] for p in range(self._num_players)],
+               "current_player": cur,
+               "serialized_state": []}
+        if self._include_full_state:
+            obs["serialized_state"] = pyspiel.serialize_game_and_state(self._game, self.get_state)
+        discounts = None
+        if step_type == StepType.MID:
+            discounts = list(self._discounts)
+        elif step_type == StepType.LAST:
+            discounts = [0.0 for _ in self._discounts]
+        self._last = obs
+        return TimeStep(observations=obs, rewards=rewards, discounts=discounts, step_type=step_type)
+
+    def _query(self):
+        q = self._env.query(obs=self._use_observation, info_state=not self._use_observation)
+        return {k: v.cpu().numpy()[0] for k, v in q.items()}
+
+    def _sample_external_events(self):
+        """rl_environment.py:369-382 with a caller-supplied sampler."""
+        while True:
+            q = self._query()
+            if int(q["current_player"]) != pyspiel.PlayerId.CHANCE:
+                return q
+            outcome = self._sampler(self.get_state)
+            self._env.apply_action(torch.tensor([int(outcome)], dtype=torch.int8))
+
+    # ------------------------------------------------------------ public API
+    def seed(self, seed=None):
+        """Re-key the env's chance stream (ChanceEventSampler.seed)."""
+        if self._sampler is not None:
+            self._sampler.seed(seed)
+            return
+        self._seed = int(seed or 0)
+        self._make_env()
+        self._should_reset = True
+
+    def get_time_step(self):
+        q = self._query()
+        step_type = StepType.LAST if int(q["terminal"]) else StepType.MID
+        self._should_reset = step_type == StepType.LAST
+        return self._time_step(q, step_type, [float(x) for x in q["rewards"]])
+
+    def step(self, actions):
+        assert len(actions) == self.num_actions_per_step, (
+            "Invalid number of actions! Expected {}".format(self.num_actions_per_step))
+        if self._should_reset:
+            return self.reset()
+        if self._enable_legality_check:
+            legal = self._last["legal_actions"][self._last["current_player"]] if self._last else []
+            if actions[0] not in legal:
+                raise RuntimeError(f"step() called on illegal action {actions[0]}")
+        a = torch.tensor([int(actions[0])], dtype=torch.int8)
+        if self._sampler is None:
+            self._env.step(a)
+        else:
+            self._env.apply_action(a)
+            self._sample_external_events()
+        if self._env.error_count():
+            raise pyspiel.SpielError(f"illegal action {actions[0]}")
+        return self.get_time_step()
+
+    def reset(self):
+        self._should_reset = False
+        if self._sampler is None:
+            self._env.reset()
+            q = self._query()
+        else:
+            self._env.new_initial_state()
+            q = self._sample_external_events()
+        return self._time_step(q, StepType.FIRST, None)
+
+    def observation_spec(self):
+        return dict(
+            info_state=tuple([self._game.observation_tensor_size() if self._use_observation
+                              else self._game.information_state_tensor_size()]),
+            legal_actions=(self._game.num_distinct_actions(),),
+            current_player=(),
+            serialized_state=(),
+        )
+
+    def action_spec(self):
+        return dict(num_actions=self._game.num_distinct_actions(), min=0,
+                    max=self._game.num_distinct_actions() - 1, dtype=int)
+
+    @property
+    def use_observation(self):
+        return self._use_observation
+
+    @property
+    def name(self):
+        return self._game.get_type().short_name
+
+    @property
+    def num_players(self):
+        return self._game.num_players()
+
+    @property
+    def num_actions_per_step(self):
+        return 1
+
+    @property
+    def is_turn_based(self):
+        return True
+
+    @property
+    def max_game_length(self):
+        return self._game.max_game_length()
+
+    @property
+    def is_chance_node(self):
+        return int(self._query()["current_player"]) == pyspiel.PlayerId.CHANCE
+
+    @property
+    def game(self):
+        return self._game
+
+    @property
+    def get_state(self):
+        """A pyspiel-shaped CoupState snapshot of the env's lane."""
+        words, hist = self._state_view()
+        return pyspiel.CoupState(self._game, words, hist, self._history_list(words, hist))
+
+    def set_state(self, new_state):
+        assert new_state.get_game() == self.game, "State must have been created by the same game."
+        rec = torch.from_numpy(new_state.packed_record().view(np.int32).reshape(1, 4))
+        self._env.import_state(rec)
+        self._env.import_history(torch.from_numpy(new_state.history_bytes().reshape(1, HISTORY_BYTES)))
+
+    @property
+    def mfg_distribution(self):
+        return None
