@@ -1,13 +1,18 @@
 """Coup env-steps/sec on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4r]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c3i|c2|c2r]
 
-Workload (default, configs[2] of BASELINE.json, the batch-2^20 config the
+Workload (default c3 = configs[2] of BASELINE.json, the batch-2^20 config the
 metric is quoted on): 2-player Coup, B = 2^20 lanes per GPU, uniform-random
 policy drawn in-kernel, one env step per lane per launch, with the
 ObservationTensor of both players written out (fp32 [B][2][98]) every step
 plus actions, rewards, step types and legal masks -- the batched
 rl_environment/SyncVectorEnv step.  Synthetic data: the games themselves.
+
+Other configs (secondary lines, not the headline):
+  c3i  as c3 but InformationStateTensor x2 (fp32 [B][2][2492]) instead, B = 2^18
+  c2   configs[1]: B = 65,536, no observations, one launch per step
+  c2r  configs[1] fused: B = 65,536, `steps` env steps in ONE launch (coup_rollout)
 
 A "step" is one batched env step over all B lanes; value = env-steps/s of
 the whole job (N x B x K / max-over-ranks wall time).  Multi-GPU: one
@@ -15,11 +20,11 @@ process per GPU (torchrun), global env ids sharded by rank, no collective
 inside the step loop; the timed region ends with one RCCL all-gather of
 the ranks' final per-lane rewards/step types (trajectory collation).
 
-roofline: algorithmic bytes per launch (824 B x B)
-over the step kernel's average duration from HIP events on the launch
-stream; traffic: HBM bytes per launch from the rocprofv3 PMC pass recorded
-in profiles/ (null if absent).  cpu_baseline: the C oracle (a scalar port
-of the reference rules) on one host core, same workload per lane.
+roofline: algorithmic bytes per launch over the step
+kernel's average duration from HIP events on the launch stream; traffic:
+HBM bytes per launch from the rocprofv3 PMC passes recorded in profiles/
+(null if absent).  cpu_baseline: the C oracle (a scalar port of the
+reference rules) on one host core, same per-lane workload.
 """
 import argparse
 import json
@@ -31,8 +36,15 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-BYTES_PER_STEP = {"c3": 824, "c2": 40}
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
+
+# config -> (default batch, obs, info_state, fused, algorithmic bytes per lane-step, workload name)
+CONFIGS = {
+    "c3": (1 << 20, True, False, False, 824, "coup-2p-uniform-b2^20-obs"),
+    "c3i": (1 << 18, False, True, False, 40 + 2 * 2492 * 4 + 96 + 96, "coup-2p-uniform-b2^18-infostate"),
+    "c2": (65536, False, False, False, 40, "coup-2p-uniform-b65536"),
+    "c2r": (65536, False, False, True, 32, "coup-2p-uniform-b65536-fused-rollout"),
+}
 
 
 def _writer(mode_env):
@@ -47,7 +59,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="c3", choices=["c3", "c2"])
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -56,21 +68,24 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(target_s, with_obs):
+def cpu_baseline(target_s, with_obs, with_info):
     """Bounded sample of the same per-lane workload on the oracle (1 core)."""
     from oracle import oracle
-    n = 4096
+    n = 4096 if not with_info else 256
+    kw = dict(want_obs=with_obs, obs_overwrite=True, want_trajectory=False)
     t0 = time.perf_counter()
-    oracle.rollout(seed=7, n=n, steps=16, want_obs=with_obs, obs_overwrite=True, want_trajectory=False)
-    per_step = (time.perf_counter() - t0) / (n * 16)
-    steps = max(16, int(target_s / per_step / n))
+    oracle.rollout(seed=7, n=n, steps=8, want_info=with_info, **kw)
+    per_step = (time.perf_counter() - t0) / (n * 8)
+    steps = max(8, int(target_s / per_step / n))
+    if with_info:
+        steps = min(steps, 64)  # the oracle keeps every step's tensors
     t0 = time.perf_counter()
-    oracle.rollout(seed=7, n=n, steps=steps, want_obs=with_obs, obs_overwrite=True, want_trajectory=False)
+    oracle.rollout(seed=7, n=n, steps=steps, want_info=with_info, **kw)
     dt = time.perf_counter() - t0
+    what = " with ObservationTensor x2 written per step" if with_obs else ""
+    what += " with InformationStateTensor x2 written per step" if with_info else ""
     return {"value": n * steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"{n} lanes x {steps} uniform-random steps"
-                      + (" with ObservationTensor x2 written per step" if with_obs else "")
-                      + f", {dt:.1f} s, oracle/coup_oracle.c -O2"}
+            "sample": f"{n} lanes x {steps} uniform-random steps{what}, {dt:.1f} s, oracle/coup_oracle.c -O2"}
 
 
 def main():
@@ -85,47 +100,66 @@ def main():
     dev = D.init("nccl")  # RCCL over xGMI when world > 1
 
     cfg = args.config
-    B = args.batch or (1 << 20 if cfg == "c3" else 65536)
-    with_obs = cfg == "c3"
+    B0, with_obs, with_info, fused, bytes_per_lane, workload = CONFIGS[cfg]
+    B = args.batch or B0
     env = BatchedCoupEnv(B, seed=args.seed, env_id_base=D.env_id_base(rank, B), auto_reset=True, obs=with_obs,
-                         device=dev)
+                         info_state=with_info, device=dev)
 
     def barrier():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
-        env.step()
-    barrier()
-
     stream = torch.cuda.current_stream(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if fused:
+        env.rollout(args.warmup)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))]
+    else:
+        for _ in range(args.warmup):
+            env.step()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
     barrier()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        ev[k][0].record(stream)
-        env.step()
-        ev[k][1].record(stream)
+    if fused:
+        ev[0][0].record(stream)
+        env.rollout(args.steps)
+        ev[0][1].record(stream)
+    else:
+        for k in range(args.steps):
+            ev[k][0].record(stream)
+            env.step()
+            ev[k][1].record(stream)
     if world > 1:
         # collate the final step's per-lane outcome over xGMI (RCCL all-gather)
         D.collate(torch.cat([env.rewards.view(torch.uint8), env.step_type.view(-1, 1)], 1))
     barrier()
     elapsed = time.perf_counter() - t0
 
-    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps  # per env step
     elapsed = D.max_over_ranks(elapsed, dev)
     errors = env.error_count()
 
     if rank == 0:
-        bytes_per_launch = BYTES_PER_STEP[cfg] * B
-        achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+        bytes_per_launch = bytes_per_lane * B * (args.steps if fused else 1)
+        launch_ms = kern_ms * (args.steps if fused else 1)
+        achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
         traffic = None
         if os.path.exists(TRAFFIC_FILE):
             with open(TRAFFIC_FILE) as f:
                 tr = json.load(f)
             if tr.get("config") == cfg and tr.get("batch") == B:
                 traffic = tr.get("hbm_bytes_per_launch")
+        if fused:
+            kernel = "coup::k_rollout"
+        elif with_info:
+            kernel = "coup::k_step<true, 0, 256, 2>"
+        elif with_obs:
+            kernel = "coup::k_step<true, %d, %d, 0>" % _writer(os.environ.get("COUP_OBS_MODE"))
+        else:
+            kernel = "coup::k_step<true, 0, 256, 0>"
+        outputs = ("ObservationTensor fp32 [B][2][98] per step" if with_obs else
+                   "InformationStateTensor fp32 [B][2][2492] per step" if with_info else "none")
         line = {
             "metric": "Coup env-steps/sec at batch 2^20, 1/2/4/8 MI355X; HBM GB/s vs peak",
             "value": world * B * args.steps / elapsed,
@@ -139,19 +173,16 @@ def main():
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic (uniform-random self-play games)",
-            "config": {"workload": "coup-2p-uniform-b2^20-obs" if cfg == "c3" else "coup-2p-uniform-b65536",
-                       "batch_per_gpu": B, "global_batch": world * B, "players": 2,
-                       "obs": "ObservationTensor fp32 [B][2][98] per step" if with_obs else "none",
-                       "auto_reset": True, "parallelism": f"dp{world} (env-id sharding)"},
+            "config": {"workload": workload, "batch_per_gpu": B, "global_batch": world * B, "players": 2,
+                       "outputs": outputs, "auto_reset": True, "fused_steps_per_launch": args.steps if fused else 1,
+                       "parallelism": f"dp{world} (env-id sharding)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "coup::k_step<true, %s>" % (
-                             ("%d, %d" % _writer(os.environ.get("COUP_OBS_MODE"))) if with_obs else "0, 256"),
-                         "kernel_ms": kern_ms, "bytes_per_launch": bytes_per_launch},
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kernel,
+                         "kernel_ms": launch_ms, "bytes_per_launch": bytes_per_launch},
             "lane_errors": errors,
         }
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, with_obs)
+            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, with_obs, with_info)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

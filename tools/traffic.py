@@ -49,7 +49,10 @@ def main():
             cfg = args[i + 1]
         if a == "--batch":
             batch = int(args[i + 1])
-    batch = batch or (1 << 20 if cfg == "c3" else 65536)
+    sys.path.insert(0, ROOT)
+    from bench import CONFIGS
+    batch = batch or CONFIGS[cfg][0]
+    want_obs, want_info, fused = CONFIGS[cfg][1], CONFIGS[cfg][2], CONFIGS[cfg][3]
     step_kernel = os.environ.get("COUP_STEP_KERNEL", "coup::k_step<true, OBS, T> (uniform policy)")
 
     dst = os.path.join(ROOT, "profiles", tag)
@@ -71,9 +74,14 @@ def main():
         vals = []
         for r in rows(os.path.join(src, kind, "**", "*counter_collection.csv")):
             kn = r[col(r, "kernel", "name")]
-            m = re.search(r"k_step<true, (\d+), \d+>", kn) or re.search(r"k_stepILb1ELi(\d+)ELi\d+E", kn)
-            if not m or (m.group(1) == "0") != (cfg != "c3"):
-                continue
+            if fused:
+                if "k_rollout" not in kn:
+                    continue
+            else:
+                m = (re.search(r"k_step<true, (\d+), \d+, (\d+)>", kn) or
+                     re.search(r"k_stepILb1ELi(\d+)ELi\d+ELi(\d+)E", kn))
+                if not m or (m.group(1) != "0") != want_obs or (m.group(2) == "2") != want_info:
+                    continue
             if r[col(r, "counter", "name")] != cname:
                 continue
             vals.append(float(r[col(r, "counter", "value")]))
