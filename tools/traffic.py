@@ -64,7 +64,7 @@ def main():
         shutil.copy(stats[0], os.path.join(dst, "kernel_stats.csv"))
         for r in rows(stats[0]):
             name = r[col(r, "name")]
-            if "k_step" in name:
+            if "k_step" in name or "k_rollout" in name:
                 summary.setdefault("kernels", {})[name] = {
                     "calls": int(r[col(r, "calls")]),
                     "avg_ns": float(r[col(r, "average")]),
