@@ -458,7 +458,7 @@ enum ObsMode : int {
 // every applied action is recorded in `hist`.
 template <bool UNIFORM, class H>
 __device__ __forceinline__ void step_lane(const StepArgs& a, int64_t i, Lane& L, int& act, uint32_t& st,
-                                          int32_t& rew, const H& hist) {
+                                          int32_t& rew, H& hist) {
   Rng rng{a.seed_lo, a.seed_hi, a.env_id_base + (uint32_t)i, 0u, make_uint4(0, 0, 0, 0)};
   act = -1;
   rew = 0;
@@ -560,10 +560,14 @@ __device__ __forceinline__ void step_group(const StepArgs& a, int64_t grp, StepL
     int act;
     uint32_t st;
     int32_t rew;
-    if (INFO != kInfoNone)
-      step_lane<UNIFORM>(a, i, L, act, st, rew, ByteHistory{lds.hist + threadIdx.x * kHist});
-    else
-      step_lane<UNIFORM>(a, i, L, act, st, rew, NoHistory{});
+    if (INFO != kInfoNone) {
+      RegHistory rec;
+      step_lane<UNIFORM>(a, i, L, act, st, rew, rec);
+      rec.flush(lds.hist + threadIdx.x * kHist);
+    } else {
+      NoHistory none;
+      step_lane<UNIFORM>(a, i, L, act, st, rew, none);
+    }
     a.state[i] = pack(L);
     if (a.actions) a.actions[i] = (int8_t)act;
     if (a.rewards) {
@@ -672,10 +676,13 @@ __global__ __launch_bounds__(kThreads) void k_reset(uint4* state, int64_t n, con
   Lane L = initial_lane(ep);
   if (deal) {
     Rng rng{seed_lo, seed_hi, env_id_base + (uint32_t)i, 0u, make_uint4(0, 0, 0, 0)};
-    if (hist)
-      resolve_chance(L, rng, ByteHistory{hist + i * kHist});
-    else
+    if (hist) {
+      RegHistory rec;
+      resolve_chance(L, rng, rec);
+      rec.flush(hist + i * kHist);
+    } else {
       resolve_chance(L, rng);
+    }
   }
   state[i] = pack(L);
 }
@@ -690,14 +697,18 @@ __global__ __launch_bounds__(kThreads) void k_apply(uint4* state, int64_t n, con
   if (x < 0) return;
   Lane L = unpack(state[i]);
   const uint32_t err_before = L.err;
-  const bool ok = hist ? apply_action(L, (uint32_t)x, ByteHistory{hist + i * kHist})
-                       : apply_action(L, (uint32_t)x, NoHistory{});
-  if (!ok) {
+  // the history entry is formed before and stored after the transition, so
+  // the byte store stays out of the inlined rules
+  const uint32_t idx = L.move;
+  const uint32_t entry = is_chance(L) ? hist_deal((uint32_t)x, L.qids & 1u) : hist_decision((uint32_t)x, L.M);
+  NoHistory none;
+  if (!apply_action(L, (uint32_t)x, none)) {
     count_error(err_count);
     return;
   }
   if (L.err && !err_before) count_error(err_count);
   state[i] = pack(L);
+  if (hist && idx < (uint32_t)kHist) hist[i * kHist + idx] = (uint8_t)entry;
 }
 
 struct QueryArgs {

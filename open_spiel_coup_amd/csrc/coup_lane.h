@@ -524,14 +524,36 @@ __device__ __forceinline__ uint32_t hist_decision(uint32_t a, uint32_t player) {
 __device__ __forceinline__ uint32_t hist_deal(uint32_t type, uint32_t to) { return type | 0x20u | (to << 6); }
 
 struct NoHistory {
-  __device__ __forceinline__ void record(uint32_t, uint32_t) const {}
+  __device__ __forceinline__ void record(uint32_t, uint32_t) {}
 };
 
-// Records into a byte array (a lane's slot in LDS or in global memory).
-struct ByteHistory {
-  uint8_t* p;
-  __device__ __forceinline__ void record(uint32_t idx, uint32_t entry) const {
-    if (idx < kHistoryBytes) p[idx] = (uint8_t)entry;
+// Entries recorded during one transition, held in registers as 16-bit
+// (index << 8 | byte) records in a 12-deep shift register (newest in the low
+// bits of q0).  One env step records at most 4 pending deals + 1 decision +
+// 3 deals + 4 deals of an auto-reset = 12.  The rules themselves never touch
+// memory; the kernel flushes the records afterwards, oldest first.
+struct RegHistory {
+  uint64_t q0 = 0, q1 = 0, q2 = 0;
+  uint32_t count = 0;
+  __device__ __forceinline__ void record(uint32_t idx, uint32_t entry) {
+    q2 = (q2 << 16) | (q1 >> 48);
+    q1 = (q1 << 16) | (q0 >> 48);
+    q0 = (q0 << 16) | (uint64_t)((idx << 8) | (entry & 0xFFu));
+    count += 1u;
+  }
+  // record k, 0 = newest
+  __device__ __forceinline__ uint32_t get(uint32_t k) const {
+    const uint64_t w = k < 4u ? q0 : (k < 8u ? q1 : q2);
+    return (uint32_t)(w >> (16u * (k & 3u))) & 0xFFFFu;
+  }
+  // write the records into a lane's history bytes, oldest first
+  __device__ __forceinline__ void flush(uint8_t* __restrict__ bytes) const {
+    const uint32_t n = count < 12u ? count : 12u;
+    for (uint32_t k = n; k-- > 0;) {
+      const uint32_t r = get(k);
+      const uint32_t idx = r >> 8;
+      if (idx < kHistoryBytes) bytes[idx] = (uint8_t)(r & 0xFFu);
+    }
   }
 };
 
@@ -539,7 +561,7 @@ struct ByteHistory {
 // (lane untouched) for an illegal action.  The history entry is recorded at
 // index move_number_, like history_.push_back.
 template <class H>
-__device__ __forceinline__ bool apply_action(Lane& L, uint32_t a, const H& hist) {
+__device__ __forceinline__ bool apply_action(Lane& L, uint32_t a, H& hist) {
   if (a > 17u) return false;
   const uint32_t m = legal_mask(L);
   if (((m >> a) & 1u) == 0u) return false;
@@ -617,7 +639,7 @@ __device__ __forceinline__ uint32_t sample_action(uint32_t mask, uint32_t u) {
 // rl_environment._sample_external_events (rl_environment.py:369-382):
 // deal until a decision node or a terminal state.
 template <class H>
-__device__ __forceinline__ void resolve_chance(Lane& L, Rng& rng, const H& hist) {
+__device__ __forceinline__ void resolve_chance(Lane& L, Rng& rng, H& hist) {
   while (L.qlen != 0u && !is_terminal(L)) {
     const uint32_t u = rng.draw(L.episode, L.move);
     const uint32_t t = sample_card(L.deck, u);
@@ -627,6 +649,9 @@ __device__ __forceinline__ void resolve_chance(Lane& L, Rng& rng, const H& hist)
   }
 }
 
-__device__ __forceinline__ void resolve_chance(Lane& L, Rng& rng) { resolve_chance(L, rng, NoHistory{}); }
+__device__ __forceinline__ void resolve_chance(Lane& L, Rng& rng) {
+  NoHistory none;
+  resolve_chance(L, rng, none);
+}
 
 }  // namespace coup
