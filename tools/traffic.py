@@ -94,6 +94,8 @@ def main():
     traffic = None
     if fetch_kb is not None and write_kb is not None:
         traffic = (2.0 * fetch_kb + write_kb) * 1024.0
+    if traffic is None:
+        sys.exit(f"no FETCH_SIZE / WRITE_SIZE records for the step kernel under {src}; nothing written")
     summary["hbm_bytes_per_launch"] = traffic
     summary["correction"] = "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE halving)"
     summary["step_kernel"] = step_kernel
