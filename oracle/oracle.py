@@ -53,6 +53,27 @@ class _RolloutArgs(ctypes.Structure):
                 ("return_sum_p0", ctypes.c_void_p)]
 
 
+class _NpPlayer(ctypes.Structure):
+    _fields_ = [("cards", _OcCard * 4), ("ncards", ctypes.c_int), ("coins", ctypes.c_int),
+                ("last_action", ctypes.c_int), ("lost_challenge", ctypes.c_int)]
+
+
+class _NpState(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int), ("deck", ctypes.c_int * 5), ("pl", _NpPlayer * 6),
+                ("queue", ctypes.c_int * 8), ("qlen", ctypes.c_int), ("init_left", ctypes.c_int),
+                ("T", ctypes.c_int), ("M", ctypes.c_int), ("O", ctypes.c_int), ("begin", ctypes.c_int),
+                ("turn", ctypes.c_int), ("move", ctypes.c_int), ("rewards", ctypes.c_int * 6),
+                ("error", ctypes.c_int)]
+
+
+class _NpRolloutArgs(ctypes.Structure):
+    _fields_ = [("n_players", ctypes.c_int), ("seed", ctypes.c_uint64), ("env_id_base", ctypes.c_uint32),
+                ("n", ctypes.c_int64), ("steps", ctypes.c_int64), ("auto_reset", ctypes.c_int),
+                ("actions", ctypes.c_void_p), ("rewards", ctypes.c_void_p), ("step_type", ctypes.c_void_p),
+                ("legal", ctypes.c_void_p), ("obs", ctypes.c_void_p), ("final_state", ctypes.c_void_p),
+                ("episodes_done", ctypes.c_void_p), ("return_sum_p0", ctypes.c_void_p)]
+
+
 _lib = None
 
 
@@ -63,8 +84,9 @@ def build():
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(_LIB_PATH) or (
-                os.path.getmtime(_LIB_PATH) < os.path.getmtime(os.path.join(_HERE, "coup_oracle.c"))):
+        srcs = ["coup_oracle.c", "coup_oracle.h", "coup_nplayer.c", "coup_nplayer.h"]
+        if not os.path.exists(_LIB_PATH) or any(
+                os.path.getmtime(_LIB_PATH) < os.path.getmtime(os.path.join(_HERE, f)) for f in srcs):
             build()
         L = ctypes.CDLL(_LIB_PATH)
         P = ctypes.POINTER(_OcState)
@@ -89,6 +111,17 @@ def lib():
         L.oc_draw.restype = ctypes.c_uint32
         L.oc_philox4x32_10.argtypes = [ctypes.POINTER(ctypes.c_uint32)] * 2 + [ctypes.POINTER(ctypes.c_uint32)]
         L.oc_rollout.argtypes = [ctypes.POINTER(_RolloutArgs)]
+        NP = ctypes.POINTER(_NpState)
+        L.np_init.argtypes = [NP, ctypes.c_int]
+        L.np_is_terminal.argtypes = [NP]
+        L.np_current_player.argtypes = [NP]
+        L.np_legal_mask.argtypes = [NP]
+        L.np_legal_mask.restype = ctypes.c_uint32
+        L.np_apply_action.argtypes = [NP, ctypes.c_int]
+        L.np_returns.argtypes = [NP, ctypes.POINTER(ctypes.c_int)]
+        L.np_observation_tensor.argtypes = [NP, ctypes.c_int, ctypes.POINTER(ctypes.c_float)]
+        L.np_pack.argtypes = [NP, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
+        L.np_rollout.argtypes = [ctypes.POINTER(_NpRolloutArgs)]
         _lib = L
     return _lib
 
@@ -245,4 +278,86 @@ def rollout(seed, n, steps, env_id_base=0, auto_reset=True, want_obs=False,
     a.episodes_done = buf("episodes_done", (1,), np.int64)
     a.return_sum_p0 = buf("return_sum_p0", (1,), np.int64)
     lib().oc_rollout(ctypes.byref(a))
+    return out
+
+
+class NpState:
+    """One game of the N-player extension (coup_nplayer.h)."""
+
+    def __init__(self, n):
+        self.n = n
+        self._s = _NpState()
+        lib().np_init(ctypes.byref(self._s), n)
+
+    def is_terminal(self):
+        return bool(lib().np_is_terminal(ctypes.byref(self._s)))
+
+    def current_player(self):
+        return lib().np_current_player(ctypes.byref(self._s))
+
+    def is_chance_node(self):
+        return self.current_player() == -1
+
+    def legal_mask(self):
+        return lib().np_legal_mask(ctypes.byref(self._s))
+
+    def legal_actions(self):
+        m = self.legal_mask()
+        k = 5 if m & (1 << 31) else 18
+        return [a for a in range(k) if (m >> a) & 1]
+
+    def apply_action(self, a):
+        err = lib().np_apply_action(ctypes.byref(self._s), int(a))
+        if err:
+            raise RuntimeError(f"np_apply_action({a}) failed with code {err}")
+
+    def returns(self):
+        buf = (ctypes.c_int * 6)()
+        lib().np_returns(ctypes.byref(self._s), buf)
+        return list(buf[:self.n])
+
+    def rewards(self):
+        return list(self._s.rewards[:self.n])
+
+    def observation_tensor(self, player):
+        out = np.zeros(49 * self.n, np.float32)
+        lib().np_observation_tensor(ctypes.byref(self._s), player,
+                                    out.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+        return out
+
+    def pack(self, episode=0):
+        out = (ctypes.c_uint32 * 12)()
+        lib().np_pack(ctypes.byref(self._s), episode, out)
+        return list(out)
+
+    def coins(self, p):
+        return self._s.pl[p].coins
+
+    def cards(self, p):
+        pl = self._s.pl[p]
+        return [(pl.cards[i].value, pl.cards[i].state) for i in range(pl.ncards)]
+
+
+def np_rollout(n_players, seed, n, steps, env_id_base=0, auto_reset=True, want_obs=False):
+    """Uniform-random rollout of the N-player extension (step-major arrays)."""
+    out = {}
+    a = _NpRolloutArgs()
+    a.n_players, a.seed, a.env_id_base, a.n, a.steps, a.auto_reset = (
+        n_players, seed, env_id_base, n, steps, int(auto_reset))
+
+    def buf(name, shape, dtype):
+        arr = np.zeros(shape, dtype)
+        out[name] = arr
+        return arr.ctypes.data
+
+    a.actions = buf("actions", (steps, n), np.int8)
+    a.rewards = buf("rewards", (steps, n, n_players), np.int8)
+    a.step_type = buf("step_type", (steps, n), np.uint8)
+    a.legal = buf("legal", (steps, n), np.uint32)
+    if want_obs:
+        a.obs = buf("obs", (steps, n, n_players, 49 * n_players), np.float32)
+    a.final_state = buf("final_state", (n, 12), np.uint32)
+    a.episodes_done = buf("episodes_done", (1,), np.int64)
+    a.return_sum_p0 = buf("return_sum_p0", (1,), np.int64)
+    lib().np_rollout(ctypes.byref(a))
     return out
