@@ -1,6 +1,6 @@
 """Coup env-steps/sec on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c3i|c2|c2r]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c3i|c2|c2r|c4|c4r]
 
 Workload (default c3 = configs[2] of BASELINE.json, the batch-2^20 config the
 metric is quoted on): 2-player Coup, B = 2^20 lanes per GPU, uniform-random
@@ -13,6 +13,9 @@ Other configs (secondary lines, not the headline):
   c3i  as c3 but InformationStateTensor x2 (fp32 [B][2][2492]) instead, B = 2^18
   c2   configs[1]: B = 65,536, no observations, one launch per step
   c2r  configs[1] fused: B = 65,536, `steps` env steps in ONE launch (coup_rollout)
+  c4   configs[3]: 6-player extension, B = 2^20, no observations (parity
+       unpinned w.r.t. the 2-player reference; pinned to oracle/coup_nplayer.c)
+  c4r  c4 fused: `steps` 6-player env steps in ONE launch
 
 A "step" is one batched env step over all B lanes; value = env-steps/s of
 the whole job (N x B x K / max-over-ranks wall time).  Multi-GPU: one
@@ -38,12 +41,15 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
 
-# config -> (default batch, obs, info_state, fused, algorithmic bytes per lane-step, workload name)
+# config -> (default batch, obs, info_state, fused, algorithmic bytes per lane-step, workload name, players)
 CONFIGS = {
-    "c3": (1 << 20, True, False, False, 824, "coup-2p-uniform-b2^20-obs"),
-    "c3i": (1 << 18, False, True, False, 40 + 2 * 2492 * 4 + 96 + 96, "coup-2p-uniform-b2^18-infostate"),
-    "c2": (65536, False, False, False, 40, "coup-2p-uniform-b65536"),
-    "c2r": (65536, False, False, True, 32, "coup-2p-uniform-b65536-fused-rollout"),
+    "c3": (1 << 20, True, False, False, 824, "coup-2p-uniform-b2^20-obs", 2),
+    "c3i": (1 << 18, False, True, False, 40 + 2 * 2492 * 4 + 96 + 96, "coup-2p-uniform-b2^18-infostate", 2),
+    "c2": (65536, False, False, False, 40, "coup-2p-uniform-b65536", 2),
+    "c2r": (65536, False, False, True, 32, "coup-2p-uniform-b65536-fused-rollout", 2),
+    # 2 x 48 B state + mask 4 + action 1 + rewards 6 + 1
+    "c4": (1 << 20, False, False, False, 108, "coup-6p-uniform-b2^20", 6),
+    "c4r": (1 << 20, False, False, True, 96, "coup-6p-uniform-b2^20-fused-rollout", 6),
 }
 
 
@@ -68,9 +74,21 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(target_s, with_obs, with_info):
+def cpu_baseline(target_s, with_obs, with_info, players=2):
     """Bounded sample of the same per-lane workload on the oracle (1 core)."""
     from oracle import oracle
+    if players != 2:
+        n = 1024
+        t0 = time.perf_counter()
+        oracle.np_rollout(players, seed=7, n=n, steps=8)
+        per_step = (time.perf_counter() - t0) / (n * 8)
+        steps = max(8, int(target_s / per_step / n))
+        t0 = time.perf_counter()
+        oracle.np_rollout(players, seed=7, n=n, steps=steps)
+        dt = time.perf_counter() - t0
+        return {"value": n * steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+                "sample": f"{n} lanes x {steps} uniform-random {players}-player steps, {dt:.1f} s, "
+                          "oracle/coup_nplayer.c -O2"}
     n = 4096 if not with_info else 256
     kw = dict(want_obs=with_obs, obs_overwrite=True, want_trajectory=False)
     t0 = time.perf_counter()
@@ -100,10 +118,10 @@ def main():
     dev = D.init("nccl")  # RCCL over xGMI when world > 1
 
     cfg = args.config
-    B0, with_obs, with_info, fused, bytes_per_lane, workload = CONFIGS[cfg]
+    B0, with_obs, with_info, fused, bytes_per_lane, workload, players = CONFIGS[cfg]
     B = args.batch or B0
     env = BatchedCoupEnv(B, seed=args.seed, env_id_base=D.env_id_base(rank, B), auto_reset=True, obs=with_obs,
-                         info_state=with_info, device=dev)
+                         info_state=with_info, device=dev, num_players=players)
 
     def barrier():
         if world > 1:
@@ -148,9 +166,12 @@ def main():
         if os.path.exists(TRAFFIC_FILE):
             with open(TRAFFIC_FILE) as f:
                 tr = json.load(f)
-            if tr.get("config") == cfg and tr.get("batch") == B:
-                traffic = tr.get("hbm_bytes_per_launch")
-        if fused:
+            ent = tr.get(cfg)
+            if ent and ent.get("batch") == B:
+                traffic = ent.get("hbm_bytes_per_launch")
+        if players != 2:
+            kernel = "coup::np::k_rollout<%d>" % players if fused else "coup::np::k_step<%d, true>" % players
+        elif fused:
             kernel = "coup::k_rollout"
         elif with_info:
             kernel = "coup::k_step<true, 0, 256, 2>"
@@ -173,7 +194,7 @@ def main():
             "vs_baseline": None,
             "dtype": "int32",
             "data": "synthetic (uniform-random self-play games)",
-            "config": {"workload": workload, "batch_per_gpu": B, "global_batch": world * B, "players": 2,
+            "config": {"workload": workload, "batch_per_gpu": B, "global_batch": world * B, "players": players,
                        "outputs": outputs, "auto_reset": True, "fused_steps_per_launch": args.steps if fused else 1,
                        "parallelism": f"dp{world} (env-id sharding)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -182,7 +203,7 @@ def main():
             "lane_errors": errors,
         }
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, with_obs, with_info)
+            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, with_obs, with_info, players)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -27,9 +27,10 @@
 extern "C" {
 #endif
 
-#define COUP_ABI_VERSION 2
+#define COUP_ABI_VERSION 3
 
 #define COUP_NUM_PLAYERS 2          /* coup.h:42 */
+#define COUP_MAX_PLAYERS 6          /* N-player extension */
 #define COUP_NUM_ACTIONS 18         /* coup.h:203 NumDistinctActions */
 #define COUP_NUM_CARD_TYPES 5       /* coup.h:44, MaxChanceOutcomes */
 #define COUP_OBS_SIZE 98            /* coup.cc:1118-1130 ObservationTensorShape */
@@ -37,10 +38,12 @@ extern "C" {
 #define COUP_MAX_GAME_LENGTH 90     /* coup.h:219 */
 #define COUP_STATE_BYTES 16         /* packed lane record */
 #define COUP_HISTORY_BYTES 96       /* per-lane history: one byte per history index */
+#define COUP_NP_STATE_BYTES 32      /* N-player engine lane record */
 
 /* coup_create flags */
 #define COUP_FLAG_AUTO_RESET 1      /* SyncVectorEnv(reset_if_done=True) semantics */
 #define COUP_FLAG_HISTORY 2         /* keep per-lane histories (InformationStateTensor, strings) */
+#define COUP_FLAG_GENERIC 4         /* use the N-player engine also at N = 2 (cross-checks) */
 
 /* rl_environment.StepType (rl_environment.py:96-103) */
 #define COUP_STEP_FIRST 0
@@ -63,6 +66,11 @@ extern "C" {
 #define COUP_E_LANES 3      /* one or more lanes rejected an action (see coup_error_count) */
 
 typedef struct coup_env coup_env;
+
+/* Shapes below are for the 2-player game.  An env of N players
+ * (coup_create_ex) has rewards / returns [B][N] and obs [B][N][49N]
+ * (the N-player ObservationTensor); its records are
+ * COUP_NP_STATE_BYTES long and it has no history / info_state. */
 
 /* Outputs of one batched env step; every pointer optional (NULL = skip). */
 typedef struct {
@@ -109,10 +117,18 @@ const char* coup_last_error(void);
  * InformationStateTensor.  The env starts with every lane reset and dealt
  * (rl_environment.reset, rl_environment.py:324-367).  Synchronous. */
 int coup_create(int64_t batch, uint64_t seed, uint32_t env_id_base, int flags, coup_env** out);
+/* coup_create with a player count: 2 is the reference game; 3..6 (and 2
+ * with COUP_FLAG_GENERIC) run the N-player extension, whose rules reduce to
+ * the reference's at N = 2 (the reference game is 2-player only, coup.h:42;
+ * DESIGN.md section 11 has the extension's rules).  Synchronous. */
+int coup_create_ex(int64_t batch, uint64_t seed, uint32_t env_id_base, int flags, int num_players, coup_env** out);
 int coup_destroy(coup_env* env);
 /* Use this HIP stream (hipStream_t, may be NULL = default) for later calls. */
 int coup_set_stream(coup_env* env, void* hip_stream);
 int64_t coup_batch(const coup_env* env);
+/* NumPlayers() (coup.h:205) of the env, and its lane record size in bytes. */
+int coup_num_players(const coup_env* env);
+int coup_state_bytes(const coup_env* env);
 
 /* Reset lanes (all if lane_mask == NULL, else lanes with lane_mask[i] != 0):
  * next episode, fresh CoupState, chance deals resolved (FIRST step). */
@@ -144,7 +160,8 @@ int coup_apply_action(coup_env* env, const int8_t* actions);
 /* Per-lane accessors of the current state. */
 int coup_query(coup_env* env, const coup_query_outputs* out);
 
-/* Copy the packed lane records ([B][4] uint32, device) out of / into the env. */
+/* Copy the packed lane records ([B][coup_state_bytes / 4] uint32, device)
+ * out of / into the env. */
 int coup_export_state(coup_env* env, uint32_t* dst);
 int coup_import_state(coup_env* env, const uint32_t* src);
 /* Copy the per-lane histories ([B][96] bytes, device; COUP_FLAG_HISTORY). */

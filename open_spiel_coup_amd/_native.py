@@ -9,16 +9,17 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libcoup_mi355x.so")
-ABI_VERSION = 2
-FLAG_AUTO_RESET, FLAG_HISTORY = 1, 2
+ABI_VERSION = 3
+FLAG_AUTO_RESET, FLAG_HISTORY, FLAG_GENERIC = 1, 2, 4
+MAX_PLAYERS = 6
 HISTORY_BYTES = 96
 
 COUP_OK, COUP_E_INVALID, COUP_E_HIP, COUP_E_LANES = 0, 1, 2, 3
 
 # Every symbol declared in include/coup_mi355x.h
 SYMBOLS = (
-    "coup_abi_version", "coup_last_error", "coup_create", "coup_destroy",
-    "coup_set_stream", "coup_batch", "coup_reset", "coup_step", "coup_rollout",
+    "coup_abi_version", "coup_last_error", "coup_create", "coup_create_ex", "coup_destroy",
+    "coup_set_stream", "coup_batch", "coup_num_players", "coup_state_bytes", "coup_reset", "coup_step", "coup_rollout",
     "coup_new_initial_state", "coup_apply_action", "coup_query",
     "coup_export_state", "coup_import_state", "coup_export_history",
     "coup_import_history", "coup_error_count",
@@ -66,9 +67,12 @@ def load():
         "coup_abi_version": ([], i32),
         "coup_last_error": ([], ctypes.c_char_p),
         "coup_create": ([i64, ctypes.c_uint64, ctypes.c_uint32, i32, ctypes.POINTER(vp)], i32),
+        "coup_create_ex": ([i64, ctypes.c_uint64, ctypes.c_uint32, i32, i32, ctypes.POINTER(vp)], i32),
         "coup_destroy": ([vp], i32),
         "coup_set_stream": ([vp, vp], i32),
         "coup_batch": ([vp], i64),
+        "coup_num_players": ([vp], i32),
+        "coup_state_bytes": ([vp], i32),
         "coup_reset": ([vp, vp], i32),
         "coup_step": ([vp, vp, ctypes.POINTER(StepOutputs)], i32),
         "coup_rollout": ([vp, i64, ctypes.POINTER(RolloutStats)], i32),

@@ -15,6 +15,7 @@
 
 #include "coup_lane.h"
 #include "coup_mi355x.h"
+#include "coup_np.h"
 
 namespace coup {
 
@@ -777,7 +778,9 @@ struct coup_env {
   uint64_t seed;
   uint32_t env_id_base;
   int flags;
-  uint4* state;
+  int players;
+  bool generic;   // N-player engine (coup_nplayer.hip): num_players != 2 or COUP_FLAG_GENERIC
+  uint4* state;   // [B] records, or the N-player engine's two [B] planes back to back
   uint8_t* hist;  // [B][96] when COUP_FLAG_HISTORY
   uint32_t* err_count;
   hipStream_t stream;
@@ -825,8 +828,29 @@ unsigned step_grid(int64_t groups, int T) {
 
 unsigned grid_for(int64_t n) { return (unsigned)((n + coup::kThreads - 1) / coup::kThreads); }
 
+coup::np::Env np_env(const coup_env* env) {
+  coup::np::Env e;
+  e.sa = env->state;
+  e.sb = env->state + env->batch;
+  e.n = env->batch;
+  e.players = env->players;
+  e.seed_lo = (uint32_t)env->seed;
+  e.seed_hi = (uint32_t)(env->seed >> 32);
+  e.env_id_base = env->env_id_base;
+  e.auto_reset = (env->flags & COUP_FLAG_AUTO_RESET) ? 1 : 0;
+  e.err_count = env->err_count;
+  e.stream = env->stream;
+  return e;
+}
+
+int np_result(hipError_t e, const char* what) {
+  if (e != hipSuccess) return fail(COUP_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+  return COUP_OK;
+}
+
 int launch_reset(coup_env* env, const uint8_t* mask, int mode, int deal) {
   if (env->batch == 0) return COUP_OK;
+  if (env->generic) return np_result(coup::np::launch_reset(np_env(env), mask, mode, deal), "reset");
   coup::k_reset<<<grid_for(env->batch), coup::kThreads, 0, env->stream>>>(
       env->state, env->batch, mask, mode, deal, (uint32_t)env->seed, (uint32_t)(env->seed >> 32), env->env_id_base,
       env->hist);
@@ -850,21 +874,33 @@ int coup_abi_version(void) { return COUP_ABI_VERSION; }
 const char* coup_last_error(void) { return g_last_error.c_str(); }
 
 int coup_create(int64_t batch, uint64_t seed, uint32_t env_id_base, int flags, coup_env** out) {
+  return coup_create_ex(batch, seed, env_id_base, flags, COUP_NUM_PLAYERS, out);
+}
+
+int coup_create_ex(int64_t batch, uint64_t seed, uint32_t env_id_base, int flags, int num_players, coup_env** out) {
   if (!out) return fail(COUP_E_INVALID, "coup_create: out is null");
   *out = nullptr;
   if (batch < 0 || batch > (int64_t(1) << 32)) return fail(COUP_E_INVALID, "coup_create: batch out of range");
-  if (flags & ~(COUP_FLAG_AUTO_RESET | COUP_FLAG_HISTORY)) return fail(COUP_E_INVALID, "coup_create: unknown flags");
+  if (flags & ~(COUP_FLAG_AUTO_RESET | COUP_FLAG_HISTORY | COUP_FLAG_GENERIC))
+    return fail(COUP_E_INVALID, "coup_create: unknown flags");
+  if (num_players < 2 || num_players > COUP_MAX_PLAYERS)
+    return fail(COUP_E_INVALID, "coup_create: num_players must be 2..6");
+  const bool generic = num_players != 2 || (flags & COUP_FLAG_GENERIC);
+  if (generic && (flags & COUP_FLAG_HISTORY))
+    return fail(COUP_E_INVALID, "coup_create: COUP_FLAG_HISTORY is 2-player only (no N-player InformationStateTensor)");
   coup_env* env = new coup_env();
   env->batch = batch;
   env->seed = seed;
   env->env_id_base = env_id_base;
   env->flags = flags;
+  env->players = num_players;
+  env->generic = generic;
   env->stream = nullptr;
   env->state = nullptr;
   env->hist = nullptr;
   env->err_count = nullptr;
   const size_t lanes = (size_t)(batch > 0 ? batch : 1);
-  hipError_t e = hipMalloc(&env->state, lanes * sizeof(uint4));
+  hipError_t e = hipMalloc(&env->state, lanes * sizeof(uint4) * (generic ? 2 : 1));
   if (e == hipSuccess) e = hipMalloc(&env->err_count, sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemset(env->err_count, 0, sizeof(uint32_t));
   if (e == hipSuccess && (flags & COUP_FLAG_HISTORY)) {
@@ -904,6 +940,10 @@ int coup_set_stream(coup_env* env, void* hip_stream) {
 
 int64_t coup_batch(const coup_env* env) { return env ? env->batch : -1; }
 
+int coup_num_players(const coup_env* env) { return env ? env->players : -1; }
+
+int coup_state_bytes(const coup_env* env) { return env ? (env->generic ? 32 : COUP_STATE_BYTES) : -1; }
+
 int coup_reset(coup_env* env, const uint8_t* lane_mask) {
   COUP_CHECK_ENV(env);
   return launch_reset(env, lane_mask, /*mode=*/1, /*deal=*/1);
@@ -917,6 +957,10 @@ int coup_new_initial_state(coup_env* env, const uint8_t* lane_mask) {
 int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out) {
   COUP_CHECK_ENV(env);
   if (env->batch == 0) return COUP_OK;
+  if (env->generic) {
+    if (out && out->info_state) return fail(COUP_E_INVALID, "coup_step: info_state is 2-player only");
+    return np_result(coup::np::launch_step(np_env(env), actions, out), "coup_step");
+  }
   coup::StepArgs a;
   std::memset(&a, 0, sizeof(a));
   a.state = env->state;
@@ -982,6 +1026,7 @@ int coup_rollout(coup_env* env, int64_t steps, const coup_rollout_stats* stats) 
   if (steps < 0) return fail(COUP_E_INVALID, "coup_rollout: negative steps");
   if (env->hist) return fail(COUP_E_INVALID, "coup_rollout: not available on an env with COUP_FLAG_HISTORY");
   if (env->batch == 0 || steps == 0) return COUP_OK;
+  if (env->generic) return np_result(coup::np::launch_rollout(np_env(env), steps, stats), "coup_rollout");
   coup::RolloutArgs a;
   std::memset(&a, 0, sizeof(a));
   a.state = env->state;
@@ -1005,6 +1050,7 @@ int coup_apply_action(coup_env* env, const int8_t* actions) {
   COUP_CHECK_ENV(env);
   if (!actions) return fail(COUP_E_INVALID, "coup_apply_action: actions is null");
   if (env->batch == 0) return COUP_OK;
+  if (env->generic) return np_result(coup::np::launch_apply(np_env(env), actions), "coup_apply_action");
   coup::k_apply<<<grid_for(env->batch), coup::kThreads, 0, env->stream>>>(env->state, env->batch, actions,
                                                                           env->hist, env->err_count);
   COUP_HIP_TRY(hipGetLastError());
@@ -1017,6 +1063,7 @@ int coup_query(coup_env* env, const coup_query_outputs* out) {
   if (out->info_state && !env->hist)
     return fail(COUP_E_INVALID, "coup_query: info_state needs an env created with COUP_FLAG_HISTORY");
   if (env->batch == 0) return COUP_OK;
+  if (env->generic) return np_result(coup::np::launch_query(np_env(env), out), "coup_query");
   coup::QueryArgs a;
   a.state = env->state;
   a.n = env->batch;
@@ -1045,6 +1092,7 @@ int coup_query(coup_env* env, const coup_query_outputs* out) {
 int coup_export_state(coup_env* env, uint32_t* dst) {
   COUP_CHECK_ENV(env);
   if (!dst) return fail(COUP_E_INVALID, "coup_export_state: dst is null");
+  if (env->generic) return np_result(coup::np::launch_export(np_env(env), dst), "coup_export_state");
   COUP_HIP_TRY(hipMemcpyAsync(dst, env->state, (size_t)env->batch * sizeof(uint4), hipMemcpyDeviceToDevice,
                               env->stream));
   return COUP_OK;
@@ -1053,6 +1101,7 @@ int coup_export_state(coup_env* env, uint32_t* dst) {
 int coup_import_state(coup_env* env, const uint32_t* src) {
   COUP_CHECK_ENV(env);
   if (!src) return fail(COUP_E_INVALID, "coup_import_state: src is null");
+  if (env->generic) return np_result(coup::np::launch_import(np_env(env), src), "coup_import_state");
   COUP_HIP_TRY(hipMemcpyAsync(env->state, src, (size_t)env->batch * sizeof(uint4), hipMemcpyDeviceToDevice,
                               env->stream));
   return COUP_OK;

@@ -1,0 +1,377 @@
+// coup_nplayer.hip -- gfx950 kernels of the N-player extension (N = 2..6).
+//
+// Same execution model as coup_kernels.hip: one thread per lane, the
+// 32-byte record loaded as two fully coalesced uint4 planes, the rules run
+// in registers (coup_nlane.h), the record stored back.  The
+// ObservationTensor is produced by a separate expansion kernel (k_obs):
+// with N players a lane's tensor is N x 49N floats (7 KiB at N = 6), so it
+// is written by all threads of a block as one contiguous stream of
+// non-temporal float4 stores decoded from the block's records in LDS.
+#include <hip/hip_runtime.h>
+
+#include "coup_nlane.h"
+#include "coup_np.h"
+
+namespace coup {
+namespace np {
+
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ void count_error(uint32_t* err_count) { atomicAdd(err_count, 1u); }
+
+struct StepArgs {
+  uint4* sa;
+  uint4* sb;
+  int64_t n;
+  uint32_t seed_lo, seed_hi, env_id_base;
+  int auto_reset;
+  const int8_t* actions_in;
+  int8_t* actions;
+  int8_t* rewards;  // [B][N]
+  uint8_t* step_type;
+  uint32_t* legal;
+  int8_t* cur_player;
+  uint32_t* err_count;
+};
+
+// One rl_environment step per lane (step_lane, coup_nlane.h).
+template <int N, bool UNIFORM>
+__global__ __launch_bounds__(kThreads) void k_step(StepArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= a.n) return;
+  NLane<N> L = unpack<N>(a.sa[i], a.sb[i]);
+  NRng rng{a.seed_lo, a.seed_hi, a.env_id_base + (uint32_t)i, 0u, make_uint4(0, 0, 0, 0)};
+  int act;
+  uint32_t st, rl, rc;
+  bool error;
+  step_lane<N, UNIFORM>(L, rng, UNIFORM ? 0u : (uint32_t)(uint8_t)a.actions_in[i], a.auto_reset != 0, act, st, rl,
+                        rc, error);
+  if (error) count_error(a.err_count);
+  uint4 wa, wb;
+  pack(L, wa, wb);
+  a.sa[i] = wa;
+  a.sb[i] = wb;
+  if (a.actions) a.actions[i] = (int8_t)act;
+  if (a.rewards) {
+#pragma unroll
+    for (int p = 0; p < N; ++p)
+      a.rewards[i * N + p] = (int8_t)((uint32_t)p == rl ? -(int32_t)((N - 1) * rc) : (int32_t)rc);
+  }
+  if (a.step_type) a.step_type[i] = (uint8_t)st;
+  if (a.legal) a.legal[i] = legal_mask(L);
+  if (a.cur_player) a.cur_player[i] = (int8_t)current_player(L);
+}
+
+struct RolloutArgs {
+  uint4* sa;
+  uint4* sb;
+  int64_t n;
+  uint32_t seed_lo, seed_hi, env_id_base;
+  int64_t steps;
+  int32_t* episodes;
+  int32_t* return_sum;
+  int32_t* length_sum;
+  uint32_t* err_count;
+};
+
+// `steps` uniform-random env steps per lane with auto-reset in one launch.
+template <int N>
+__global__ __launch_bounds__(kThreads) void k_rollout(RolloutArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= a.n) return;
+  NLane<N> L = unpack<N>(a.sa[i], a.sb[i]);
+  NRng rng{a.seed_lo, a.seed_hi, a.env_id_base + (uint32_t)i, 0u, make_uint4(0, 0, 0, 0)};
+  int32_t eps = 0, ret = 0, len = 0, cur = 0;
+  uint32_t errs = 0;
+  for (int64_t s = 0; s < a.steps; ++s) {
+    if (is_terminal(L)) L = initial_lane<N>(L.episode + 1u);
+    resolve_chance(L, rng);
+    const uint32_t m = decision_mask(L);
+    if (m == 0u) {
+      errs += 1u;
+      break;
+    }
+    const uint32_t err_before = L.err;
+    apply_decision(L, sample_action(m, rng.draw(L.episode, L.move)));
+    L.move += 1u;
+    resolve_chance(L, rng);
+    errs += (L.err && !err_before) ? 1u : 0u;
+    cur += 1;
+    if (is_terminal(L)) {
+      eps += 1;
+      ret += returns(L, 0u);
+      len += cur;
+      cur = 0;
+      L = initial_lane<N>(L.episode + 1u);
+      resolve_chance(L, rng);
+    }
+  }
+  uint4 wa, wb;
+  pack(L, wa, wb);
+  a.sa[i] = wa;
+  a.sb[i] = wb;
+  if (a.episodes) a.episodes[i] += eps;
+  if (a.return_sum) a.return_sum[i] += ret;
+  if (a.length_sum) a.length_sum[i] += len;
+  if (errs) atomicAdd(a.err_count, errs);
+}
+
+template <int N>
+__global__ __launch_bounds__(kThreads) void k_reset(uint4* sa, uint4* sb, int64_t n, const uint8_t* mask, int mode,
+                                                  int deal, uint32_t seed_lo, uint32_t seed_hi,
+                                                  uint32_t env_id_base) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  if (mask && mask[i] == 0) return;
+  const uint32_t ep = mode == 0 ? 0u : (sb[i].w & kEpisodeMask) + 1u;
+  NLane<N> L = initial_lane<N>(ep);
+  if (deal) {
+    NRng rng{seed_lo, seed_hi, env_id_base + (uint32_t)i, 0u, make_uint4(0, 0, 0, 0)};
+    resolve_chance(L, rng);
+  }
+  uint4 wa, wb;
+  pack(L, wa, wb);
+  sa[i] = wa;
+  sb[i] = wb;
+}
+
+template <int N>
+__global__ __launch_bounds__(kThreads) void k_apply(uint4* sa, uint4* sb, int64_t n, const int8_t* actions,
+                                                  uint32_t* err_count) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  const int x = actions[i];
+  if (x < 0) return;
+  NLane<N> L = unpack<N>(sa[i], sb[i]);
+  const uint32_t err_before = L.err;
+  if (!apply_action(L, (uint32_t)x)) {
+    count_error(err_count);
+    return;
+  }
+  if (L.err && !err_before) count_error(err_count);
+  uint4 wa, wb;
+  pack(L, wa, wb);
+  sa[i] = wa;
+  sb[i] = wb;
+}
+
+struct QueryArgs {
+  const uint4* sa;
+  const uint4* sb;
+  int64_t n;
+  uint32_t* legal;
+  int8_t* cur_player;
+  uint8_t* terminal;
+  int8_t* rewards;  // [B][N]
+  int8_t* returns;  // [B][N]
+};
+
+template <int N>
+__global__ __launch_bounds__(kThreads) void k_query(QueryArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= a.n) return;
+  const NLane<N> L = unpack<N>(a.sa[i], a.sb[i]);
+  if (a.legal) a.legal[i] = legal_mask(L);
+  if (a.cur_player) a.cur_player[i] = (int8_t)current_player(L);
+  if (a.terminal) a.terminal[i] = is_terminal(L) ? 1 : 0;
+#pragma unroll
+  for (int p = 0; p < N; ++p) {
+    if (a.rewards) a.rewards[i * N + p] = (int8_t)reward(L, (uint32_t)p);
+    if (a.returns) a.returns[i * N + p] = (int8_t)returns(L, (uint32_t)p);
+  }
+}
+
+// ------------------------------------------------------ observation tensor
+//
+// CoupObserver::WriteTensor (coup.cc:248-287) with num_players_ = N; one
+// observer row is
+//   [observer N | cards 20N | cur_move N | cards_state 8N | coins N | last_action 18N]
+// and a lane's N rows are contiguous.  A block expands kObsLanes lanes: the
+// records go to LDS (hands, coins, last actions, mover or 7 when terminal),
+// then the block's kObsLanes x N x 49N floats are stored as one stream of
+// float4 (the span starts 16-byte aligned since kObsLanes x N x 49N x 4 is a
+// multiple of 16).
+constexpr int kObsLanes = 32;
+
+template <int N>
+__global__ __launch_bounds__(kThreads) void k_obs(const uint4* sa, const uint4* sb, int64_t n, float* obs) {
+  constexpr uint32_t kRow = 49u * N, kLane = N * kRow;
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  __shared__ uint32_t rec[kObsLanes][8];
+  const int64_t lane0 = (int64_t)blockIdx.x * kObsLanes;
+  const int64_t left = n - lane0;
+  const uint32_t nv = left >= kObsLanes ? (uint32_t)kObsLanes : (uint32_t)left;
+  if (threadIdx.x < nv) {
+    const uint4 wa = sa[lane0 + threadIdx.x], wb = sb[lane0 + threadIdx.x];
+    const NLane<N> L = unpack<N>(wa, wb);
+    obs_record(L, rec[threadIdx.x]);
+  }
+  __syncthreads();
+  float* base = obs + lane0 * kLane;
+  const uint32_t total = nv * kLane, nf4 = total / 4u;
+  for (uint32_t j = threadIdx.x; j < nf4; j += kThreads) {
+    const uint32_t e = 4u * j;
+    uint32_t lane = e / kLane, rem = e - lane * kLane;
+    uint32_t o = rem / kRow, pos = rem - o * kRow;
+    float v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[k] = obs_elem<N>(rec[lane], o, pos);
+      if (++pos == kRow) {
+        pos = 0;
+        if (++o == (uint32_t)N) {
+          o = 0;
+          ++lane;
+        }
+      }
+    }
+    v4f w = {v[0], v[1], v[2], v[3]};
+    __builtin_nontemporal_store(w, reinterpret_cast<v4f*>(base) + j);
+  }
+  if (threadIdx.x == 0) {
+    for (uint32_t e = 4u * nf4; e < total; ++e) {
+      const uint32_t lane = e / kLane, rem = e - lane * kLane, o = rem / kRow;
+      base[e] = obs_elem<N>(rec[lane], o, rem - o * kRow);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void k_export(const uint4* sa, const uint4* sb, int64_t n, uint4* dst) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  dst[2 * i] = sa[i];
+  dst[2 * i + 1] = sb[i];
+}
+
+__global__ __launch_bounds__(kThreads) void k_import(uint4* sa, uint4* sb, int64_t n, const uint4* src) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  sa[i] = src[2 * i];
+  sb[i] = src[2 * i + 1];
+}
+
+// ------------------------------------------------------------ launchers
+
+namespace {
+
+unsigned grid_for(int64_t n, int per_block) { return (unsigned)((n + per_block - 1) / per_block); }
+
+// calls f(std::integral_constant<int, N>) for the env's player count
+template <class F>
+hipError_t dispatch(int players, F&& f) {
+  switch (players) {
+    case 2: f(std::integral_constant<int, 2>()); break;
+    case 3: f(std::integral_constant<int, 3>()); break;
+    case 4: f(std::integral_constant<int, 4>()); break;
+    case 5: f(std::integral_constant<int, 5>()); break;
+    case 6: f(std::integral_constant<int, 6>()); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_reset(const Env& e, const uint8_t* mask, int mode, int deal) {
+  if (e.n == 0) return hipSuccess;
+  return dispatch(e.players, [&](auto np) {
+    constexpr int N = decltype(np)::value;
+    k_reset<N><<<grid_for(e.n, kThreads), kThreads, 0, e.stream>>>(e.sa, e.sb, e.n, mask, mode, deal, e.seed_lo,
+                                                                    e.seed_hi, e.env_id_base);
+  });
+}
+
+hipError_t launch_step(const Env& e, const int8_t* actions, const coup_step_outputs* out) {
+  if (e.n == 0) return hipSuccess;
+  StepArgs a{};
+  a.sa = e.sa;
+  a.sb = e.sb;
+  a.n = e.n;
+  a.seed_lo = e.seed_lo;
+  a.seed_hi = e.seed_hi;
+  a.env_id_base = e.env_id_base;
+  a.auto_reset = e.auto_reset;
+  a.actions_in = actions;
+  a.err_count = e.err_count;
+  float* obs = nullptr;
+  if (out) {
+    a.actions = out->actions;
+    a.rewards = out->rewards;
+    a.step_type = out->step_type;
+    a.legal = out->legal_mask;
+    a.cur_player = out->cur_player;
+    obs = out->obs;
+  }
+  return dispatch(e.players, [&](auto np) {
+    constexpr int N = decltype(np)::value;
+    if (actions)
+      k_step<N, false><<<grid_for(e.n, kThreads), kThreads, 0, e.stream>>>(a);
+    else
+      k_step<N, true><<<grid_for(e.n, kThreads), kThreads, 0, e.stream>>>(a);
+    if (obs) k_obs<N><<<grid_for(e.n, kObsLanes), kThreads, 0, e.stream>>>(e.sa, e.sb, e.n, obs);
+  });
+}
+
+hipError_t launch_rollout(const Env& e, int64_t steps, const coup_rollout_stats* stats) {
+  if (e.n == 0 || steps == 0) return hipSuccess;
+  RolloutArgs a{};
+  a.sa = e.sa;
+  a.sb = e.sb;
+  a.n = e.n;
+  a.seed_lo = e.seed_lo;
+  a.seed_hi = e.seed_hi;
+  a.env_id_base = e.env_id_base;
+  a.steps = steps;
+  a.err_count = e.err_count;
+  if (stats) {
+    a.episodes = stats->episodes;
+    a.return_sum = stats->return_sum;
+    a.length_sum = stats->length_sum;
+  }
+  return dispatch(e.players, [&](auto np) {
+    constexpr int N = decltype(np)::value;
+    k_rollout<N><<<grid_for(e.n, kThreads), kThreads, 0, e.stream>>>(a);
+  });
+}
+
+hipError_t launch_apply(const Env& e, const int8_t* actions) {
+  if (e.n == 0) return hipSuccess;
+  return dispatch(e.players, [&](auto np) {
+    constexpr int N = decltype(np)::value;
+    k_apply<N><<<grid_for(e.n, kThreads), kThreads, 0, e.stream>>>(e.sa, e.sb, e.n, actions, e.err_count);
+  });
+}
+
+hipError_t launch_query(const Env& e, const coup_query_outputs* out) {
+  if (e.n == 0) return hipSuccess;
+  QueryArgs a{};
+  a.sa = e.sa;
+  a.sb = e.sb;
+  a.n = e.n;
+  a.legal = out->legal_mask;
+  a.cur_player = out->cur_player;
+  a.terminal = out->terminal;
+  a.rewards = out->rewards;
+  a.returns = out->returns;
+  return dispatch(e.players, [&](auto np) {
+    constexpr int N = decltype(np)::value;
+    k_query<N><<<grid_for(e.n, kThreads), kThreads, 0, e.stream>>>(a);
+    if (out->obs) k_obs<N><<<grid_for(e.n, kObsLanes), kThreads, 0, e.stream>>>(e.sa, e.sb, e.n, out->obs);
+  });
+}
+
+hipError_t launch_export(const Env& e, uint32_t* dst) {
+  if (e.n == 0) return hipSuccess;
+  k_export<<<grid_for(e.n, kThreads), kThreads, 0, e.stream>>>(e.sa, e.sb, e.n, reinterpret_cast<uint4*>(dst));
+  return hipGetLastError();
+}
+
+hipError_t launch_import(const Env& e, const uint32_t* src) {
+  if (e.n == 0) return hipSuccess;
+  k_import<<<grid_for(e.n, kThreads), kThreads, 0, e.stream>>>(e.sa, e.sb, e.n,
+                                                                reinterpret_cast<const uint4*>(src));
+  return hipGetLastError();
+}
+
+}  // namespace np
+}  // namespace coup

@@ -28,8 +28,15 @@ def _addr(t):
     return t.data_ptr() if t is not None else None
 
 
+def obs_size(num_players):
+    """ObservationTensor size per player: 98 for the 2-player game
+    (coup.cc:1118-1130), 49 N for the N-player extension."""
+    return 49 * num_players
+
+
 class BatchedCoupEnv:
-    """B independent 2-player Coup games stepped together.
+    """B independent Coup games stepped together (2 players: the reference
+    game; 3..6: the N-player extension).
 
     Args:
       batch: number of lanes B.
@@ -43,10 +50,13 @@ class BatchedCoupEnv:
         (implies history).
       history: keep per-lane histories (InformationStateTensor, strings).
       device: CUDA (HIP) device.
+      num_players: 2 (the reference game) .. 6.  N > 2 has no history /
+        info_state; rewards / returns are [B, N], obs [B, N, 49 N].
+      generic: run the N-player engine also at N = 2 (cross-checks).
     """
 
     def __init__(self, batch, seed=0, env_id_base=0, auto_reset=True, obs=True, info_state=False,
-                 history=False, device=None):
+                 history=False, device=None, num_players=2, generic=False):
         self.lib = _native.load()
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
@@ -56,17 +66,22 @@ class BatchedCoupEnv:
         self.env_id_base = int(env_id_base)
         self.auto_reset = bool(auto_reset)
         self.history = bool(history or info_state)
-        flags = (_native.FLAG_AUTO_RESET if self.auto_reset else 0) | (_native.FLAG_HISTORY if self.history else 0)
+        self.num_players = int(num_players)
+        self.obs_size = obs_size(self.num_players)
+        flags = ((_native.FLAG_AUTO_RESET if self.auto_reset else 0) | (_native.FLAG_HISTORY if self.history else 0)
+                 | (_native.FLAG_GENERIC if generic else 0))
         self._h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
-            _native.check(self.lib.coup_create(self.batch, self.seed, self.env_id_base, flags, ctypes.byref(self._h)))
-        B, dev = self.batch, self.device
+            _native.check(self.lib.coup_create_ex(self.batch, self.seed, self.env_id_base, flags, self.num_players,
+                                                  ctypes.byref(self._h)))
+        self.state_words = self.lib.coup_state_bytes(self._h) // 4
+        B, dev, P = self.batch, self.device, self.num_players
         self.actions = torch.empty(B, dtype=torch.int8, device=dev)
-        self.rewards = torch.zeros(B, 2, dtype=torch.int8, device=dev)
+        self.rewards = torch.zeros(B, P, dtype=torch.int8, device=dev)
         self.step_type = torch.zeros(B, dtype=torch.uint8, device=dev)
         self.legal_mask = torch.zeros(B, dtype=torch.int32, device=dev)
         self.cur_player = torch.zeros(B, dtype=torch.int8, device=dev)
-        self.obs = torch.zeros(B, 2, OBS_SIZE, dtype=torch.float32, device=dev) if obs else None
+        self.obs = torch.zeros(B, P, self.obs_size, dtype=torch.float32, device=dev) if obs else None
         self.info_state = (torch.zeros(B, 2, INFO_STATE_SIZE, dtype=torch.float32, device=dev)
                            if info_state else None)
         self._out = _native.StepOutputs(
@@ -158,14 +173,14 @@ class BatchedCoupEnv:
 
     def query(self, obs=True, info_state=False):
         self._bind_stream()
-        B, dev = self.batch, self.device
+        B, dev, P = self.batch, self.device, self.num_players
         q = {"legal_mask": torch.empty(B, dtype=torch.int32, device=dev),
              "current_player": torch.empty(B, dtype=torch.int8, device=dev),
              "terminal": torch.empty(B, dtype=torch.uint8, device=dev),
-             "rewards": torch.empty(B, 2, dtype=torch.int8, device=dev),
-             "returns": torch.empty(B, 2, dtype=torch.int8, device=dev)}
+             "rewards": torch.empty(B, P, dtype=torch.int8, device=dev),
+             "returns": torch.empty(B, P, dtype=torch.int8, device=dev)}
         if obs:
-            q["obs"] = torch.empty(B, 2, OBS_SIZE, dtype=torch.float32, device=dev)
+            q["obs"] = torch.empty(B, P, self.obs_size, dtype=torch.float32, device=dev)
         if info_state:
             q["info_state"] = torch.empty(B, 2, INFO_STATE_SIZE, dtype=torch.float32, device=dev)
         qo = _native.QueryOutputs(*[_addr(q.get(k)) for k in
@@ -176,15 +191,15 @@ class BatchedCoupEnv:
 
     def export_state(self):
         self._bind_stream()
-        out = torch.empty(self.batch, 4, dtype=torch.int32, device=self.device)
+        out = torch.empty(self.batch, self.state_words, dtype=torch.int32, device=self.device)
         _native.check(self.lib.coup_export_state(self._h, _ptr(out)))
         return out
 
     def import_state(self, packed):
         self._bind_stream()
         packed = packed.to(device=self.device, dtype=torch.int32).contiguous()
-        if packed.shape != (self.batch, 4):
-            raise ValueError("packed state must be [B, 4] int32")
+        if packed.shape != (self.batch, self.state_words):
+            raise ValueError(f"packed state must be [B, {self.state_words}] int32")
         self._keep_state = packed
         _native.check(self.lib.coup_import_state(self._h, _ptr(packed)))
 

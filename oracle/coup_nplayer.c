@@ -427,6 +427,8 @@ int np_apply_action(np_state* s, int a) {
     sort_hand(p);
   } else {
     do_decision(s, a);
+    for (int i = 1; i < s->qlen; ++i)
+      if (s->queue[i] != s->queue[0]) s->error = 4; /* the packed queue is (player, length) */
   }
   s->move++;
   return s->error;
@@ -469,7 +471,10 @@ void np_observation_tensor(const np_state* s, int player, float* out) {
 }
 
 void np_pack(const np_state* s, uint32_t episode, uint32_t* w) {
-  memset(w, 0, 12 * sizeof(uint32_t));
+  /* 32-byte record: a step has at most one card
+   * loser, so Rewards() is (loser, count); deals pending after the initial
+   * ones all go to one player, so the queue is (player, length) */
+  memset(w, 0, 8 * sizeof(uint32_t));
   uint32_t hands[6];
   for (int p = 0; p < 6; ++p) {
     hands[p] = 0xFFFFu;
@@ -482,27 +487,28 @@ void np_pack(const np_state* s, uint32_t episode, uint32_t* w) {
   w[0] = hands[0] | (hands[1] << 16);
   w[1] = hands[2] | (hands[3] << 16);
   w[2] = hands[4] | (hands[5] << 16);
-  uint32_t deck = 0;
-  for (int t = 0; t < 5; ++t) deck |= (uint32_t)s->deck[t] << (4 * t);
-  w[3] = deck | ((uint32_t)s->init_left << 20) | ((uint32_t)s->qlen << 24) | ((uint32_t)s->begin << 27) |
-         ((uint32_t)(s->error ? 1 : 0) << 28) | ((uint32_t)s->T << 29);
-  uint32_t coins = 0, last = 0, lost = 0, rew = 0, q = 0;
-  for (int p = 0; p < s->n; ++p) {
+  uint32_t coins = 0, last = 0, lost = 0, rloser = 0, rcount = 0, deck = 0;
+  for (int p = 0; p < 6; ++p) {
+    if (p >= s->n) {
+      last |= 31u << (5 * p);
+      continue;
+    }
     coins |= (uint32_t)s->pl[p].coins << (4 * p);
     last |= (uint32_t)(s->pl[p].last_action == OC_NONE ? 31 : s->pl[p].last_action) << (5 * p);
     lost |= (uint32_t)s->pl[p].lost_challenge << p;
-    rew |= (uint32_t)(s->rewards[p] + 16) << (5 * p);
+    if (s->rewards[p] < 0) {
+      rloser = (uint32_t)p;
+      rcount = (uint32_t)(-s->rewards[p] / (s->n - 1));
+    }
   }
-  for (int p = s->n; p < 6; ++p) {
-    last |= 31u << (5 * p);
-    rew |= 16u << (5 * p);
-  }
-  for (int i = 0; i < s->qlen; ++i) q |= (uint32_t)s->queue[i] << (3 * i);
-  w[4] = coins | ((uint32_t)s->M << 24) | ((uint32_t)s->O << 27);
-  w[5] = last;
-  w[6] = q | ((uint32_t)s->move << 12) | ((uint32_t)s->turn << 21);
-  w[7] = rew;
-  w[8] = (episode & 0x1FFFFFFu) | (lost << 25);
+  for (int t = 0; t < 5; ++t) deck |= (uint32_t)s->deck[t] << (4 * t);
+  const uint32_t qp = s->qlen ? (uint32_t)s->queue[0] : 0u;
+  w[3] = coins | (lost << 24) | ((uint32_t)s->begin << 30) | ((uint32_t)(s->error ? 1 : 0) << 31);
+  w[4] = last | (rcount << 30);
+  w[5] = deck | ((uint32_t)s->init_left << 20) | ((uint32_t)s->qlen << 24) | (qp << 26) | ((uint32_t)s->T << 29);
+  w[6] = (uint32_t)s->move | ((uint32_t)s->turn << 9) | ((uint32_t)s->M << 18) | ((uint32_t)s->O << 21) |
+         (rloser << 24);
+  w[7] = episode & 0x1FFFFFFu;
 }
 
 /* ------------------------------------------------------------- rollouts */
@@ -578,7 +584,7 @@ int np_rollout(const np_rollout_args* a) {
       if (a->obs)
         for (int p = 0; p < P; ++p) np_observation_tensor(&s, p, a->obs + (o * P + p) * 49 * P);
     }
-    if (a->final_state) np_pack(&s, ep, a->final_state + 12 * lane);
+    if (a->final_state) np_pack(&s, ep, a->final_state + 8 * lane);
   }
   if (a->episodes_done) *a->episodes_done = done;
   if (a->return_sum_p0) *a->return_sum_p0 = ret_sum;

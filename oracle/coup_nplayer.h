@@ -64,8 +64,8 @@ int np_apply_action(np_state* s, int a);    /* 0 ok, else error code */
 void np_returns(const np_state* s, int* out);
 int np_obs_size(int n);                     /* 49 n */
 void np_observation_tensor(const np_state* s, int player, float* out);
-/* 48-byte record (12 x u32), layout in DESIGN.md section 11 */
-void np_pack(const np_state* s, uint32_t episode, uint32_t* out12);
+/* 32-byte record (8 x u32), layout in DESIGN.md section 11 */
+void np_pack(const np_state* s, uint32_t episode, uint32_t* out8);
 
 /* uniform-random rollout under the sampling contract (coup_oracle.h) */
 typedef struct {
@@ -79,7 +79,7 @@ typedef struct {
   uint8_t* step_type;  /* [steps][n] */
   uint32_t* legal;     /* [steps][n] */
   float* obs;          /* [steps][n][P][49P] or NULL */
-  uint32_t* final_state; /* [n][12] */
+  uint32_t* final_state; /* [n][8] */
   int64_t* episodes_done;
   int64_t* return_sum_p0;
 } np_rollout_args;

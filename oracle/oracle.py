@@ -326,7 +326,7 @@ class NpState:
         return out
 
     def pack(self, episode=0):
-        out = (ctypes.c_uint32 * 12)()
+        out = (ctypes.c_uint32 * 8)()
         lib().np_pack(ctypes.byref(self._s), episode, out)
         return list(out)
 
@@ -356,7 +356,7 @@ def np_rollout(n_players, seed, n, steps, env_id_base=0, auto_reset=True, want_o
     a.legal = buf("legal", (steps, n), np.uint32)
     if want_obs:
         a.obs = buf("obs", (steps, n, n_players, 49 * n_players), np.float32)
-    a.final_state = buf("final_state", (n, 12), np.uint32)
+    a.final_state = buf("final_state", (n, 8), np.uint32)
     a.episodes_done = buf("episodes_done", (1,), np.int64)
     a.return_sum_p0 = buf("return_sum_p0", (1,), np.int64)
     lib().np_rollout(ctypes.byref(a))

@@ -41,6 +41,22 @@ def test_abi_version_and_error_plumbing():
         _native.check(rc)
 
 
+def test_create_ex_validates_players_and_flags():
+    """Argument errors are reported before any HIP call (no GPU needed)."""
+    L = _native.load()
+    h = ctypes.c_void_p()
+    for players in (0, 1, 7):
+        assert L.coup_create_ex(16, 0, 0, 1, players, ctypes.byref(h)) == _native.COUP_E_INVALID
+        assert b"num_players" in L.coup_last_error()
+    # no N-player history / InformationStateTensor
+    assert L.coup_create_ex(16, 0, 0, _native.FLAG_HISTORY, 3, ctypes.byref(h)) == _native.COUP_E_INVALID
+    assert L.coup_create_ex(16, 0, 0, _native.FLAG_HISTORY | _native.FLAG_GENERIC, 2,
+                            ctypes.byref(h)) == _native.COUP_E_INVALID
+    assert L.coup_create_ex(16, 0, 0, 64, 2, ctypes.byref(h)) == _native.COUP_E_INVALID
+    assert not h.value
+    assert L.coup_num_players(None) == -1 and L.coup_state_bytes(None) == -1
+
+
 def test_create_fails_loudly_without_gpu():
     import torch
     if torch.cuda.is_available():

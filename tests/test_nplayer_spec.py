@@ -43,19 +43,20 @@ def test_n2_spec_playthrough():
             st.apply_action(hist[k])
 
 
-def _to_2p_record(w12):
+def _to_2p_record(w8):
     """N-player record at N = 2 -> the 2-player 16-byte record."""
-    w = [int(x) for x in w12]
-    deck, coins, last, q = w[3] & 0xFFFFF, w[4] & 0xFFFFFF, w[5], w[6] & 0xFFF
-    qlen, begin, err, T = (w[3] >> 24) & 7, (w[3] >> 27) & 1, (w[3] >> 28) & 1, (w[3] >> 29) & 7
-    M = (w[4] >> 24) & 7
-    move, turn = (w[6] >> 12) & 0x1FF, (w[6] >> 21) & 0x1FF
-    r0 = (w[7] & 31) - 16
-    ep, lost = w[8] & 0x1FFFFFF, (w[8] >> 25) & 0x3F
+    w = [int(x) for x in w8]
+    coins, lost, begin, err = w[3] & 0xFFFFFF, (w[3] >> 24) & 0x3F, (w[3] >> 30) & 1, w[3] >> 31
+    last, rcount = w[4] & 0x3FFFFFFF, w[4] >> 30
+    deck, qlen, qp, T = w[5] & 0xFFFFF, (w[5] >> 24) & 3, (w[5] >> 26) & 7, w[5] >> 29
+    move, turn, M, rloser = w[6] & 0x1FF, (w[6] >> 9) & 0x1FF, (w[6] >> 18) & 7, (w[6] >> 24) & 7
+    ep = w[7] & 0x1FFFFFF
+    r0 = -rcount if rloser == 0 else rcount
+    qids = (1 << qlen) - 1 if qp == 1 else 0
     return [w[0],
             deck | ((coins & 0xF) << 20) | (((coins >> 4) & 0xF) << 24) | ((r0 + 2) << 28) | (err << 31),
             (last & 31) | (((last >> 5) & 31) << 5) | ((lost & 1) << 10) | (((lost >> 1) & 1) << 11) |
-            (qlen << 12) | (q << 15) | (T << 19) | (M << 20) | (begin << 21) | (move << 22),
+            (qlen << 12) | (qids << 15) | (T << 19) | (M << 20) | (begin << 21) | (move << 22),
             turn | (ep << 7)]
 
 
@@ -90,12 +91,13 @@ def test_n_player_invariants(n):
         o = obs[t]
         assert np.all(o[:, np.arange(n), np.arange(n)] == 1)  # observer one-hot
     assert finished > 20
-    # every card is somewhere: deck + hands = 15
+    # every card is somewhere: deck + hands = 15; no lane hit an error
     w = out["final_state"]
+    assert not np.any(w[:, 3] >> 31)
     for lane in range(64):
         hands = [int(w[lane, k // 2]) >> (16 * (k % 2)) & 0xFFFF for k in range(n)]
         cards = sum(sum(1 for i in range(4) if (h >> (4 * i)) & 0xF != 0xF) for h in hands)
-        deck = sum((int(w[lane, 3]) >> (4 * t)) & 0xF for t in range(5))
+        deck = sum((int(w[lane, 5]) >> (4 * t)) & 0xF for t in range(5))
         assert deck + cards == 15
 
 

@@ -1,10 +1,10 @@
 """Condense rocprofv3 output (tools/profile_gpu.sh) into committed evidence.
 
-    python tools/traffic.py gpurun_out/prof/<tag> [bench.py args]
+    python tools/traffic.py gpurun_out/prof/<tag>/<config> --config <config> [bench.py args]
 
-Writes profiles/<tag>/kernel_stats.csv (the --stats summary as produced),
-profiles/<tag>/summary.json, and profiles/traffic.json, which bench.py
-reads for roofline.traffic.
+Writes profiles/<tag>/<config>/kernel_stats.csv (the --stats summary as
+produced), profiles/<tag>/<config>/summary.json, and the config's entry of
+profiles/traffic.json, which bench.py reads for roofline.traffic.
 
 HBM bytes per launch follow MI355X_MICROARCH.md (HBM section): FETCH_SIZE and
 WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of a wide
@@ -41,7 +41,7 @@ def col(row, *needles):
 def main():
     src = sys.argv[1]
     args = sys.argv[2:]
-    tag = os.path.basename(os.path.normpath(src))
+    tag = os.path.basename(os.path.dirname(os.path.normpath(src)))
     cfg = "c3"
     batch = None
     for i, a in enumerate(args):
@@ -52,19 +52,34 @@ def main():
     sys.path.insert(0, ROOT)
     from bench import CONFIGS
     batch = batch or CONFIGS[cfg][0]
-    want_obs, want_info, fused = CONFIGS[cfg][1], CONFIGS[cfg][2], CONFIGS[cfg][3]
-    step_kernel = os.environ.get("COUP_STEP_KERNEL", "coup::k_step<true, OBS, T> (uniform policy)")
+    want_obs, want_info, fused, players = CONFIGS[cfg][1], CONFIGS[cfg][2], CONFIGS[cfg][3], CONFIGS[cfg][6]
 
-    dst = os.path.join(ROOT, "profiles", tag)
+    dst = os.path.join(ROOT, "profiles", tag, cfg)
     os.makedirs(dst, exist_ok=True)
     summary = {"tag": tag, "config": cfg, "batch": batch}
+
+    def timed_kernel(kn):
+        """Is `kn` the kernel bench.py times for this config?"""
+        if players != 2:
+            if fused:
+                return bool(re.search(r"np::k_rollout<%d>|2np9k_rolloutILi%dE" % (players, players), kn))
+            return bool(re.search(r"np::k_step<%d, true>|2np6k_stepILi%dELb1E" % (players, players), kn))
+        if "np::" in kn or "2np" in kn:
+            return False
+        if fused:
+            return "k_rollout" in kn
+        m = (re.search(r"k_step<true, (\d+), \d+, (\d+)>", kn) or
+             re.search(r"k_stepILb1ELi(\d+)ELi\d+ELi(\d+)E", kn))
+        return bool(m) and (m.group(1) != "0") == want_obs and (m.group(2) == "2") == want_info
 
     stats = glob.glob(os.path.join(src, "trace", "**", "*kernel_stats.csv"), recursive=True)
     if stats:
         shutil.copy(stats[0], os.path.join(dst, "kernel_stats.csv"))
         for r in rows(stats[0]):
             name = r[col(r, "name")]
-            if "k_step" in name or "k_rollout" in name:
+            if timed_kernel(name):
+                summary["timed_kernel"] = name
+            if "k_step" in name or "k_rollout" in name or "k_obs" in name:
                 summary.setdefault("kernels", {})[name] = {
                     "calls": int(r[col(r, "calls")]),
                     "avg_ns": float(r[col(r, "average")]),
@@ -74,14 +89,8 @@ def main():
         vals = []
         for r in rows(os.path.join(src, kind, "**", "*counter_collection.csv")):
             kn = r[col(r, "kernel", "name")]
-            if fused:
-                if "k_rollout" not in kn:
-                    continue
-            else:
-                m = (re.search(r"k_step<true, (\d+), \d+, (\d+)>", kn) or
-                     re.search(r"k_stepILb1ELi(\d+)ELi\d+ELi(\d+)E", kn))
-                if not m or (m.group(1) != "0") != want_obs or (m.group(2) == "2") != want_info:
-                    continue
+            if not timed_kernel(kn):
+                continue
             if r[col(r, "counter", "name")] != cname:
                 continue
             vals.append(float(r[col(r, "counter", "value")]))
@@ -98,13 +107,16 @@ def main():
         sys.exit(f"no FETCH_SIZE / WRITE_SIZE records for the step kernel under {src}; nothing written")
     summary["hbm_bytes_per_launch"] = traffic
     summary["correction"] = "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE halving)"
-    summary["step_kernel"] = step_kernel
     with open(os.path.join(dst, "summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
-    if traffic is not None:
-        with open(os.path.join(ROOT, "profiles", "traffic.json"), "w") as f:
-            json.dump({"config": cfg, "batch": batch, "hbm_bytes_per_launch": traffic,
-                       "source": f"profiles/{tag}/summary.json"}, f, indent=1)
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    table = {}
+    if os.path.exists(path):
+        with open(path) as f:
+            table = json.load(f)
+    table[cfg] = {"batch": batch, "hbm_bytes_per_launch": traffic, "source": f"profiles/{tag}/{cfg}/summary.json"}
+    with open(path, "w") as f:
+        json.dump(table, f, indent=1, sort_keys=True)
     print(json.dumps(summary, indent=1))
 
 
