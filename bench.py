@@ -74,36 +74,62 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(target_s, with_obs, with_info, players=2):
-    """Bounded sample of the same per-lane workload on the oracle (1 core)."""
+def _cpu_threads():
+    """Host threads for the all-cores sample: the job's CPU share (the GPU
+    box exports OMP_NUM_THREADS = its share), at most the affinity set."""
+    avail = len(os.sched_getaffinity(0))
+    want = int(os.environ.get("OMP_NUM_THREADS", avail) or avail)
+    return max(1, min(avail, want))
+
+
+def _oracle_sample(players, with_obs, with_info, n, steps, env_id_base=0):
     from oracle import oracle
     if players != 2:
-        n = 1024
+        oracle.np_rollout(players, seed=7, n=n, steps=steps, env_id_base=env_id_base)
+    else:
+        oracle.rollout(seed=7, n=n, steps=steps, env_id_base=env_id_base, want_obs=with_obs, obs_overwrite=True,
+                       want_trajectory=False, want_info=with_info)
+
+
+def cpu_baseline(target_s, with_obs, with_info, players=2):
+    """Bounded sample of the same per-lane workload on the C oracle: one core
+    (the reference's single-threaded path), then the same sample split over
+    all of the job's host cores (ctypes releases the GIL, so Python threads
+    run the C rollouts in parallel, one lane range per thread)."""
+    import threading
+    n = 1024 if players != 2 else (4096 if not with_info else 256)
+    _oracle_sample(players, with_obs, with_info, n, 2)  # load / build the oracle
+    steps, dt = 4, 0.0
+    while dt < target_s / 16 and not (with_info and steps >= 64):
+        steps *= 2
         t0 = time.perf_counter()
-        oracle.np_rollout(players, seed=7, n=n, steps=8)
-        per_step = (time.perf_counter() - t0) / (n * 8)
-        steps = max(8, int(target_s / per_step / n))
-        t0 = time.perf_counter()
-        oracle.np_rollout(players, seed=7, n=n, steps=steps)
+        _oracle_sample(players, with_obs, with_info, n, steps)
         dt = time.perf_counter() - t0
-        return {"value": n * steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-                "sample": f"{n} lanes x {steps} uniform-random {players}-player steps, {dt:.1f} s, "
-                          "oracle/coup_nplayer.c -O2"}
-    n = 4096 if not with_info else 256
-    kw = dict(want_obs=with_obs, obs_overwrite=True, want_trajectory=False)
-    t0 = time.perf_counter()
-    oracle.rollout(seed=7, n=n, steps=8, want_info=with_info, **kw)
-    per_step = (time.perf_counter() - t0) / (n * 8)
-    steps = max(8, int(target_s / per_step / n))
+    steps = max(steps, int(steps * target_s / max(dt, 1e-9)))
     if with_info:
         steps = min(steps, 64)  # the oracle keeps every step's tensors
     t0 = time.perf_counter()
-    oracle.rollout(seed=7, n=n, steps=steps, want_info=with_info, **kw)
+    _oracle_sample(players, with_obs, with_info, n, steps)
     dt = time.perf_counter() - t0
     what = " with ObservationTensor x2 written per step" if with_obs else ""
     what += " with InformationStateTensor x2 written per step" if with_info else ""
-    return {"value": n * steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"{n} lanes x {steps} uniform-random steps{what}, {dt:.1f} s, oracle/coup_oracle.c -O2"}
+    src = "oracle/coup_nplayer.c" if players != 2 else "oracle/coup_oracle.c"
+    out = {"value": n * steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+           "sample": f"{n} lanes x {steps} uniform-random {players}-player steps{what}, {dt:.1f} s, {src} -O2"}
+    k = _cpu_threads()
+    if k > 1:
+        # same total work per thread as the 1-core sample, k lane ranges
+        th = [threading.Thread(target=_oracle_sample, args=(players, with_obs, with_info, n, steps, i * n))
+              for i in range(k)]
+        t0 = time.perf_counter()
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        dk = time.perf_counter() - t0
+        out["all_cores"] = {"value": k * n * steps / dk, "cores": k,
+                            "sample": f"{k} threads x ({n} lanes x {steps} steps), {dk:.1f} s"}
+    return out
 
 
 def main():

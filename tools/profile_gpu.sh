@@ -2,7 +2,8 @@
 # Profile one bench.py config on the GPU box (run from the repo root through
 # gpurun).  Three separate rocprofv3 runs, as MI355X_MICROARCH.md's rocprofv3
 # section prescribes: a kernel trace with --stats, then one PMC pass per TCC
-# counter (FETCH_SIZE and WRITE_SIZE do not fit in one pass).  Outputs land
+# counter (FETCH_SIZE and WRITE_SIZE do not fit in one pass), then one SQ +
+# GRBM pass for the issue mix (VALU busy, wave wait share).  Outputs land
 # in gpurun_out/prof/<tag>/<config>/; tools/traffic.py condenses them into
 # profiles/<tag>/<config>/ and profiles/traffic.json.
 #   usage: tools/profile_gpu.sh <tag> <config> [bench.py args...]
@@ -22,5 +23,10 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch"
   -- python3 "$R/bench.py" --config "$CFG" $ARGS --no-cpu-baseline > "$OUT/fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run \
   -- python3 "$R/bench.py" --config "$CFG" $ARGS --no-cpu-baseline > "$OUT/write.log" 2>&1
+# issue mix: a failed pass (e.g. a counter this ROCm does not list) only
+# drops the issue block from the summary
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU \
+  SQ_INSTS_VALU SQ_WAIT_ANY GRBM_GUI_ACTIVE --output-format csv -d "$OUT/sq" -o run \
+  -- python3 "$R/bench.py" --config "$CFG" $ARGS --no-cpu-baseline > "$OUT/sq.log" 2>&1 || echo "SQ pass failed (rc=$?)"
 cd "$R"
 python3 tools/traffic.py "$OUT" --config "$CFG" $ARGS
