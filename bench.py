@@ -71,6 +71,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target duration of the bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
+                    help="replay the K timed steps from one HIP graph (auto: on for c2, whose "
+                         "11 us step kernel is shorter than a host launch)")
     return ap.parse_args()
 
 
@@ -155,7 +158,13 @@ def main():
         torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream(dev)
-    if fused:
+    graph = None
+    if not fused and (args.graph == "on" or (args.graph == "auto" and cfg == "c2")):
+        for _ in range(args.warmup):
+            env.step()
+        graph = env.capture_steps(args.steps)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))]
+    elif fused:
         env.rollout(args.warmup)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))]
     else:
@@ -165,7 +174,11 @@ def main():
               for _ in range(args.steps)]
     barrier()
     t0 = time.perf_counter()
-    if fused:
+    if graph is not None:
+        ev[0][0].record(stream)
+        graph.replay()
+        ev[0][1].record(stream)
+    elif fused:
         ev[0][0].record(stream)
         env.rollout(args.steps)
         ev[0][1].record(stream)
@@ -180,7 +193,8 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
 
-    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps  # per env step
+    # per env step; with a graph, the replay's duration / K (launch gaps included)
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
     elapsed = D.max_over_ranks(elapsed, dev)
     errors = env.error_count()
 
@@ -222,6 +236,7 @@ def main():
             "data": "synthetic (uniform-random self-play games)",
             "config": {"workload": workload, "batch_per_gpu": B, "global_batch": world * B, "players": players,
                        "outputs": outputs, "auto_reset": True, "fused_steps_per_launch": args.steps if fused else 1,
+                       "hip_graph": graph is not None,
                        "parallelism": f"dp{world} (env-id sharding)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kernel,

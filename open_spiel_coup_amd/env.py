@@ -144,6 +144,28 @@ class BatchedCoupEnv:
             out["info_state"] = self.info_state
         return out
 
+    def capture_steps(self, steps, actions=None):
+        """Record `steps` batched env steps (uniform policy, or the fixed
+        `actions` tensor every step) as one HIP graph; `graph.replay()` then
+        runs them with a single launch, writing the usual output buffers.
+        Removes the per-step host overhead where a step's kernel is short
+        (small B).  The env must outlive the graph."""
+        a = None
+        if actions is not None:
+            actions = actions.to(device=self.device, dtype=torch.int8).contiguous()
+            self._graph_actions = actions
+            a = _ptr(actions)
+        g = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.graph(g, stream=side):
+            self._bind_stream()
+            for _ in range(int(steps)):
+                _native.check(self.lib.coup_step(self._h, a, ctypes.byref(self._out)))
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        self._bind_stream()
+        return g
+
     def rollout(self, steps, stats=None):
         """`steps` uniform-random steps per lane in one launch.  stats: optional
         dict with int32 [B] tensors 'episodes', 'return_sum', 'length_sum'

@@ -277,3 +277,20 @@ def test_determinism_full_batch():
     for _ in range(50):
         b.step()
     assert torch.equal(a.export_state(), b.export_state())
+
+
+def test_graph_replay_matches_eager():
+    """K steps captured in one HIP graph (BatchedCoupEnv.capture_steps, used
+    by bench.py for short kernels) == K eager coup_step calls."""
+    a = BatchedCoupEnv(4096, seed=5, obs=True)
+    b = BatchedCoupEnv(4096, seed=5, obs=True)
+    g = b.capture_steps(10)
+    for _ in range(3):
+        for _ in range(10):
+            oa = a.step()
+        g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(a.export_state(), b.export_state())
+    for k in ("actions", "rewards", "step_type", "legal_mask", "obs"):
+        assert torch.equal(oa[k], getattr(b, "cur_player" if k == "current_player" else k)), k
+    assert a.error_count() == 0 and b.error_count() == 0
