@@ -1,0 +1,462 @@
+/*
+ * coup_mi355x.hpp -- C++ host layer over the C ABI (coup_mi355x.h).
+ *
+ * Header-only, C++17.  Two surfaces:
+ *
+ *   coup_amd::BatchedEnv     RAII owner of a coup_env: the batched
+ *                            reset / step / rollout / State-API calls on
+ *                            caller-owned device buffers.
+ *   coup_amd::CoupGame,      the open_spiel::Game / open_spiel::State
+ *   coup_amd::CoupState      methods the reference's C++ and Python callers
+ *                            use (spiel.h:210-1035, coup.h:111-231), one
+ *                            game per object.
+ *
+ * A CoupState keeps its 16-byte lane record and 96 history bytes on the host.
+ * Every rules operation (ApplyAction, LegalActions, tensors, ...) uploads
+ * them to a one-lane scratch env and runs the HIP kernels; there is no CPU
+ * rules engine.  Strings are formatted on the host from the record and the
+ * history (coup.cc:60-135, 290-373, 945-987), as open_spiel_coup_amd/strings.py
+ * does.  Errors throw coup_amd::SpielError (SpielFatalError,
+ * spiel_utils.cc:132-136; pyspiel.SpielError).
+ *
+ * Link with libcoup_mi355x.so and libamdhip64.so.  Needs <hip/hip_runtime_api.h>
+ * (define __HIP_PLATFORM_AMD__ when compiling with g++).
+ */
+#ifndef COUP_MI355X_HPP_
+#define COUP_MI355X_HPP_
+
+#include <hip/hip_runtime_api.h>
+
+#include <array>
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "coup_mi355x.h"
+
+namespace coup_amd {
+
+using Action = int64_t;
+using Player = int;
+constexpr Player kChancePlayerId = COUP_CHANCE_PLAYER;      // spiel_globals.h:34
+constexpr Player kTerminalPlayerId = COUP_TERMINAL_PLAYER;  // spiel_globals.h:28
+
+class SpielError : public std::runtime_error {
+ public:
+  using std::runtime_error::runtime_error;
+};
+
+inline void Check(int rc, const char* what) {
+  if (rc != COUP_OK) throw SpielError(std::string(what) + ": " + coup_last_error());
+}
+
+inline void CheckHip(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw SpielError(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// ------------------------------------------------------------ BatchedEnv
+
+class BatchedEnv {
+ public:
+  BatchedEnv(int64_t batch, uint64_t seed, uint32_t env_id_base = 0, int flags = COUP_FLAG_AUTO_RESET,
+             int num_players = COUP_NUM_PLAYERS) {
+    Check(coup_create_ex(batch, seed, env_id_base, flags, num_players, &env_), "coup_create_ex");
+  }
+  ~BatchedEnv() {
+    if (env_) coup_destroy(env_);
+  }
+  BatchedEnv(const BatchedEnv&) = delete;
+  BatchedEnv& operator=(const BatchedEnv&) = delete;
+  BatchedEnv(BatchedEnv&& o) noexcept : env_(o.env_) { o.env_ = nullptr; }
+
+  coup_env* get() const { return env_; }
+  int64_t batch() const { return coup_batch(env_); }
+  int num_players() const { return coup_num_players(env_); }
+  int state_bytes() const { return coup_state_bytes(env_); }
+  void SetStream(hipStream_t s) { Check(coup_set_stream(env_, (void*)s), "coup_set_stream"); }
+
+  // all pointers are device pointers (lane-major); see coup_mi355x.h
+  void Reset(const uint8_t* lane_mask = nullptr) { Check(coup_reset(env_, lane_mask), "coup_reset"); }
+  void Step(const int8_t* actions, const coup_step_outputs& out) {
+    Check(coup_step(env_, actions, &out), "coup_step");
+  }
+  void Rollout(int64_t steps, const coup_rollout_stats* stats = nullptr) {
+    Check(coup_rollout(env_, steps, stats), "coup_rollout");
+  }
+  void NewInitialState(const uint8_t* lane_mask = nullptr) {
+    Check(coup_new_initial_state(env_, lane_mask), "coup_new_initial_state");
+  }
+  void ApplyAction(const int8_t* actions) { Check(coup_apply_action(env_, actions), "coup_apply_action"); }
+  void Query(const coup_query_outputs& out) { Check(coup_query(env_, &out), "coup_query"); }
+  void ExportState(uint32_t* dst) { Check(coup_export_state(env_, dst), "coup_export_state"); }
+  void ImportState(const uint32_t* src) { Check(coup_import_state(env_, src), "coup_import_state"); }
+  void ExportHistory(uint8_t* dst) { Check(coup_export_history(env_, dst), "coup_export_history"); }
+  void ImportHistory(const uint8_t* src) { Check(coup_import_history(env_, src), "coup_import_history"); }
+  int64_t ErrorCount() {
+    int64_t n = 0;
+    Check(coup_error_count(env_, &n), "coup_error_count");
+    return n;
+  }
+
+ private:
+  coup_env* env_ = nullptr;
+};
+
+// --------------------------------------------------------------- strings
+
+namespace detail {
+
+inline const char* CardName(int t) {
+  static const char* k[] = {"Assassin", "Ambassador", "Captain", "Contessa", "Duke"};
+  return k[t];
+}
+
+inline const char* ActionName(int a) {
+  static const char* k[] = {"Income",           "ForeignAid",       "Coup",      "Tax",
+                            "Assassinate",      "Exchange",         "Steal",     "LoseCard1",
+                            "LoseCard2",        "Pass",             "Block",     "Challenge",
+                            "ExchangeReturn12", "ExchangeReturn13", "ExchangeReturn14",
+                            "ExchangeReturn23", "ExchangeReturn24", "ExchangeReturn34"};
+  return k[a];
+}
+
+// fields of the 16-byte record
+struct Fields {
+  std::array<std::vector<std::pair<int, int>>, 2> cards;  // (type, face) per slot
+  std::array<int, 5> deck;
+  std::array<int, 2> coins, last;  // last: -1 = None
+  int move_player, move_number, turn_number;
+};
+
+inline Fields Decode(const std::array<uint32_t, 4>& w) {
+  Fields f;
+  for (int p = 0; p < 2; ++p) {
+    const uint32_t h = (w[0] >> (16 * p)) & 0xFFFFu;
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t k = (h >> (4 * i)) & 0xFu;
+      if (k == 0xFu) break;
+      f.cards[p].emplace_back((int)(k >> 1), (int)(k & 1u));
+    }
+    f.coins[p] = (int)((w[1] >> (20 + 4 * p)) & 0xFu);
+    const int l = (int)((w[2] >> (5 * p)) & 0x1Fu);
+    f.last[p] = l == 31 ? -1 : l;
+  }
+  for (int t = 0; t < 5; ++t) f.deck[t] = (int)((w[1] >> (4 * t)) & 0xFu);
+  f.move_player = (int)((w[2] >> 20) & 1u);
+  f.move_number = (int)((w[2] >> 22) & 0x7Fu);
+  f.turn_number = (int)(w[3] & 0x7Fu);
+  return f;
+}
+
+inline std::string CardRow(int slot, const std::string& value, int face) {
+  std::string v = value;
+  if (v.size() < 11) v.append(11 - v.size(), ' ');
+  return "Card " + std::to_string(slot + 1) + ": " + v + "| " + (face ? "FaceUp" : "FaceDown") + "\n";
+}
+
+inline std::string LastAction(int a) { return a < 0 ? "None" : ActionName(a); }
+
+// CoupObserver::StringFrom (coup.cc:290-373); observer < 0 = ToString
+// (coup.cc:945-987, every card shown)
+inline std::string StateString(const Fields& f, const uint8_t* hist, int observer, bool perfect_recall) {
+  std::string s;
+  if (observer >= 0) s += "Observer: P" + std::to_string(observer + 1) + "\n";
+  s += "Turn: " + std::to_string(f.turn_number) + "\n";
+  s += "Move: P" + std::to_string(f.move_player + 1) + "\n";
+  for (int p = 0; p < 2; ++p) {
+    s += "P" + std::to_string(p + 1) + "\n        Card         State\n";
+    for (size_t i = 0; i < f.cards[p].size(); ++i) {
+      const auto& c = f.cards[p][i];
+      const bool shown = observer < 0 || c.second == 1 || p == observer;
+      s += CardRow((int)i, shown ? CardName(c.first) : "-", c.second);
+    }
+    s += "Coins: " + std::to_string(f.coins[p]) + "\n";
+    if (perfect_recall)
+      s += "\n";
+    else
+      s += "Last Action: " + LastAction(f.last[p]) + "\n\n";
+  }
+  if (observer < 0 || perfect_recall) {
+    s += "Action Sequence: ";
+    const int n = f.move_number;
+    for (int i = 0; i < n; ++i) {
+      const uint8_t e = hist[i];
+      const bool deal = (e & 0x20) != 0;
+      const int a = e & 0x1F, who = (e >> 6) & 1;
+      if (observer < 0) {
+        s += deal ? std::string("PC-") + CardName(a) : "P" + std::to_string(who + 1) + "-" + ActionName(a);
+        if (i < n - 1) s += ", ";
+      } else if (!deal || who == observer) {
+        // deals are shown to their receiver only; the separator depends on
+        // the position in the full history (coup.cc:351-371)
+        s += deal ? std::string("PC-") + CardName(a) : "P" + std::to_string(who + 1) + "-" + ActionName(a);
+        if (i < n - 1) s += ", ";
+      }
+    }
+    s += "\n";
+  }
+  return s;
+}
+
+// One-lane scratch env with history and device buffers for single-state ops.
+class Engine {
+ public:
+  Engine() : env_(1, 0, 0, COUP_FLAG_HISTORY) {
+    CheckHip(hipMalloc(&buf_, kBytes), "hipMalloc");
+  }
+  ~Engine() { (void)hipFree(buf_); }
+
+  struct Result {
+    uint32_t legal;
+    int cur;
+    bool terminal;
+    int rewards[2], returns[2];
+  };
+
+  void NewInitial(std::array<uint32_t, 4>& rec, std::array<uint8_t, COUP_HISTORY_BYTES>& hist) {
+    env_.NewInitialState();
+    env_.ExportState(Rec());
+    CheckHip(hipMemcpy(rec.data(), Rec(), 16, hipMemcpyDeviceToHost), "hipMemcpy");
+    hist.fill(0xFF);
+  }
+
+  bool Apply(std::array<uint32_t, 4>& rec, std::array<uint8_t, COUP_HISTORY_BYTES>& hist, Action a) {
+    Load(rec, hist);
+    const int8_t x = (int8_t)a;
+    CheckHip(hipMemcpy(Act(), &x, 1, hipMemcpyHostToDevice), "hipMemcpy");
+    env_.ApplyAction(Act());
+    if (env_.ErrorCount()) return false;
+    env_.ExportState(Rec());
+    env_.ExportHistory(Hist());
+    CheckHip(hipMemcpy(rec.data(), Rec(), 16, hipMemcpyDeviceToHost), "hipMemcpy");
+    CheckHip(hipMemcpy(hist.data(), Hist(), COUP_HISTORY_BYTES, hipMemcpyDeviceToHost), "hipMemcpy");
+    return true;
+  }
+
+  Result Query(const std::array<uint32_t, 4>& rec, const std::array<uint8_t, COUP_HISTORY_BYTES>& hist,
+               float* obs, float* info) {
+    Load(rec, hist);
+    coup_query_outputs q{};
+    q.legal_mask = reinterpret_cast<uint32_t*>(buf_ + kLegal);
+    q.cur_player = reinterpret_cast<int8_t*>(buf_ + kCur);
+    q.terminal = reinterpret_cast<uint8_t*>(buf_ + kTerm);
+    q.rewards = reinterpret_cast<int8_t*>(buf_ + kRew);
+    q.returns = reinterpret_cast<int8_t*>(buf_ + kRet);
+    q.obs = obs ? reinterpret_cast<float*>(buf_ + kObs) : nullptr;
+    q.info_state = info ? reinterpret_cast<float*>(buf_ + kInfo) : nullptr;
+    env_.Query(q);
+    uint8_t small[kSmall];
+    CheckHip(hipMemcpy(small, buf_ + kLegal, kSmall, hipMemcpyDeviceToHost), "hipMemcpy");
+    Result r;
+    std::memcpy(&r.legal, small, 4);
+    r.cur = (int8_t)small[kCur - kLegal];
+    r.terminal = small[kTerm - kLegal] != 0;
+    for (int p = 0; p < 2; ++p) {
+      r.rewards[p] = (int8_t)small[kRew - kLegal + p];
+      r.returns[p] = (int8_t)small[kRet - kLegal + p];
+    }
+    if (obs) CheckHip(hipMemcpy(obs, buf_ + kObs, 2 * COUP_OBS_SIZE * 4, hipMemcpyDeviceToHost), "hipMemcpy");
+    if (info)
+      CheckHip(hipMemcpy(info, buf_ + kInfo, 2 * COUP_INFO_STATE_SIZE * 4, hipMemcpyDeviceToHost), "hipMemcpy");
+    return r;
+  }
+
+ private:
+  // device scratch layout
+  static constexpr size_t kRec = 0, kHist = 16, kAct = kHist + COUP_HISTORY_BYTES, kLegal = kAct + 16,
+                          kCur = kLegal + 4, kTerm = kCur + 1, kRew = kTerm + 1, kRet = kRew + 2,
+                          kSmall = kRet + 2 - kLegal, kObs = 256, kInfo = kObs + 2 * COUP_OBS_SIZE * 4,
+                          kBytes = kInfo + 2 * COUP_INFO_STATE_SIZE * 4;
+  uint32_t* Rec() { return reinterpret_cast<uint32_t*>(buf_ + kRec); }
+  uint8_t* Hist() { return buf_ + kHist; }
+  int8_t* Act() { return reinterpret_cast<int8_t*>(buf_ + kAct); }
+  void Load(const std::array<uint32_t, 4>& rec, const std::array<uint8_t, COUP_HISTORY_BYTES>& hist) {
+    CheckHip(hipMemcpy(Rec(), rec.data(), 16, hipMemcpyHostToDevice), "hipMemcpy");
+    CheckHip(hipMemcpy(Hist(), hist.data(), COUP_HISTORY_BYTES, hipMemcpyHostToDevice), "hipMemcpy");
+    env_.ImportState(Rec());
+    env_.ImportHistory(Hist());
+  }
+
+  BatchedEnv env_;
+  uint8_t* buf_ = nullptr;
+};
+
+inline Engine& TheEngine() {
+  static Engine e;  // one per process (current HIP device at first use)
+  return e;
+}
+
+}  // namespace detail
+
+// ---------------------------------------------------------- Game / State
+
+class CoupGame;
+
+struct PlayerAction {
+  Player player;
+  Action action;
+};
+
+// open_spiel::coup::CoupState (coup.h:111-197) on the GPU engine.
+class CoupState {
+ public:
+  explicit CoupState(const CoupGame* game) : game_(game) { detail::TheEngine().NewInitial(rec_, hist_); }
+
+  Player CurrentPlayer() const { return Q().cur; }
+  bool IsTerminal() const { return Q().terminal; }
+  bool IsChanceNode() const { return CurrentPlayer() == kChancePlayerId; }
+  bool IsPlayerNode() const { return CurrentPlayer() >= 0; }
+  int NumPlayers() const { return COUP_NUM_PLAYERS; }
+  int NumDistinctActions() const { return COUP_NUM_ACTIONS; }
+
+  // LegalActions (coup.cc:824-938): ascending
+  std::vector<Action> LegalActions() const {
+    std::vector<Action> out;
+    if (IsTerminal()) return out;
+    const uint32_t m = Q().legal & 0x3FFFFu;
+    for (int a = 0; a < COUP_NUM_ACTIONS; ++a)
+      if ((m >> a) & 1u) out.push_back(a);
+    return out;
+  }
+  std::vector<Action> LegalActions(Player p) const {
+    return p == CurrentPlayer() ? LegalActions() : std::vector<Action>();
+  }
+  // LegalActionsMask (spiel.cc:371-377): 5 entries at chance nodes
+  std::vector<int> LegalActionsMask() const {
+    std::vector<int> mask(IsChanceNode() ? COUP_NUM_CARD_TYPES : COUP_NUM_ACTIONS, 0);
+    for (Action a : LegalActions()) mask[a] = 1;
+    return mask;
+  }
+  // ChanceOutcomes (coup.cc:1062-1077)
+  std::vector<std::pair<Action, double>> ChanceOutcomes() const {
+    if (!IsChanceNode()) throw SpielError("ChanceOutcomes() at a non-chance node");
+    const detail::Fields f = detail::Decode(rec_);
+    double total = 0;
+    for (int t = 0; t < 5; ++t) total += f.deck[t];
+    std::vector<std::pair<Action, double>> out;
+    for (int t = 0; t < 5; ++t)
+      if (f.deck[t] > 0) out.emplace_back(t, f.deck[t] / total);
+    return out;
+  }
+
+  // State::ApplyAction (spiel.cc:322-331); throws for an illegal action
+  void ApplyAction(Action a) {
+    const Player p = CurrentPlayer();
+    if (!detail::TheEngine().Apply(rec_, hist_, a))
+      throw SpielError("ApplyAction: illegal action " + std::to_string(a));
+    history_.push_back({p, a});
+    valid_ = false;
+  }
+  std::unique_ptr<CoupState> Child(Action a) const {
+    auto c = Clone();
+    c->ApplyAction(a);
+    return c;
+  }
+  std::unique_ptr<CoupState> Clone() const { return std::unique_ptr<CoupState>(new CoupState(*this)); }
+
+  std::vector<double> Rewards() const { return {(double)Q().rewards[0], (double)Q().rewards[1]}; }
+  std::vector<double> Returns() const { return {(double)Q().returns[0], (double)Q().returns[1]}; }
+  double PlayerReturn(Player p) const { return Returns()[p]; }
+
+  std::vector<float> ObservationTensor(Player p) const {
+    float both[2 * COUP_OBS_SIZE];
+    detail::TheEngine().Query(rec_, hist_, both, nullptr);
+    return std::vector<float>(both + p * COUP_OBS_SIZE, both + (p + 1) * COUP_OBS_SIZE);
+  }
+  std::vector<float> InformationStateTensor(Player p) const {
+    std::vector<float> both(2 * COUP_INFO_STATE_SIZE);
+    detail::TheEngine().Query(rec_, hist_, nullptr, both.data());
+    return std::vector<float>(both.begin() + p * COUP_INFO_STATE_SIZE,
+                              both.begin() + (p + 1) * COUP_INFO_STATE_SIZE);
+  }
+
+  std::string ObservationString(Player p) const {
+    return detail::StateString(detail::Decode(rec_), hist_.data(), p, false);
+  }
+  std::string InformationStateString(Player p) const {
+    return detail::StateString(detail::Decode(rec_), hist_.data(), p, true);
+  }
+  std::string ToString() const { return detail::StateString(detail::Decode(rec_), hist_.data(), -1, false); }
+  std::string ActionToString(Player p, Action a) const;
+
+  std::vector<Action> History() const {
+    std::vector<Action> h;
+    for (const auto& pa : history_) h.push_back(pa.action);
+    return h;
+  }
+  const std::vector<PlayerAction>& FullHistory() const { return history_; }
+  int MoveNumber() const { return detail::Decode(rec_).move_number; }
+  // State::Serialize (spiel.cc:297-311)
+  std::string Serialize() const {
+    std::string s;
+    for (const auto& pa : history_) s += std::to_string(pa.action) + "\n";
+    return s;
+  }
+  const std::array<uint32_t, 4>& PackedRecord() const { return rec_; }
+
+ private:
+  const detail::Engine::Result& Q() const {
+    if (!valid_) {
+      q_ = detail::TheEngine().Query(rec_, hist_, nullptr, nullptr);
+      valid_ = true;
+    }
+    return q_;
+  }
+
+  const CoupGame* game_;
+  std::array<uint32_t, 4> rec_{};
+  std::array<uint8_t, COUP_HISTORY_BYTES> hist_{};
+  std::vector<PlayerAction> history_;
+  mutable detail::Engine::Result q_{};
+  mutable bool valid_ = false;
+};
+
+// open_spiel::coup::CoupGame (coup.h:199-231)
+class CoupGame {
+ public:
+  std::unique_ptr<CoupState> NewInitialState() const { return std::unique_ptr<CoupState>(new CoupState(this)); }
+  int NumDistinctActions() const { return COUP_NUM_ACTIONS; }
+  int MaxChanceOutcomes() const { return COUP_NUM_CARD_TYPES; }
+  int NumPlayers() const { return COUP_NUM_PLAYERS; }
+  double MinUtility() const { return -2; }
+  double MaxUtility() const { return 2; }
+  double UtilitySum() const { return 0; }
+  int MaxGameLength() const { return COUP_MAX_GAME_LENGTH; }
+  int MaxChanceNodesInHistory() const { return 45; }
+  std::vector<int> ObservationTensorShape() const { return {COUP_OBS_SIZE}; }
+  std::vector<int> InformationStateTensorShape() const { return {COUP_INFO_STATE_SIZE}; }
+  // ActionToString (coup.cc:1143-1149)
+  std::string ActionToString(Player p, Action a) const {
+    return p == kChancePlayerId ? std::string("Chance drawn card:") + detail::CardName((int)a)
+                                : std::string(detail::ActionName((int)a));
+  }
+  std::string ToString() const { return "coup()"; }
+  // Game::DeserializeState (spiel.cc:393-425): replay the history
+  std::unique_ptr<CoupState> DeserializeState(const std::string& text) const {
+    auto st = NewInitialState();
+    size_t i = 0;
+    while (i < text.size()) {
+      size_t j = text.find('\n', i);
+      if (j == std::string::npos) j = text.size();
+      if (j > i) st->ApplyAction(std::stoll(text.substr(i, j - i)));
+      i = j + 1;
+    }
+    return st;
+  }
+};
+
+inline std::string CoupState::ActionToString(Player p, Action a) const { return game_->ActionToString(p, a); }
+
+// LoadGame (spiel.h:1081-1090) for the one game this build provides
+inline std::shared_ptr<const CoupGame> LoadGame(const std::string& name) {
+  if (name.substr(0, name.find('(')) != "coup") throw SpielError("unknown game '" + name + "'");
+  return std::make_shared<const CoupGame>();
+}
+
+}  // namespace coup_amd
+
+#endif  // COUP_MI355X_HPP_

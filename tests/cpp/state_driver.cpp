@@ -1,0 +1,107 @@
+// Drives the C++ host layer (include/coup_mi355x.hpp) through one game and
+// prints one JSON object per state, so tests/test_gpu_cpp_api.py can compare
+// it with the reference's golden transcript.  Test tooling.
+//   state_driver <action> <action> ...      (the history to replay)
+//   state_driver --illegal                  (error behaviour check)
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+
+#include "coup_mi355x.hpp"
+
+using namespace coup_amd;
+
+static std::string Quote(const std::string& s) {
+  std::string o = "\"";
+  for (char c : s) {
+    if (c == '"' || c == '\\') {
+      o += '\\';
+      o += c;
+    } else if (c == '\n') {
+      o += "\\n";
+    } else {
+      o += c;
+    }
+  }
+  return o + "\"";
+}
+
+template <class V>
+static std::string List(const V& v) {
+  std::string o = "[";
+  for (size_t i = 0; i < v.size(); ++i) o += (i ? "," : "") + std::to_string(v[i]);
+  return o + "]";
+}
+
+// sparse [[index, value], ...] like tests/golden/playthrough_coup.json
+static std::string Sparse(const std::vector<float>& v) {
+  std::string o = "[";
+  bool first = true;
+  for (size_t i = 0; i < v.size(); ++i) {
+    if (v[i] == 0.0f) continue;
+    o += (first ? "[" : ",[") + std::to_string(i) + "," + std::to_string((int)v[i]) + "]";
+    first = false;
+  }
+  return o + "]";
+}
+
+static void Dump(const CoupState& s) {
+  std::string o = "{\"history\":" + List(s.History());
+  o += ",\"current_player\":" + std::to_string(s.CurrentPlayer());
+  o += ",\"is_terminal\":" + std::string(s.IsTerminal() ? "true" : "false");
+  o += ",\"is_chance\":" + std::string(s.IsChanceNode() ? "true" : "false");
+  o += ",\"legal_actions\":" + List(s.LegalActions());
+  if (s.IsChanceNode()) {
+    o += ",\"chance_outcomes\":[";
+    const auto co = s.ChanceOutcomes();
+    for (size_t i = 0; i < co.size(); ++i) {
+      char buf[64];
+      std::snprintf(buf, sizeof buf, "%s[%lld,%.17g]", i ? "," : "", (long long)co[i].first, co[i].second);
+      o += buf;
+    }
+    o += "]";
+  }
+  o += ",\"rewards\":" + List(s.Rewards()) + ",\"returns\":" + List(s.Returns());
+  o += ",\"to_string\":" + Quote(s.ToString());
+  for (int p = 0; p < 2; ++p) {
+    const std::string k = std::to_string(p);
+    o += ",\"obs" + k + "\":" + Sparse(s.ObservationTensor(p));
+    o += ",\"info" + k + "\":" + Sparse(s.InformationStateTensor(p));
+    o += ",\"obs_str" + k + "\":" + Quote(s.ObservationString(p));
+    o += ",\"info_str" + k + "\":" + Quote(s.InformationStateString(p));
+  }
+  o += ",\"serialize\":" + Quote(s.Serialize()) + "}";
+  std::printf("%s\n", o.c_str());
+}
+
+int main(int argc, char** argv) {
+  try {
+    auto game = LoadGame("coup");
+    auto state = game->NewInitialState();
+    if (argc == 2 && std::string(argv[1]) == "--illegal") {
+      for (int a : {4, 3, 2, 0}) state->ApplyAction(a);
+      const auto before = state->History();
+      try {
+        state->ApplyAction(9);  // Pass at the first decision
+        std::printf("{\"illegal\":\"accepted\"}\n");
+        return 1;
+      } catch (const SpielError& e) {
+        auto clone = state->Clone();
+        auto child = state->Child(0);
+        std::printf("{\"illegal\":\"rejected\",\"history\":%s,\"clone\":%s,\"child\":%s,\"roundtrip\":%s}\n",
+                    List(before).c_str(), List(clone->History()).c_str(), List(child->History()).c_str(),
+                    List(game->DeserializeState(child->Serialize())->History()).c_str());
+        return 0;
+      }
+    }
+    Dump(*state);
+    for (int i = 1; i < argc; ++i) {
+      state->ApplyAction(std::atoll(argv[i]));
+      Dump(*state);
+    }
+  } catch (const SpielError& e) {
+    std::fprintf(stderr, "SpielError: %s\n", e.what());
+    return 2;
+  }
+  return 0;
+}
