@@ -814,17 +814,8 @@ int obs_mode() {
   return (m >= 1 && m <= 7) ? m : kDefaultObsMode;
 }
 
-// Blocks of the step kernel: one per group of T lanes, or at most
-// COUP_STEP_WAVES_PER_CU x 256 CUs worth of waves (grid-stride) when set.
-unsigned step_grid(int64_t groups, int T) {
-  const char* e = std::getenv("COUP_STEP_WAVES_PER_CU");
-  int64_t g = groups;
-  if (e && std::atoi(e) > 0) {
-    const int64_t cap = (int64_t)std::atoi(e) * 256 * 64 / T;
-    g = groups < cap ? groups : cap;
-  }
-  return (unsigned)(g > 0 ? g : 1);
-}
+// Blocks of the step kernel: one per group of T lanes.
+unsigned step_grid(int64_t groups, int) { return (unsigned)(groups > 0 ? groups : 1); }
 
 unsigned grid_for(int64_t n) { return (unsigned)((n + coup::kThreads - 1) / coup::kThreads); }
 
