@@ -53,9 +53,20 @@ __global__ __launch_bounds__(kThreads) void k_step(StepArgs a) {
   a.sb[i] = wb;
   if (a.actions) a.actions[i] = (int8_t)act;
   if (a.rewards) {
+    // Rewards(): rc to everybody, -(N-1) rc to the loser; an even-N row
+    // starts 2-byte aligned, so it goes out as N/2 16-bit stores
+    const uint32_t win = rc & 0xFFu, lose = (uint32_t)(-(int32_t)((N - 1) * rc)) & 0xFFu;
+    if (N % 2 == 0) {
+      uint16_t* row = reinterpret_cast<uint16_t*>(a.rewards + i * N);
 #pragma unroll
-    for (int p = 0; p < N; ++p)
-      a.rewards[i * N + p] = (int8_t)((uint32_t)p == rl ? -(int32_t)((N - 1) * rc) : (int32_t)rc);
+      for (int k = 0; k < N / 2; ++k) {
+        const uint32_t lo = (uint32_t)(2 * k) == rl ? lose : win, hi = (uint32_t)(2 * k + 1) == rl ? lose : win;
+        row[k] = (uint16_t)(lo | (hi << 8));
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < N; ++p) a.rewards[i * N + p] = (int8_t)((uint32_t)p == rl ? lose : win);
+    }
   }
   if (a.step_type) a.step_type[i] = (uint8_t)st;
   if (a.legal) a.legal[i] = legal_mask(L);
