@@ -546,13 +546,18 @@ struct RegHistory {
     const uint64_t w = k < 4u ? q0 : (k < 8u ? q1 : q2);
     return (uint32_t)(w >> (16u * (k & 3u))) & 0xFFFFu;
   }
-  // write the records into a lane's history bytes, oldest first
+  // write the records into a lane's history bytes, oldest first.  Fully
+  // unrolled so every get() has a constant k: a run-time k selects between
+  // the three words, which LLVM lowers to an indexed load from scratch.
   __device__ __forceinline__ void flush(uint8_t* __restrict__ bytes) const {
     const uint32_t n = count < 12u ? count : 12u;
-    for (uint32_t k = n; k-- > 0;) {
-      const uint32_t r = get(k);
-      const uint32_t idx = r >> 8;
-      if (idx < kHistoryBytes) bytes[idx] = (uint8_t)(r & 0xFFu);
+#pragma unroll
+    for (int k = 11; k >= 0; --k) {
+      if ((uint32_t)k < n) {
+        const uint32_t r = get((uint32_t)k);
+        const uint32_t idx = r >> 8;
+        if (idx < kHistoryBytes) bytes[idx] = (uint8_t)(r & 0xFFu);
+      }
     }
   }
 };

@@ -114,27 +114,31 @@ __device__ __forceinline__ NLane<N> initial_lane(uint32_t episode) {
 
 // ------------------------------------------------------ per-seat fields
 
+// Seat p's hand.  Written as arithmetic on the three words (no select
+// between struct fields): LLVM turns a select of two fields of the lane
+// into an indexed load, which puts the whole lane in scratch memory.
 template <int N>
 __device__ __forceinline__ uint32_t hand(const NLane<N>& L, uint32_t p) {
-  const uint32_t w = (N <= 2 || p < 2u) ? L.hA : ((N <= 4 || p < 4u) ? L.hB : L.hC);
-  return (w >> (16u * (p & 1u))) & 0xFFFFu;
+  if (N <= 2) return (L.hA >> (16u * p)) & 0xFFFFu;
+  const uint64_t lo = ((uint64_t)L.hB << 32) | L.hA;  // seats 0..3
+  const uint32_t a = (uint32_t)(lo >> (16u * (p & 3u)));
+  if (N <= 4) return a & 0xFFFFu;
+  const uint32_t c = L.hC >> (16u * (p & 1u));  // seats 4, 5
+  const uint32_t hi = 0u - (uint32_t)(p >= 4u);  // all ones for seats 4, 5
+  return ((a & ~hi) | (c & hi)) & 0xFFFFu;
 }
 
 template <int N>
 __device__ __forceinline__ void set_hand(NLane<N>& L, uint32_t p, uint32_t h) {
   const uint32_t sh = 16u * (p & 1u);
-  const uint32_t keep = ~(0xFFFFu << sh), v = h << sh;
-  if (N <= 2) {
-    L.hA = (L.hA & keep) | v;
-    return;
-  }
-  L.hA = p < 2u ? ((L.hA & keep) | v) : L.hA;
-  if (N <= 4) {
-    L.hB = p >= 2u ? ((L.hB & keep) | v) : L.hB;
-    return;
-  }
-  L.hB = (p >= 2u && p < 4u) ? ((L.hB & keep) | v) : L.hB;
-  L.hC = p >= 4u ? ((L.hC & keep) | v) : L.hC;
+  const uint32_t field = 0xFFFFu << sh, v = h << sh;
+  // all-ones masks of the word that holds seat p
+  const uint32_t inA = 0u - (uint32_t)(p < 2u);
+  const uint32_t inB = 0u - (uint32_t)(p - 2u < 2u);
+  const uint32_t inC = 0u - (uint32_t)(p >= 4u);
+  L.hA = (L.hA & ~(field & inA)) | (v & inA);
+  if (N > 2) L.hB = (L.hB & ~(field & inB)) | (v & inB);
+  if (N > 4) L.hC = (L.hC & ~(field & inC)) | (v & inC);
 }
 
 template <int N>

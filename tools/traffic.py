@@ -107,15 +107,17 @@ def main():
         sys.exit(f"no FETCH_SIZE / WRITE_SIZE records for the step kernel under {src}; nothing written")
     summary["hbm_bytes_per_launch"] = traffic
     summary["correction"] = "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE halving)"
-    # issue mix of the timed kernel (SQ counters count quad-cycles; the
-    # VALUBusy formula is the gfx94x one rocprofv3 falls back to on gfx950:
-    # 100 x SQ_ACTIVE_INST_VALU x 4 / SIMDs / GRBM_GUI_ACTIVE, 1024 SIMDs)
+    # issue mix of the timed kernel.  SQ counters count quad-cycles, summed
+    # over all waves; GRBM_GUI_ACTIVE is summed over the 8 XCDs (per XCD it
+    # equals the kernel duration x ~2.4 GHz, checked below).  VALU busy =
+    # SIMD-cycles issuing VALU / SIMD-cycles available, 1024 SIMDs.
     sq = {c: counter("sq", c) for c in ("SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_ACTIVE_INST_ANY",
                                          "SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU", "SQ_WAIT_ANY", "GRBM_GUI_ACTIVE")}
     if all(v is not None for v in sq.values()) and sq["SQ_WAVE_CYCLES"] and sq["GRBM_GUI_ACTIVE"]:
         summary["issue"] = {
             "counters": sq,
-            "valu_busy_pct": 100.0 * sq["SQ_ACTIVE_INST_VALU"] * 4 / 1024 / sq["GRBM_GUI_ACTIVE"],
+            "valu_busy_pct": 100.0 * sq["SQ_ACTIVE_INST_VALU"] * 4 / 1024 / (sq["GRBM_GUI_ACTIVE"] / 8),
+            "gui_active_per_xcd_us_at_2.4GHz": sq["GRBM_GUI_ACTIVE"] / 8 / 2400.0,
             "wave_active_inst_frac": sq["SQ_ACTIVE_INST_ANY"] / sq["SQ_WAVE_CYCLES"],
             "wave_wait_frac": sq["SQ_WAIT_ANY"] / sq["SQ_WAVE_CYCLES"],
             "valu_insts_per_wave": sq["SQ_INSTS_VALU"] / max(sq["SQ_WAVES"], 1.0),
