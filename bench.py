@@ -18,7 +18,10 @@ Other configs (secondary lines, not the headline):
   c4r  c4 fused: `steps` 6-player env steps in ONE launch
 
 A "step" is one batched env step over all B lanes; value = env-steps/s of
-the whole job (N x B x K / max-over-ranks wall time).  Multi-GPU: one
+the whole job (N x B x K / max-over-ranks wall time).  Before the W warmup
+steps, --settle (default 256) untimed steps run through the fused rollout so
+the lanes are spread over game phases as in a long run (a freshly reset batch
+is in lock-step, and its first steps diverge less).  Multi-GPU: one
 process per GPU (torchrun), global env ids sharded by rank, no collective
 inside the step loop; the timed region ends with one RCCL all-gather of
 the ranks' final per-lane rewards/step types (trajectory collation).
@@ -68,6 +71,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--settle", type=int, default=256,
+                    help="untimed env steps run first through the fused rollout (same trajectories as "
+                         "coup_step), so the timed steps see the steady-state mix of game phases rather "
+                         "than 2^20 lanes that all started together (not for info-state configs)")
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--seed", type=int, default=1)
@@ -161,6 +168,8 @@ def main():
         torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream(dev)
+    if args.settle > 0 and not with_info:
+        env.rollout(args.settle)
     graph = None
     if not fused and (args.graph == "on" or (args.graph == "auto" and cfg in GRAPH_AUTO)):
         for _ in range(args.warmup):
@@ -231,6 +240,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle_steps": args.settle if not with_info else 0,
             "ms_per_step": elapsed * 1e3 / args.steps,
             "higher_is_better": True,
             "scaling": "weak",
