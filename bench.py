@@ -41,9 +41,11 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# configs whose step kernel (9 us, 45 us) is shorter than the host's
-# per-step launch cost: their K timed steps replay from one HIP graph
-GRAPH_AUTO = ("c2", "c4")
+# configs whose K timed steps replay from one HIP graph: c2 and c4, whose
+# step kernels (9 us, 60 us) are shorter than the host's per-step launch
+# cost, and c3, where the graph removes the ~6 us gap per step that eager
+# launches leave between kernels
+GRAPH_AUTO = ("c2", "c3", "c4")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
 
@@ -82,8 +84,8 @@ def parse():
                     help="target duration of the bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
-                    help="replay the K timed steps from one HIP graph (auto: on for c2 and c4, "
-                         "whose step kernels are shorter than the host's per-step launch cost)")
+                    help="replay the K timed steps from one HIP graph (auto: on for c2, c3 and c4, "
+                         "where it removes the per-step launch gaps)")
     return ap.parse_args()
 
 
@@ -184,6 +186,10 @@ def main():
             env.step()
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(args.steps)]
+    if world > 1:
+        # first all-gather outside the timed region (RCCL sets up its
+        # all-gather channels lazily on first use)
+        D.collate(torch.cat([env.rewards.view(torch.uint8), env.step_type.view(-1, 1)], 1))
     barrier()
     t0 = time.perf_counter()
     if graph is not None:

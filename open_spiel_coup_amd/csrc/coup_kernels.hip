@@ -440,10 +440,24 @@ struct StepArgs {
   uint8_t* hist;   // [B][96] history bytes (INFO != kInfoNone)
   float* info;     // [B][2][2492] (INFO == kInfoWrite)
   uint32_t* err_count;
+  int xcd_remap;   // block -> lane group mapping (xcd_group)
 };
 
+// Lane group of block b in a grid of G.  Blocks are dealt round-robin over
+// the 8 XCDs (MI355X_MICROARCH.md, workgroup dispatch), so without a remap
+// neighbouring groups -- and their neighbouring obs rows -- land on
+// different XCDs.  The remap gives XCD x the contiguous run of groups
+// [x G/8, (x+1) G/8) in dispatch order; blocks past the last full round of 8
+// keep their own index.  A bijection on [0, G).  Measured on the obs store
+// stream alone: 157 -> 143 us (tools/store_probe.hip).
+__device__ __forceinline__ uint32_t xcd_group(uint32_t b, uint32_t G) {
+  const uint32_t full = G & ~7u;
+  if (b >= full) return b;
+  return (b & 7u) * (full >> 3) + (b >> 3);
+}
+
 // Observation write-out variants (COUP_OBS_MODE selects one at run time for
-// A/B measurements; kObsBlockBits at 1024 threads is the default):
+// A/B measurements; kObsWaveBits is the default):
 //   1 per-lane rows (each lane stores its own 784 B; uncoalesced)
 //   2/3 wave-cooperative, ds_bpermute keys + descriptor table (plain / nt)
 //   4 wave-cooperative from the LDS bitmap, nt stores
@@ -535,7 +549,8 @@ __global__ __launch_bounds__(T, INFO == kInfoNone ? 8 : 4) void k_step(StepArgs 
   // One group of T lanes per block.  (A grid-stride "persistent" variant,
   // where a wave's stores for one group drain while it steps the next, was
   // measured no faster and raised register pressure)
-  step_group<UNIFORM, OBS, T, INFO>(a, blockIdx.x, lds);
+  const uint32_t grp = a.xcd_remap ? xcd_group(blockIdx.x, gridDim.x) : blockIdx.x;
+  step_group<UNIFORM, OBS, T, INFO>(a, grp, lds);
 }
 
 template <bool UNIFORM, int OBS, int T, int INFO>
@@ -814,6 +829,13 @@ int obs_mode() {
   return (m >= 1 && m <= 7) ? m : kDefaultObsMode;
 }
 
+// COUP_XCD_REMAP=0 turns off the XCD-aware block -> lane group mapping of
+// the step kernel (coup::xcd_group; A/B measurements).
+int xcd_remap() {
+  const char* e = std::getenv("COUP_XCD_REMAP");
+  return e ? (std::atoi(e) != 0) : 1;
+}
+
 // Blocks of the step kernel: one per group of T lanes.
 unsigned step_grid(int64_t groups, int) { return (unsigned)(groups > 0 ? groups : 1); }
 
@@ -963,6 +985,10 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
   a.actions_in = actions;
   a.err_count = env->err_count;
   a.hist = env->hist;
+  a.xcd_remap = xcd_remap();
+  // COUP_STEP_DYN_LDS: extra LDS per block, to cap blocks per CU (A/B only)
+  const char* dl = std::getenv("COUP_STEP_DYN_LDS");
+  const unsigned dyn_lds = dl ? (unsigned)std::atoi(dl) : 0u;
   if (out) {
     a.actions = out->actions;
     a.rewards = out->rewards;
@@ -981,7 +1007,7 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
   hipStream_t s = env->stream;
   const int64_t n = env->batch;
 #define COUP_LAUNCH_STEP(U, M, T, I) \
-  coup::k_step<U, M, T, I><<<step_grid((n + (T)-1) / (T), T), T, 0, s>>>(a)
+  coup::k_step<U, M, T, I><<<step_grid((n + (T)-1) / (T), T), T, dyn_lds, s>>>(a)
 #define COUP_LAUNCH_MODES(U)                                                                         \
   if (info == coup::kInfoNone) {                                                                     \
     switch (mode) {                                                                                  \
@@ -989,10 +1015,10 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
       case 1: COUP_LAUNCH_STEP(U, coup::kObsLaneRows, 256, coup::kInfoNone); break;                  \
       case 2: COUP_LAUNCH_STEP(U, coup::kObsWave, 256, coup::kInfoNone); break;                      \
       case 3: COUP_LAUNCH_STEP(U, coup::kObsWaveNT, 256, coup::kInfoNone); break;                    \
-      case 4: COUP_LAUNCH_STEP(U, coup::kObsWaveBits, 256, coup::kInfoNone); break;                  \
       case 5: COUP_LAUNCH_STEP(U, coup::kObsBlockBits, 256, coup::kInfoNone); break;                 \
       case 6: COUP_LAUNCH_STEP(U, coup::kObsBlockBits, 1024, coup::kInfoNone); break;                \
-      default: COUP_LAUNCH_STEP(U, coup::kObsBlockBitsNT, 1024, coup::kInfoNone); break;             \
+      case 7: COUP_LAUNCH_STEP(U, coup::kObsBlockBitsNT, 1024, coup::kInfoNone); break;              \
+      default: COUP_LAUNCH_STEP(U, coup::kObsWaveBits, 256, coup::kInfoNone); break;                 \
     }                                                                                                \
   } else if (info == coup::kInfoHistory) {                                                           \
     if (mode == 0) COUP_LAUNCH_STEP(U, coup::kObsNone, 256, coup::kInfoHistory);                     \

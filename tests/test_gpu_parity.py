@@ -113,12 +113,16 @@ def test_uniform_rollout_matches_oracle(auto_reset):
 
 
 @pytest.mark.parametrize("mode", ["1", "2", "3", "4", "5", "6", "7"])
-def test_obs_writers_match_oracle(mode, monkeypatch):
-    """Every observation writer (per-lane rows, wave-cooperative, wave +
-    non-temporal) gives the oracle's tensors, including a ragged last wave
-    (1000 lanes = 15 full waves + 40)."""
+@pytest.mark.parametrize("n,remap", [(1000, "1"), (8 * 256 * 3 + 1000, "1"), (8 * 256 * 3 + 1000, "0")])
+def test_obs_writers_match_oracle(mode, n, remap, monkeypatch):
+    """Every observation writer (per-lane rows, wave-cooperative from keys,
+    bitmap, block-cooperative; plain / nt stores) gives
+    the oracle's tensors, including a ragged last wave (1000 lanes = 15 full
+    waves + 40) and, at 7144 lanes (27 full blocks + 232 lanes), the
+    XCD-aware block -> group remap with blocks past the last round of 8."""
     monkeypatch.setenv("COUP_OBS_MODE", mode)
-    n, steps, seed = 1000, 40, 17
+    monkeypatch.setenv("COUP_XCD_REMAP", remap)
+    steps, seed = 40, 17
     ref = oracle.rollout(seed=seed, n=n, steps=steps, want_obs=True)
     env = BatchedCoupEnv(n, seed=seed, obs=True)
     guard = torch.full((n + 64, 2, 98), -7.0, device="cuda")

@@ -1,0 +1,152 @@
+// store_probe.hip -- store-order probe for the ObservationTensor write-out
+// (DESIGN.md section 5).  Every variant writes the same 784 MiB buffer
+// ([2^20][2][98] fp32) with no compute, under the step kernel's constraint
+// that a wave (or block) owns the rows of its own lanes; only the order,
+// the cache policy, the block size and the block -> chunk mapping change.
+// Measurement tool only.
+//   hipcc --offload-arch=gfx950 -O3 -o tools/store_probe tools/store_probe.hip
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+
+typedef float v4f __attribute__((ext_vector_type(4)));
+
+constexpr int kRowF4 = 49;              // float4 per lane (2 x 98 floats)
+constexpr int kWaveF4 = 64 * kRowF4;    // 3136 float4 = 50,176 B per wave
+
+// cache policy of one 16-byte store: 0 plain, 1 nt, 2 sc1, 3 sc0 sc1, 4 sc0 sc1 nt
+template <int POL>
+__device__ __forceinline__ void st(v4f* p, v4f v) {
+  if (POL == 0) {
+    *p = v;
+  } else if (POL == 1) {
+    __builtin_nontemporal_store(v, p);
+  } else if (POL == 2) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+  } else if (POL == 3) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+  } else {
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");
+  }
+}
+
+// XCD-aware chunk id: blocks are dealt round-robin over the 8 XCDs, so
+// block b runs on XCD b % 8; give XCD x the contiguous run of chunks
+// [x * G/8, (x+1) * G/8) in dispatch order.
+// With S < G/8, XCD x owns every 8th run of S consecutive chunks instead.
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t G, uint32_t S) {
+  if (S == 0u) S = G / 8u;
+  const uint32_t r = b / 8u;  // rank of the block among its XCD's blocks
+  return (r / S) * 8u * S + (b % 8u) * S + r % S;
+}
+
+// Wave chunks: each wave writes its own 50 KiB as 49 x 1 KiB instructions.
+// ROT: wave w starts at iteration w % 49 (spreads concurrent writes over rows).
+template <int T, int POL, bool XCD, bool ROT>
+__global__ __launch_bounds__(T) void k_wave_chunks(v4f* __restrict__ dst, uint32_t waves, uint32_t S) {
+  const v4f z = {0.f, 1.f, 0.f, 0.f};
+  const uint32_t b = XCD ? xcd_remap(blockIdx.x, gridDim.x, S) : blockIdx.x;
+  const uint32_t wave = b * (T / 64) + threadIdx.x / 64;
+  const uint32_t lane = threadIdx.x & 63u;
+  if (wave >= waves) return;
+  v4f* base = dst + (size_t)wave * kWaveF4;
+  const uint32_t r = ROT ? wave % kRowF4 : 0u;
+#pragma unroll 7
+  for (uint32_t j = 0; j < (uint32_t)kRowF4; ++j) {
+    uint32_t jj = j + r;
+    jj = jj >= (uint32_t)kRowF4 ? jj - kRowF4 : jj;
+    st<POL>(base + 64u * jj + lane, z);
+  }
+}
+
+// Block chunks: the block's T lanes own T x 784 B; iteration j writes T float4.
+template <int T, int POL, bool XCD>
+__global__ __launch_bounds__(T) void k_block_chunks(v4f* __restrict__ dst, uint32_t S) {
+  const v4f z = {0.f, 1.f, 0.f, 0.f};
+  const uint32_t b = XCD ? xcd_remap(blockIdx.x, gridDim.x, S) : blockIdx.x;
+  v4f* base = dst + (size_t)b * T * kRowF4;
+#pragma unroll 7
+  for (uint32_t j = 0; j < (uint32_t)kRowF4; ++j) st<POL>(base + T * j + threadIdx.x, z);
+}
+
+// Unconstrained reference: grid-stride float4 sweep.
+template <int POL>
+__global__ __launch_bounds__(256) void k_sweep(v4f* __restrict__ dst, size_t n) {
+  const v4f z = {0.f, 1.f, 0.f, 0.f};
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) st<POL>(dst + i, z);
+}
+
+#define CK(x)                                                    \
+  do {                                                           \
+    hipError_t e = (x);                                          \
+    if (e != hipSuccess) {                                       \
+      std::printf("%s: %s\n", #x, hipGetErrorString(e));         \
+      return 1;                                                  \
+    }                                                            \
+  } while (0)
+
+int main() {
+  const size_t lanes = (size_t)1 << 20;
+  const size_t bytes = lanes * 784;
+  const size_t n = bytes / 16;
+  const uint32_t waves = (uint32_t)(lanes / 64);
+  v4f* a;
+  CK(hipMalloc(&a, bytes));
+  CK(hipMemset(a, 0, bytes));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const int reps = 20;
+  auto timed = [&](const char* name, int grid, int block, auto launch) -> int {
+    for (int w = 0; w < 3; ++w) launch();
+    CK(hipGetLastError());
+    CK(hipEventRecord(e0));
+    for (int r = 0; r < reps; ++r) launch();
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    std::printf("{\"kernel\": \"%s\", \"grid\": %d, \"block\": %d, \"bytes\": %.0f, \"us\": %.2f, \"GBps\": %.1f}\n",
+                name, grid, block, (double)bytes, ms * 1e3 / reps, (double)bytes / (ms * 1e-3 / reps) / 1e9);
+    std::fflush(stdout);
+    return 0;
+  };
+  char name[96];
+#define WAVE(T, POL, XCD, S)                                                                      \
+  std::snprintf(name, sizeof name, "wave_t%d_pol%d_xcd%d_S%d", T, POL, (int)XCD, S);              \
+  timed(name, (int)(waves / (T / 64)), T,                                                        \
+        [&] { k_wave_chunks<T, POL, XCD, false><<<waves / (T / 64), T>>>(a, waves, S); })
+  WAVE(256, 1, false, 0);
+  WAVE(256, 0, false, 0);
+  WAVE(256, 0, true, 0);
+  WAVE(256, 2, true, 0);
+  WAVE(256, 3, true, 0);
+  WAVE(64, 0, true, 0);
+  WAVE(64, 2, true, 0);
+  WAVE(128, 0, true, 0);
+  WAVE(512, 0, true, 0);
+  WAVE(1024, 0, true, 0);
+  for (int S : {1, 2, 4, 8, 16, 32, 64, 128, 256}) {
+    WAVE(256, 0, true, S);
+  }
+  for (int S : {4, 16, 64, 256, 1024}) {
+    WAVE(64, 0, true, S);
+  }
+#undef WAVE
+#define BLOCK(T, POL, XCD, S)                                                                     \
+  std::snprintf(name, sizeof name, "block_t%d_pol%d_xcd%d_S%d", T, POL, (int)XCD, S);             \
+  timed(name, (int)(lanes / T), T, [&] { k_block_chunks<T, POL, XCD><<<lanes / T, T>>>(a, S); })
+  BLOCK(256, 0, true, 0);
+  BLOCK(256, 2, true, 0);
+  BLOCK(1024, 0, true, 0);
+  BLOCK(1024, 2, true, 0);
+  BLOCK(1024, 2, false, 0);
+  BLOCK(512, 0, true, 0);
+#undef BLOCK
+  for (int grid : {65536, 131072}) {
+    timed("sweep_plain", grid, 256, [&] { k_sweep<0><<<grid, 256>>>(a, n); });
+    timed("sweep_nt", grid, 256, [&] { k_sweep<1><<<grid, 256>>>(a, n); });
+  }
+  CK(hipFree(a));
+  return 0;
+}
