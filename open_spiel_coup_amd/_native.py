@@ -8,7 +8,9 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libcoup_mi355x.so")
+# COUP_LIB_PATH: load another build of the same library (A/B timing of two
+# builds, tools/ab_builds.sh); there is still no fallback
+LIB_PATH = os.environ.get("COUP_LIB_PATH") or os.path.join(HERE, "libcoup_mi355x.so")
 ABI_VERSION = 3
 FLAG_AUTO_RESET, FLAG_HISTORY, FLAG_GENERIC = 1, 2, 4
 MAX_PLAYERS = 6

@@ -20,9 +20,9 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("COUP_OFFLOAD_ARCH", "gfx950")
 
 
-def command(resource_usage=False):
+def command(resource_usage=False, out=OUT, defines=()):
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-I", os.path.join(ROOT, "include"), "-o", OUT] + SOURCES
+           "-Wall", "-I", os.path.join(ROOT, "include"), "-o", out] + [f"-D{d}" for d in defines] + SOURCES
     if resource_usage:
         cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
     return cmd
@@ -49,7 +49,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--out", default=None, help="measurement builds: write the library elsewhere")
+    ap.add_argument("--define", action="append", default=[], help="measurement builds: e.g. COUP_WAVE_TRACE")
     a = ap.parse_args()
+    if a.out or a.define:
+        out = os.path.abspath(a.out or OUT)
+        subprocess.check_call(command(a.verbose, out, a.define))
+        print(out)
+        return
     print(build(force=a.force, verbose=a.verbose))
 
 

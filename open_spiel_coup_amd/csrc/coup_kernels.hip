@@ -246,16 +246,35 @@ __device__ __forceinline__ void obs_bits_to_lds(const Lane& L, uint32_t* __restr
 
 // wave_bits: this wave's 64 x 8 LDS words, written by obs_bits_to_lds and
 // made visible by a barrier before the call.
+// Store policy of the wave-bitmap writer: 0 plain, 1 non-temporal (global
+// stores), 2 sc1 write-through (buffer stores through a wave-uniform
+// resource whose range ends at the wave's last row, so rows past the batch
+// are dropped by the range check instead of a per-store predicate).
+template <int POL, class V>
+__device__ __forceinline__ void store_f4(V* p, const V& v) {
+  if (POL == 0)
+    *p = v;
+  else
+    __builtin_nontemporal_store(v, p);
+}
+
+// FULL: all 64 rows of the wave exist (no per-store predicate, so the
+// unrolled iterations' LDS reads can be hoisted ahead of their stores).
+// (x, o, c) = (64 j + lane, x / 49, x % 49) advance incrementally: x += 64
+// is one row (49) plus 15.
+template <int POL, bool FULL>
 __device__ __forceinline__ void write_obs_wave_bits(float* __restrict__ wave_obs, const uint32_t* __restrict__ wave_bits,
                                                     uint32_t n_valid) {
   typedef float v4f __attribute__((ext_vector_type(4)));
-  v4f* dst = reinterpret_cast<v4f*>(wave_obs);
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
   const uint32_t lane = threadIdx.x & 63u;
+  v4f* dst = reinterpret_cast<v4f*>(wave_obs) + lane;
+  __amdgpu_buffer_rsrc_t rsrc;
+  if (POL == 2) rsrc = __builtin_amdgcn_make_buffer_rsrc(wave_obs, (short)0, (int)(n_valid * 2u * kObsSize * 4u), 0x00020000);
+  uint32_t o = lane >= (uint32_t)kRowF4 ? 1u : 0u;
+  uint32_t c = lane - o * (uint32_t)kRowF4;
 #pragma unroll 7
   for (uint32_t j = 0; j < (uint32_t)kRowF4; ++j) {
-    const uint32_t x = 64u * j + lane;
-    const uint32_t o = x / (uint32_t)kRowF4;
-    const uint32_t c = x - o * (uint32_t)kRowF4;
     const uint32_t word = wave_bits[8u * o + (c >> 3)];
     const uint32_t coins = wave_bits[8u * o + 7u];
     const uint32_t nb = word >> (4u * (c & 7u));
@@ -269,7 +288,15 @@ __device__ __forceinline__ void write_obs_wave_bits(float* __restrict__ wave_obs
     v.y = c == 15u ? c1 : v.y;
     v.z = c == 39u ? c0 : v.z;
     v.w = c == 39u ? c1 : v.w;
-    if (o < n_valid) __builtin_nontemporal_store(v, dst + x);
+    if (POL == 2)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), rsrc, (int)(16u * (64u * j + lane)), 0, 16);
+    else if (FULL || o < n_valid)
+      store_f4<POL>(dst + 64u * j, v);
+    c += 15u;
+    o += 1u;
+    const bool wrap = c >= (uint32_t)kRowF4;
+    c = wrap ? c - (uint32_t)kRowF4 : c;
+    o += wrap ? 1u : 0u;
   }
 }
 
@@ -441,7 +468,26 @@ struct StepArgs {
   float* info;     // [B][2][2492] (INFO == kInfoWrite)
   uint32_t* err_count;
   int xcd_remap;   // block -> lane group mapping (xcd_group)
+#ifdef COUP_WAVE_TRACE
+  // measurement builds only (tools/wave_trace.py): per wave, 100 MHz
+  // timestamps at entry, end of the step, end of store issue, stores
+  // drained, then HW_ID << 32 | XCC_ID, then the state load's return
+  uint64_t* trace;
+#endif
 };
+
+#ifdef COUP_WAVE_TRACE
+#define COUP_TRACE(a, k)                                                                           \
+  do {                                                                                             \
+    if ((a).trace && (threadIdx.x & 63u) == 0u)                                                    \
+      (a).trace[((size_t)blockIdx.x * (blockDim.x / 64u) + threadIdx.x / 64u) * 6u + (k)] =       \
+          __builtin_amdgcn_s_memrealtime();                                                        \
+  } while (0)
+#else
+#define COUP_TRACE(a, k) \
+  do {                   \
+  } while (0)
+#endif
 
 // Lane group of block b in a grid of G.  Blocks are dealt round-robin over
 // the 8 XCDs (MI355X_MICROARCH.md, workgroup dispatch), so without a remap
@@ -463,10 +509,13 @@ __device__ __forceinline__ uint32_t xcd_group(uint32_t b, uint32_t G) {
 //   4 wave-cooperative from the LDS bitmap, nt stores
 //   5/6 block-cooperative from the LDS bitmap, 256 / 1024 threads, plain stores
 //   7 block-cooperative, 1024 threads, nt stores
+//   8/9 as 4 with plain / sc1 (write-through) stores
 enum ObsMode : int {
   kObsNone = 0, kObsLaneRows = 1, kObsWave = 2, kObsWaveNT = 3, kObsWaveBits = 4,
-  kObsBlockBits = 5, kObsBlockBitsNT = 7
+  kObsBlockBits = 5, kObsBlockBitsNT = 7, kObsWaveBitsPlain = 8, kObsWaveBitsSc1 = 9
 };
+constexpr bool is_wave_bits(int m) { return m == kObsWaveBits || m == kObsWaveBitsPlain || m == kObsWaveBitsSc1; }
+constexpr int wave_bits_policy(int m) { return m == kObsWaveBitsPlain ? 0 : (m == kObsWaveBitsSc1 ? 2 : 1); }
 
 // The per-lane part of one env step: returns the decision applied (-1 if
 // none), the step type and player 0's reward; L is updated in place and
@@ -527,7 +576,7 @@ enum InfoMode : int { kInfoNone = 0, kInfoHistory = 1, kInfoWrite = 2 };
 template <int OBS, int T, int INFO>
 struct StepLds {
   static constexpr bool kDesc = OBS == kObsWave || OBS == kObsWaveNT;
-  static constexpr bool kBits = OBS == kObsWaveBits || OBS == kObsBlockBits || OBS == kObsBlockBitsNT;
+  static constexpr bool kBits = is_wave_bits(OBS) || OBS == kObsBlockBits || OBS == kObsBlockBitsNT;
   uint4 desc[kDesc ? kRowF4 : 1];
   uint32_t bits[kBits ? T * 8 : 1];
   uint8_t hist[INFO != kInfoNone ? T * kHist : 16];
@@ -535,7 +584,14 @@ struct StepLds {
 };
 
 template <bool UNIFORM, int OBS, int T, int INFO>
-__device__ __forceinline__ void step_group(const StepArgs& a, int64_t grp, StepLds<OBS, T, INFO>& lds);
+__device__ __forceinline__ void step_group(const StepArgs& a, int64_t grp, StepLds<OBS, T, INFO>& lds, uint4 rec);
+
+// This thread's lane record of group grp (zeros past the batch).
+template <int T>
+__device__ __forceinline__ uint4 load_record(const StepArgs& a, int64_t grp) {
+  const int64_t i = grp * T + threadIdx.x;
+  return i < a.n ? a.state[i] : make_uint4(0u, 0u, 0u, 0u);
+}
 
 // One rl_environment step per lane (rl_environment.py:282-322), optionally
 // with SyncVectorEnv auto-reset (vector_env.py:40-67).  T threads per block.
@@ -546,15 +602,51 @@ template <bool UNIFORM, int OBS, int T, int INFO>
 __global__ __launch_bounds__(T, INFO == kInfoNone ? 8 : 4) void k_step(StepArgs a) {
   __shared__ StepLds<OBS, T, INFO> lds;
   if (StepLds<OBS, T, INFO>::kDesc) load_obs_desc(reinterpret_cast<uint32_t*>(lds.desc));
-  // One group of T lanes per block.  (A grid-stride "persistent" variant,
-  // where a wave's stores for one group drain while it steps the next, was
-  // measured no faster and raised register pressure)
+  // One group of T lanes per block.  (A persistent variant -- a resident
+  // grid looping over groups, loading the next group's records one group
+  // ahead -- measured no faster: DESIGN.md section 5.)
+  COUP_TRACE(a, 0);
   const uint32_t grp = a.xcd_remap ? xcd_group(blockIdx.x, gridDim.x) : blockIdx.x;
-  step_group<UNIFORM, OBS, T, INFO>(a, grp, lds);
+  step_group<UNIFORM, OBS, T, INFO>(a, grp, lds, load_record<T>(a, grp));
+#ifdef COUP_WAVE_TRACE
+  COUP_TRACE(a, 2);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  COUP_TRACE(a, 3);
+  if (a.trace && (threadIdx.x & 63u) == 0u)
+    a.trace[((size_t)blockIdx.x * (blockDim.x / 64u) + threadIdx.x / 64u) * 6u + 4u] =
+        ((uint64_t)__builtin_amdgcn_s_getreg(4 | (31 << 11)) << 32) | (uint32_t)__builtin_amdgcn_s_getreg(20 | (31 << 11));
+#endif
+}
+
+// Obs store loop of a wave-bitmap group whose words are in LDS.
+template <int OBS, int T, int INFO>
+__device__ __forceinline__ void step_group_store(const StepArgs& a, int64_t grp, StepLds<OBS, T, INFO>& lds) {
+  const uint32_t wl = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x & ~63u));
+  const int64_t wave0 = grp * T + wl;
+  const int64_t wleft = a.n - wave0;
+  const uint32_t wave_valid = wleft >= 64 ? 64u : (wleft > 0 ? (uint32_t)wleft : 0u);  // wave-uniform
+  float* wave_obs = a.obs + wave0 * (2 * kObsSize);
+  if (wave_valid == 64u)
+    write_obs_wave_bits<wave_bits_policy(OBS), true>(wave_obs, lds.bits + wl * 8u, 64u);
+  else if (wave_valid > 0u)
+    write_obs_wave_bits<wave_bits_policy(OBS), false>(wave_obs, lds.bits + wl * 8u, wave_valid);
+  wave_sync();  // words read before the next group overwrites them
+}
+
+// Step of group grp up to (for the wave-bitmap writers) the words in LDS.
+template <bool UNIFORM, int OBS, int T, int INFO>
+__device__ __forceinline__ void step_group_compute(const StepArgs& a, int64_t grp, StepLds<OBS, T, INFO>& lds,
+                                                   uint4 rec);
+
+template <bool UNIFORM, int OBS, int T, int INFO>
+__device__ __forceinline__ void step_group(const StepArgs& a, int64_t grp, StepLds<OBS, T, INFO>& lds, uint4 rec) {
+  step_group_compute<UNIFORM, OBS, T, INFO>(a, grp, lds, rec);
+  if (is_wave_bits(OBS)) step_group_store<OBS, T, INFO>(a, grp, lds);
 }
 
 template <bool UNIFORM, int OBS, int T, int INFO>
-__device__ __forceinline__ void step_group(const StepArgs& a, int64_t grp, StepLds<OBS, T, INFO>& lds) {
+__device__ __forceinline__ void step_group_compute(const StepArgs& a, int64_t grp, StepLds<OBS, T, INFO>& lds,
+                                                   uint4 rec) {
   constexpr bool kDesc = StepLds<OBS, T, INFO>::kDesc;
   constexpr bool kBits = StepLds<OBS, T, INFO>::kBits;
   const int64_t i = grp * T + threadIdx.x;
@@ -572,7 +664,11 @@ __device__ __forceinline__ void step_group(const StepArgs& a, int64_t grp, StepL
   }
   Lane L = initial_lane(0);
   if (active) {
-    L = unpack(a.state[i]);
+    L = unpack(rec);
+#ifdef COUP_WAVE_TRACE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    COUP_TRACE(a, 5);
+#endif
     int act;
     uint32_t st;
     int32_t rew;
@@ -603,7 +699,8 @@ __device__ __forceinline__ void step_group(const StepArgs& a, int64_t grp, StepL
       write_info_wave(a.info + wave0 * (2 * kInfoSize), hist_wave, lds.pre + wl * kPreWords, wave_valid);
     wave_sync();  // this group's LDS words read before the next group reuses them
   }
-  if (OBS == kObsWaveBits) {
+  COUP_TRACE(a, 1);
+  if (is_wave_bits(OBS)) {
     // each wave reads only its own lanes' words: a wave-scope hand-off
     obs_bits_to_lds(L, lds.bits + threadIdx.x * 8u);
     wave_sync();
@@ -617,14 +714,8 @@ __device__ __forceinline__ void step_group(const StepArgs& a, int64_t grp, StepL
     const int64_t left = a.n - block0;
     const uint32_t n_valid = left >= T ? (uint32_t)T : (uint32_t)left;  // block-uniform, > 0
     write_obs_block_bits<T, OBS == kObsBlockBitsNT>(a.obs + block0 * (2 * kObsSize), lds.bits, n_valid);
-  } else if (kDesc || OBS == kObsWaveBits) {
-    if (wave_valid > 0) {
-      if (OBS == kObsWaveBits)
-        write_obs_wave_bits(a.obs + wave0 * (2 * kObsSize), lds.bits + wl * 8u, wave_valid);
-      else
-        write_obs_wave<OBS == kObsWaveNT>(a.obs + wave0 * (2 * kObsSize), obs_key(L), wave_valid, lds.desc);
-    }
-    if (OBS == kObsWaveBits) wave_sync();  // words read before the next group overwrites them
+  } else if (kDesc && wave_valid > 0) {
+    write_obs_wave<OBS == kObsWaveNT>(a.obs + wave0 * (2 * kObsSize), obs_key(L), wave_valid, lds.desc);
   }
 }
 
@@ -773,7 +864,7 @@ __global__ __launch_bounds__(kThreads) void k_query(QueryArgs a) {
   if (OBS) {
     obs_bits_to_lds(L, bits + threadIdx.x * 8u);
     wave_sync();
-    if (wave_valid) write_obs_wave_bits(a.obs + wave0 * (2 * kObsSize), bits + wl * 8u, wave_valid);
+    if (wave_valid) write_obs_wave_bits<1, false>(a.obs + wave0 * (2 * kObsSize), bits + wl * 8u, wave_valid);
   }
   if (INFO) {
     if (wave_valid)
@@ -819,14 +910,14 @@ int fail(int code, const std::string& msg) {
 #define COUP_CHECK_ENV(env) \
   if (!(env)) return fail(COUP_E_INVALID, "null coup_env")
 
-// COUP_OBS_MODE=1..7 overrides the observation writer (A/B measurements;
+// COUP_OBS_MODE=1..9 overrides the observation writer (A/B measurements;
 // the modes are listed at coup::ObsMode).  4 = wave-cooperative bitmap,
 // non-temporal stores.
 constexpr int kDefaultObsMode = 4;
 int obs_mode() {
   const char* e = std::getenv("COUP_OBS_MODE");
   const int m = e ? std::atoi(e) : kDefaultObsMode;
-  return (m >= 1 && m <= 7) ? m : kDefaultObsMode;
+  return (m >= 1 && m <= 9) ? m : kDefaultObsMode;
 }
 
 // COUP_XCD_REMAP=0 turns off the XCD-aware block -> lane group mapping of
@@ -839,6 +930,10 @@ int xcd_remap() {
 // Blocks of the step kernel: one per group of T lanes.
 unsigned step_grid(int64_t groups, int) { return (unsigned)(groups > 0 ? groups : 1); }
 
+template <bool U, int M, int T, int I>
+void launch_step(const coup_env*, const coup::StepArgs& a, int64_t n, unsigned dyn_lds, hipStream_t s) {
+  coup::k_step<U, M, T, I><<<step_grid((n + T - 1) / T, T), T, dyn_lds, s>>>(a);
+}
 unsigned grid_for(int64_t n) { return (unsigned)((n + coup::kThreads - 1) / coup::kThreads); }
 
 coup::np::Env np_env(const coup_env* env) {
@@ -967,6 +1062,16 @@ int coup_new_initial_state(coup_env* env, const uint8_t* lane_mask) {
   return launch_reset(env, lane_mask, /*mode=*/1, /*deal=*/0);
 }
 
+#ifdef COUP_WAVE_TRACE
+static uint64_t* g_trace = nullptr;
+// measurement builds only: per-wave timestamps of the following coup_step
+// launches go to `buf` ([blocks * waves per block][5] u64), or nowhere (null)
+int coup_debug_set_trace(uint64_t* buf) {
+  g_trace = buf;
+  return COUP_OK;
+}
+#endif
+
 int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out) {
   COUP_CHECK_ENV(env);
   if (env->batch == 0) return COUP_OK;
@@ -986,6 +1091,9 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
   a.err_count = env->err_count;
   a.hist = env->hist;
   a.xcd_remap = xcd_remap();
+#ifdef COUP_WAVE_TRACE
+  a.trace = g_trace;
+#endif
   // COUP_STEP_DYN_LDS: extra LDS per block, to cap blocks per CU (A/B only)
   const char* dl = std::getenv("COUP_STEP_DYN_LDS");
   const unsigned dyn_lds = dl ? (unsigned)std::atoi(dl) : 0u;
@@ -1006,8 +1114,7 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
   if (info != coup::kInfoNone && mode != coup::kObsNone) mode = coup::kObsWaveBits;
   hipStream_t s = env->stream;
   const int64_t n = env->batch;
-#define COUP_LAUNCH_STEP(U, M, T, I) \
-  coup::k_step<U, M, T, I><<<step_grid((n + (T)-1) / (T), T), T, dyn_lds, s>>>(a)
+#define COUP_LAUNCH_STEP(U, M, T, I) launch_step<U, M, T, I>(env, a, n, dyn_lds, s)
 #define COUP_LAUNCH_MODES(U)                                                                         \
   if (info == coup::kInfoNone) {                                                                     \
     switch (mode) {                                                                                  \
@@ -1018,6 +1125,8 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
       case 5: COUP_LAUNCH_STEP(U, coup::kObsBlockBits, 256, coup::kInfoNone); break;                 \
       case 6: COUP_LAUNCH_STEP(U, coup::kObsBlockBits, 1024, coup::kInfoNone); break;                \
       case 7: COUP_LAUNCH_STEP(U, coup::kObsBlockBitsNT, 1024, coup::kInfoNone); break;              \
+      case 8: COUP_LAUNCH_STEP(U, coup::kObsWaveBitsPlain, 256, coup::kInfoNone); break;             \
+      case 9: COUP_LAUNCH_STEP(U, coup::kObsWaveBitsSc1, 256, coup::kInfoNone); break;               \
       default: COUP_LAUNCH_STEP(U, coup::kObsWaveBits, 256, coup::kInfoNone); break;                 \
     }                                                                                                \
   } else if (info == coup::kInfoHistory) {                                                           \

@@ -112,7 +112,7 @@ def test_uniform_rollout_matches_oracle(auto_reset):
     assert env.error_count() == 0
 
 
-@pytest.mark.parametrize("mode", ["1", "2", "3", "4", "5", "6", "7"])
+@pytest.mark.parametrize("mode", ["1", "2", "3", "4", "5", "6", "7", "8", "9"])
 @pytest.mark.parametrize("n,remap", [(1000, "1"), (8 * 256 * 3 + 1000, "1"), (8 * 256 * 3 + 1000, "0")])
 def test_obs_writers_match_oracle(mode, n, remap, monkeypatch):
     """Every observation writer (per-lane rows, wave-cooperative from keys,

@@ -76,6 +76,37 @@ __global__ __launch_bounds__(256) void k_sweep(v4f* __restrict__ dst, size_t n) 
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) st<POL>(dst + i, z);
 }
 
+// Expansion of 32-byte per-lane bitmap records (7 words of the 196-bit
+// observation string + coins, as the step kernel stages them in LDS) into
+// the [B][2][98] fp32 tensor in sweep order: thread t of the grid writes
+// float4 x = t, t + stride, ...  (a split design: the step kernel writes the
+// records, this kernel is a pure store stream).
+template <int PER>
+__global__ __launch_bounds__(256) void k_expand(const uint32_t* __restrict__ rec, v4f* __restrict__ dst, uint32_t nf4) {
+  const uint32_t stride = gridDim.x * 256u;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const uint32_t x = blockIdx.x * 256u + threadIdx.x + (uint32_t)k * stride;
+    if (x >= nf4) return;
+    const uint32_t o = x / (uint32_t)kRowF4;
+    const uint32_t c = x - o * (uint32_t)kRowF4;
+    const uint32_t word = rec[8u * o + (c >> 3)];
+    const uint32_t coins = rec[8u * o + 7u];
+    const uint32_t nb = word >> (4u * (c & 7u));
+    v4f v;
+    v.x = (float)(nb & 1u);
+    v.y = (float)((nb >> 1) & 1u);
+    v.z = (float)((nb >> 2) & 1u);
+    v.w = (float)((nb >> 3) & 1u);
+    const float c0 = (float)(coins & 0xFFu), c1 = (float)(coins >> 8);
+    v.x = c == 15u ? c0 : v.x;
+    v.y = c == 15u ? c1 : v.y;
+    v.z = c == 39u ? c0 : v.z;
+    v.w = c == 39u ? c1 : v.w;
+    dst[x] = v;
+  }
+}
+
 #define CK(x)                                                    \
   do {                                                           \
     hipError_t e = (x);                                          \
@@ -143,6 +174,17 @@ int main() {
   BLOCK(1024, 2, false, 0);
   BLOCK(512, 0, true, 0);
 #undef BLOCK
+  {
+    uint32_t* rec;
+    CK(hipMalloc(&rec, lanes * 32));
+    CK(hipMemset(rec, 0x5A, lanes * 32));
+    const uint32_t nf4 = (uint32_t)n;
+    const int g1 = (int)((n + 255) / 256), g2 = (int)((n + 511) / 512), g4 = (int)((n + 1023) / 1024);
+    timed("expand_per1", g1, 256, [&] { k_expand<1><<<g1, 256>>>(rec, a, nf4); });
+    timed("expand_per2", g2, 256, [&] { k_expand<2><<<g2, 256>>>(rec, a, nf4); });
+    timed("expand_per4", g4, 256, [&] { k_expand<4><<<g4, 256>>>(rec, a, nf4); });
+    CK(hipFree(rec));
+  }
   for (int grid : {65536, 131072}) {
     timed("sweep_plain", grid, 256, [&] { k_sweep<0><<<grid, 256>>>(a, n); });
     timed("sweep_nt", grid, 256, [&] { k_sweep<1><<<grid, 256>>>(a, n); });
