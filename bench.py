@@ -63,9 +63,10 @@ CONFIGS = {
 
 def _writer(mode_env):
     """(ObsMode template value, block size) of the step kernel that
-    coup_step launches for COUP_OBS_MODE (default 4; csrc/coup_kernels.hip)."""
-    m = int(mode_env) if mode_env and mode_env.isdigit() and 1 <= int(mode_env) <= 7 else 4
-    return {1: (1, 256), 2: (2, 256), 3: (3, 256), 4: (4, 256), 5: (5, 256), 6: (5, 1024), 7: (7, 1024)}[m]
+    coup_step launches for COUP_OBS_MODE (default 9; csrc/coup_kernels.hip)."""
+    m = int(mode_env) if mode_env and mode_env.isdigit() and 1 <= int(mode_env) <= 9 else 9
+    return {1: (1, 256), 2: (2, 256), 3: (3, 256), 4: (4, 256), 5: (5, 256), 6: (5, 1024), 7: (7, 1024),
+            8: (8, 256), 9: (9, 256)}[m]
 
 
 def parse():

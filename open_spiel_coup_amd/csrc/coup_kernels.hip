@@ -503,7 +503,7 @@ __device__ __forceinline__ uint32_t xcd_group(uint32_t b, uint32_t G) {
 }
 
 // Observation write-out variants (COUP_OBS_MODE selects one at run time for
-// A/B measurements; kObsWaveBits is the default):
+// A/B measurements; kObsWaveBitsSc1 is the default):
 //   1 per-lane rows (each lane stores its own 784 B; uncoalesced)
 //   2/3 wave-cooperative, ds_bpermute keys + descriptor table (plain / nt)
 //   4 wave-cooperative from the LDS bitmap, nt stores
@@ -911,9 +911,11 @@ int fail(int code, const std::string& msg) {
   if (!(env)) return fail(COUP_E_INVALID, "null coup_env")
 
 // COUP_OBS_MODE=1..9 overrides the observation writer (A/B measurements;
-// the modes are listed at coup::ObsMode).  4 = wave-cooperative bitmap,
-// non-temporal stores.
-constexpr int kDefaultObsMode = 4;
+// the modes are listed at coup::ObsMode).  Default 9: wave-cooperative
+// bitmap, sc1 (write-through) buffer stores -- 1-4 us per 2^20-lane step
+// faster than the non-temporal stores of mode 4 in every same-process A/B
+// (tools/ab_step.py).
+constexpr int kDefaultObsMode = 9;
 int obs_mode() {
   const char* e = std::getenv("COUP_OBS_MODE");
   const int m = e ? std::atoi(e) : kDefaultObsMode;
@@ -1126,8 +1128,8 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
       case 6: COUP_LAUNCH_STEP(U, coup::kObsBlockBits, 1024, coup::kInfoNone); break;                \
       case 7: COUP_LAUNCH_STEP(U, coup::kObsBlockBitsNT, 1024, coup::kInfoNone); break;              \
       case 8: COUP_LAUNCH_STEP(U, coup::kObsWaveBitsPlain, 256, coup::kInfoNone); break;             \
-      case 9: COUP_LAUNCH_STEP(U, coup::kObsWaveBitsSc1, 256, coup::kInfoNone); break;               \
-      default: COUP_LAUNCH_STEP(U, coup::kObsWaveBits, 256, coup::kInfoNone); break;                 \
+      default: COUP_LAUNCH_STEP(U, coup::kObsWaveBitsSc1, 256, coup::kInfoNone); break;              \
+      case 4: COUP_LAUNCH_STEP(U, coup::kObsWaveBits, 256, coup::kInfoNone); break;                  \
     }                                                                                                \
   } else if (info == coup::kInfoHistory) {                                                           \
     if (mode == 0) COUP_LAUNCH_STEP(U, coup::kObsNone, 256, coup::kInfoHistory);                     \

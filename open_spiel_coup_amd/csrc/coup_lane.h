@@ -589,7 +589,10 @@ __device__ __forceinline__ bool apply_action(Lane& L, uint32_t a, H& hist) {
 // multiplies of the round.
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
-  for (int r = 0; r < 10; ++r) {
+#ifndef COUP_ABLATE_PHILOX_ROUNDS
+#define COUP_ABLATE_PHILOX_ROUNDS 10  // measurement builds may time fewer rounds (wrong streams)
+#endif
+  for (int r = 0; r < COUP_ABLATE_PHILOX_ROUNDS; ++r) {
     const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
     const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
