@@ -934,7 +934,8 @@ unsigned step_grid(int64_t groups, int) { return (unsigned)(groups > 0 ? groups 
 
 template <bool U, int M, int T, int I>
 void launch_step(const coup_env*, const coup::StepArgs& a, int64_t n, unsigned dyn_lds, hipStream_t s) {
-  coup::k_step<U, M, T, I><<<step_grid((n + T - 1) / T, T), T, dyn_lds, s>>>(a);
+  const int64_t groups = (n + T - 1) / T;
+  coup::k_step<U, M, T, I><<<step_grid(groups, T), T, dyn_lds, s>>>(a);
 }
 unsigned grid_for(int64_t n) { return (unsigned)((n + coup::kThreads - 1) / coup::kThreads); }
 
