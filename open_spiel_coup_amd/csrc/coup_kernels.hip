@@ -13,6 +13,19 @@
 #include <cstring>
 #include <string>
 
+#ifdef COUP_COUNT_PHILOX
+// Measurement builds: [0] wave-level Philox evaluations, [1] lanes active in
+// them (coup_debug_philox_counts).
+__device__ unsigned long long g_philox_counts[2];
+__device__ __forceinline__ void count_philox_eval() {
+  const uint64_t ex = __builtin_amdgcn_read_exec();
+  if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(ex)) {
+    atomicAdd(&g_philox_counts[0], 1ull);
+    atomicAdd(&g_philox_counts[1], (unsigned long long)__builtin_popcountll(ex));
+  }
+}
+#define COUP_PHILOX_HOOK() count_philox_eval()
+#endif
 #include "coup_lane.h"
 #include "coup_mi355x.h"
 #include "coup_np.h"
@@ -1266,3 +1279,14 @@ int coup_error_count(coup_env* env, int64_t* out) {
 }
 
 }  // extern "C"
+
+#ifdef COUP_COUNT_PHILOX
+extern "C" int coup_debug_philox_counts(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_philox_counts), sizeof(unsigned long long) * 2) != hipSuccess) return 2;
+  if (reset) {
+    const unsigned long long z[2] = {0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_philox_counts), z, sizeof(z)) != hipSuccess) return 2;
+  }
+  return 0;
+}
+#endif

@@ -587,7 +587,11 @@ __device__ __forceinline__ bool apply_action(Lane& L, uint32_t a, H& hist) {
 // Each 32x32 -> 64-bit product is one v_mad_u64_u32 (both halves at once)
 // instead of a v_mul_lo_u32 + v_mul_hi_u32 pair: half the quarter-rate
 // multiplies of the round.
+#ifndef COUP_PHILOX_HOOK
+#define COUP_PHILOX_HOOK()  // measurement builds count evaluations (COUP_COUNT_PHILOX)
+#endif
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
+  COUP_PHILOX_HOOK();
 #pragma unroll
 #ifndef COUP_ABLATE_PHILOX_ROUNDS
 #define COUP_ABLATE_PHILOX_ROUNDS 10  // measurement builds may time fewer rounds (wrong streams)

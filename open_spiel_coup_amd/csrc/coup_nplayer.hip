@@ -9,6 +9,19 @@
 // non-temporal float4 stores decoded from the block's records in LDS.
 #include <hip/hip_runtime.h>
 
+#ifdef COUP_COUNT_PHILOX
+// Measurement builds: [0] wave-level Philox evaluations, [1] lanes active in
+// them (coup_debug_philox_counts).
+__device__ unsigned long long g_philox_counts[2];
+__device__ __forceinline__ void count_philox_eval() {
+  const uint64_t ex = __builtin_amdgcn_read_exec();
+  if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(ex)) {
+    atomicAdd(&g_philox_counts[0], 1ull);
+    atomicAdd(&g_philox_counts[1], (unsigned long long)__builtin_popcountll(ex));
+  }
+}
+#define COUP_PHILOX_HOOK() count_philox_eval()
+#endif
 #include "coup_nlane.h"
 #include "coup_np.h"
 
@@ -386,3 +399,14 @@ hipError_t launch_import(const Env& e, const uint32_t* src) {
 
 }  // namespace np
 }  // namespace coup
+
+#ifdef COUP_COUNT_PHILOX
+extern "C" int coup_debug_philox_counts_np(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_philox_counts), sizeof(unsigned long long) * 2) != hipSuccess) return 2;
+  if (reset) {
+    const unsigned long long z[2] = {0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_philox_counts), z, sizeof(z)) != hipSuccess) return 2;
+  }
+  return 0;
+}
+#endif
