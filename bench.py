@@ -84,6 +84,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target duration of the bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
+                    help="collectives of a multi-process run: nccl (RCCL over xGMI, one GPU per rank) or gloo "
+                         "(a rehearsal of the multi-GPU path with several ranks sharing a GPU)")
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
                     help="replay the K timed steps from one HIP graph (auto: on for c2, c3 and c4, "
                          "where it removes the per-step launch gaps)")
@@ -157,7 +160,7 @@ def main():
     from open_spiel_coup_amd import distributed as D
 
     rank, world, _ = D.world_info()
-    dev = D.init("nccl")  # RCCL over xGMI when world > 1
+    dev = D.init(args.dist_backend, gpu=True)  # RCCL over xGMI when world > 1
 
     cfg = args.config
     B0, with_obs, with_info, fused, bytes_per_lane, workload, players = CONFIGS[cfg]
@@ -257,7 +260,8 @@ def main():
             "config": {"workload": workload, "batch_per_gpu": B, "global_batch": world * B, "players": players,
                        "outputs": outputs, "auto_reset": True, "fused_steps_per_launch": args.steps if fused else 1,
                        "hip_graph": graph is not None,
-                       "parallelism": f"dp{world} (env-id sharding)"},
+                       "parallelism": f"dp{world} (env-id sharding)" + ("" if args.dist_backend == "nccl" else
+                                                                   " [gloo rehearsal, ranks share GPUs]")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kernel,
                          "kernel_ms": launch_ms, "bytes_per_launch": bytes_per_launch},

@@ -24,12 +24,18 @@ def env_id_base(rank, lanes_per_rank):
     return rank * lanes_per_rank
 
 
-def init(backend="nccl"):
+def init(backend="nccl", gpu=None):
     """Initialise the process group for a torchrun launch (no-op for one
-    process).  Returns the torch device of this rank."""
+    process).  Returns the torch device of this rank: cuda:LOCAL_RANK for
+    nccl (RCCL); for gloo the CPU, or with gpu=True a GPU shared round-robin
+    by the ranks (a rehearsal of the multi-GPU path on a box with fewer GPUs
+    than ranks; RCCL refuses two ranks on one GPU)."""
     rank, world, local = world_info()
     if backend == "nccl":
         dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+    elif gpu:
+        dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
         torch.cuda.set_device(dev)
     else:
         dev = torch.device("cpu")
