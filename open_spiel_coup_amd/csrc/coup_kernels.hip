@@ -370,6 +370,10 @@ constexpr int kInfoHalfF4 = kInfoSize / 4;       // 623 float4 per player
 constexpr int kInfoF4 = 2 * kInfoHalfF4;         // 1246 float4 per lane
 constexpr int kPreWords = 6;
 constexpr int kHist = (int)kHistoryBytes;
+#ifndef COUP_INFO_STORE_POLICY
+#define COUP_INFO_STORE_POLICY 2  // 2 sc1 buffer stores (4% faster than 1, non-temporal: DESIGN.md section 5)
+#endif
+constexpr int kInfoStorePolicy = COUP_INFO_STORE_POLICY;
 
 __device__ __forceinline__ void info_prefix_to_lds(const Lane& L, uint32_t* __restrict__ pre) {
   const bool term = is_terminal(L);
@@ -383,51 +387,67 @@ __device__ __forceinline__ void info_prefix_to_lds(const Lane& L, uint32_t* __re
   pre[5] = 0;
 }
 
-// All 64 lanes of the wave must call this.
+// All 64 lanes of the wave must call this.  (x, o, c) = (64 j + lane,
+// x / 1246, x % 1246) advance incrementally.  A float4 whose first element
+// lies in a history row at or past the lane's history length is zero (most
+// of the [135][18] block: a uniform-random game is ~21 moves long), and the
+// 64 float4 of one store mostly belong to one lane, so the decode below is
+// skipped wave-wide for those stores (the writer was VALU-bound: 85% busy).
+template <int POL>
 __device__ __forceinline__ void write_info_wave(float* __restrict__ wave_info, const uint8_t* __restrict__ hist,
                                                 const uint32_t* __restrict__ pre, uint32_t n_valid) {
   typedef float v4f __attribute__((ext_vector_type(4)));
-  v4f* dst = reinterpret_cast<v4f*>(wave_info);
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
   const uint32_t lane = threadIdx.x & 63u;
+  v4f* dst = reinterpret_cast<v4f*>(wave_info) + lane;
+  __amdgpu_buffer_rsrc_t rsrc;
+  if (POL == 2)
+    rsrc = __builtin_amdgcn_make_buffer_rsrc(wave_info, (short)0, (int)(n_valid * 2u * kInfoSize * 4u), 0x00020000);
+  uint32_t o = 0u, c = lane;
 #pragma unroll 2
   for (uint32_t j = 0; j < (uint32_t)kInfoF4; ++j) {
-    const uint32_t x = 64u * j + lane;
-    const uint32_t o = x / (uint32_t)kInfoF4;
-    const uint32_t c = x - o * (uint32_t)kInfoF4;
     const uint32_t p = c >= (uint32_t)kInfoHalfF4;
     const int f0 = 4 * (int)(c - p * (uint32_t)kInfoHalfF4);
     const uint32_t* po = pre + kPreWords * o;
-    const uint2 pw = reinterpret_cast<const uint2*>(po)[p];
-    const uint64_t prefix = (uint64_t)pw.x | ((uint64_t)pw.y << 32);
     const uint32_t meta = po[4];
     const uint32_t len = meta >> 16;
-    // history rows touched by elements f0..f0+3 (t = f - 62; two rows at most)
-    const int t0 = f0 - 62;
-    const uint32_t r0 = t0 < 0 ? 0u : (uint32_t)t0 / 18u;
-    const int col0 = t0 - 18 * (int)r0;
-    uint32_t va[2];
+    v4f w = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (f0 < 62 + 18 * (int)len) {
+      const uint2 pw = reinterpret_cast<const uint2*>(po)[p];
+      const uint64_t prefix = (uint64_t)pw.x | ((uint64_t)pw.y << 32);
+      // history rows touched by elements f0..f0+3 (t = f - 62; two rows at most)
+      const int t0 = f0 - 62;
+      const uint32_t r0 = t0 < 0 ? 0u : (uint32_t)t0 / 18u;
+      const int col0 = t0 - 18 * (int)r0;
+      uint32_t va[2];
 #pragma unroll
-    for (uint32_t k = 0; k < 2; ++k) {
-      const uint32_t r = r0 + k;
-      const uint32_t e = hist[kHist * o + (r < (uint32_t)kHist ? r : 0u)];
-      const bool seen = (e & 0x20u) == 0u || ((e >> 6) & 1u) == p;  // deals: observer's only
-      va[k] = (r < len && seen) ? (e & 0x1Fu) : 31u;
-    }
-    float v[4];
+      for (uint32_t k = 0; k < 2; ++k) {
+        const uint32_t r = r0 + k;
+        const uint32_t e = hist[kHist * o + (r < (uint32_t)kHist ? r : 0u)];
+        const bool seen = (e & 0x20u) == 0u || ((e >> 6) & 1u) == p;  // deals: observer's only
+        va[k] = (r < len && seen) ? (e & 0x1Fu) : 31u;
+      }
+      float v[4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int f = f0 + e;
-      const int col = col0 + e;
-      const uint32_t row_act = col >= 18 ? va[1] : va[0];
-      const float h = (row_act == (uint32_t)(col >= 18 ? col - 18 : col)) ? 1.0f : 0.0f;
-      const float pb = (float)((uint32_t)(prefix >> (f & 63)) & 1u);
-      const float coin = (float)(f == 60 ? (meta & 0xFFu) : ((meta >> 8) & 0xFFu));
-      v[e] = f < 60 ? pb : (f < 62 ? coin : h);
+      for (int e = 0; e < 4; ++e) {
+        const int f = f0 + e;
+        const int col = col0 + e;
+        const uint32_t row_act = col >= 18 ? va[1] : va[0];
+        const float h = (row_act == (uint32_t)(col >= 18 ? col - 18 : col)) ? 1.0f : 0.0f;
+        const float pb = (float)((uint32_t)(prefix >> (f & 63)) & 1u);
+        const float coin = (float)(f == 60 ? (meta & 0xFFu) : ((meta >> 8) & 0xFFu));
+        v[e] = f < 60 ? pb : (f < 62 ? coin : h);
+      }
+      w = v4f{v[0], v[1], v[2], v[3]};
     }
-    if (o < n_valid) {
-      v4f w = {v[0], v[1], v[2], v[3]};
-      __builtin_nontemporal_store(w, dst + x);
-    }
+    if (POL == 2)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, w), rsrc, (int)(16u * (64u * j + lane)), 0, 16);
+    else if (o < n_valid)
+      __builtin_nontemporal_store(w, dst + 64u * j);
+    c += 64u;
+    const bool wrap = c >= (uint32_t)kInfoF4;
+    c = wrap ? c - (uint32_t)kInfoF4 : c;
+    o += wrap ? 1u : 0u;
   }
 }
 
@@ -709,7 +729,8 @@ __device__ __forceinline__ void step_group_compute(const StepArgs& a, int64_t gr
     wave_sync();
     if (wave_valid) wave_hist_copy<false>(a.hist + wave0 * kHist, hist_wave, wave_valid);
     if (INFO == kInfoWrite && wave_valid)
-      write_info_wave(a.info + wave0 * (2 * kInfoSize), hist_wave, lds.pre + wl * kPreWords, wave_valid);
+      write_info_wave<kInfoStorePolicy>(a.info + wave0 * (2 * kInfoSize), hist_wave, lds.pre + wl * kPreWords,
+                                        wave_valid);
     wave_sync();  // this group's LDS words read before the next group reuses them
   }
   COUP_TRACE(a, 1);
@@ -884,7 +905,9 @@ __global__ __launch_bounds__(kThreads) void k_query(QueryArgs a) {
       wave_hist_copy<true>(const_cast<uint8_t*>(a.hist) + wave0 * kHist, hist + wl * kHist, wave_valid);
     info_prefix_to_lds(L, pre + threadIdx.x * kPreWords);
     wave_sync();
-    if (wave_valid) write_info_wave(a.info + wave0 * (2 * kInfoSize), hist + wl * kHist, pre + wl * kPreWords, wave_valid);
+    if (wave_valid)
+      write_info_wave<kInfoStorePolicy>(a.info + wave0 * (2 * kInfoSize), hist + wl * kHist, pre + wl * kPreWords,
+                                        wave_valid);
   }
 }
 

@@ -1,7 +1,7 @@
 """Interleaved A/B timing of step-kernel variants in ONE process (box-to-box
 HBM variance is larger than the differences being measured).
 
-    python tools/ab_step.py [--batch B] [--obs 0|1] [--players N] [--rounds R] [--steps K] VAR=VAL[,VAR=VAL...] ...
+    python tools/ab_step.py [--batch B] [--obs 0|1] [--info 0|1] [--players N] [--rounds R] [--steps K] VAR=VAL[,...] ...
 
 Each positional argument is one variant: a comma-separated list of
 environment settings read by coup_step at launch (COUP_OBS_MODE,
@@ -29,13 +29,19 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--players", type=int, default=2)
+    ap.add_argument("--info", type=int, default=0, help="write the InformationStateTensor (c3i) instead")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     import torch
 
     from open_spiel_coup_amd import BatchedCoupEnv
-    env = BatchedCoupEnv(a.batch, seed=1, auto_reset=True, obs=bool(a.obs), device="cuda:0", num_players=a.players)
-    env.rollout(256)
+    env = BatchedCoupEnv(a.batch, seed=1, auto_reset=True, obs=bool(a.obs) and not a.info, info_state=bool(a.info),
+                         device="cuda:0", num_players=a.players)
+    if a.info:
+        for _ in range(32):  # histories: no fused rollout
+            env.step()
+    else:
+        env.rollout(256)
     stream = torch.cuda.current_stream()
     times = {v: [] for v in a.variants}
     for _ in range(a.rounds):
