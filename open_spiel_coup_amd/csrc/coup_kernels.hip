@@ -561,8 +561,7 @@ __device__ __forceinline__ void step_lane(const StepArgs& a, int64_t i, Lane& L,
   rew = 0;
   if (is_terminal(L)) {
     // step() after LAST starts a new episode (rl_environment.py:310-311)
-    L = initial_lane(L.episode + 1u);
-    resolve_chance(L, rng, hist);
+    L = new_episode(L.episode + 1u, rng, hist);
     st = COUP_STEP_FIRST;
     return;
   }
@@ -591,8 +590,7 @@ __device__ __forceinline__ void step_lane(const StepArgs& a, int64_t i, Lane& L,
     st = COUP_STEP_LAST;
     if (a.auto_reset) {
       // SyncVectorEnv.step(reset_if_done=True) (vector_env.py:62-65)
-      L = initial_lane(L.episode + 1u);
-      resolve_chance(L, rng, hist);
+      L = new_episode(L.episode + 1u, rng, hist);
     }
   }
 }
@@ -771,13 +769,12 @@ __global__ __launch_bounds__(kThreads) void k_rollout(RolloutArgs a) {
   if (i >= a.n) return;
   Lane L = unpack(a.state[i]);
   Rng rng{a.seed_lo, a.seed_hi, a.env_id_base + (uint32_t)i, 0u, make_uint4(0, 0, 0, 0)};
+  NoHistory none;
   int32_t eps = 0, ret = 0, len = 0, cur = 0;
   uint32_t errs = 0;
   for (int64_t s = 0; s < a.steps; ++s) {
-    if (is_terminal(L)) {
-      L = initial_lane(L.episode + 1u);
-    }
-    resolve_chance(L, rng);
+    if (is_terminal(L)) L = new_episode(L.episode + 1u, rng, none);  // a terminal starting record
+    resolve_chance(L, rng);  // a lane left at a chance node
     const uint32_t m = decision_mask(L);
     if (m == 0u) {
       errs += 1u;
@@ -794,8 +791,7 @@ __global__ __launch_bounds__(kThreads) void k_rollout(RolloutArgs a) {
       ret += return0(L);
       len += cur;
       cur = 0;
-      L = initial_lane(L.episode + 1u);
-      resolve_chance(L, rng);
+      L = new_episode(L.episode + 1u, rng, none);
     }
   }
   a.state[i] = pack(L);

@@ -671,4 +671,30 @@ __device__ __forceinline__ void resolve_chance(Lane& L, Rng& rng) {
   resolve_chance(L, rng, none);
 }
 
+// CoupState::CoupState (coup.cc:393-428) followed by its four chance deals
+// (coup.cc:491-520, rl_environment.py:369-382): initial_lane + resolve_chance
+// in straight-line form.  The queue is [P1, P2, P1, P2], deal k draws slot k
+// of the episode from the full deck minus the earlier deals, and each hand
+// ends as its two face-down kinds in ascending order.  Every wave with a
+// finishing lane runs this on an auto-reset step.
+template <class H>
+__device__ __forceinline__ Lane new_episode(uint32_t episode, Rng& rng, H& hist) {
+  Lane L = initial_lane(episode);
+  uint32_t t[4];
+#pragma unroll
+  for (uint32_t k = 0; k < 4u; ++k) {
+    t[k] = sample_card(L.deck, rng.draw(L.episode, k));
+    L.deck -= 1u << (4u * t[k]);
+    hist.record(k, hist_deal(t[k], k & 1u));
+  }
+  const uint32_t p0 = t[0] < t[2] ? t[0] : t[2], q0 = t[0] < t[2] ? t[2] : t[0];
+  const uint32_t p1 = t[1] < t[3] ? t[1] : t[3], q1 = t[1] < t[3] ? t[3] : t[1];
+  L.h0 = (2u * p0) | ((2u * q0) << 4) | 0xFF00u;
+  L.h1 = (2u * p1) | ((2u * q1) << 4) | 0xFF00u;
+  L.qlen = 0u;
+  L.qids = 0u;
+  L.move = 4u;
+  return L;
+}
+
 }  // namespace coup
