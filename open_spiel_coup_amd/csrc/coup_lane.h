@@ -655,15 +655,19 @@ __device__ __forceinline__ uint32_t sample_action(uint32_t mask, uint32_t u) {
 
 // rl_environment._sample_external_events (rl_environment.py:369-382):
 // deal until a decision node or a terminal state.
+// A deal adds a face-down card, so a player alive before it is alive after
+// it: once the state is not terminal, only truncation (move_number_ > 90,
+// coup.cc:989-992) can end the deals early.
 template <class H>
 __device__ __forceinline__ void resolve_chance(Lane& L, Rng& rng, H& hist) {
-  while (L.qlen != 0u && !is_terminal(L)) {
+  if (L.qlen == 0u || is_terminal(L)) return;
+  do {
     const uint32_t u = rng.draw(L.episode, L.move);
     const uint32_t t = sample_card(L.deck, u);
     hist.record(L.move, hist_deal(t, L.qids & 1u));
     apply_deal(L, t);
     L.move += 1u;
-  }
+  } while (L.qlen != 0u && L.move <= kMaxGameLength);
 }
 
 __device__ __forceinline__ void resolve_chance(Lane& L, Rng& rng) {
