@@ -581,12 +581,37 @@ struct NRng {
   }
 };
 
+// A deal adds a face-down card, so it cannot end the game except by
+// truncation (MaxGameLength 45 N): one terminal test, then the bound.
 template <int N>
 __device__ __forceinline__ void resolve_chance(NLane<N>& L, NRng& rng) {
-  while (is_chance(L) && !is_terminal(L)) {
+  if (!is_chance(L) || is_terminal(L)) return;
+  do {
     apply_deal(L, sample_card(L.deck, rng.draw(L.episode, L.move)));
     L.move += 1u;
+  } while (is_chance(L) && L.move <= 45u * N);
+}
+
+// initial_lane + its 2N deals in straight-line form: deal k (slot k) goes to
+// seat k mod N, so seat s holds the face-down kinds of deals s and s + N in
+// ascending order.
+template <int N>
+__device__ __forceinline__ NLane<N> new_episode(uint32_t episode, NRng& rng) {
+  NLane<N> L = initial_lane<N>(episode);
+  uint32_t t[2 * N];
+#pragma unroll
+  for (int k = 0; k < 2 * N; ++k) {
+    t[k] = sample_card(L.deck, rng.draw(L.episode, (uint32_t)k));
+    L.deck -= 1u << (4u * t[k]);
   }
+#pragma unroll
+  for (int p = 0; p < N; ++p) {
+    const uint32_t lo = t[p] < t[p + N] ? t[p] : t[p + N], hi = t[p] < t[p + N] ? t[p + N] : t[p];
+    set_hand(L, (uint32_t)p, (2u * lo) | ((2u * hi) << 4) | 0xFF00u);
+  }
+  L.init_left = 0u;
+  L.move = 2u * N;
+  return L;
 }
 
 // ObservationTensor (CoupObserver::WriteTensor, coup.cc:248-287, with
@@ -637,8 +662,7 @@ __device__ __forceinline__ void step_lane(NLane<N>& L, NRng& rng, uint32_t x, bo
   rc = 0;
   error = false;
   if (is_terminal(L)) {
-    L = initial_lane<N>(L.episode + 1u);
-    resolve_chance(L, rng);
+    L = new_episode<N>(L.episode + 1u, rng);
     st = 0;  // FIRST
     return;
   }
@@ -660,10 +684,7 @@ __device__ __forceinline__ void step_lane(NLane<N>& L, NRng& rng, uint32_t x, bo
   rc = L.rcount;
   if (is_terminal(L)) {
     st = 2;  // LAST
-    if (auto_reset) {
-      L = initial_lane<N>(L.episode + 1u);
-      resolve_chance(L, rng);
-    }
+    if (auto_reset) L = new_episode<N>(L.episode + 1u, rng);
   }
 }
 

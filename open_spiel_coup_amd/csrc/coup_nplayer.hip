@@ -108,8 +108,8 @@ __global__ __launch_bounds__(kThreads) void k_rollout(RolloutArgs a) {
   int32_t eps = 0, ret = 0, len = 0, cur = 0;
   uint32_t errs = 0;
   for (int64_t s = 0; s < a.steps; ++s) {
-    if (is_terminal(L)) L = initial_lane<N>(L.episode + 1u);
-    resolve_chance(L, rng);
+    if (is_terminal(L)) L = new_episode<N>(L.episode + 1u, rng);  // a terminal starting record
+    resolve_chance(L, rng);  // a lane left at a chance node
     const uint32_t m = decision_mask(L);
     if (m == 0u) {
       errs += 1u;
@@ -126,8 +126,7 @@ __global__ __launch_bounds__(kThreads) void k_rollout(RolloutArgs a) {
       ret += returns(L, 0u);
       len += cur;
       cur = 0;
-      L = initial_lane<N>(L.episode + 1u);
-      resolve_chance(L, rng);
+      L = new_episode<N>(L.episode + 1u, rng);
     }
   }
   uint4 wa, wb;
