@@ -35,6 +35,19 @@ namespace coup {
 constexpr int kThreads = 256;
 constexpr int kObsSize = COUP_OBS_SIZE;
 
+// The RNG key of lane i (global env id).  A measurement
+// build with -DCOUP_ABLATE_SAME_STREAM gives every lane the same stream, so
+// all lanes play the same game and the waves do not diverge (wrong results;
+// it times the step without divergence).
+__device__ __forceinline__ uint32_t lane_stream_id(uint32_t env_id_base, int64_t i) {
+#ifdef COUP_ABLATE_SAME_STREAM
+  (void)i;
+  return env_id_base;
+#else
+  return env_id_base + (uint32_t)i;
+#endif
+}
+
 // ------------------------------------------------------- observation tensor
 
 // CoupObserver::WriteTensor with kDefaultObsType (coup.cc:248-287,
@@ -556,7 +569,7 @@ constexpr int wave_bits_policy(int m) { return m == kObsWaveBitsPlain ? 0 : (m =
 template <bool UNIFORM, class H>
 __device__ __forceinline__ void step_lane(const StepArgs& a, int64_t i, Lane& L, int& act, uint32_t& st,
                                           int32_t& rew, H& hist) {
-  Rng rng{a.seed_lo, a.seed_hi, a.env_id_base + (uint32_t)i, 0u, make_uint4(0, 0, 0, 0)};
+  Rng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, i), 0u, make_uint4(0, 0, 0, 0)};
   act = -1;
   rew = 0;
   if (is_terminal(L)) {
@@ -768,7 +781,7 @@ __global__ __launch_bounds__(kThreads) void k_rollout(RolloutArgs a) {
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= a.n) return;
   Lane L = unpack(a.state[i]);
-  Rng rng{a.seed_lo, a.seed_hi, a.env_id_base + (uint32_t)i, 0u, make_uint4(0, 0, 0, 0)};
+  Rng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, i), 0u, make_uint4(0, 0, 0, 0)};
   NoHistory none;
   int32_t eps = 0, ret = 0, len = 0, cur = 0;
   uint32_t errs = 0;
@@ -812,7 +825,7 @@ __global__ __launch_bounds__(kThreads) void k_reset(uint4* state, int64_t n, con
   const uint32_t ep = mode == 0 ? 0u : unpack(state[i]).episode + 1u;
   Lane L = initial_lane(ep);
   if (deal) {
-    Rng rng{seed_lo, seed_hi, env_id_base + (uint32_t)i, 0u, make_uint4(0, 0, 0, 0)};
+    Rng rng{seed_lo, seed_hi, lane_stream_id(env_id_base, i), 0u, make_uint4(0, 0, 0, 0)};
     if (hist) {
       RegHistory rec;
       resolve_chance(L, rng, rec);
