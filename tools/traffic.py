@@ -85,6 +85,22 @@ def main():
                     "avg_ns": float(r[col(r, "average")]),
                 }
 
+    # the bench line printed by the traced command itself (trace.log): its
+    # live HIP-event kernel time must agree with the trace's average
+    trace_log = os.path.join(src, "trace.log")
+    if os.path.exists(trace_log):
+        with open(trace_log) as f:
+            for line in f:
+                if line.startswith("{") and '"metric"' in line:
+                    bench = json.loads(line)
+                    summary["bench_line_of_traced_command"] = {
+                        "value": bench["value"], "ms_per_step": bench["ms_per_step"],
+                        "kernel_ms": bench["roofline"]["kernel_ms"], "frac": bench["roofline"]["frac"]}
+                    tk = summary.get("timed_kernel")
+                    if tk and tk in summary.get("kernels", {}):
+                        rp = summary["kernels"][tk]["avg_ns"] * 1e-6
+                        summary["bench_vs_rocprof_kernel_ms"] = [bench["roofline"]["kernel_ms"], rp]
+
     def counter(kind, cname):
         vals = []
         for r in rows(os.path.join(src, kind, "**", "*counter_collection.csv")):
