@@ -517,7 +517,8 @@ struct StepArgs {
 #ifdef COUP_WAVE_TRACE
   // measurement builds only (tools/wave_trace.py): per wave, 100 MHz
   // timestamps at entry, end of the step, end of store issue, stores
-  // drained, then HW_ID << 32 | XCC_ID, then the state load's return
+  // drained, then HW_ID << 32 | XCC_ID, then the state load's return, then
+  // (first active lane) action drawn, decision applied, deals done, step done
   uint64_t* trace;
 #endif
 };
@@ -526,12 +527,22 @@ struct StepArgs {
 #define COUP_TRACE(a, k)                                                                           \
   do {                                                                                             \
     if ((a).trace && (threadIdx.x & 63u) == 0u)                                                    \
-      (a).trace[((size_t)blockIdx.x * (blockDim.x / 64u) + threadIdx.x / 64u) * 6u + (k)] =       \
+      (a).trace[((size_t)blockIdx.x * (blockDim.x / 64u) + threadIdx.x / 64u) * 10u + (k)] =      \
           __builtin_amdgcn_s_memrealtime();                                                        \
+  } while (0)
+// stamp by the first active lane (inside code some lanes have left)
+#define COUP_TRACE_ANY(a, k)                                                                        \
+  do {                                                                                              \
+    if ((a).trace && (threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec()))  \
+      (a).trace[((size_t)blockIdx.x * (blockDim.x / 64u) + threadIdx.x / 64u) * 10u + (k)] =        \
+          __builtin_amdgcn_s_memrealtime();                                                         \
   } while (0)
 #else
 #define COUP_TRACE(a, k) \
   do {                   \
+  } while (0)
+#define COUP_TRACE_ANY(a, k) \
+  do {                       \
   } while (0)
 #endif
 
@@ -586,6 +597,7 @@ __device__ __forceinline__ void step_lane(const StepArgs& a, int64_t i, Lane& L,
   } else {
     x = (uint32_t)(uint8_t)a.actions_in[i];
   }
+  COUP_TRACE_ANY(a, 6);
   st = COUP_STEP_MID;
   if (x > 17u || ((m >> x) & 1u) == 0u || is_terminal(L)) {
     count_error(a.err_count);
@@ -595,7 +607,9 @@ __device__ __forceinline__ void step_lane(const StepArgs& a, int64_t i, Lane& L,
   hist.record(L.move, hist_decision(x, L.M));
   apply_decision(L, x);
   L.move += 1u;
+  COUP_TRACE_ANY(a, 7);
   resolve_chance(L, rng, hist);
+  COUP_TRACE_ANY(a, 8);
   if (L.err && !err_before) count_error(a.err_count);
   act = (int)x;
   rew = L.r0;
@@ -606,6 +620,7 @@ __device__ __forceinline__ void step_lane(const StepArgs& a, int64_t i, Lane& L,
       L = new_episode(L.episode + 1u, rng, hist);
     }
   }
+  COUP_TRACE_ANY(a, 9);
 }
 
 // Wave-scope hand-off of LDS data between lanes of one wave.
@@ -657,7 +672,7 @@ __global__ __launch_bounds__(T, INFO == kInfoNone ? 8 : 4) void k_step(StepArgs 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   COUP_TRACE(a, 3);
   if (a.trace && (threadIdx.x & 63u) == 0u)
-    a.trace[((size_t)blockIdx.x * (blockDim.x / 64u) + threadIdx.x / 64u) * 6u + 4u] =
+    a.trace[((size_t)blockIdx.x * (blockDim.x / 64u) + threadIdx.x / 64u) * 10u + 4u] =
         ((uint64_t)__builtin_amdgcn_s_getreg(4 | (31 << 11)) << 32) | (uint32_t)__builtin_amdgcn_s_getreg(20 | (31 << 11));
 #endif
 }

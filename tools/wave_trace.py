@@ -45,7 +45,7 @@ def main():
     for _ in range(5):
         env.step()
     waves = (a.batch + 255) // 256 * 4
-    buf = torch.zeros(waves * 6, dtype=torch.int64, device="cuda:0")
+    buf = torch.zeros(waves * 10, dtype=torch.int64, device="cuda:0")
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     lib.coup_debug_set_trace(ctypes.c_void_p(buf.data_ptr()))
     for _ in range(a.steps):
@@ -54,7 +54,7 @@ def main():
         e1.record()
     torch.cuda.synchronize()
     lib.coup_debug_set_trace(None)
-    tr = buf.view(waves, 6).cpu().numpy()
+    tr = buf.view(waves, 10).cpu().numpy()
     tr = tr[tr[:, 0] != 0]  # a persistent grid has fewer waves than groups
     waves = len(tr)
     t = (tr[:, :4] - tr[:, 0].min()).astype(np.float64) / 100.0  # us
@@ -64,6 +64,16 @@ def main():
     comp, issue, drain = t[:, 1] - t[:, 0], t[:, 2] - t[:, 1], t[:, 3] - t[:, 2]
     load = (tr[:, 5] - tr[:, 0]).astype(np.float64) / 100.0  # state load latency (us)
     late = t[:, 0] > 0.75 * t[:, 0].max()
+    # step segments (stamps 5..9: record loaded, action drawn, decision applied,
+    # deals resolved, end of the step incl. the reset of finished lanes)
+    seg = {}
+    for name, k0, k1 in (("mask_and_draw", 5, 6), ("apply_decision", 6, 7), ("deals", 7, 8), ("reset", 8, 9),
+                         ("outputs_and_obs_bits", 9, None)):
+        a0 = tr[:, k0].astype(np.float64)
+        a1 = (tr[:, k1] if k1 is not None else tr[:, 0] + (t[:, 1] * 100.0).astype(np.int64)).astype(np.float64)
+        ok = (tr[:, k0] != 0) & ((tr[:, k1] != 0) if k1 is not None else True)
+        if ok.any():
+            seg[name] = [round(float(v), 2) for v in np.percentile((a1[ok] - a0[ok]) / 100.0, [5, 50, 95])]
     q = lambda x: [round(float(v), 2) for v in np.percentile(x, [5, 50, 95])]
     summary = {"mode": a.mode, "event_us": round(e0.elapsed_time(e1) * 1e3, 2), "span_us": round(float(span), 2), "waves": int(waves),
                "compute_us_p5_50_95": q(comp), "issue_us_p5_50_95": q(issue), "drain_us_p5_50_95": q(drain),
@@ -71,7 +81,8 @@ def main():
                "late_waves_compute_us_p5_50_95": q(comp[late]),
                "first_store_issue_us": round(float(t[:, 1].min()), 2),
                "last_entry_us": round(float(t[:, 0].max()), 2),
-               "xcc_counts": np.bincount(xcc, minlength=8).tolist()}
+               "xcc_counts": np.bincount(xcc, minlength=8).tolist(),
+               "segments_us_p5_50_95": seg}
     print(json.dumps(summary))
     nb = int(np.ceil(span / a.bin_us))
     rows = []
