@@ -30,6 +30,17 @@ namespace np {
 
 constexpr int kThreads = 256;
 
+// The RNG key of lane i; -DCOUP_ABLATE_SAME_STREAM: one stream for every lane
+// (measurement builds: the step without divergence, wrong results).
+__device__ __forceinline__ uint32_t lane_stream_id(uint32_t env_id_base, int64_t i) {
+#ifdef COUP_ABLATE_SAME_STREAM
+  (void)i;
+  return env_id_base;
+#else
+  return env_id_base + (uint32_t)i;
+#endif
+}
+
 __device__ __forceinline__ void count_error(uint32_t* err_count) { atomicAdd(err_count, 1u); }
 
 struct StepArgs {
@@ -53,7 +64,7 @@ __global__ __launch_bounds__(kThreads) void k_step(StepArgs a) {
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= a.n) return;
   NLane<N> L = unpack<N>(a.sa[i], a.sb[i]);
-  NRng rng{a.seed_lo, a.seed_hi, a.env_id_base + (uint32_t)i, 0u, make_uint4(0, 0, 0, 0)};
+  NRng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, i), 0u, make_uint4(0, 0, 0, 0)};
   int act;
   uint32_t st, rl, rc;
   bool error;
@@ -104,7 +115,7 @@ __global__ __launch_bounds__(kThreads) void k_rollout(RolloutArgs a) {
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= a.n) return;
   NLane<N> L = unpack<N>(a.sa[i], a.sb[i]);
-  NRng rng{a.seed_lo, a.seed_hi, a.env_id_base + (uint32_t)i, 0u, make_uint4(0, 0, 0, 0)};
+  NRng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, i), 0u, make_uint4(0, 0, 0, 0)};
   int32_t eps = 0, ret = 0, len = 0, cur = 0;
   uint32_t errs = 0;
   for (int64_t s = 0; s < a.steps; ++s) {
@@ -149,7 +160,7 @@ __global__ __launch_bounds__(kThreads) void k_reset(uint4* sa, uint4* sb, int64_
   const uint32_t ep = mode == 0 ? 0u : (sb[i].w & kEpisodeMask) + 1u;
   NLane<N> L = initial_lane<N>(ep);
   if (deal) {
-    NRng rng{seed_lo, seed_hi, env_id_base + (uint32_t)i, 0u, make_uint4(0, 0, 0, 0)};
+    NRng rng{seed_lo, seed_hi, lane_stream_id(env_id_base, i), 0u, make_uint4(0, 0, 0, 0)};
     resolve_chance(L, rng);
   }
   uint4 wa, wb;
