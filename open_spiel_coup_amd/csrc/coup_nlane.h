@@ -654,17 +654,19 @@ __device__ __forceinline__ float obs_elem(const uint32_t* r, uint32_t o, uint32_
 // to apply (the uniform policy's draw when UNIFORM).  Outputs: the applied
 // action (-1 if none), the step type, Rewards() as (loser, count), and
 // whether the lane rejected the action or hit a rules error.
+// First half of step_lane, up to the decision to apply: a lane that was
+// terminal starts a new episode (FIRST), pending deals are resolved, the
+// uniform policy draws x.  Returns kStepDone when nothing is left to apply
+// (the reset, or a rejected action: `error`), else the action x.
+constexpr uint32_t kStepDone = 18u;
+
 template <int N, bool UNIFORM>
-__device__ __forceinline__ void step_lane(NLane<N>& L, NRng& rng, uint32_t x, bool auto_reset, int& act,
-                                          uint32_t& st, uint32_t& rl, uint32_t& rc, bool& error) {
-  act = -1;
-  rl = 0;
-  rc = 0;
+__device__ __forceinline__ uint32_t step_lane_pre(NLane<N>& L, NRng& rng, uint32_t& x, uint32_t& st, bool& error) {
   error = false;
   if (is_terminal(L)) {
     L = new_episode<N>(L.episode + 1u, rng);
     st = 0;  // FIRST
-    return;
+    return kStepDone;
   }
   resolve_chance(L, rng);
   const uint32_t m = decision_mask(L);
@@ -672,8 +674,15 @@ __device__ __forceinline__ void step_lane(NLane<N>& L, NRng& rng, uint32_t x, bo
   st = 1;  // MID
   if (x > 17u || ((m >> x) & 1u) == 0u || is_terminal(L)) {
     error = true;
-    return;
+    return kStepDone;
   }
+  return x;
+}
+
+// Second half: apply decision x, resolve the deals, auto-reset.
+template <int N>
+__device__ __forceinline__ void step_lane_post(NLane<N>& L, NRng& rng, uint32_t x, bool auto_reset, int& act,
+                                               uint32_t& st, uint32_t& rl, uint32_t& rc, bool& error) {
   const uint32_t err_before = L.err;
   apply_decision(L, x);
   L.move += 1u;
@@ -686,6 +695,16 @@ __device__ __forceinline__ void step_lane(NLane<N>& L, NRng& rng, uint32_t x, bo
     st = 2;  // LAST
     if (auto_reset) L = new_episode<N>(L.episode + 1u, rng);
   }
+}
+
+template <int N, bool UNIFORM>
+__device__ __forceinline__ void step_lane(NLane<N>& L, NRng& rng, uint32_t x, bool auto_reset, int& act,
+                                          uint32_t& st, uint32_t& rl, uint32_t& rc, bool& error) {
+  act = -1;
+  rl = 0;
+  rc = 0;
+  if (step_lane_pre<N, UNIFORM>(L, rng, x, st, error) != kStepDone)
+    step_lane_post<N>(L, rng, x, auto_reset, act, st, rl, rc, error);
 }
 
 }  // namespace np

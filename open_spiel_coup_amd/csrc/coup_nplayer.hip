@@ -58,23 +58,11 @@ struct StepArgs {
   uint32_t* err_count;
 };
 
-// One rl_environment step per lane (step_lane, coup_nlane.h).
-template <int N, bool UNIFORM>
-__global__ __launch_bounds__(kThreads) void k_step(StepArgs a) {
-  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (i >= a.n) return;
-  NLane<N> L = unpack<N>(a.sa[i], a.sb[i]);
-  NRng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, i), 0u, make_uint4(0, 0, 0, 0)};
-  int act;
-  uint32_t st, rl, rc;
-  bool error;
-  step_lane<N, UNIFORM>(L, rng, UNIFORM ? 0u : (uint32_t)(uint8_t)a.actions_in[i], a.auto_reset != 0, act, st, rl,
-                        rc, error);
-  if (error) count_error(a.err_count);
-  uint4 wa, wb;
-  pack(L, wa, wb);
-  a.sa[i] = wa;
-  a.sb[i] = wb;
+// The per-lane outputs of a step: applied action, Rewards() as (loser,
+// count), step type, post-step legal mask and current player.
+template <int N>
+__device__ __forceinline__ void store_step_outputs(const StepArgs& a, int64_t i, int act, uint32_t st, uint32_t rl,
+                                                   uint32_t rc, uint32_t legal, int cp) {
   if (a.actions) a.actions[i] = (int8_t)act;
   if (a.rewards) {
     // Rewards(): rc to everybody, -(N-1) rc to the loser; an even-N row
@@ -93,8 +81,157 @@ __global__ __launch_bounds__(kThreads) void k_step(StepArgs a) {
     }
   }
   if (a.step_type) a.step_type[i] = (uint8_t)st;
-  if (a.legal) a.legal[i] = legal_mask(L);
-  if (a.cur_player) a.cur_player[i] = (int8_t)current_player(L);
+  if (a.legal) a.legal[i] = legal;
+  if (a.cur_player) a.cur_player[i] = (int8_t)cp;
+}
+
+// One rl_environment step per lane (step_lane, coup_nlane.h), lanes in
+// place: the wave runs the union of its lanes' branches of the rules.
+template <int N, bool UNIFORM>
+__global__ __launch_bounds__(kThreads) void k_step(StepArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= a.n) return;
+  NLane<N> L = unpack<N>(a.sa[i], a.sb[i]);
+  NRng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, i), 0u, make_uint4(0, 0, 0, 0)};
+  int act;
+  uint32_t st, rl, rc;
+  bool error;
+  step_lane<N, UNIFORM>(L, rng, UNIFORM ? 0u : (uint32_t)(uint8_t)a.actions_in[i], a.auto_reset != 0, act, st, rl,
+                        rc, error);
+  if (error) count_error(a.err_count);
+  uint4 wa, wb;
+  pack(L, wa, wb);
+  a.sa[i] = wa;
+  a.sb[i] = wb;
+  store_step_outputs<N>(a, i, act, st, rl, rc, legal_mask(L), current_player(L));
+}
+
+// The same step with the block's lanes regrouped by decision before the
+// rules run (default; COUP_NP_SORT=0 selects k_step).  Phase 1: each thread
+// takes its lane up to the decision (step_lane_pre) and the block
+// counting-sorts its lanes by that decision through LDS, so a wave of the
+// apply phase holds lanes playing the same action: the union of branches it
+// executes shrinks to what those lanes need.  Phase 2: thread t applies
+// slot t's decision and resolves the deals.  The lanes that finished and
+// auto-reset are listed in LDS and dealt their new episode by the first
+// threads of the block (new_episode needs only the episode number and the
+// lane's RNG stream), so the 2N-deal reset runs in one wave instead of in
+// every wave holding a finished lane.  Phase 3: each thread stores its own
+// lane's record and outputs back in place, coalesced.  The RNG is
+// stateless per (lane, episode, draw), so results equal k_step's.
+constexpr uint32_t kKeyPad = 19u;  // past-the-end lanes of the last block
+
+template <int N, bool UNIFORM>
+__global__ __launch_bounds__(kThreads) void k_step_sorted(StepArgs a) {
+  __shared__ uint4 s_a[kThreads], s_b[kThreads];
+  __shared__ uint32_t s_meta[kThreads];   // slot -> owner thread | key << 8 | st << 13 | error << 15
+  __shared__ uint32_t s_out[kThreads];    // slot -> act + 1 | st << 5 | rl << 7 | rc << 10 | error << 13 | cp << 24
+  __shared__ uint32_t s_legal[kThreads];  // slot -> post-step legal mask
+  __shared__ uint32_t s_reset[kThreads];  // slots whose lane auto-resets
+  __shared__ uint32_t s_bin[32];
+  __shared__ uint32_t s_nreset;
+  const uint32_t t = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * kThreads;
+  const int64_t i = base + t;
+  const bool live = i < a.n;
+  if (t < 32u) s_bin[t] = 0u;
+  if (t == 0u) s_nreset = 0u;
+
+  // phase 1: up to the decision
+  NLane<N> L;
+  uint32_t key = kKeyPad, st = 0u;
+  bool error = false;
+  if (live) {
+    L = unpack<N>(a.sa[i], a.sb[i]);
+    NRng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, i), 0u, make_uint4(0, 0, 0, 0)};
+    uint32_t x = UNIFORM ? 0u : (uint32_t)(uint8_t)a.actions_in[i];
+    key = step_lane_pre<N, UNIFORM>(L, rng, x, st, error);
+    if (error) count_error(a.err_count);
+  }
+  __syncthreads();
+  const uint32_t rank = atomicAdd(&s_bin[key], 1u);
+  __syncthreads();
+  if (t < 64u) {  // exclusive scan of the 20 bin counts in wave 0
+    const uint32_t v = t < 32u ? s_bin[t] : 0u;
+    uint32_t inc = v;
+#pragma unroll
+    for (int d = 1; d < 32; d <<= 1) {
+      const uint32_t u = __shfl_up(inc, d, 64);
+      if (t >= (uint32_t)d) inc += u;
+    }
+    if (t < 32u) s_bin[t] = inc - v;
+  }
+  __syncthreads();
+  const uint32_t pos = s_bin[key] + rank;
+  if (live) {
+    uint4 wa, wb;
+    pack(L, wa, wb);
+    s_a[pos] = wa;
+    s_b[pos] = wb;
+  }
+  s_meta[pos] = t | (key << 8) | (st << 13) | ((uint32_t)error << 15);
+  __syncthreads();
+
+  // phase 2: thread t runs slot t's decision
+  {
+    const uint32_t m = s_meta[t], k = (m >> 8) & 31u;
+    if (k <= kStepDone) {
+      L = unpack<N>(s_a[t], s_b[t]);
+      uint32_t out = (m >> 13) & 3u, legal = 0u;  // a lane finished in phase 1: no action, its st
+      bool pending = false;
+      if (k < kStepDone) {
+        NRng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, base + (m & 255u)), 0u,
+                 make_uint4(0, 0, 0, 0)};
+        const uint32_t err_before = L.err;
+        apply_decision(L, k);
+        L.move += 1u;
+        resolve_chance(L, rng);
+        const bool err = L.err && !err_before;
+        if (err) count_error(a.err_count);
+        const bool term = is_terminal(L);
+        out = (k + 1u) | ((term ? 2u : 1u) << 5) | (L.rloser << 7) | (L.rcount << 10) | ((uint32_t)err << 13);
+        pending = term && a.auto_reset != 0;
+        if (pending) s_reset[atomicAdd(&s_nreset, 1u)] = t;
+        uint4 wa, wb;
+        pack(L, wa, wb);
+        s_a[t] = wa;
+        s_b[t] = wb;
+      } else {
+        out = 0u | (((m >> 13) & 3u) << 5);
+      }
+      if (!pending) {
+        legal = legal_mask(L);
+        out |= ((uint32_t)current_player(L) & 0xFFu) << 24;
+      }
+      s_out[t] = out;
+      s_legal[t] = legal;
+    }
+  }
+  __syncthreads();
+
+  // the auto-resets, packed onto the first threads
+  const uint32_t nreset = s_nreset;
+  for (uint32_t j = t; j < nreset; j += kThreads) {
+    const uint32_t slot = s_reset[j];
+    NRng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, base + (s_meta[slot] & 255u)), 0u,
+             make_uint4(0, 0, 0, 0)};
+    const NLane<N> R = new_episode<N>((s_b[slot].w & kEpisodeMask) + 1u, rng);
+    uint4 wa, wb;
+    pack(R, wa, wb);
+    s_a[slot] = wa;
+    s_b[slot] = wb;
+    s_legal[slot] = legal_mask(R);
+    s_out[slot] = (s_out[slot] & 0x00FFFFFFu) | (((uint32_t)current_player(R) & 0xFFu) << 24);
+  }
+  __syncthreads();
+
+  // phase 3: each thread stores its own lane
+  if (!live) return;
+  a.sa[i] = s_a[pos];
+  a.sb[i] = s_b[pos];
+  const uint32_t o = s_out[pos];
+  store_step_outputs<N>(a, i, (int)(o & 31u) - 1, (o >> 5) & 3u, (o >> 7) & 7u, (o >> 10) & 7u, s_legal[pos],
+                        (int)(int8_t)(o >> 24));
 }
 
 struct RolloutArgs {
@@ -288,6 +425,12 @@ __global__ __launch_bounds__(kThreads) void k_import(uint4* sa, uint4* sb, int64
 
 namespace {
 
+// COUP_NP_SORT=0 selects the in-place step kernel (A/B measurements).
+bool np_sort() {
+  const char* e = std::getenv("COUP_NP_SORT");
+  return e ? (std::atoi(e) != 0) : true;
+}
+
 unsigned grid_for(int64_t n, int per_block) { return (unsigned)((n + per_block - 1) / per_block); }
 
 // calls f(std::integral_constant<int, N>) for the env's player count
@@ -338,10 +481,17 @@ hipError_t launch_step(const Env& e, const int8_t* actions, const coup_step_outp
   }
   return dispatch(e.players, [&](auto np) {
     constexpr int N = decltype(np)::value;
-    if (actions)
-      k_step<N, false><<<grid_for(e.n, kThreads), kThreads, 0, e.stream>>>(a);
-    else
-      k_step<N, true><<<grid_for(e.n, kThreads), kThreads, 0, e.stream>>>(a);
+    const unsigned grid = grid_for(e.n, kThreads);
+    if (np_sort()) {
+      if (actions)
+        k_step_sorted<N, false><<<grid, kThreads, 0, e.stream>>>(a);
+      else
+        k_step_sorted<N, true><<<grid, kThreads, 0, e.stream>>>(a);
+    } else if (actions) {
+      k_step<N, false><<<grid, kThreads, 0, e.stream>>>(a);
+    } else {
+      k_step<N, true><<<grid, kThreads, 0, e.stream>>>(a);
+    }
     if (obs) k_obs<N><<<grid_for(e.n, kObsLanes), kThreads, 0, e.stream>>>(e.sa, e.sb, e.n, obs);
   });
 }

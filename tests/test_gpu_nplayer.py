@@ -141,3 +141,37 @@ def test_six_player_full_batch_properties():
     assert np.all(deck + cards == 15)
     assert not np.any(w[:, 3] >> 31)
     assert env.error_count() == 0
+
+
+@pytest.mark.parametrize("n_players", [2, 4, 6])
+@pytest.mark.parametrize("auto_reset", [True, False])
+def test_regrouped_step_equals_in_place_step(monkeypatch, n_players, auto_reset):
+    """k_step_sorted (lanes counting-sorted by decision through LDS, resets
+    dealt by the first threads) == k_step (lanes in place), ragged batch,
+    both the uniform policy and caller actions (about 1 in 8 illegal, so
+    the rejected-action path is in the sort too)."""
+    n, steps, seed = 1000, 150, 11 + n_players
+    envs = {}
+    for knob in ("0", "1"):
+        monkeypatch.setenv("COUP_NP_SORT", knob)
+        envs[knob] = BatchedCoupEnv(n, seed=seed, auto_reset=auto_reset, obs=False, num_players=n_players,
+                                    generic=True)
+    g = torch.Generator().manual_seed(seed)
+    for t in range(steps):
+        acts = None
+        if t % 3 == 2:
+            legal = envs["0"].query(obs=False)["legal_mask"].cpu().to(torch.int64)
+            acts = torch.randint(0, 18, (n,), generator=g, dtype=torch.int64)
+            ok = ((legal >> acts) & 1) == 1
+            keep = torch.rand(n, generator=g) < 0.875
+            # pick a legal action where there is one, except for the kept illegal ones
+            first = torch.where(legal != 0, (legal & -legal).float().log2().to(torch.int64), acts)
+            acts = torch.where(ok | ~keep, acts, first).to(torch.int8)
+        outs = {}
+        for knob, env in envs.items():
+            monkeypatch.setenv("COUP_NP_SORT", knob)
+            outs[knob] = {k: v.clone() for k, v in env.step(acts).items()}
+        for k in ("actions", "rewards", "step_type", "legal_mask", "current_player"):
+            assert torch.equal(outs["0"][k], outs["1"][k]), (t, k)
+        assert torch.equal(envs["0"].export_state(), envs["1"].export_state()), t
+    assert envs["0"].error_count() == envs["1"].error_count()
