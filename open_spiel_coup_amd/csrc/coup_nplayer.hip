@@ -287,6 +287,127 @@ __global__ __launch_bounds__(kThreads) void k_rollout(RolloutArgs a) {
   if (errs) atomicAdd(a.err_count, errs);
 }
 
+// The same rollout with the block's lanes regrouped by decision every step
+// (default; COUP_NP_SORT=0 selects k_rollout).  A lane's next decision is
+// drawn at the end of the step before (its "key"); the block counting-sorts
+// its lanes by key through LDS, and thread t plays the lane in slot t, so
+// the waves applying a step hold lanes playing the same action.  A lane
+// that finished gets key kReset: the finished lanes of a block land in one
+// wave, which deals their new episodes, draws and applies.  Lanes wander
+// between threads from step to step (the RNG is keyed by lane, and the
+// per-lane statistics live in LDS by lane) and go home at the end.
+// Results equal k_rollout's.
+constexpr uint32_t kKeyReset = 18u, kKeyDead = 19u;
+
+// Exclusive prefix of the 20 bin counts below `key` (5 broadcast LDS reads).
+__device__ __forceinline__ uint32_t bins_below(const uint32_t* bin, uint32_t key) {
+  uint32_t below = 0u;
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    const uint4 b = reinterpret_cast<const uint4*>(bin)[q];
+    below += (4u * q + 0u < key ? b.x : 0u) + (4u * q + 1u < key ? b.y : 0u) + (4u * q + 2u < key ? b.z : 0u) +
+             (4u * q + 3u < key ? b.w : 0u);
+  }
+  return below;
+}
+
+// The decision key of a lane at a decision node: the uniform policy's draw,
+// or kKeyDead (counted as an error) if the node has no legal decision.
+template <int N>
+__device__ __forceinline__ uint32_t draw_key(const NLane<N>& L, NRng& rng, uint32_t& errs) {
+  const uint32_t m = decision_mask(L);
+  if (m == 0u) {
+    errs += 1u;
+    return kKeyDead;
+  }
+  return sample_action(m, rng.draw(L.episode, L.move));
+}
+
+// 8 waves per SIMD (64 VGPRs, a few spilled): 29.1 vs 30.3 us per step at
+// 6 waves.  Carrying each lane's cached Philox block through LDS with the
+// record measured no faster (30.2 us) and was dropped.
+template <int N>
+__global__ __launch_bounds__(kThreads, 8) void k_rollout_sorted(RolloutArgs a) {
+  __shared__ uint4 s_a[kThreads], s_b[kThreads];
+  __shared__ uint32_t s_meta[kThreads];  // slot -> lane | key << 8 | decisions this episode << 13
+  __shared__ int32_t s_eps[kThreads], s_ret[kThreads], s_len[kThreads];  // by lane
+  __shared__ __attribute__((aligned(16))) uint32_t s_bin[2][32];
+  const uint32_t t = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * kThreads;
+  const bool live = base + t < a.n;
+  if (t < 64u) s_bin[t >> 5][t & 31u] = 0u;
+  s_eps[t] = 0;
+  s_ret[t] = 0;
+  s_len[t] = 0;
+  NRng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, base + t), 0u, make_uint4(0, 0, 0, 0)};
+  NLane<N> L = initial_lane<N>(0u);
+  uint32_t lane = t, cur = 0u, key = kKeyDead, errs = 0u;
+  if (live) {
+    L = unpack<N>(a.sa[base + t], a.sb[base + t]);
+    if (is_terminal(L)) L = new_episode<N>(L.episode + 1u, rng);  // a terminal starting record
+    resolve_chance(L, rng);  // a lane left at a chance node
+    key = draw_key(L, rng, errs);
+  }
+  for (int64_t s = 0; s < a.steps; ++s) {
+    uint32_t* bin = s_bin[s & 1];
+    __syncthreads();  // this step's bins are zero; last step's slots are read
+    const uint32_t rank = atomicAdd(&bin[key], 1u);
+    __syncthreads();
+    const uint32_t pos = bins_below(bin, key) + rank;
+    if (t < 32u) s_bin[(s + 1) & 1][t] = 0u;  // read for the last time in step s - 1
+    uint4 wa, wb;
+    pack(L, wa, wb);
+    s_a[pos] = wa;
+    s_b[pos] = wb;
+    s_meta[pos] = lane | (key << 8) | (cur << 13);
+    __syncthreads();
+    const uint32_t m = s_meta[t];
+    lane = m & 255u;
+    key = (m >> 8) & 31u;
+    cur = m >> 13;
+    L = unpack<N>(s_a[t], s_b[t]);
+    if (key == kKeyDead) continue;
+    rng.env_id = lane_stream_id(a.env_id_base, base + lane);
+    rng.blk_tag = 0u;
+    if (key == kKeyReset) {
+      L = new_episode<N>(L.episode + 1u, rng);
+      key = draw_key(L, rng, errs);
+      if (key == kKeyDead) continue;
+    }
+    const uint32_t err_before = L.err;
+    apply_decision(L, key);
+    L.move += 1u;
+    resolve_chance(L, rng);
+    errs += (L.err && !err_before) ? 1u : 0u;
+    cur += 1u;
+    if (is_terminal(L)) {
+      s_eps[lane] += 1;
+      s_ret[lane] += returns(L, 0u);
+      s_len[lane] += (int32_t)cur;
+      cur = 0u;
+      key = kKeyReset;
+    } else if (s + 1 < a.steps) {
+      key = draw_key(L, rng, errs);
+    }
+  }
+  if (key == kKeyReset) L = new_episode<N>(L.episode + 1u, rng);  // finished on the last step
+  __syncthreads();
+  uint4 wa, wb;
+  pack(L, wa, wb);
+  s_a[lane] = wa;
+  s_b[lane] = wb;
+  __syncthreads();
+  if (live) {
+    const int64_t i = base + t;
+    a.sa[i] = s_a[t];
+    a.sb[i] = s_b[t];
+    if (a.episodes) a.episodes[i] += s_eps[t];
+    if (a.return_sum) a.return_sum[i] += s_ret[t];
+    if (a.length_sum) a.length_sum[i] += s_len[t];
+  }
+  if (errs) atomicAdd(a.err_count, errs);
+}
+
 template <int N>
 __global__ __launch_bounds__(kThreads) void k_reset(uint4* sa, uint4* sb, int64_t n, const uint8_t* mask, int mode,
                                                   int deal, uint32_t seed_lo, uint32_t seed_hi,
@@ -514,7 +635,11 @@ hipError_t launch_rollout(const Env& e, int64_t steps, const coup_rollout_stats*
   }
   return dispatch(e.players, [&](auto np) {
     constexpr int N = decltype(np)::value;
-    k_rollout<N><<<grid_for(e.n, kThreads), kThreads, 0, e.stream>>>(a);
+    const unsigned grid = grid_for(e.n, kThreads);
+    if (np_sort())
+      k_rollout_sorted<N><<<grid, kThreads, 0, e.stream>>>(a);
+    else
+      k_rollout<N><<<grid, kThreads, 0, e.stream>>>(a);
   });
 }
 

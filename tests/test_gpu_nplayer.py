@@ -175,3 +175,33 @@ def test_regrouped_step_equals_in_place_step(monkeypatch, n_players, auto_reset)
             assert torch.equal(outs["0"][k], outs["1"][k]), (t, k)
         assert torch.equal(envs["0"].export_state(), envs["1"].export_state()), t
     assert envs["0"].error_count() == envs["1"].error_count()
+
+
+@pytest.mark.parametrize("n_players", [2, 5, 6])
+def test_regrouped_rollout_equals_in_place_rollout(monkeypatch, n_players):
+    """k_rollout_sorted (lanes re-sorted by their next decision every step,
+    finished lanes reset together) == k_rollout: records and per-lane
+    statistics, ragged batch, launches of 1, 7 and 150 steps, and a start
+    from terminal records (auto_reset off) and mid-deal records."""
+    n, seed = 1000, 21 + n_players
+    envs, stats = {}, {}
+    for knob in ("0", "1"):
+        monkeypatch.setenv("COUP_NP_SORT", knob)
+        env = BatchedCoupEnv(n, seed=seed, auto_reset=False, obs=False, num_players=n_players, generic=True)
+        for _ in range(40):
+            env.step()  # some lanes end terminal (no auto-reset)
+        envs[knob], stats[knob] = env, env.new_stats()
+    assert torch.equal(envs["0"].export_state(), envs["1"].export_state())
+    for k in (1, 7, 150):
+        for knob, env in envs.items():
+            monkeypatch.setenv("COUP_NP_SORT", knob)
+            env.rollout(k, stats[knob])
+        assert torch.equal(envs["0"].export_state(), envs["1"].export_state()), k
+        for key in ("episodes", "return_sum", "length_sum"):
+            assert torch.equal(stats["0"][key], stats["1"][key]), (k, key)
+    for knob, env in envs.items():  # records at the first chance node, deals pending
+        monkeypatch.setenv("COUP_NP_SORT", knob)
+        env.new_initial_state()
+        env.rollout(9, stats[knob])
+    assert torch.equal(envs["0"].export_state(), envs["1"].export_state())
+    assert envs["0"].error_count() == envs["1"].error_count() == 0

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--players", type=int, default=2)
     ap.add_argument("--info", type=int, default=0, help="write the InformationStateTensor (c3i) instead")
+    ap.add_argument("--fused", type=int, default=0, help="time coup_rollout launches of this many steps instead")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     import torch
@@ -52,15 +53,21 @@ def main():
                 if kv:
                     k, val = kv.split("=")
                     os.environ[k] = val
-            for _ in range(3):
-                env.step()
+            if a.fused:
+                env.rollout(a.fused)
+            else:
+                for _ in range(3):
+                    env.step()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            for _ in range(a.steps):
-                env.step()
+            if a.fused:
+                env.rollout(a.fused * a.steps)
+            else:
+                for _ in range(a.steps):
+                    env.step()
             e1.record(stream)
             e1.synchronize()
-            times[v].append(e0.elapsed_time(e1) * 1e3 / a.steps)
+            times[v].append(e0.elapsed_time(e1) * 1e3 / (a.steps * max(a.fused, 1)))  # us per env step
     assert env.error_count() == 0
     for v in a.variants:
         t = times[v]
