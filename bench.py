@@ -61,6 +61,17 @@ CONFIGS = {
 }
 
 
+def _regrouped(batch):
+    """Does the library regroup lanes by decision for a launch of `batch`
+    lanes (the *_sorted step / rollout kernels)?  Mirrors
+    coup::regroup_lanes (csrc/coup_regroup.h): COUP_REGROUP forces it,
+    else batches of 2^18 lanes and more."""
+    e = os.environ.get("COUP_REGROUP")
+    if e is not None:
+        return int(e) != 0
+    return batch >= (1 << 18)
+
+
 def _writer(mode_env):
     """(ObsMode template value, block size) of the step kernel that
     coup_step launches for COUP_OBS_MODE (default 9; csrc/coup_kernels.hip)."""
@@ -231,10 +242,12 @@ def main():
             ent = tr.get(cfg)
             if ent and ent.get("batch") == B:
                 traffic = ent.get("hbm_bytes_per_launch")
+        sorted_ = "_sorted" if _regrouped(B) else ""
         if players != 2:
-            kernel = "coup::np::k_rollout<%d>" % players if fused else "coup::np::k_step<%d, true>" % players
+            kernel = ("coup::np::k_rollout%s<%d>" % (sorted_, players) if fused else
+                      "coup::np::k_step%s<%d, true>" % (sorted_, players))
         elif fused:
-            kernel = "coup::k_rollout"
+            kernel = "coup::k_rollout" + sorted_
         elif with_info:
             kernel = "coup::k_step<true, 0, 256, 2>"
         elif with_obs:

@@ -29,6 +29,7 @@ __device__ __forceinline__ void count_philox_eval() {
 #include "coup_lane.h"
 #include "coup_mi355x.h"
 #include "coup_np.h"
+#include "coup_regroup.h"
 
 namespace coup {
 
@@ -829,6 +830,99 @@ __global__ __launch_bounds__(kThreads) void k_rollout(RolloutArgs a) {
   if (errs) atomicAdd(a.err_count, errs);
 }
 
+// The decision key of a lane at a decision node: the uniform policy's draw,
+// or kKeyDead (counted as an error) if the node has no legal decision.
+__device__ __forceinline__ uint32_t draw_key(const Lane& L, Rng& rng, uint32_t& errs) {
+  const uint32_t m = decision_mask(L);
+  if (m == 0u) {
+    errs += 1u;
+    return kKeyDead;
+  }
+  return sample_action(m, rng.draw(L.episode, L.move));
+}
+
+// k_rollout with the block's lanes regrouped by decision every step
+// (batches of 2^18 lanes and more: coup_regroup.h).  A lane's
+// next decision is drawn at the end of the step before; the block sorts its
+// lanes by it through LDS and thread t plays the lane in slot t.  Finished
+// lanes get kKeyReset and are dealt their next episode together, in one
+// wave.  Per-lane statistics live in LDS by lane; the lanes go home at the
+// end.  Same results as k_rollout.
+__global__ __launch_bounds__(kThreads, 8) void k_rollout_sorted(RolloutArgs a) {
+  __shared__ uint4 s_rec[kThreads];
+  __shared__ uint32_t s_meta[kThreads];  // slot -> lane | key << 8 | decisions this episode << 13
+  __shared__ int32_t s_eps[kThreads], s_ret[kThreads], s_len[kThreads];  // by lane
+  __shared__ __attribute__((aligned(16))) uint32_t s_bin[2][32];
+  const uint32_t t = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * kThreads;
+  const bool live = base + t < a.n;
+  if (t < 64u) s_bin[t >> 5][t & 31u] = 0u;
+  s_eps[t] = 0;
+  s_ret[t] = 0;
+  s_len[t] = 0;
+  Rng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, base + t), 0u, make_uint4(0, 0, 0, 0)};
+  NoHistory none;
+  Lane L = initial_lane(0u);
+  uint32_t lane = t, cur = 0u, key = kKeyDead, errs = 0u;
+  if (live) {
+    L = unpack(a.state[base + t]);
+    if (is_terminal(L)) L = new_episode(L.episode + 1u, rng, none);  // a terminal starting record
+    resolve_chance(L, rng);  // a lane left at a chance node
+    key = draw_key(L, rng, errs);
+  }
+  for (int64_t s = 0; s < a.steps; ++s) {
+    uint32_t* bin = s_bin[s & 1];
+    __syncthreads();  // this step's bins are zero; last step's slots are read
+    const uint32_t rank = atomicAdd(&bin[key], 1u);
+    __syncthreads();
+    const uint32_t pos = bins_below(bin, key) + rank;
+    if (t < 32u) s_bin[(s + 1) & 1][t] = 0u;  // read for the last time in step s - 1
+    s_rec[pos] = pack(L);
+    s_meta[pos] = lane | (key << 8) | (cur << 13);
+    __syncthreads();
+    const uint32_t m = s_meta[t];
+    lane = m & 255u;
+    key = (m >> 8) & 31u;
+    cur = m >> 13;
+    L = unpack(s_rec[t]);
+    if (key == kKeyDead) continue;
+    rng.env_id = lane_stream_id(a.env_id_base, base + lane);
+    rng.blk_tag = 0u;
+    if (key == kKeyReset) {
+      L = new_episode(L.episode + 1u, rng, none);
+      key = draw_key(L, rng, errs);
+      if (key == kKeyDead) continue;
+    }
+    const uint32_t err_before = L.err;
+    apply_decision(L, key);
+    L.move += 1u;
+    resolve_chance(L, rng);
+    errs += (L.err && !err_before) ? 1u : 0u;
+    cur += 1u;
+    if (is_terminal(L)) {
+      s_eps[lane] += 1;
+      s_ret[lane] += return0(L);
+      s_len[lane] += (int32_t)cur;
+      cur = 0u;
+      key = kKeyReset;
+    } else if (s + 1 < a.steps) {
+      key = draw_key(L, rng, errs);
+    }
+  }
+  if (key == kKeyReset) L = new_episode(L.episode + 1u, rng, none);  // finished on the last step
+  __syncthreads();
+  s_rec[lane] = pack(L);
+  __syncthreads();
+  if (live) {
+    const int64_t i = base + t;
+    a.state[i] = s_rec[t];
+    if (a.episodes) a.episodes[i] += s_eps[t];
+    if (a.return_sum) a.return_sum[i] += s_ret[t];
+    if (a.length_sum) a.length_sum[i] += s_len[t];
+  }
+  if (errs) atomicAdd(a.err_count, errs);
+}
+
 // NewInitialState / reset of selected lanes.  mode 0: fresh env (episode 0);
 // mode 1: next episode.  deal: resolve the four initial deals.
 __global__ __launch_bounds__(kThreads) void k_reset(uint4* state, int64_t n, const uint8_t* mask, int mode, int deal,
@@ -1230,7 +1324,10 @@ int coup_rollout(coup_env* env, int64_t steps, const coup_rollout_stats* stats) 
     a.return_sum = stats->return_sum;
     a.length_sum = stats->length_sum;
   }
-  coup::k_rollout<<<grid_for(env->batch), coup::kThreads, 0, env->stream>>>(a);
+  if (coup::regroup_lanes(env->batch))
+    coup::k_rollout_sorted<<<grid_for(env->batch), coup::kThreads, 0, env->stream>>>(a);
+  else
+    coup::k_rollout<<<grid_for(env->batch), coup::kThreads, 0, env->stream>>>(a);
   COUP_HIP_TRY(hipGetLastError());
   return COUP_OK;
 }

@@ -24,6 +24,7 @@ __device__ __forceinline__ void count_philox_eval() {
 #endif
 #include "coup_nlane.h"
 #include "coup_np.h"
+#include "coup_regroup.h"
 
 namespace coup {
 namespace np {
@@ -107,7 +108,7 @@ __global__ __launch_bounds__(kThreads) void k_step(StepArgs a) {
 }
 
 // The same step with the block's lanes regrouped by decision before the
-// rules run (default; COUP_NP_SORT=0 selects k_step).  Phase 1: each thread
+// rules run (batches of 2^18 lanes and more: coup_regroup.h).  Phase 1: each thread
 // takes its lane up to the decision (step_lane_pre) and the block
 // counting-sorts its lanes by that decision through LDS, so a wave of the
 // apply phase holds lanes playing the same action: the union of branches it
@@ -119,8 +120,6 @@ __global__ __launch_bounds__(kThreads) void k_step(StepArgs a) {
 // every wave holding a finished lane.  Phase 3: each thread stores its own
 // lane's record and outputs back in place, coalesced.  The RNG is
 // stateless per (lane, episode, draw), so results equal k_step's.
-constexpr uint32_t kKeyPad = 19u;  // past-the-end lanes of the last block
-
 template <int N, bool UNIFORM>
 __global__ __launch_bounds__(kThreads) void k_step_sorted(StepArgs a) {
   __shared__ uint4 s_a[kThreads], s_b[kThreads];
@@ -139,7 +138,7 @@ __global__ __launch_bounds__(kThreads) void k_step_sorted(StepArgs a) {
 
   // phase 1: up to the decision
   NLane<N> L;
-  uint32_t key = kKeyPad, st = 0u;
+  uint32_t key = kKeyDead, st = 0u;
   bool error = false;
   if (live) {
     L = unpack<N>(a.sa[i], a.sb[i]);
@@ -288,7 +287,7 @@ __global__ __launch_bounds__(kThreads) void k_rollout(RolloutArgs a) {
 }
 
 // The same rollout with the block's lanes regrouped by decision every step
-// (default; COUP_NP_SORT=0 selects k_rollout).  A lane's next decision is
+// (batches of 2^18 lanes and more: coup_regroup.h).  A lane's next decision is
 // drawn at the end of the step before (its "key"); the block counting-sorts
 // its lanes by key through LDS, and thread t plays the lane in slot t, so
 // the waves applying a step hold lanes playing the same action.  A lane
@@ -297,20 +296,6 @@ __global__ __launch_bounds__(kThreads) void k_rollout(RolloutArgs a) {
 // between threads from step to step (the RNG is keyed by lane, and the
 // per-lane statistics live in LDS by lane) and go home at the end.
 // Results equal k_rollout's.
-constexpr uint32_t kKeyReset = 18u, kKeyDead = 19u;
-
-// Exclusive prefix of the 20 bin counts below `key` (5 broadcast LDS reads).
-__device__ __forceinline__ uint32_t bins_below(const uint32_t* bin, uint32_t key) {
-  uint32_t below = 0u;
-#pragma unroll
-  for (int q = 0; q < 5; ++q) {
-    const uint4 b = reinterpret_cast<const uint4*>(bin)[q];
-    below += (4u * q + 0u < key ? b.x : 0u) + (4u * q + 1u < key ? b.y : 0u) + (4u * q + 2u < key ? b.z : 0u) +
-             (4u * q + 3u < key ? b.w : 0u);
-  }
-  return below;
-}
-
 // The decision key of a lane at a decision node: the uniform policy's draw,
 // or kKeyDead (counted as an error) if the node has no legal decision.
 template <int N>
@@ -546,12 +531,6 @@ __global__ __launch_bounds__(kThreads) void k_import(uint4* sa, uint4* sb, int64
 
 namespace {
 
-// COUP_NP_SORT=0 selects the in-place step kernel (A/B measurements).
-bool np_sort() {
-  const char* e = std::getenv("COUP_NP_SORT");
-  return e ? (std::atoi(e) != 0) : true;
-}
-
 unsigned grid_for(int64_t n, int per_block) { return (unsigned)((n + per_block - 1) / per_block); }
 
 // calls f(std::integral_constant<int, N>) for the env's player count
@@ -603,7 +582,7 @@ hipError_t launch_step(const Env& e, const int8_t* actions, const coup_step_outp
   return dispatch(e.players, [&](auto np) {
     constexpr int N = decltype(np)::value;
     const unsigned grid = grid_for(e.n, kThreads);
-    if (np_sort()) {
+    if (regroup_lanes(e.n)) {
       if (actions)
         k_step_sorted<N, false><<<grid, kThreads, 0, e.stream>>>(a);
       else
@@ -636,7 +615,7 @@ hipError_t launch_rollout(const Env& e, int64_t steps, const coup_rollout_stats*
   return dispatch(e.players, [&](auto np) {
     constexpr int N = decltype(np)::value;
     const unsigned grid = grid_for(e.n, kThreads);
-    if (np_sort())
+    if (regroup_lanes(e.n))
       k_rollout_sorted<N><<<grid, kThreads, 0, e.stream>>>(a);
     else
       k_rollout<N><<<grid, kThreads, 0, e.stream>>>(a);

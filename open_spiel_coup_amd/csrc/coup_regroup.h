@@ -1,0 +1,50 @@
+// coup_regroup.h -- block-level regrouping of lanes by their next decision
+// (the sorted step / rollout kernels of both engines).
+//
+// A wave executes the union of its lanes' branches of the rules.  The
+// sorted kernels give every lane a small key (its decision 0..17, or
+// kKeyReset / kKeyDead), counting-sort the block's lanes by key through
+// LDS (one LDS atomic per lane for its rank within the key, an exclusive
+// prefix over the key counts for the key's base), and let thread t play
+// the lane in slot t, so the waves of the apply phase hold lanes taking the
+// same branch.  The RNG is stateless per (lane, episode, draw index), so a
+// lane can be played by any thread with the same results.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <cstdlib>
+
+namespace coup {
+
+constexpr uint32_t kKeyReset = 18u;  // the lane finished: deal its next episode, then decide
+constexpr uint32_t kKeyDead = 19u;   // no decision to play (errored lane, or past the batch)
+constexpr uint32_t kKeyCount = 20u;
+
+// Exclusive prefix of the key counts below `key`: five broadcast 16-byte
+// LDS reads (every lane reads the same addresses, no bank conflicts).
+__device__ __forceinline__ uint32_t bins_below(const uint32_t* bin, uint32_t key) {
+  uint32_t below = 0u;
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    const uint4 b = reinterpret_cast<const uint4*>(bin)[q];
+    below += (4u * q + 0u < key ? b.x : 0u) + (4u * q + 1u < key ? b.y : 0u) + (4u * q + 2u < key ? b.z : 0u) +
+             (4u * q + 3u < key ? b.w : 0u);
+  }
+  return below;
+}
+
+// Host side: regroup a launch of n lanes?  Measured on MI355X (tools/ab_step.py,
+// DESIGN.md section 5): the sort's barriers and LDS round trips cost more
+// than the divergence they remove below ~4 waves per SIMD (2^18 lanes on 256
+// CUs) and win above it (2-player rollout 2^20: 20.5 -> 18.6 us per step;
+// 6-player 2^20: step 56.8 -> 43.0, rollout 41.5 -> 29.1).  COUP_REGROUP=0/1
+// forces it off/on (A/B runs and tests).
+constexpr int64_t kRegroupMinLanes = int64_t{1} << 18;
+
+inline bool regroup_lanes(int64_t n) {
+  const char* e = std::getenv("COUP_REGROUP");
+  if (e) return std::atoi(e) != 0;
+  return n >= kRegroupMinLanes;
+}
+
+}  // namespace coup

@@ -21,12 +21,15 @@ def _np(t):
     return t.detach().cpu().numpy()
 
 
+@pytest.mark.parametrize("regroup", ["1", "0"], ids=["regrouped", "in-place"])
 @pytest.mark.parametrize("n_players", [2, 3, 4, 5, 6])
 @pytest.mark.parametrize("auto_reset", [True, False])
-def test_uniform_steps_match_spec(n_players, auto_reset):
+def test_uniform_steps_match_spec(monkeypatch, n_players, auto_reset, regroup):
     """coup_step (uniform policy) == np_rollout: actions, rewards [B, N],
     step types, legal masks, ObservationTensor [B, N, 49N] at every step and
-    the final 32-byte records."""
+    the final 32-byte records; step kernel with the lanes regrouped by
+    decision (coup_regroup.h, the default from 2^18 lanes) and in place."""
+    monkeypatch.setenv("COUP_REGROUP", regroup)
     n, steps, seed, base = 512, 200, 40 + n_players, 7000
     ref = oracle.np_rollout(n_players, seed=seed, n=n, steps=steps, env_id_base=base, auto_reset=auto_reset,
                             want_obs=True)
@@ -57,8 +60,10 @@ def test_generic_engine_equals_two_player_engine():
     assert a.error_count() == 0 and b.error_count() == 0
 
 
+@pytest.mark.parametrize("regroup", ["1", "0"], ids=["regrouped", "in-place"])
 @pytest.mark.parametrize("n_players", [3, 6])
-def test_fused_rollout_matches_spec(n_players):
+def test_fused_rollout_matches_spec(monkeypatch, n_players, regroup):
+    monkeypatch.setenv("COUP_REGROUP", regroup)
     n, steps, seed = 4096, 300, 5 + n_players
     ref = oracle.np_rollout(n_players, seed=seed, n=n, steps=steps, auto_reset=True)
     env = BatchedCoupEnv(n, seed=seed, obs=False, num_players=n_players)
@@ -153,7 +158,7 @@ def test_regrouped_step_equals_in_place_step(monkeypatch, n_players, auto_reset)
     n, steps, seed = 1000, 150, 11 + n_players
     envs = {}
     for knob in ("0", "1"):
-        monkeypatch.setenv("COUP_NP_SORT", knob)
+        monkeypatch.setenv("COUP_REGROUP", knob)
         envs[knob] = BatchedCoupEnv(n, seed=seed, auto_reset=auto_reset, obs=False, num_players=n_players,
                                     generic=True)
     g = torch.Generator().manual_seed(seed)
@@ -169,7 +174,7 @@ def test_regrouped_step_equals_in_place_step(monkeypatch, n_players, auto_reset)
             acts = torch.where(ok | ~keep, acts, first).to(torch.int8)
         outs = {}
         for knob, env in envs.items():
-            monkeypatch.setenv("COUP_NP_SORT", knob)
+            monkeypatch.setenv("COUP_REGROUP", knob)
             outs[knob] = {k: v.clone() for k, v in env.step(acts).items()}
         for k in ("actions", "rewards", "step_type", "legal_mask", "current_player"):
             assert torch.equal(outs["0"][k], outs["1"][k]), (t, k)
@@ -186,7 +191,7 @@ def test_regrouped_rollout_equals_in_place_rollout(monkeypatch, n_players):
     n, seed = 1000, 21 + n_players
     envs, stats = {}, {}
     for knob in ("0", "1"):
-        monkeypatch.setenv("COUP_NP_SORT", knob)
+        monkeypatch.setenv("COUP_REGROUP", knob)
         env = BatchedCoupEnv(n, seed=seed, auto_reset=False, obs=False, num_players=n_players, generic=True)
         for _ in range(40):
             env.step()  # some lanes end terminal (no auto-reset)
@@ -194,13 +199,13 @@ def test_regrouped_rollout_equals_in_place_rollout(monkeypatch, n_players):
     assert torch.equal(envs["0"].export_state(), envs["1"].export_state())
     for k in (1, 7, 150):
         for knob, env in envs.items():
-            monkeypatch.setenv("COUP_NP_SORT", knob)
+            monkeypatch.setenv("COUP_REGROUP", knob)
             env.rollout(k, stats[knob])
         assert torch.equal(envs["0"].export_state(), envs["1"].export_state()), k
         for key in ("episodes", "return_sum", "length_sum"):
             assert torch.equal(stats["0"][key], stats["1"][key]), (k, key)
     for knob, env in envs.items():  # records at the first chance node, deals pending
-        monkeypatch.setenv("COUP_NP_SORT", knob)
+        monkeypatch.setenv("COUP_REGROUP", knob)
         env.new_initial_state()
         env.rollout(9, stats[knob])
     assert torch.equal(envs["0"].export_state(), envs["1"].export_state())

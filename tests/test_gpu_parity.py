@@ -208,10 +208,14 @@ def test_external_actions_replay():
     assert env.error_count() == 0
 
 
-def test_fused_rollout_matches_oracle():
-    """coup_rollout (K steps per launch, registers only) lands on the same
-    states and episode statistics as the oracle."""
-    n, steps, seed = 4096, 300, 21
+@pytest.mark.parametrize("regroup", ["1", "0"], ids=["regrouped", "in-place"])
+def test_fused_rollout_matches_oracle(monkeypatch, regroup):
+    """coup_rollout (K steps per launch) lands on the same states and episode
+    statistics as the oracle, with the lanes regrouped by decision every
+    step (coup_regroup.h, the default from 2^18 lanes) and in place.
+    Ragged batch."""
+    monkeypatch.setenv("COUP_REGROUP", regroup)
+    n, steps, seed = 4000, 300, 21
     ref = oracle.rollout(seed=seed, n=n, steps=steps, auto_reset=True, want_trajectory=False)
     env = BatchedCoupEnv(n, seed=seed, auto_reset=True, obs=False)
     stats = env.new_stats()
@@ -221,6 +225,30 @@ def test_fused_rollout_matches_oracle():
     assert int(stats["episodes"].sum()) == int(ref["episodes_done"][0])
     assert int(stats["return_sum"].sum()) == int(ref["return_sum_p0"][0])
     assert env.error_count() == 0
+
+
+def test_regrouped_rollout_equals_in_place_rollout(monkeypatch):
+    """k_rollout_sorted == k_rollout lane by lane (records and per-lane
+    statistics), starting from terminal records (auto_reset off) and from
+    records at the first chance node, launches of 1, 5 and 120 steps."""
+    n, seed = 1500, 31
+    envs, stats = {}, {}
+    for knob in ("0", "1"):
+        monkeypatch.setenv("COUP_REGROUP", knob)
+        env = BatchedCoupEnv(n, seed=seed, auto_reset=False, obs=False)
+        for _ in range(30):
+            env.step()
+        envs[knob], stats[knob] = env, env.new_stats()
+    for k in (1, 5, 120, -7):
+        for knob, env in envs.items():
+            monkeypatch.setenv("COUP_REGROUP", knob)
+            if k < 0:
+                env.new_initial_state()
+            env.rollout(abs(k), stats[knob])
+        assert torch.equal(envs["0"].export_state(), envs["1"].export_state()), k
+        for key in ("episodes", "return_sum", "length_sum"):
+            assert torch.equal(stats["0"][key], stats["1"][key]), (k, key)
+    assert envs["0"].error_count() == envs["1"].error_count() == 0
 
 
 def test_illegal_action_rejected():

@@ -62,8 +62,10 @@ def main():
         """Is `kn` the kernel bench.py times for this config?"""
         if players != 2:
             if fused:
-                return bool(re.search(r"np::k_rollout<%d>|2np9k_rolloutILi%dE" % (players, players), kn))
-            return bool(re.search(r"np::k_step<%d, true>|2np6k_stepILi%dELb1E" % (players, players), kn))
+                return bool(re.search(r"np::k_rollout(_sorted)?<%d>|2np(9k_rollout|16k_rollout_sorted)ILi%dE"
+                                      % (players, players), kn))
+            return bool(re.search(r"np::k_step(_sorted)?<%d, true>|2np(6k_step|13k_step_sorted)ILi%dELb1E"
+                                  % (players, players), kn))
         if "np::" in kn or "2np" in kn:
             return False
         if fused:
