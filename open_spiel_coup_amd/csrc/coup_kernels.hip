@@ -830,6 +830,120 @@ __global__ __launch_bounds__(kThreads) void k_rollout(RolloutArgs a) {
   if (errs) atomicAdd(a.err_count, errs);
 }
 
+// The bare step (no observations, no history) with the block's lanes
+// regrouped by decision (batches of 2^18 lanes and more: coup_regroup.h),
+// the 2-player form of np::k_step_sorted.  Phase 1: each thread takes its
+// lane up to the decision (step_lane's first half); the block counting-sorts
+// the lanes by decision through LDS.  Phase 2: thread t applies slot t's
+// decision and resolves the deals; finished lanes are listed and dealt their
+// next episode by the block's first threads.  Phase 3: each thread stores
+// its own lane's record and outputs, coalesced.  Same results as k_step.
+template <bool UNIFORM>
+__global__ __launch_bounds__(kThreads, 8) void k_step_sorted(StepArgs a) {
+  __shared__ uint4 s_rec[kThreads];
+  __shared__ uint32_t s_meta[kThreads];   // slot -> owner thread | key << 8 | st << 13
+  __shared__ uint32_t s_out[kThreads];    // slot -> act + 1 | st << 5 | (rew + 2) << 7 | cp << 24
+  __shared__ uint32_t s_legal[kThreads];  // slot -> post-step legal mask
+  __shared__ uint32_t s_reset[kThreads];  // slots whose lane auto-resets
+  __shared__ uint32_t s_bin[32];
+  __shared__ uint32_t s_nreset;
+  const uint32_t t = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * kThreads;
+  const int64_t i = base + t;
+  const bool live = i < a.n;
+  if (t < 32u) s_bin[t] = 0u;
+  if (t == 0u) s_nreset = 0u;
+  NoHistory none;
+
+  // phase 1: up to the decision (step_lane)
+  Lane L = initial_lane(0u);
+  uint32_t key = kKeyDead, st = COUP_STEP_MID;
+  if (live) {
+    L = unpack(a.state[i]);
+    Rng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, i), 0u, make_uint4(0, 0, 0, 0)};
+    if (is_terminal(L)) {
+      L = new_episode(L.episode + 1u, rng, none);  // step() after LAST (rl_environment.py:310-311)
+      st = COUP_STEP_FIRST;
+      key = kKeyReset;  // nothing left to apply
+    } else {
+      resolve_chance(L, rng);
+      const uint32_t m = decision_mask(L);
+      const uint32_t x = UNIFORM ? (m ? sample_action(m, rng.draw(L.episode, L.move)) : 32u)
+                                 : (uint32_t)(uint8_t)a.actions_in[i];
+      if (x > 17u || ((m >> x) & 1u) == 0u || is_terminal(L)) {
+        count_error(a.err_count);
+        key = kKeyReset;  // rejected: nothing to apply either
+      } else {
+        key = x;
+      }
+    }
+  }
+  __syncthreads();
+  const uint32_t rank = atomicAdd(&s_bin[key], 1u);
+  __syncthreads();
+  const uint32_t pos = bins_below(s_bin, key) + rank;
+  s_rec[pos] = pack(L);
+  s_meta[pos] = t | (key << 8) | (st << 13);
+  __syncthreads();
+
+  // phase 2: thread t runs slot t's decision
+  {
+    const uint32_t m = s_meta[t], k = (m >> 8) & 31u;
+    if (k != kKeyDead) {
+      L = unpack(s_rec[t]);
+      uint32_t out = ((m >> 13) & 3u) << 5 | (2u << 7), legal = 0u;  // no action, reward 0
+      bool pending = false;
+      if (k < kKeyReset) {
+        Rng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, base + (m & 255u)), 0u, make_uint4(0, 0, 0, 0)};
+        const uint32_t err_before = L.err;
+        apply_decision(L, k);
+        L.move += 1u;
+        resolve_chance(L, rng);
+        if (L.err && !err_before) count_error(a.err_count);
+        const bool term = is_terminal(L);
+        out = (k + 1u) | ((term ? COUP_STEP_LAST : COUP_STEP_MID) << 5) | ((uint32_t)(L.r0 + 2) << 7);
+        pending = term && a.auto_reset != 0;
+        if (pending) s_reset[atomicAdd(&s_nreset, 1u)] = t;
+        s_rec[t] = pack(L);
+      }
+      if (!pending) {
+        legal = legal_mask(L);
+        out |= ((uint32_t)current_player(L) & 0xFFu) << 24;
+      }
+      s_out[t] = out;
+      s_legal[t] = legal;
+    }
+  }
+  __syncthreads();
+
+  // the auto-resets (vector_env.py:62-65), packed onto the first threads
+  const uint32_t nreset = s_nreset;
+  for (uint32_t j = t; j < nreset; j += kThreads) {
+    const uint32_t slot = s_reset[j];
+    Rng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, base + (s_meta[slot] & 255u)), 0u,
+            make_uint4(0, 0, 0, 0)};
+    const Lane R = new_episode(unpack(s_rec[slot]).episode + 1u, rng, none);
+    s_rec[slot] = pack(R);
+    s_legal[slot] = legal_mask(R);
+    s_out[slot] = (s_out[slot] & 0x00FFFFFFu) | (((uint32_t)current_player(R) & 0xFFu) << 24);
+  }
+  __syncthreads();
+
+  // phase 3: each thread stores its own lane
+  if (!live) return;
+  a.state[i] = s_rec[pos];
+  const uint32_t o = s_out[pos];
+  const int32_t rew = (int32_t)((o >> 7) & 7u) - 2;
+  if (a.actions) a.actions[i] = (int8_t)((int32_t)(o & 31u) - 1);
+  if (a.rewards) {
+    a.rewards[2 * i] = (int8_t)rew;
+    a.rewards[2 * i + 1] = (int8_t)(-rew);
+  }
+  if (a.step_type) a.step_type[i] = (uint8_t)((o >> 5) & 3u);
+  if (a.legal) a.legal[i] = s_legal[pos];
+  if (a.cur_player) a.cur_player[i] = (int8_t)(o >> 24);
+}
+
 // The decision key of a lane at a decision node: the uniform policy's draw,
 // or kKeyDead (counted as an error) if the node has no legal decision.
 __device__ __forceinline__ uint32_t draw_key(const Lane& L, Rng& rng, uint32_t& errs) {
@@ -1271,6 +1385,14 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
   if (info != coup::kInfoNone && mode != coup::kObsNone) mode = coup::kObsWaveBits;
   hipStream_t s = env->stream;
   const int64_t n = env->batch;
+  if (info == coup::kInfoNone && mode == coup::kObsNone && coup::regroup_lanes(n)) {
+    if (uniform)
+      coup::k_step_sorted<true><<<grid_for(n), coup::kThreads, 0, s>>>(a);
+    else
+      coup::k_step_sorted<false><<<grid_for(n), coup::kThreads, 0, s>>>(a);
+    COUP_HIP_TRY(hipGetLastError());
+    return COUP_OK;
+  }
 #define COUP_LAUNCH_STEP(U, M, T, I) launch_step<U, M, T, I>(env, a, n, dyn_lds, s)
 #define COUP_LAUNCH_MODES(U)                                                                         \
   if (info == coup::kInfoNone) {                                                                     \

@@ -210,3 +210,22 @@ def test_regrouped_rollout_equals_in_place_rollout(monkeypatch, n_players):
         env.rollout(9, stats[knob])
     assert torch.equal(envs["0"].export_state(), envs["1"].export_state())
     assert envs["0"].error_count() == envs["1"].error_count() == 0
+
+
+@pytest.mark.parametrize("fused", [False, True], ids=["step", "rollout"])
+def test_six_player_full_batch_sampled_lanes_match_spec(fused):
+    """B = 2^20 six-player lanes (the c4 / c4r kernels, regrouped by
+    decision): three 256-lane slices after 80 steps == np_rollout on those
+    env ids alone."""
+    B, steps, seed = 1 << 20, 80, 17
+    env = BatchedCoupEnv(B, seed=seed, obs=False, num_players=6)
+    if fused:
+        env.rollout(steps)
+    else:
+        for _ in range(steps):
+            env.step()
+    words = _np(env.export_state()).astype(np.uint32)
+    for k in (0, 300_001, B - 256):
+        ref = oracle.np_rollout(6, seed=seed, n=256, steps=steps, env_id_base=k, auto_reset=True)
+        np.testing.assert_array_equal(words[k:k + 256], ref["final_state"], err_msg=f"slice {k}")
+    assert env.error_count() == 0

@@ -251,6 +251,36 @@ def test_regrouped_rollout_equals_in_place_rollout(monkeypatch):
     assert envs["0"].error_count() == envs["1"].error_count() == 0
 
 
+@pytest.mark.parametrize("auto_reset", [True, False])
+def test_regrouped_step_equals_in_place_step(monkeypatch, auto_reset):
+    """k_step_sorted (the bare step with lanes counting-sorted by decision,
+    resets dealt by the first threads; default from 2^18 lanes) == k_step,
+    ragged batch, uniform policy and caller actions (about 1 in 8 illegal)."""
+    n, steps, seed = 1000, 150, 41
+    envs = {}
+    for knob in ("0", "1"):
+        monkeypatch.setenv("COUP_REGROUP", knob)
+        envs[knob] = BatchedCoupEnv(n, seed=seed, auto_reset=auto_reset, obs=False)
+    g = torch.Generator().manual_seed(seed)
+    for t in range(steps):
+        acts = None
+        if t % 3 == 2:
+            legal = envs["0"].query(obs=False)["legal_mask"].cpu().to(torch.int64)
+            acts = torch.randint(0, 18, (n,), generator=g, dtype=torch.int64)
+            ok = ((legal >> acts) & 1) == 1
+            keep = torch.rand(n, generator=g) < 0.875
+            first = torch.where(legal != 0, (legal & -legal).float().log2().to(torch.int64), acts)
+            acts = torch.where(ok | ~keep, acts, first).to(torch.int8)
+        outs = {}
+        for knob, env in envs.items():
+            monkeypatch.setenv("COUP_REGROUP", knob)
+            outs[knob] = {k: v.clone() for k, v in env.step(acts).items()}
+        for k in ("actions", "rewards", "step_type", "legal_mask", "current_player"):
+            assert torch.equal(outs["0"][k], outs["1"][k]), (t, k)
+        assert torch.equal(envs["0"].export_state(), envs["1"].export_state()), t
+    assert envs["0"].error_count() == envs["1"].error_count()
+
+
 def test_illegal_action_rejected():
     env = BatchedCoupEnv(4, seed=0, obs=False)
     before = _np(env.export_state()).copy()
@@ -326,3 +356,17 @@ def test_graph_replay_matches_eager():
     for k in ("actions", "rewards", "step_type", "legal_mask", "obs"):
         assert torch.equal(oa[k], getattr(b, "cur_player" if k == "current_player" else k)), k
     assert a.error_count() == 0 and b.error_count() == 0
+
+
+def test_full_batch_sampled_lanes_match_oracle():
+    """At the benchmark batch, where the fused rollout regroups lanes by
+    decision (coup_regroup.h): three 256-lane slices of a 2^20-lane env
+    after 120 rollout steps == the oracle run on those env ids alone."""
+    B, steps, seed = 1 << 20, 120, 13
+    env = BatchedCoupEnv(B, seed=seed, obs=False)
+    env.rollout(steps)
+    words = _np(env.export_state()).astype(np.uint32)
+    for k in (0, 524_288 + 77, B - 256):
+        ref = oracle.rollout(seed=seed, n=256, steps=steps, env_id_base=k, auto_reset=True, want_trajectory=False)
+        np.testing.assert_array_equal(words[k:k + 256], ref["final_state"], err_msg=f"slice {k}")
+    assert env.error_count() == 0
