@@ -159,8 +159,8 @@ def test_regrouped_step_equals_in_place_step(monkeypatch, n_players, auto_reset)
     envs = {}
     for knob in ("0", "1"):
         monkeypatch.setenv("COUP_REGROUP", knob)
-        envs[knob] = BatchedCoupEnv(n, seed=seed, auto_reset=auto_reset, obs=False, num_players=n_players,
-                                    generic=True)
+        envs[knob] = BatchedCoupEnv(n, seed=seed, env_id_base=3 << 20, auto_reset=auto_reset, obs=False,
+                                    num_players=n_players, generic=True)
     g = torch.Generator().manual_seed(seed)
     for t in range(steps):
         acts = None

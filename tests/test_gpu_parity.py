@@ -260,7 +260,7 @@ def test_regrouped_step_equals_in_place_step(monkeypatch, auto_reset):
     envs = {}
     for knob in ("0", "1"):
         monkeypatch.setenv("COUP_REGROUP", knob)
-        envs[knob] = BatchedCoupEnv(n, seed=seed, auto_reset=auto_reset, obs=False)
+        envs[knob] = BatchedCoupEnv(n, seed=seed, env_id_base=123_457, auto_reset=auto_reset, obs=False)
     g = torch.Generator().manual_seed(seed)
     for t in range(steps):
         acts = None
