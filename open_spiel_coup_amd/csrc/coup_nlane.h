@@ -648,12 +648,6 @@ __device__ __forceinline__ float obs_elem(const uint32_t* r, uint32_t o, uint32_
   return ((r[4] >> (5u * q)) & 31u) == x - 18u * q ? 1.0f : 0.0f;
 }
 
-// One rl_environment step of one lane (rl_environment.py:282-322), with
-// SyncVectorEnv auto-reset when `auto_reset` (vector_env.py:40-67): the
-// 2-player engine's step_lane with the N-player rules.  x is the decision
-// to apply (the uniform policy's draw when UNIFORM).  Outputs: the applied
-// action (-1 if none), the step type, Rewards() as (loser, count), and
-// whether the lane rejected the action or hit a rules error.
 // First half of step_lane, up to the decision to apply: a lane that was
 // terminal starts a new episode (FIRST), pending deals are resolved, the
 // uniform policy draws x.  Returns kStepDone when nothing is left to apply
@@ -697,6 +691,12 @@ __device__ __forceinline__ void step_lane_post(NLane<N>& L, NRng& rng, uint32_t 
   }
 }
 
+// One rl_environment step of one lane (rl_environment.py:282-322), with
+// SyncVectorEnv auto-reset when `auto_reset` (vector_env.py:40-67): the
+// 2-player engine's step_lane with the N-player rules.  x is the decision
+// to apply (the uniform policy's draw when UNIFORM).  Outputs: the applied
+// action (-1 if none), the step type, Rewards() as (loser, count), and
+// whether the lane rejected the action or hit a rules error.
 template <int N, bool UNIFORM>
 __device__ __forceinline__ void step_lane(NLane<N>& L, NRng& rng, uint32_t x, bool auto_reset, int& act,
                                           uint32_t& st, uint32_t& rl, uint32_t& rc, bool& error) {
