@@ -244,8 +244,10 @@ def main():
                 traffic = ent.get("hbm_bytes_per_launch")
         sorted_ = "_sorted" if _regrouped(B) else ""
         if players != 2:
+            ahead = os.environ.get("COUP_AHEAD", "1") != "0"
             kernel = ("coup::np::k_rollout%s<%d>" % (sorted_, players) if fused else
-                      "coup::np::k_step%s<%d, true>" % (sorted_, players))
+                      "coup::np::k_step_sorted<%d, true, %s>" % (players, "true" if ahead else "false") if sorted_ else
+                      "coup::np::k_step<%d, true>" % players)
         elif fused:
             kernel = "coup::k_rollout" + sorted_
         elif with_info:

@@ -120,7 +120,16 @@ __global__ __launch_bounds__(kThreads) void k_step(StepArgs a) {
 // every wave holding a finished lane.  Phase 3: each thread stores its own
 // lane's record and outputs back in place, coalesced.  The RNG is
 // stateless per (lane, episode, draw), so results equal k_step's.
-template <int N, bool UNIFORM>
+// Decision drawn ahead (AHEAD): a uniform step also draws each lane's next
+// decision where phase 2 has the lane's post-step legal mask in hand, in
+// regrouped order, and parks it in bits [29:25] of record word 7 (+1; 0 =
+// none).  The next uniform step takes it instead of running step_lane_pre
+// on the unsorted lanes.  Every other kernel's pack() clears the field, and
+// export masks it, so a parked decision never outlives the state it was
+// drawn for.
+constexpr uint32_t kAheadShift = 25u;
+
+template <int N, bool UNIFORM, bool AHEAD>
 __global__ __launch_bounds__(kThreads) void k_step_sorted(StepArgs a) {
   __shared__ uint4 s_a[kThreads], s_b[kThreads];
   __shared__ uint32_t s_meta[kThreads];   // slot -> owner thread | key << 8 | st << 13 | error << 15
@@ -141,11 +150,18 @@ __global__ __launch_bounds__(kThreads) void k_step_sorted(StepArgs a) {
   uint32_t key = kKeyDead, st = 0u;
   bool error = false;
   if (live) {
-    L = unpack<N>(a.sa[i], a.sb[i]);
-    NRng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, i), 0u, make_uint4(0, 0, 0, 0)};
-    uint32_t x = UNIFORM ? 0u : (uint32_t)(uint8_t)a.actions_in[i];
-    key = step_lane_pre<N, UNIFORM>(L, rng, x, st, error);
-    if (error) count_error(a.err_count);
+    const uint4 rb = a.sb[i];
+    L = unpack<N>(a.sa[i], rb);
+    const uint32_t parked = (rb.w >> kAheadShift) & 31u;
+    if (UNIFORM && AHEAD && parked != 0u) {
+      key = parked - 1u;  // drawn by the last step for this state: a decision node
+      st = 1u;            // MID
+    } else {
+      NRng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, i), 0u, make_uint4(0, 0, 0, 0)};
+      uint32_t x = UNIFORM ? 0u : (uint32_t)(uint8_t)a.actions_in[i];
+      key = step_lane_pre<N, UNIFORM>(L, rng, x, st, error);
+      if (error) count_error(a.err_count);
+    }
   }
   __syncthreads();
   const uint32_t rank = atomicAdd(&s_bin[key], 1u);
@@ -178,9 +194,8 @@ __global__ __launch_bounds__(kThreads) void k_step_sorted(StepArgs a) {
       L = unpack<N>(s_a[t], s_b[t]);
       uint32_t out = (m >> 13) & 3u, legal = 0u;  // a lane finished in phase 1: no action, its st
       bool pending = false;
+      NRng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, base + (m & 255u)), 0u, make_uint4(0, 0, 0, 0)};
       if (k < kStepDone) {
-        NRng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, base + (m & 255u)), 0u,
-                 make_uint4(0, 0, 0, 0)};
         const uint32_t err_before = L.err;
         apply_decision(L, k);
         L.move += 1u;
@@ -200,7 +215,10 @@ __global__ __launch_bounds__(kThreads) void k_step_sorted(StepArgs a) {
       }
       if (!pending) {
         legal = legal_mask(L);
-        out |= ((uint32_t)current_player(L) & 0xFFu) << 24;
+        const int cp = current_player(L);
+        out |= ((uint32_t)cp & 0xFFu) << 24;
+        if (UNIFORM && AHEAD && k < kStepDone && cp >= 0)
+          s_b[t].w |= (sample_action(legal, rng.draw(L.episode, L.move)) + 1u) << kAheadShift;
       }
       s_out[t] = out;
       s_legal[t] = legal;
@@ -219,8 +237,10 @@ __global__ __launch_bounds__(kThreads) void k_step_sorted(StepArgs a) {
     pack(R, wa, wb);
     s_a[slot] = wa;
     s_b[slot] = wb;
-    s_legal[slot] = legal_mask(R);
+    const uint32_t legal = legal_mask(R);
+    s_legal[slot] = legal;
     s_out[slot] = (s_out[slot] & 0x00FFFFFFu) | (((uint32_t)current_player(R) & 0xFFu) << 24);
+    if (UNIFORM && AHEAD) s_b[slot].w |= (sample_action(legal, rng.draw(R.episode, R.move)) + 1u) << kAheadShift;
   }
   __syncthreads();
 
@@ -517,14 +537,18 @@ __global__ __launch_bounds__(kThreads) void k_export(const uint4* sa, const uint
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= n) return;
   dst[2 * i] = sa[i];
-  dst[2 * i + 1] = sb[i];
+  uint4 b = sb[i];
+  b.w &= kEpisodeMask;  // a parked decision (k_step_sorted) is not state
+  dst[2 * i + 1] = b;
 }
 
 __global__ __launch_bounds__(kThreads) void k_import(uint4* sa, uint4* sb, int64_t n, const uint4* src) {
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= n) return;
   sa[i] = src[2 * i];
-  sb[i] = src[2 * i + 1];
+  uint4 b = src[2 * i + 1];
+  b.w &= kEpisodeMask;
+  sb[i] = b;
 }
 
 // ------------------------------------------------------------ launchers
@@ -583,10 +607,14 @@ hipError_t launch_step(const Env& e, const int8_t* actions, const coup_step_outp
     constexpr int N = decltype(np)::value;
     const unsigned grid = grid_for(e.n, kThreads);
     if (regroup_lanes(e.n)) {
+      const char* ah = std::getenv("COUP_AHEAD");  // 0: no decision drawn ahead (A/B)
+      const bool ahead = ah ? std::atoi(ah) != 0 : true;
       if (actions)
-        k_step_sorted<N, false><<<grid, kThreads, 0, e.stream>>>(a);
+        k_step_sorted<N, false, false><<<grid, kThreads, 0, e.stream>>>(a);
+      else if (ahead)
+        k_step_sorted<N, true, true><<<grid, kThreads, 0, e.stream>>>(a);
       else
-        k_step_sorted<N, true><<<grid, kThreads, 0, e.stream>>>(a);
+        k_step_sorted<N, true, false><<<grid, kThreads, 0, e.stream>>>(a);
     } else if (actions) {
       k_step<N, false><<<grid, kThreads, 0, e.stream>>>(a);
     } else {

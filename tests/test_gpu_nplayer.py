@@ -148,13 +148,17 @@ def test_six_player_full_batch_properties():
     assert env.error_count() == 0
 
 
+@pytest.mark.parametrize("ahead", ["1", "0"], ids=["drawn-ahead", "drawn-in-step"])
 @pytest.mark.parametrize("n_players", [2, 4, 6])
 @pytest.mark.parametrize("auto_reset", [True, False])
-def test_regrouped_step_equals_in_place_step(monkeypatch, n_players, auto_reset):
+def test_regrouped_step_equals_in_place_step(monkeypatch, n_players, auto_reset, ahead):
     """k_step_sorted (lanes counting-sorted by decision through LDS, resets
     dealt by the first threads) == k_step (lanes in place), ragged batch,
     both the uniform policy and caller actions (about 1 in 8 illegal, so
-    the rejected-action path is in the sort too)."""
+    the rejected-action path is in the sort too); with the next uniform
+    decision drawn ahead and parked in the record (the default) and without.
+    Exported records carry no parked decision."""
+    monkeypatch.setenv("COUP_AHEAD", ahead)
     n, steps, seed = 1000, 150, 11 + n_players
     envs = {}
     for knob in ("0", "1"):

@@ -64,7 +64,7 @@ def main():
             if fused:
                 return bool(re.search(r"np::k_rollout(_sorted)?<%d>|2np(9k_rollout|16k_rollout_sorted)ILi%dE"
                                       % (players, players), kn))
-            return bool(re.search(r"np::k_step(_sorted)?<%d, true>|2np(6k_step|13k_step_sorted)ILi%dELb1E"
+            return bool(re.search(r"np::k_step(_sorted)?<%d, true(, (true|false))?>|2np(6k_step|13k_step_sorted)ILi%dELb1E"
                                   % (players, players), kn))
         if "np::" in kn or "2np" in kn:
             return False
