@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define COUP_ABI_VERSION 3
+#define COUP_ABI_VERSION 4
 
 #define COUP_NUM_PLAYERS 2          /* coup.h:42 */
 #define COUP_MAX_PLAYERS 6          /* N-player extension */
@@ -94,6 +94,26 @@ typedef struct {
   float* info_state;    /* [B][2][2492] InformationStateTensor (coup.cc:1044-1049); needs COUP_FLAG_HISTORY */
 } coup_query_outputs;
 
+/* Result of coup_slot_op for its lane (128 bytes, host memory). */
+typedef struct {
+  uint32_t record[4];    /* packed lane record (coup_export_state layout) */
+  uint8_t history[96];   /* history bytes (coup_export_history layout) */
+  uint32_t legal_mask;   /* as coup_query_outputs.legal_mask */
+  int8_t cur_player;     /* CurrentPlayer() (coup.cc:458-466) */
+  uint8_t terminal;      /* IsTerminal() (coup.cc:989-1010) */
+  uint8_t ok;            /* 0: the action was rejected (lane left unchanged) */
+  uint8_t reserved;
+  int8_t rewards[2];     /* Rewards() (coup.cc:1012-1014) */
+  int8_t returns[2];     /* Returns() (coup.cc:1016-1032) */
+  uint8_t pad[4];
+} coup_slot_result;
+
+/* coup_slot_op flags */
+#define COUP_SLOT_INIT 1       /* put the lane in NewInitialState() first (coup.cc:393-428) */
+#define COUP_SLOT_OBS 2        /* append ObservationTensor [2][98] float to the result */
+#define COUP_SLOT_INFO 4       /* append InformationStateTensor [2][2492] float (after obs if both) */
+#define COUP_SLOT_NO_RESULT 8  /* asynchronous: no result, host_out may be NULL */
+
 /* Per-lane rollout statistics accumulated by coup_rollout (device, [B]). */
 typedef struct {
   int32_t* episodes;    /* [B] episodes finished */
@@ -159,6 +179,23 @@ int coup_new_initial_state(coup_env* env, const uint8_t* lane_mask);
 int coup_apply_action(coup_env* env, const int8_t* actions);
 /* Per-lane accessors of the current state. */
 int coup_query(coup_env* env, const coup_query_outputs* out);
+
+/* Lane-pool op of the per-game State facade: one launch on one lane of a
+ * 2-player COUP_FLAG_HISTORY env, the lane standing for one open_spiel
+ * State.  In order: if src_env is not NULL, lane `lane` becomes a copy of
+ * src_env's lane `src_lane` (State::Clone, spiel.h:822; src_env may be env);
+ * COUP_SLOT_INIT resets it to NewInitialState (coup.cc:393-428, history
+ * cleared); action >= 0 applies State::ApplyAction (spiel.cc:322-331) --
+ * an illegal action leaves the lane unchanged and sets result.ok = 0, the
+ * SpielError of coup.cc:492-495 & co; then, unless COUP_SLOT_NO_RESULT,
+ * the lane's coup_slot_result (followed by the tensors the flags ask for)
+ * is copied to host_out and the call synchronises the env's stream.
+ * Replaces the per-state calls of the reference's C ABI
+ * (rust_open_spiel.h:34-73: StateClone, StateApplyAction,
+ * StateLegalActions, StateCurrentPlayer, StateIsTerminal, StateReturns,
+ * StateObservationTensor, StateInformationStateTensor) with one round trip. */
+int coup_slot_op(coup_env* env, int64_t lane, const coup_env* src_env, int64_t src_lane, int action, int flags,
+                 void* host_out);
 
 /* Copy the packed lane records ([B][coup_state_bytes / 4] uint32, device)
  * out of / into the env. */

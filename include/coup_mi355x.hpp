@@ -202,92 +202,46 @@ inline std::string StateString(const Fields& f, const uint8_t* hist, int observe
   return s;
 }
 
-// One-lane scratch env with history and device buffers for single-state ops.
-class Engine {
+// Device-resident lane pool: every live CoupState owns one lane of a
+// 2-player history env (segments of kSeg lanes, grown on demand); each State
+// op is one coup_slot_op launch on that lane, and only ops that need an
+// answer copy the 128-byte coup_slot_result back.
+class Pool {
  public:
-  Engine() : env_(1, 0, 0, COUP_FLAG_HISTORY) {
-    CheckHip(hipMalloc(&buf_, kBytes), "hipMalloc");
-  }
-  ~Engine() { (void)hipFree(buf_); }
-
-  struct Result {
-    uint32_t legal;
-    int cur;
-    bool terminal;
-    int rewards[2], returns[2];
+  static constexpr int64_t kSeg = 4096;
+  struct Slot {
+    int seg = -1;
+    int64_t lane = 0;
   };
 
-  void NewInitial(std::array<uint32_t, 4>& rec, std::array<uint8_t, COUP_HISTORY_BYTES>& hist) {
-    env_.NewInitialState();
-    env_.ExportState(Rec());
-    CheckHip(hipMemcpy(rec.data(), Rec(), 16, hipMemcpyDeviceToHost), "hipMemcpy");
-    hist.fill(0xFF);
-  }
-
-  bool Apply(std::array<uint32_t, 4>& rec, std::array<uint8_t, COUP_HISTORY_BYTES>& hist, Action a) {
-    Load(rec, hist);
-    const int8_t x = (int8_t)a;
-    CheckHip(hipMemcpy(Act(), &x, 1, hipMemcpyHostToDevice), "hipMemcpy");
-    env_.ApplyAction(Act());
-    if (env_.ErrorCount()) return false;
-    env_.ExportState(Rec());
-    env_.ExportHistory(Hist());
-    CheckHip(hipMemcpy(rec.data(), Rec(), 16, hipMemcpyDeviceToHost), "hipMemcpy");
-    CheckHip(hipMemcpy(hist.data(), Hist(), COUP_HISTORY_BYTES, hipMemcpyDeviceToHost), "hipMemcpy");
-    return true;
-  }
-
-  Result Query(const std::array<uint32_t, 4>& rec, const std::array<uint8_t, COUP_HISTORY_BYTES>& hist,
-               float* obs, float* info) {
-    Load(rec, hist);
-    coup_query_outputs q{};
-    q.legal_mask = reinterpret_cast<uint32_t*>(buf_ + kLegal);
-    q.cur_player = reinterpret_cast<int8_t*>(buf_ + kCur);
-    q.terminal = reinterpret_cast<uint8_t*>(buf_ + kTerm);
-    q.rewards = reinterpret_cast<int8_t*>(buf_ + kRew);
-    q.returns = reinterpret_cast<int8_t*>(buf_ + kRet);
-    q.obs = obs ? reinterpret_cast<float*>(buf_ + kObs) : nullptr;
-    q.info_state = info ? reinterpret_cast<float*>(buf_ + kInfo) : nullptr;
-    env_.Query(q);
-    uint8_t small[kSmall];
-    CheckHip(hipMemcpy(small, buf_ + kLegal, kSmall, hipMemcpyDeviceToHost), "hipMemcpy");
-    Result r;
-    std::memcpy(&r.legal, small, 4);
-    r.cur = (int8_t)small[kCur - kLegal];
-    r.terminal = small[kTerm - kLegal] != 0;
-    for (int p = 0; p < 2; ++p) {
-      r.rewards[p] = (int8_t)small[kRew - kLegal + p];
-      r.returns[p] = (int8_t)small[kRet - kLegal + p];
+  Slot Alloc() {
+    if (free_.empty()) {
+      segs_.emplace_back(new BatchedEnv(kSeg, 0, 0, COUP_FLAG_HISTORY));
+      const int k = (int)segs_.size() - 1;
+      for (int64_t i = kSeg - 1; i >= 0; --i) free_.push_back({k, i});
     }
-    if (obs) CheckHip(hipMemcpy(obs, buf_ + kObs, 2 * COUP_OBS_SIZE * 4, hipMemcpyDeviceToHost), "hipMemcpy");
-    if (info)
-      CheckHip(hipMemcpy(info, buf_ + kInfo, 2 * COUP_INFO_STATE_SIZE * 4, hipMemcpyDeviceToHost), "hipMemcpy");
-    return r;
+    Slot s = free_.back();
+    free_.pop_back();
+    return s;
+  }
+  void Release(const Slot& s) {
+    if (s.seg >= 0) free_.push_back(s);
+  }
+  // host_out: coup_slot_result followed by the tensors the flags ask for
+  void Op(const Slot& s, const Slot* src, int action, int flags, void* host_out) {
+    coup_env* src_env = src ? segs_[src->seg]->get() : nullptr;
+    Check(coup_slot_op(segs_[s.seg]->get(), s.lane, src_env, src ? src->lane : 0, action, flags, host_out),
+          "coup_slot_op");
   }
 
  private:
-  // device scratch layout
-  static constexpr size_t kRec = 0, kHist = 16, kAct = kHist + COUP_HISTORY_BYTES, kLegal = kAct + 16,
-                          kCur = kLegal + 4, kTerm = kCur + 1, kRew = kTerm + 1, kRet = kRew + 2,
-                          kSmall = kRet + 2 - kLegal, kObs = 256, kInfo = kObs + 2 * COUP_OBS_SIZE * 4,
-                          kBytes = kInfo + 2 * COUP_INFO_STATE_SIZE * 4;
-  uint32_t* Rec() { return reinterpret_cast<uint32_t*>(buf_ + kRec); }
-  uint8_t* Hist() { return buf_ + kHist; }
-  int8_t* Act() { return reinterpret_cast<int8_t*>(buf_ + kAct); }
-  void Load(const std::array<uint32_t, 4>& rec, const std::array<uint8_t, COUP_HISTORY_BYTES>& hist) {
-    CheckHip(hipMemcpy(Rec(), rec.data(), 16, hipMemcpyHostToDevice), "hipMemcpy");
-    CheckHip(hipMemcpy(Hist(), hist.data(), COUP_HISTORY_BYTES, hipMemcpyHostToDevice), "hipMemcpy");
-    env_.ImportState(Rec());
-    env_.ImportHistory(Hist());
-  }
-
-  BatchedEnv env_;
-  uint8_t* buf_ = nullptr;
+  std::vector<std::unique_ptr<BatchedEnv>> segs_;
+  std::vector<Slot> free_;
 };
 
-inline Engine& TheEngine() {
-  static Engine e;  // one per process (current HIP device at first use)
-  return e;
+inline Pool& ThePool() {
+  static Pool p;  // one per process (current HIP device at first use)
+  return p;
 }
 
 }  // namespace detail
@@ -304,10 +258,19 @@ struct PlayerAction {
 // open_spiel::coup::CoupState (coup.h:111-197) on the GPU engine.
 class CoupState {
  public:
-  explicit CoupState(const CoupGame* game) : game_(game) { detail::TheEngine().NewInitial(rec_, hist_); }
+  explicit CoupState(const CoupGame* game) : game_(game), slot_(detail::ThePool().Alloc()) {
+    detail::ThePool().Op(slot_, nullptr, -1, COUP_SLOT_INIT, &q_);
+  }
+  // State::Clone (spiel.h:822): a device-side lane copy, no round trip
+  CoupState(const CoupState& o)
+      : game_(o.game_), slot_(detail::ThePool().Alloc()), history_(o.history_), q_(o.q_) {
+    detail::ThePool().Op(slot_, &o.slot_, -1, COUP_SLOT_NO_RESULT, nullptr);
+  }
+  CoupState& operator=(const CoupState&) = delete;
+  ~CoupState() { detail::ThePool().Release(slot_); }
 
-  Player CurrentPlayer() const { return Q().cur; }
-  bool IsTerminal() const { return Q().terminal; }
+  Player CurrentPlayer() const { return Q().cur_player; }
+  bool IsTerminal() const { return Q().terminal != 0; }
   bool IsChanceNode() const { return CurrentPlayer() == kChancePlayerId; }
   bool IsPlayerNode() const { return CurrentPlayer() >= 0; }
   int NumPlayers() const { return COUP_NUM_PLAYERS; }
@@ -317,7 +280,7 @@ class CoupState {
   std::vector<Action> LegalActions() const {
     std::vector<Action> out;
     if (IsTerminal()) return out;
-    const uint32_t m = Q().legal & 0x3FFFFu;
+    const uint32_t m = Q().legal_mask & 0x3FFFFu;
     for (int a = 0; a < COUP_NUM_ACTIONS; ++a)
       if ((m >> a) & 1u) out.push_back(a);
     return out;
@@ -334,7 +297,7 @@ class CoupState {
   // ChanceOutcomes (coup.cc:1062-1077)
   std::vector<std::pair<Action, double>> ChanceOutcomes() const {
     if (!IsChanceNode()) throw SpielError("ChanceOutcomes() at a non-chance node");
-    const detail::Fields f = detail::Decode(rec_);
+    const detail::Fields f = detail::Decode(Rec());
     double total = 0;
     for (int t = 0; t < 5; ++t) total += f.deck[t];
     std::vector<std::pair<Action, double>> out;
@@ -346,10 +309,16 @@ class CoupState {
   // State::ApplyAction (spiel.cc:322-331); throws for an illegal action
   void ApplyAction(Action a) {
     const Player p = CurrentPlayer();
-    if (!detail::TheEngine().Apply(rec_, hist_, a))
+    if (a < 0 || a >= COUP_NUM_ACTIONS || !((Q().legal_mask >> a) & 1u) || p == kTerminalPlayerId)
       throw SpielError("ApplyAction: illegal action " + std::to_string(a));
+    coup_slot_result r;
+    detail::ThePool().Op(slot_, nullptr, (int)a, 0, &r);
+    if (!r.ok) {
+      detail::ThePool().Op(slot_, nullptr, -1, 0, &q_);
+      throw SpielError("ApplyAction: illegal action " + std::to_string(a));
+    }
+    q_ = r;
     history_.push_back({p, a});
-    valid_ = false;
   }
   std::unique_ptr<CoupState> Child(Action a) const {
     auto c = Clone();
@@ -363,24 +332,25 @@ class CoupState {
   double PlayerReturn(Player p) const { return Returns()[p]; }
 
   std::vector<float> ObservationTensor(Player p) const {
-    float both[2 * COUP_OBS_SIZE];
-    detail::TheEngine().Query(rec_, hist_, both, nullptr);
+    std::vector<uint8_t> buf(sizeof(coup_slot_result) + 2 * COUP_OBS_SIZE * 4);
+    detail::ThePool().Op(slot_, nullptr, -1, COUP_SLOT_OBS, buf.data());
+    const float* both = reinterpret_cast<const float*>(buf.data() + sizeof(coup_slot_result));
     return std::vector<float>(both + p * COUP_OBS_SIZE, both + (p + 1) * COUP_OBS_SIZE);
   }
   std::vector<float> InformationStateTensor(Player p) const {
-    std::vector<float> both(2 * COUP_INFO_STATE_SIZE);
-    detail::TheEngine().Query(rec_, hist_, nullptr, both.data());
-    return std::vector<float>(both.begin() + p * COUP_INFO_STATE_SIZE,
-                              both.begin() + (p + 1) * COUP_INFO_STATE_SIZE);
+    std::vector<uint8_t> buf(sizeof(coup_slot_result) + 2 * COUP_INFO_STATE_SIZE * 4);
+    detail::ThePool().Op(slot_, nullptr, -1, COUP_SLOT_INFO, buf.data());
+    const float* both = reinterpret_cast<const float*>(buf.data() + sizeof(coup_slot_result));
+    return std::vector<float>(both + p * COUP_INFO_STATE_SIZE, both + (p + 1) * COUP_INFO_STATE_SIZE);
   }
 
   std::string ObservationString(Player p) const {
-    return detail::StateString(detail::Decode(rec_), hist_.data(), p, false);
+    return detail::StateString(detail::Decode(Rec()), q_.history, p, false);
   }
   std::string InformationStateString(Player p) const {
-    return detail::StateString(detail::Decode(rec_), hist_.data(), p, true);
+    return detail::StateString(detail::Decode(Rec()), q_.history, p, true);
   }
-  std::string ToString() const { return detail::StateString(detail::Decode(rec_), hist_.data(), -1, false); }
+  std::string ToString() const { return detail::StateString(detail::Decode(Rec()), q_.history, -1, false); }
   std::string ActionToString(Player p, Action a) const;
 
   std::vector<Action> History() const {
@@ -389,30 +359,24 @@ class CoupState {
     return h;
   }
   const std::vector<PlayerAction>& FullHistory() const { return history_; }
-  int MoveNumber() const { return detail::Decode(rec_).move_number; }
+  int MoveNumber() const { return detail::Decode(Rec()).move_number; }
   // State::Serialize (spiel.cc:297-311)
   std::string Serialize() const {
     std::string s;
     for (const auto& pa : history_) s += std::to_string(pa.action) + "\n";
     return s;
   }
-  const std::array<uint32_t, 4>& PackedRecord() const { return rec_; }
+  std::array<uint32_t, 4> PackedRecord() const { return Rec(); }
 
  private:
-  const detail::Engine::Result& Q() const {
-    if (!valid_) {
-      q_ = detail::TheEngine().Query(rec_, hist_, nullptr, nullptr);
-      valid_ = true;
-    }
-    return q_;
-  }
+  // the result of the last op on this lane (every op refreshes it)
+  const coup_slot_result& Q() const { return q_; }
+  std::array<uint32_t, 4> Rec() const { return {q_.record[0], q_.record[1], q_.record[2], q_.record[3]}; }
 
   const CoupGame* game_;
-  std::array<uint32_t, 4> rec_{};
-  std::array<uint8_t, COUP_HISTORY_BYTES> hist_{};
+  detail::Pool::Slot slot_;
   std::vector<PlayerAction> history_;
-  mutable detail::Engine::Result q_{};
-  mutable bool valid_ = false;
+  coup_slot_result q_{};
 };
 
 // open_spiel::coup::CoupGame (coup.h:199-231)

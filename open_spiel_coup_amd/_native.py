@@ -11,7 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # COUP_LIB_PATH: load another build of the same library (A/B timing of two
 # builds, tools/ab_builds.sh); there is still no fallback
 LIB_PATH = os.environ.get("COUP_LIB_PATH") or os.path.join(HERE, "libcoup_mi355x.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 FLAG_AUTO_RESET, FLAG_HISTORY, FLAG_GENERIC = 1, 2, 4
 MAX_PLAYERS = 6
 HISTORY_BYTES = 96
@@ -24,8 +24,12 @@ SYMBOLS = (
     "coup_set_stream", "coup_batch", "coup_num_players", "coup_state_bytes", "coup_reset", "coup_step", "coup_rollout",
     "coup_new_initial_state", "coup_apply_action", "coup_query",
     "coup_export_state", "coup_import_state", "coup_export_history",
-    "coup_import_history", "coup_error_count",
+    "coup_import_history", "coup_error_count", "coup_slot_op",
 )
+
+# coup_slot_op flags and result layout (coup_slot_result, 128 bytes)
+SLOT_INIT, SLOT_OBS, SLOT_INFO, SLOT_NO_RESULT = 1, 2, 4, 8
+SLOT_RESULT_BYTES = 128
 
 
 class StepOutputs(ctypes.Structure):
@@ -86,6 +90,7 @@ def load():
         "coup_export_history": ([vp, vp], i32),
         "coup_import_history": ([vp, vp], i32),
         "coup_error_count": ([vp, ctypes.POINTER(i64)], i32),
+        "coup_slot_op": ([vp, i64, vp, i64, i32, i32, vp], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -1143,6 +1143,113 @@ __global__ __launch_bounds__(kThreads) void k_query(QueryArgs a) {
   }
 }
 
+
+// Lane-pool op of the per-game State facade (coup_slot_op): one wave, one
+// lane.  Thread 0 runs the transition and the accessors; the history bytes
+// go through LDS so the copy, the new entry and the write-back are ordered
+// by wave barriers.  The
+// tensor writers are the batched ones with n_valid = 1, so the LDS arrays
+// keep their 64-lane shape (the writers index them before their predicate).
+static_assert(sizeof(coup_slot_result) == 128, "coup_slot_result layout");
+
+struct SlotArgs {
+  uint4* dst_state;
+  uint8_t* dst_hist;
+  const uint4* src_state;  // null: no copy
+  const uint8_t* src_hist;
+  int action;              // < 0: none
+  int init;
+  int store;               // write the lane back (copy, init or action)
+  coup_slot_result* out;   // null: no result
+  float* obs;              // [2][98] or null
+  float* info;             // [2][2492] or null
+};
+
+// Out-of-line pieces of k_slot.  slot_transition applies action x to the
+// packed record `w` (State::ApplyAction with its legality check) into *out
+// and returns bit 0 = accepted without a new error, bit 1 = history entry to
+// store, bits 8..15 its index, bits 16..23 the entry byte.
+__device__ __noinline__ uint32_t slot_transition(uint4 w, uint32_t x, uint4* out) {
+  Lane L = unpack(w);
+  const uint32_t idx = L.move;
+  const uint32_t entry = is_chance(L) ? hist_deal(x, L.qids & 1u) : hist_decision(x, L.M);
+  const uint32_t err_before = L.err;
+  NoHistory none;
+  if (!apply_action(L, x, none)) {  // an illegal action leaves the record untouched
+    *out = w;
+    return 0u;
+  }
+  *out = pack(L);
+  const uint32_t ok = (L.err && !err_before) ? 0u : 1u;
+  const uint32_t store = idx < (uint32_t)kHist ? 2u : 0u;
+  return ok | store | (idx << 8) | (entry << 16);
+}
+
+__device__ __noinline__ void slot_result(uint4 w, uint32_t ok, coup_slot_result* out) {
+  const Lane L = unpack(w);
+  out->record[0] = w.x;
+  out->record[1] = w.y;
+  out->record[2] = w.z;
+  out->record[3] = w.w;
+  out->legal_mask = legal_mask(L);
+  out->cur_player = (int8_t)current_player(L);
+  out->terminal = is_terminal(L) ? 1 : 0;
+  out->ok = (uint8_t)ok;
+  out->reserved = 0;
+  out->rewards[0] = (int8_t)L.r0;
+  out->rewards[1] = (int8_t)(-L.r0);
+  const int32_t r0 = return0(L);
+  out->returns[0] = (int8_t)r0;
+  out->returns[1] = (int8_t)(-r0);
+}
+
+template <bool OBS, bool INFO>
+__global__ __launch_bounds__(64) void k_slot(SlotArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t hist[INFO ? 64 * kHist : kHist];
+  __shared__ __attribute__((aligned(16))) uint32_t bits[OBS ? 64 * 8 : 1];
+  __shared__ __attribute__((aligned(16))) uint32_t pre[INFO ? 64 * kPreWords : 1];
+  const uint32_t t = threadIdx.x;
+  const uint4* rs = a.src_state ? a.src_state : a.dst_state;
+  const uint8_t* hs = a.src_state ? a.src_hist : a.dst_hist;
+  if (t < 6u)
+    reinterpret_cast<uint4*>(hist)[t] =
+        a.init ? make_uint4(~0u, ~0u, ~0u, ~0u) : reinterpret_cast<const uint4*>(hs)[t];
+  wave_sync();
+  // Thread 0 runs the rules (the other threads only copy history bytes and
+  // store tensors).  The transition and the accessors are out-of-line
+  // functions (VGPR arguments), so they compile as the per-lane code of the
+  // batched kernels: inlined here on the wave-uniform record, the compiler
+  // moved them to scalar code and produced wrong records.
+  Lane L = initial_lane(0u);
+  if (t == 0u) {
+    uint4 rec = a.init ? pack(initial_lane(0u)) : *rs;
+    uint32_t ok = 1u;
+    if (a.action >= 0) {
+      const uint32_t r = slot_transition(rec, (uint32_t)a.action, &rec);
+      ok = r & 1u;
+      if (r & 2u) hist[(r >> 8) & 0xFFu] = (uint8_t)(r >> 16);
+    }
+    if (a.store) *a.dst_state = rec;
+    if (a.out) slot_result(rec, ok, a.out);
+    L = unpack(rec);
+  }
+  wave_sync();
+  if (t < 6u) {
+    const uint4 h = reinterpret_cast<const uint4*>(hist)[t];
+    if (a.store) reinterpret_cast<uint4*>(a.dst_hist)[t] = h;
+    if (a.out) reinterpret_cast<uint4*>(a.out->history)[t] = h;
+  }
+  if (OBS) {
+    if (t == 0u) obs_bits_to_lds(L, bits);
+    wave_sync();
+    write_obs_wave_bits<0, false>(a.obs, bits, 1u);
+  }
+  if (INFO) {
+    if (t == 0u) info_prefix_to_lds(L, pre);
+    wave_sync();
+    write_info_wave<0>(a.info, hist, pre, 1u);
+  }
+}
 }  // namespace coup
 
 // ====================================================================== C ABI
@@ -1158,6 +1265,7 @@ struct coup_env {
   uint8_t* hist;  // [B][96] when COUP_FLAG_HISTORY
   uint32_t* err_count;
   hipStream_t stream;
+  uint8_t* slot_scratch;  // device staging of coup_slot_op results (lazy)
 };
 
 namespace {
@@ -1241,6 +1349,7 @@ void release(coup_env* env) {
   (void)hipFree(env->state);
   (void)hipFree(env->hist);
   (void)hipFree(env->err_count);
+  (void)hipFree(env->slot_scratch);
   delete env;
 }
 
@@ -1278,6 +1387,7 @@ int coup_create_ex(int64_t batch, uint64_t seed, uint32_t env_id_base, int flags
   env->state = nullptr;
   env->hist = nullptr;
   env->err_count = nullptr;
+  env->slot_scratch = nullptr;
   const size_t lanes = (size_t)(batch > 0 ? batch : 1);
   hipError_t e = hipMalloc(&env->state, lanes * sizeof(uint4) * (generic ? 2 : 1));
   if (e == hipSuccess) e = hipMalloc(&env->err_count, sizeof(uint32_t));
@@ -1494,6 +1604,55 @@ int coup_query(coup_env* env, const coup_query_outputs* out) {
   else
     coup::k_query<false, false><<<g, coup::kThreads, 0, s>>>(a);
   COUP_HIP_TRY(hipGetLastError());
+  return COUP_OK;
+}
+
+int coup_slot_op(coup_env* env, int64_t lane, const coup_env* src_env, int64_t src_lane, int action, int flags,
+                 void* host_out) {
+  COUP_CHECK_ENV(env);
+  if (env->generic || !env->hist)
+    return fail(COUP_E_INVALID, "coup_slot_op: needs a 2-player env created with COUP_FLAG_HISTORY");
+  if (flags & ~(COUP_SLOT_INIT | COUP_SLOT_OBS | COUP_SLOT_INFO | COUP_SLOT_NO_RESULT))
+    return fail(COUP_E_INVALID, "coup_slot_op: unknown flags");
+  if (lane < 0 || lane >= env->batch) return fail(COUP_E_INVALID, "coup_slot_op: lane out of range");
+  if (src_env) {
+    if (src_env->generic || !src_env->hist)
+      return fail(COUP_E_INVALID, "coup_slot_op: src_env needs COUP_FLAG_HISTORY (2 players)");
+    if (src_lane < 0 || src_lane >= src_env->batch) return fail(COUP_E_INVALID, "coup_slot_op: src_lane out of range");
+  }
+  if (action < -1 || action >= COUP_NUM_ACTIONS) return fail(COUP_E_INVALID, "coup_slot_op: action out of range");
+  const bool result = !(flags & COUP_SLOT_NO_RESULT);
+  if (result && !host_out) return fail(COUP_E_INVALID, "coup_slot_op: host_out is null");
+  const bool obs = result && (flags & COUP_SLOT_OBS), info = result && (flags & COUP_SLOT_INFO);
+  const size_t obs_bytes = 2u * COUP_OBS_SIZE * sizeof(float), info_bytes = 2u * COUP_INFO_STATE_SIZE * sizeof(float);
+  if (result && !env->slot_scratch)
+    COUP_HIP_TRY(hipMalloc(&env->slot_scratch, sizeof(coup_slot_result) + obs_bytes + info_bytes));
+  coup::SlotArgs a;
+  a.dst_state = env->state + lane;
+  a.dst_hist = env->hist + lane * COUP_HISTORY_BYTES;
+  a.src_state = src_env ? src_env->state + src_lane : nullptr;
+  a.src_hist = src_env ? src_env->hist + src_lane * COUP_HISTORY_BYTES : nullptr;
+  a.action = action;
+  a.init = (flags & COUP_SLOT_INIT) ? 1 : 0;
+  a.store = (src_env || a.init || action >= 0) ? 1 : 0;
+  uint8_t* sc = env->slot_scratch;
+  a.out = result ? reinterpret_cast<coup_slot_result*>(sc) : nullptr;
+  a.obs = obs ? reinterpret_cast<float*>(sc + sizeof(coup_slot_result)) : nullptr;
+  a.info = info ? reinterpret_cast<float*>(sc + sizeof(coup_slot_result) + (obs ? obs_bytes : 0)) : nullptr;
+  hipStream_t s = env->stream;
+  if (obs && info)
+    coup::k_slot<true, true><<<1, 64, 0, s>>>(a);
+  else if (obs)
+    coup::k_slot<true, false><<<1, 64, 0, s>>>(a);
+  else if (info)
+    coup::k_slot<false, true><<<1, 64, 0, s>>>(a);
+  else
+    coup::k_slot<false, false><<<1, 64, 0, s>>>(a);
+  COUP_HIP_TRY(hipGetLastError());
+  if (!result) return COUP_OK;
+  const size_t n = sizeof(coup_slot_result) + (obs ? obs_bytes : 0) + (info ? info_bytes : 0);
+  COUP_HIP_TRY(hipMemcpyAsync(host_out, sc, n, hipMemcpyDeviceToHost, s));
+  COUP_HIP_TRY(hipStreamSynchronize(s));
   return COUP_OK;
 }
 

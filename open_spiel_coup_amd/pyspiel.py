@@ -9,21 +9,23 @@ same surface with only an import swap:
     game = pyspiel.load_game("coup")
     state = game.new_initial_state()
 
-A `CoupState` holds its 16-byte lane record and its history bytes on the
-host; every rules operation (apply_action, legal actions, tensors, ...)
-runs the HIP kernels on a one-lane scratch env through the C ABI -- there
-is no CPU rules engine in the product.  Query results are cached until the
-state changes.  Strings are formatted on the host (strings.py).
+A `CoupState` owns one lane of a device-resident lane pool; every rules
+operation (apply_action, legal actions, tensors, ...) is one coup_slot_op
+launch on that lane through the C ABI -- there is no CPU rules engine in
+the product.  The 128-byte result of the last op (record, history bytes,
+legal mask, player, rewards, returns) is kept on the host and serves the
+accessors until the state changes; a clone is a device-side lane copy.  Strings are formatted on the host (strings.py).
 This is the compatibility path; batched learners use BatchedCoupEnv.
 """
+import ctypes
 import enum
 
 import numpy as np
 import torch
 
-from . import packed, strings
+from . import _native, packed, strings
 from ._native import CoupError
-from .env import BatchedCoupEnv, HISTORY_BYTES, INFO_STATE_SIZE, OBS_SIZE
+from .env import BatchedCoupEnv, INFO_STATE_SIZE, OBS_SIZE
 
 SpielError = CoupError
 
@@ -85,45 +87,80 @@ class GameType:
         self.parameter_specification = {}
 
 
-class _Engine:
-    """One-lane scratch env (history kept) that runs single-state ops."""
+class _Pool:
+    """Device-resident lane pool: every live CoupState owns one lane of a
+    2-player history env (segments of SEG lanes, grown on demand).  Each
+    State op is one coup_slot_op launch on its lane, and only ops that need
+    an answer copy a 128-byte result back (one synchronisation); a clone is
+    a device-to-device lane copy with no round trip."""
+
+    SEG = 4096
 
     def __init__(self, device):
-        self.env = BatchedCoupEnv(1, seed=0, auto_reset=False, obs=False, history=True, device=device)
-        self.device = self.env.device
+        self.device = torch.device(device)
+        self.lib = _native.load()
+        self.segs = []
+        self.free = []
+        nbytes = _native.SLOT_RESULT_BYTES + 2 * OBS_SIZE * 4 + 2 * INFO_STATE_SIZE * 4
+        self.host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+        self.buf = self.host.numpy()
 
-    def _load(self, rec, hist):
-        self.env.import_state(torch.from_numpy(rec.view(np.int32).reshape(1, 4)))
-        self.env.import_history(torch.from_numpy(hist.reshape(1, HISTORY_BYTES)))
+    def alloc(self):
+        if not self.free:
+            env = BatchedCoupEnv(self.SEG, seed=0, auto_reset=False, obs=False, history=True, device=self.device)
+            k = len(self.segs)
+            self.segs.append(env)
+            self.free.extend((k, i) for i in range(self.SEG - 1, -1, -1))
+        return self.free.pop()
 
-    def new_initial(self):
-        self.env.new_initial_state()
-        return (self.env.export_state().cpu().numpy().view(np.uint32).reshape(4).copy(),
-                np.full(HISTORY_BYTES, 0xFF, np.uint8))
+    def release(self, slot):
+        self.free.append(slot)
 
-    def apply(self, rec, hist, action):
-        self._load(rec, hist)
-        self.env.apply_action(torch.tensor([int(action)], dtype=torch.int8))
-        if self.env.error_count():
-            raise SpielError(f"illegal action {action}")
-        return (self.env.export_state().cpu().numpy().view(np.uint32).reshape(4).copy(),
-                self.env.export_history().cpu().numpy().reshape(HISTORY_BYTES).copy())
+    def handle(self, slot):
+        return self.segs[slot[0]]._h
 
-    def query(self, rec, hist, obs, info):
-        self._load(rec, hist)
-        q = self.env.query(obs=obs, info_state=info)
-        return {k: v.cpu().numpy()[0] for k, v in q.items()}
+    def op(self, slot, src=None, action=-1, init=False, obs=False, info=False, result=True):
+        """coup_slot_op on `slot`; src = (coup_env handle, lane) or None."""
+        flags = ((_native.SLOT_INIT if init else 0) | (_native.SLOT_OBS if obs else 0)
+                 | (_native.SLOT_INFO if info else 0) | (0 if result else _native.SLOT_NO_RESULT))
+        env = self.segs[slot[0]]
+        env._bind_stream()
+        src_h, src_lane = src if src is not None else (None, 0)
+        _native.check(self.lib.coup_slot_op(env._h, slot[1], src_h, src_lane, int(action), flags,
+                                            ctypes.c_void_p(self.host.data_ptr()) if result else None))
+        if not result:
+            return None
+        b = self.buf
+        q = {
+            "record": b[0:16].view(np.uint32).copy(),
+            "history": b[16:112].copy(),
+            "legal_mask": int(b[112:116].view(np.uint32)[0]),
+            "current_player": int(b[116:117].view(np.int8)[0]),
+            "terminal": bool(b[117]),
+            "ok": bool(b[118]),
+            "rewards": b[120:122].view(np.int8).copy(),
+            "returns": b[122:124].view(np.int8).copy(),
+        }
+        off = _native.SLOT_RESULT_BYTES
+        if obs:
+            q["obs"] = b[off:off + 2 * OBS_SIZE * 4].view(np.float32).reshape(2, OBS_SIZE).copy()
+            off += 2 * OBS_SIZE * 4
+        if info:
+            q["info_state"] = b[off:off + 2 * INFO_STATE_SIZE * 4].view(np.float32).reshape(2, INFO_STATE_SIZE).copy()
+        return q
 
 
-_engines = {}
+_pools = {}
 
 
-def _engine(device=None):
+def _pool(device=None):
     dev = torch.device(device if device is not None else "cuda")
+    if dev.index is None:
+        dev = torch.device(dev.type, torch.cuda.current_device())
     key = (dev.type, dev.index)
-    if key not in _engines:
-        _engines[key] = _Engine(dev)
-    return _engines[key]
+    if key not in _pools:
+        _pools[key] = _Pool(dev)
+    return _pools[key]
 
 
 class CoupGame:
@@ -217,23 +254,59 @@ class CoupGame:
 class CoupState:
     """open_spiel::coup::CoupState (coup.h:111-197) over the GPU engine."""
 
-    def __init__(self, game, _rec=None, _hist=None, _history=None):
+    def __init__(self, game, _src=None, _history=None, _q=None):
         self._game = game
-        self._eng = _engine(game._device)
-        if _rec is None:
-            _rec, _hist = self._eng.new_initial()
-            _history = []
-        self._rec, self._hist, self._history = _rec, _hist, _history
-        self._q = None
+        self._pool = _pool(game._device)
+        self._slot = self._pool.alloc()
+        if _src is None:
+            self._q = self._pool.op(self._slot, init=True)
+            self._history = []
+        else:  # Clone / snapshot: a device-side lane copy
+            self._q = self._pool.op(self._slot, src=_src, result=_q is None)
+            if _q is not None:
+                self._q = dict(_q)
+            self._history = _history
+
+    def __del__(self):
+        try:
+            self._pool.release(self._slot)
+        except Exception:
+            pass
+
+    @classmethod
+    def _from_env(cls, game, env_handle, lane, history):
+        """Snapshot lane `lane` of a 2-player history env (rl_environment)."""
+        return cls(game, _src=(env_handle, lane), _history=history)
+
+    def _copy_to_env(self, env_handle, lane):
+        """Write this state into lane `lane` of a 2-player history env."""
+        env = self._pool.segs[self._slot[0]]
+        env._bind_stream()
+        _native.check(env.lib.coup_slot_op(env_handle, lane, env._h, self._slot[1], -1,
+                                           _native.SLOT_NO_RESULT, None))
 
     # ------------------------------------------------------------- internals
     def _query(self, obs=False, info=False):
-        if self._q is None or (obs and "obs" not in self._q) or (info and "info_state" not in self._q):
-            self._q = self._eng.query(self._rec, self._hist, obs, info)
+        need_obs = obs and "obs" not in self._q
+        need_info = info and "info_state" not in self._q
+        if need_obs or need_info:
+            q = self._pool.op(self._slot, obs=obs, info=info)
+            for k in ("obs", "info_state"):
+                if k not in q and k in self._q:
+                    q[k] = self._q[k]
+            self._q = q
         return self._q
 
     def _words(self):
-        return self._rec.reshape(1, 4)
+        return self._q["record"].reshape(1, 4)
+
+    @property
+    def _rec(self):
+        return self._q["record"]
+
+    @property
+    def _hist(self):
+        return self._q["history"]
 
     # ------------------------------------------------------------- State API
     def get_game(self):
@@ -301,9 +374,15 @@ class CoupState:
         """State::ApplyAction (spiel.cc:322-331) on the GPU; raises SpielError
         for an illegal action."""
         player = self.current_player()
-        self._rec, self._hist = self._eng.apply(self._rec, self._hist, action)
-        self._history = self._history + [(player, int(action))]
-        self._q = None
+        a = int(action)
+        if not 0 <= a < 18 or not (self._mask() >> a) & 1 or player == PlayerId.TERMINAL:
+            raise SpielError(f"illegal action {action}")
+        q = self._pool.op(self._slot, action=a)
+        if not q["ok"]:
+            self._q = self._pool.op(self._slot)
+            raise SpielError(f"illegal action {action}")
+        self._q = q
+        self._history = self._history + [(player, a)]
 
     def apply_action_with_legality_check(self, action):
         self.apply_action(action)
@@ -314,9 +393,8 @@ class CoupState:
         return c
 
     def clone(self):
-        c = CoupState(self._game, self._rec.copy(), self._hist.copy(), list(self._history))
-        c._q = self._q
-        return c
+        return CoupState(self._game, _src=(self._pool.handle(self._slot), self._slot[1]),
+                         _history=list(self._history), _q=self._q)
 
     def __copy__(self):
         return self.clone()

@@ -264,13 +264,12 @@ class Environment:
     def get_state(self):
         """A pyspiel-shaped CoupState snapshot of the env's lane."""
         words, hist = self._state_view()
-        return pyspiel.CoupState(self._game, words, hist, self._history_list(words, hist))
+        return pyspiel.CoupState._from_env(self._game, self._env._h, 0, self._history_list(words, hist))
 
     def set_state(self, new_state):
         assert new_state.get_game() == self.game, "State must have been created by the same game."
-        rec = torch.from_numpy(new_state.packed_record().view(np.int32).reshape(1, 4))
-        self._env.import_state(rec)
-        self._env.import_history(torch.from_numpy(new_state.history_bytes().reshape(1, HISTORY_BYTES)))
+        self._env._bind_stream()
+        new_state._copy_to_env(self._env._h, 0)
 
     @property
     def mfg_distribution(self):

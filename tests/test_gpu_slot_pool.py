@@ -1,0 +1,133 @@
+"""The device-resident lane pool behind the per-game State facade
+(coup_slot_op): clones, children and many live states, checked node by node
+against the oracle (oracle.OracleState mirrors every facade state)."""
+import time
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+from open_spiel_coup_amd import pyspiel, rl_environment  # noqa: E402
+
+
+def _same(st, ref, tensors=False):
+    assert st.packed_record().tolist() == [int(x) for x in ref.pack(0)]
+    assert st.history() == ref.history()
+    assert st.current_player() == ref.current_player()
+    assert st.is_terminal() == ref.is_terminal()
+    if not ref.is_terminal():
+        assert st.legal_actions() == ref.legal_actions()
+    assert st.returns() == [float(x) for x in ref.returns()]
+    if tensors:
+        for p in (0, 1):
+            assert st.observation_tensor(p) == list(ref.observation_tensor(p))
+            assert st.information_state_tensor(p) == list(ref.information_state_tensor(p))
+
+
+def test_tree_walk_clones_and_children_match_oracle():
+    """A Deep CFR-shaped walk: at every node expand up to 3 children
+    (child() = clone + apply), recurse to depth 8; every node against the
+    oracle, tensors on a sample."""
+    rng = np.random.default_rng(11)
+    game = pyspiel.load_game("coup")
+    nodes = [0]
+
+    def walk(st, ref, depth):
+        nodes[0] += 1
+        _same(st, ref, tensors=nodes[0] % 17 == 0)
+        if st.is_terminal() or depth == 0:
+            return
+        acts = st.legal_actions()
+        for a in rng.permutation(acts)[:3 if not st.is_chance_node() else 2]:
+            ch = st.child(int(a))
+            r2 = ref.clone()
+            r2.apply_action(int(a))
+            walk(ch, r2, depth - 1)
+        _same(st, ref)  # the parent is untouched by its children
+
+    walk(game.new_initial_state(), oracle.OracleState(), 8)
+    assert nodes[0] > 200
+
+
+def test_more_live_states_than_one_segment():
+    """Live states beyond one pool segment (4096 lanes) and slot reuse after
+    release; each state gets its own random playout."""
+    rng = np.random.default_rng(5)
+    game = pyspiel.load_game("coup")
+    root = game.new_initial_state()
+    for a in (0, 1, 2, 3):
+        root.apply_action(a)
+    states = [root.clone() for _ in range(4100 + 3)]
+    refs = []
+    r0 = oracle.OracleState()
+    for a in (0, 1, 2, 3):
+        r0.apply_action(a)
+    for i, st in enumerate(states[:64] + states[-64:]):
+        ref = r0.clone()
+        for _ in range(rng.integers(1, 12)):
+            if ref.is_terminal():
+                break
+            a = int(rng.choice(ref.legal_actions()))
+            st.apply_action(a)
+            ref.apply_action(a)
+        refs.append((st, ref))
+    for st, ref in refs:
+        _same(st, ref)
+    del states, refs
+    again = [root.clone() for _ in range(100)]  # released slots are reused
+    assert all(s.packed_record().tolist() == root.packed_record().tolist() for s in again)
+
+
+def test_illegal_action_leaves_state_and_pool_usable():
+    st = pyspiel.load_game("coup").new_initial_state()
+    for a in (0, 1, 2, 3):
+        st.apply_action(a)
+    before = st.packed_record().tolist()
+    for bad in (9, 17, 18, -1):
+        with pytest.raises(pyspiel.SpielError):
+            st.apply_action(bad)
+    assert st.packed_record().tolist() == before
+    st.apply_action(0)
+    assert st.history() == [0, 1, 2, 3, 0]
+
+
+def test_rl_environment_get_set_state_round_trip():
+    env = rl_environment.Environment("coup", seed=4)
+    ts = env.reset()
+    rng = np.random.default_rng(2)
+    for _ in range(5):
+        p = ts.observations["current_player"]
+        ts = env.step([int(rng.choice(ts.observations["legal_actions"][p]))])
+        if ts.last():
+            ts = env.reset()
+    snap = env.get_state
+    rec = snap.packed_record().tolist()
+    ref = oracle.OracleState()
+    for a in snap.history():
+        ref.apply_action(a)
+    assert snap.legal_actions() == ref.legal_actions()
+    p = ts.observations["current_player"]
+    env.step([int(ts.observations["legal_actions"][p][0])])
+    env.set_state(snap)  # back to the snapshot
+    assert env.get_state.packed_record().tolist() == rec
+
+
+def test_facade_op_latency_report():
+    """Not a pass/fail bound: prints the per-op cost of the pool facade."""
+    game = pyspiel.load_game("coup")
+    st = game.new_initial_state()
+    for a in (0, 1, 2, 3):
+        st.apply_action(a)
+    n = 200
+    t0 = time.perf_counter()
+    for _ in range(n):
+        c = st.child(0)
+        c.legal_actions()
+    t1 = time.perf_counter()
+    for _ in range(n):
+        st.clone()
+    t2 = time.perf_counter()
+    print(f"\nfacade: child+legal_actions {1e6 * (t1 - t0) / n:.1f} us, clone {1e6 * (t2 - t1) / n:.1f} us")

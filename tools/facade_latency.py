@@ -1,0 +1,71 @@
+"""Per-op latency of the per-game State facade: the lane pool (coup_slot_op,
+one launch + one 128-byte read-back per answered op) against the previous
+design (one-lane scratch env: import record + history, apply, error count,
+export record + history), timed in one process.  Measurement tool only."""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from open_spiel_coup_amd import pyspiel  # noqa: E402
+from open_spiel_coup_amd.env import BatchedCoupEnv, HISTORY_BYTES  # noqa: E402
+
+
+def scratch_apply(env, rec, hist, action):
+    env.import_state(torch.from_numpy(rec.view(np.int32).reshape(1, 4)))
+    env.import_history(torch.from_numpy(hist.reshape(1, HISTORY_BYTES)))
+    env.apply_action(torch.tensor([int(action)], dtype=torch.int8))
+    assert env.error_count() == 0
+    return (env.export_state().cpu().numpy().view(np.uint32).reshape(4).copy(),
+            env.export_history().cpu().numpy().reshape(HISTORY_BYTES).copy())
+
+
+def scratch_query(env, rec, hist):
+    env.import_state(torch.from_numpy(rec.view(np.int32).reshape(1, 4)))
+    env.import_history(torch.from_numpy(hist.reshape(1, HISTORY_BYTES)))
+    q = env.query(obs=False, info_state=False)
+    return {k: v.cpu().numpy()[0] for k, v in q.items()}
+
+
+def main(n=2000):
+    game = pyspiel.load_game("coup")
+    st = game.new_initial_state()
+    for a in (0, 1, 2, 3):
+        st.apply_action(a)
+    for _ in range(50):
+        st.child(0).legal_actions()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        st.child(0).legal_actions()
+    pool_child = (time.perf_counter() - t0) / n
+    t0 = time.perf_counter()
+    for _ in range(n):
+        st.clone()
+    pool_clone = (time.perf_counter() - t0) / n
+    t0 = time.perf_counter()
+    for _ in range(n):
+        st.observation_tensor(0)
+        st._q.pop("obs", None)
+    pool_obs = (time.perf_counter() - t0) / n
+    env = BatchedCoupEnv(1, seed=0, auto_reset=False, obs=False, history=True)
+    rec, hist = st.packed_record(), st.history_bytes()
+    for _ in range(50):
+        scratch_apply(env, rec, hist, 0)
+    t0 = time.perf_counter()
+    for _ in range(n):
+        r2, h2 = scratch_apply(env, rec, hist, 0)
+        scratch_query(env, r2, h2)
+    scratch_child = (time.perf_counter() - t0) / n
+    print(json.dumps({"tool": "facade_latency", "ops": n,
+                      "pool_child_plus_legal_us": round(1e6 * pool_child, 1),
+                      "pool_clone_us": round(1e6 * pool_clone, 1),
+                      "pool_observation_tensor_us": round(1e6 * pool_obs, 1),
+                      "scratch_env_child_plus_legal_us": round(1e6 * scratch_child, 1)}))
+
+
+if __name__ == "__main__":
+    main()

@@ -69,6 +69,36 @@ __global__ __launch_bounds__(T) void k_block_chunks(v4f* __restrict__ dst, uint3
   for (uint32_t j = 0; j < (uint32_t)kRowF4; ++j) st<POL>(base + T * j + threadIdx.x, z);
 }
 
+
+// Unit-strided lane ownership (a narrow chip-wide write window under lane
+// ownership): a block owns J units of U lanes; unit j of block b' lies at
+// global unit (s*J + j)*R + r, with s = b' / R, r = b' % R, so at sub-step j
+// the R co-resident blocks write R adjacent units (R*U*784 B) and the window
+// sweeps the buffer.  COOP: the block stores its J units in j order
+// (256 threads per iteration); otherwise wave w stores units [w*J/4, (w+1)*J/4).
+// XR: r is remapped so that each XCD (b' % 8) owns a contiguous run of units.
+template <int U, int J, bool COOP, bool XR>
+__global__ __launch_bounds__(256) void k_unit_strided(v4f* __restrict__ dst, uint32_t R) {
+  const v4f z = {0.f, 1.f, 0.f, 0.f};
+  constexpr uint32_t kUnitF4 = U * kRowF4;
+  const uint32_t s = blockIdx.x / R, r0 = blockIdx.x % R;
+  const uint32_t r = XR ? (r0 % 8u) * (R / 8u) + r0 / 8u : r0;
+  if (COOP) {
+    constexpr uint32_t tot = J * kUnitF4;
+    for (uint32_t q = threadIdx.x; q < tot; q += 256u) {
+      const uint32_t j = q / kUnitF4, f = q - j * kUnitF4;
+      st<0>(dst + ((size_t)(s * J + j) * R + r) * kUnitF4 + f, z);
+    }
+  } else {
+    constexpr uint32_t per = J / 4, tot = per * kUnitF4;
+    const uint32_t w = threadIdx.x / 64u;
+    for (uint32_t q = threadIdx.x & 63u; q < tot; q += 64u) {
+      const uint32_t j = w * per + q / kUnitF4, f = q % kUnitF4;
+      st<0>(dst + ((size_t)(s * J + j) * R + r) * kUnitF4 + f, z);
+    }
+  }
+}
+
 // Unconstrained reference: grid-stride float4 sweep.
 template <int POL>
 __global__ __launch_bounds__(256) void k_sweep(v4f* __restrict__ dst, size_t n) {
@@ -163,6 +193,20 @@ int main() {
   for (int S : {4, 16, 64, 256, 1024}) {
     WAVE(64, 0, true, S);
   }
+  for (uint32_t R : {256u, 512u, 1024u, 2048u, 4096u}) {
+    const int g = (int)(lanes / 256);
+    std::snprintf(name, sizeof name, "unit8_coop_R%u", R);
+    timed(name, g, 256, [&] { k_unit_strided<8, 32, true, false><<<g, 256>>>(a, R); });
+    std::snprintf(name, sizeof name, "unit8_wave_R%u", R);
+    timed(name, g, 256, [&] { k_unit_strided<8, 32, false, false><<<g, 256>>>(a, R); });
+    std::snprintf(name, sizeof name, "unit8_coop_xr_R%u", R);
+    timed(name, g, 256, [&] { k_unit_strided<8, 32, true, true><<<g, 256>>>(a, R); });
+    std::snprintf(name, sizeof name, "unit4_coop_R%u", R);
+    timed(name, g, 256, [&] { k_unit_strided<4, 64, true, false><<<g, 256>>>(a, R); });
+    std::snprintf(name, sizeof name, "unit16_coop_R%u", R);
+    timed(name, g, 256, [&] { k_unit_strided<16, 16, true, false><<<g, 256>>>(a, R); });
+  }
+  WAVE(256, 0, true, 0);
 #undef WAVE
 #define BLOCK(T, POL, XCD, S)                                                                     \
   std::snprintf(name, sizeof name, "block_t%d_pol%d_xcd%d_S%d", T, POL, (int)XCD, S);             \
