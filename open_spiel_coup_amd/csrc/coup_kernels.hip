@@ -1144,12 +1144,69 @@ __global__ __launch_bounds__(kThreads) void k_query(QueryArgs a) {
 }
 
 
+// InformationStateTensor of a few lanes, one thread per float4 (lane-major
+// [n][2][2492] output).  The wave-cooperative writer gives each wave 1246
+// store instructions for its 64 lanes; at one lane (the per-game State
+// facade, rl_environment) that is one wave storing alone, ~150 us.  Here the
+// 1246 float4 of a lane are spread over 1246 threads; each thread decodes its
+// lane's record and history bytes itself (L2-resident).
+__global__ __launch_bounds__(kThreads) void k_info_elems(const uint4* __restrict__ state,
+                                                        const uint8_t* __restrict__ hist, int64_t n,
+                                                        float* __restrict__ info) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  const int64_t g = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (g >= n * kInfoF4) return;
+  const int64_t lane = g / kInfoF4;
+  const uint32_t c = (uint32_t)(g - lane * kInfoF4);
+  const uint32_t p = c >= (uint32_t)kInfoHalfF4 ? 1u : 0u;
+  const int f0 = 4 * (int)(c - p * (uint32_t)kInfoHalfF4);
+  const Lane L = unpack(state[lane]);
+  uint32_t pre[kPreWords];
+  info_prefix_to_lds(L, pre);
+  const uint32_t meta = pre[4];
+  const uint32_t len = meta >> 16;
+  v4f w = {0.0f, 0.0f, 0.0f, 0.0f};
+  if (f0 < 62 + 18 * (int)len) {
+    const uint64_t prefix = (uint64_t)pre[2 * p] | ((uint64_t)pre[2 * p + 1] << 32);
+    const int t0 = f0 - 62;
+    const uint32_t r0 = t0 < 0 ? 0u : (uint32_t)t0 / 18u;
+    const int col0 = t0 - 18 * (int)r0;
+    const uint8_t* h = hist + lane * kHist;
+    uint32_t va[2];
+#pragma unroll
+    for (uint32_t k = 0; k < 2; ++k) {
+      const uint32_t r = r0 + k;
+      const uint32_t e = h[r < (uint32_t)kHist ? r : 0u];
+      const bool seen = (e & 0x20u) == 0u || ((e >> 6) & 1u) == p;  // deals: observer's only
+      va[k] = (r < len && seen) ? (e & 0x1Fu) : 31u;
+    }
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int f = f0 + e;
+      const int col = col0 + e;
+      const uint32_t row_act = col >= 18 ? va[1] : va[0];
+      const float hv = (row_act == (uint32_t)(col >= 18 ? col - 18 : col)) ? 1.0f : 0.0f;
+      const float pb = (float)((uint32_t)(prefix >> (f & 63)) & 1u);
+      const float coin = (float)(f == 60 ? (meta & 0xFFu) : ((meta >> 8) & 0xFFu));
+      v[e] = f < 60 ? pb : (f < 62 ? coin : hv);
+    }
+    w = v4f{v[0], v[1], v[2], v[3]};
+  }
+  reinterpret_cast<v4f*>(info)[g] = w;
+}
+
+// Batches up to this size take k_info_elems for the InformationStateTensor
+// of coup_query (and coup_slot_op always does).
+constexpr int64_t kInfoElemsMaxBatch = 1024;
+
 // Lane-pool op of the per-game State facade (coup_slot_op): one wave, one
 // lane.  Thread 0 runs the transition and the accessors; the history bytes
 // go through LDS so the copy, the new entry and the write-back are ordered
 // by wave barriers.  The
-// tensor writers are the batched ones with n_valid = 1, so the LDS arrays
-// keep their 64-lane shape (the writers index them before their predicate).
+// observation writer is the batched one with n_valid = 1, so its LDS array
+// keeps the 64-lane shape (the writer indexes it before its predicate); the
+// InformationStateTensor is left to k_info_elems.
 static_assert(sizeof(coup_slot_result) == 128, "coup_slot_result layout");
 
 struct SlotArgs {
@@ -1162,7 +1219,6 @@ struct SlotArgs {
   int store;               // write the lane back (copy, init or action)
   coup_slot_result* out;   // null: no result
   float* obs;              // [2][98] or null
-  float* info;             // [2][2492] or null
 };
 
 // Out-of-line pieces of k_slot.  slot_transition applies action x to the
@@ -1203,11 +1259,10 @@ __device__ __noinline__ void slot_result(uint4 w, uint32_t ok, coup_slot_result*
   out->returns[1] = (int8_t)(-r0);
 }
 
-template <bool OBS, bool INFO>
+template <bool OBS>
 __global__ __launch_bounds__(64) void k_slot(SlotArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t hist[INFO ? 64 * kHist : kHist];
+  __shared__ __attribute__((aligned(16))) uint8_t hist[kHist];
   __shared__ __attribute__((aligned(16))) uint32_t bits[OBS ? 64 * 8 : 1];
-  __shared__ __attribute__((aligned(16))) uint32_t pre[INFO ? 64 * kPreWords : 1];
   const uint32_t t = threadIdx.x;
   const uint4* rs = a.src_state ? a.src_state : a.dst_state;
   const uint8_t* hs = a.src_state ? a.src_hist : a.dst_hist;
@@ -1243,11 +1298,6 @@ __global__ __launch_bounds__(64) void k_slot(SlotArgs a) {
     if (t == 0u) obs_bits_to_lds(L, bits);
     wave_sync();
     write_obs_wave_bits<0, false>(a.obs, bits, 1u);
-  }
-  if (INFO) {
-    if (t == 0u) info_prefix_to_lds(L, pre);
-    wave_sync();
-    write_info_wave<0>(a.info, hist, pre, 1u);
   }
 }
 }  // namespace coup
@@ -1595,6 +1645,12 @@ int coup_query(coup_env* env, const coup_query_outputs* out) {
   a.info = out->info_state;
   const unsigned g = grid_for(env->batch);
   hipStream_t s = env->stream;
+  if (a.info && env->batch <= coup::kInfoElemsMaxBatch) {
+    const int64_t nf4 = env->batch * coup::kInfoF4;
+    coup::k_info_elems<<<(unsigned)((nf4 + coup::kThreads - 1) / coup::kThreads), coup::kThreads, 0, s>>>(
+        env->state, env->hist, env->batch, a.info);
+    a.info = nullptr;
+  }
   if (a.obs && a.info)
     coup::k_query<true, true><<<g, coup::kThreads, 0, s>>>(a);
   else if (a.obs)
@@ -1638,17 +1694,20 @@ int coup_slot_op(coup_env* env, int64_t lane, const coup_env* src_env, int64_t s
   uint8_t* sc = env->slot_scratch;
   a.out = result ? reinterpret_cast<coup_slot_result*>(sc) : nullptr;
   a.obs = obs ? reinterpret_cast<float*>(sc + sizeof(coup_slot_result)) : nullptr;
-  a.info = info ? reinterpret_cast<float*>(sc + sizeof(coup_slot_result) + (obs ? obs_bytes : 0)) : nullptr;
   hipStream_t s = env->stream;
-  if (obs && info)
-    coup::k_slot<true, true><<<1, 64, 0, s>>>(a);
-  else if (obs)
-    coup::k_slot<true, false><<<1, 64, 0, s>>>(a);
-  else if (info)
-    coup::k_slot<false, true><<<1, 64, 0, s>>>(a);
+  // the InformationStateTensor is written by k_info_elems after the op
+  // (1246 threads instead of one wave)
+  float* info_out = info ? reinterpret_cast<float*>(sc + sizeof(coup_slot_result) + (obs ? obs_bytes : 0)) : nullptr;
+  if (obs)
+    coup::k_slot<true><<<1, 64, 0, s>>>(a);
   else
-    coup::k_slot<false, false><<<1, 64, 0, s>>>(a);
+    coup::k_slot<false><<<1, 64, 0, s>>>(a);
   COUP_HIP_TRY(hipGetLastError());
+  if (info_out) {
+    coup::k_info_elems<<<(unsigned)((coup::kInfoF4 + coup::kThreads - 1) / coup::kThreads), coup::kThreads, 0, s>>>(
+        a.dst_state, a.dst_hist, 1, info_out);
+    COUP_HIP_TRY(hipGetLastError());
+  }
   if (!result) return COUP_OK;
   const size_t n = sizeof(coup_slot_result) + (obs ? obs_bytes : 0) + (info ? info_bytes : 0);
   COUP_HIP_TRY(hipMemcpyAsync(host_out, sc, n, hipMemcpyDeviceToHost, s));

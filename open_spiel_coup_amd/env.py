@@ -8,6 +8,7 @@ the env's device; kernels run on torch's current stream.
 """
 import ctypes
 
+import numpy as np
 import torch
 
 from . import _native
@@ -210,6 +211,44 @@ class BatchedCoupEnv:
                                      "info_state")])
         _native.check(self.lib.coup_query(self._h, ctypes.byref(qo)))
         return q
+
+    def query_host(self, obs=True, info_state=False):
+        """`query` for small batches that want the answers on the host: one
+        device buffer holds every output (lane-major sections), and one copy
+        into pinned memory brings it back (a single synchronisation).
+        Returns numpy arrays keyed like `query`."""
+        self._bind_stream()
+        B, P = self.batch, self.num_players
+        sizes = [("legal_mask", 4 * B), ("current_player", B), ("terminal", B), ("rewards", B * P),
+                 ("returns", B * P)]
+        if obs:
+            sizes.append(("obs", 4 * B * P * self.obs_size))
+        if info_state:
+            sizes.append(("info_state", 4 * B * 2 * INFO_STATE_SIZE))
+        offs, total = {}, 0
+        for k, n in sizes:
+            offs[k] = total
+            total += (n + 15) // 16 * 16
+        if getattr(self, "_qh_total", None) != total:
+            self._qh_dev = torch.empty(total, dtype=torch.uint8, device=self.device)
+            self._qh_host = torch.empty(total, dtype=torch.uint8, pin_memory=True)
+            self._qh_total = total
+        base = self._qh_dev.data_ptr()
+        qo = _native.QueryOutputs(*[(base + offs[k]) if k in offs else None for k in
+                                    ("legal_mask", "current_player", "terminal", "rewards", "returns", "obs",
+                                     "info_state")])
+        _native.check(self.lib.coup_query(self._h, ctypes.byref(qo)))
+        self._qh_host.copy_(self._qh_dev, non_blocking=True)
+        torch.cuda.current_stream(self.device).synchronize()
+        h = self._qh_host.numpy()
+        shapes = {"legal_mask": (np.int32, (B,)), "current_player": (np.int8, (B,)), "terminal": (np.uint8, (B,)),
+                  "rewards": (np.int8, (B, P)), "returns": (np.int8, (B, P)),
+                  "obs": (np.float32, (B, P, self.obs_size)), "info_state": (np.float32, (B, 2, INFO_STATE_SIZE))}
+        out = {}
+        for k, n in sizes:
+            dt, shape = shapes[k]
+            out[k] = h[offs[k]:offs[k] + n].view(dt).reshape(shape).copy()
+        return out
 
     def export_state(self):
         self._bind_stream()

@@ -120,8 +120,12 @@ class Environment:
 
     # ------------------------------------------------------------ plumbing
     def _make_env(self):
-        self._env = BatchedCoupEnv(1, seed=self._seed, auto_reset=False, obs=self._use_observation,
-                                   info_state=not self._use_observation, history=True, device=self._device)
+        # the step kernel writes no tensors here: each time step reads them
+        # (and everything else) with one query_host round trip
+        self._env = BatchedCoupEnv(1, seed=self._seed, auto_reset=False, obs=False, info_state=False,
+                                   history=True, device=self._device)
+        self._act = torch.empty(1, dtype=torch.int8, pin_memory=True)
+        self._last = None
 
     def _state_view(self):
         words = self._env.export_state().cpu().numpy().view(np.uint32).reshape(4).copy()
@@ -158,8 +162,8 @@ class Environment:
         return TimeStep(observations=obs, rewards=rewards, discounts=discounts, step_type=step_type)
 
     def _query(self):
-        q = self._env.query(obs=self._use_observation, info_state=not self._use_observation)
-        return {k: v.cpu().numpy()[0] for k, v in q.items()}
+        q = self._env.query_host(obs=self._use_observation, info_state=not self._use_observation)
+        return {k: v[0] for k, v in q.items()}
 
     def _sample_external_events(self):
         """rl_environment.py:369-382 with a caller-supplied sampler."""
@@ -195,13 +199,19 @@ class Environment:
             legal = self._last["legal_actions"][self._last["current_player"]] if self._last else []
             if actions[0] not in legal:
                 raise RuntimeError(f"step() called on illegal action {actions[0]}")
-        a = torch.tensor([int(actions[0])], dtype=torch.int8)
+        # legal per the last time step's mask (which came from the GPU): the
+        # kernel cannot reject it, so the error counter's synchronisation is
+        # skipped
+        cur = self._last["current_player"] if self._last else -1
+        known_legal = cur >= 0 and int(actions[0]) in self._last["legal_actions"][cur]
+        self._act[0] = int(actions[0])
+        a = self._act.to(self._env.device, non_blocking=True)
         if self._sampler is None:
             self._env.step(a)
         else:
             self._env.apply_action(a)
             self._sample_external_events()
-        if self._env.error_count():
+        if not known_legal and self._env.error_count():
             raise pyspiel.SpielError(f"illegal action {actions[0]}")
         return self.get_time_step()
 
@@ -270,6 +280,7 @@ class Environment:
         assert new_state.get_game() == self.game, "State must have been created by the same game."
         self._env._bind_stream()
         new_state._copy_to_env(self._env._h, 0)
+        self._last = None  # the cached legal actions no longer describe the lane
 
     @property
     def mfg_distribution(self):

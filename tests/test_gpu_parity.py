@@ -370,3 +370,14 @@ def test_full_batch_sampled_lanes_match_oracle():
         ref = oracle.rollout(seed=seed, n=256, steps=steps, env_id_base=k, auto_reset=True, want_trajectory=False)
         np.testing.assert_array_equal(words[k:k + 256], ref["final_state"], err_msg=f"slice {k}")
     assert env.error_count() == 0
+
+
+@pytest.mark.parametrize("n", [1, 300, 1100])
+def test_query_info_state_equals_step_output(n):
+    """coup_query's InformationStateTensor (one thread per float4 up to 1024
+    lanes, the wave writer above) == the step kernel's, after 30 steps."""
+    env = BatchedCoupEnv(n, seed=77, auto_reset=True, obs=False, info_state=True)
+    for _ in range(30):
+        o = env.step()
+    q = env.query(obs=False, info_state=True)
+    np.testing.assert_array_equal(_np(q["info_state"]), _np(o["info_state"]))

@@ -60,7 +60,28 @@ def main(n=2000):
         r2, h2 = scratch_apply(env, rec, hist, 0)
         scratch_query(env, r2, h2)
     scratch_child = (time.perf_counter() - t0) / n
+    from open_spiel_coup_amd import rl_environment
+    renv = rl_environment.Environment("coup", seed=3)
+    ts = renv.reset()
+    rng = np.random.default_rng(0)
+    t0 = time.perf_counter()
+    for _ in range(n):
+        p = ts.observations["current_player"]
+        ts = renv.step([int(rng.choice(ts.observations["legal_actions"][p]))]) if p >= 0 else renv.reset()
+    rl_step = (time.perf_counter() - t0) / n
+    e1 = renv._env
+    t0 = time.perf_counter()
+    for _ in range(n):
+        {k: v.cpu().numpy()[0] for k, v in e1.query(obs=False, info_state=True).items()}
+    query_per_tensor = (time.perf_counter() - t0) / n
+    t0 = time.perf_counter()
+    for _ in range(n):
+        e1.query_host(obs=False, info_state=True)
+    query_one_copy = (time.perf_counter() - t0) / n
     print(json.dumps({"tool": "facade_latency", "ops": n,
+                      "rl_environment_step_us": round(1e6 * rl_step, 1),
+                      "query_info_per_tensor_copies_us": round(1e6 * query_per_tensor, 1),
+                      "query_info_one_copy_us": round(1e6 * query_one_copy, 1),
                       "pool_child_plus_legal_us": round(1e6 * pool_child, 1),
                       "pool_clone_us": round(1e6 * pool_clone, 1),
                       "pool_observation_tensor_us": round(1e6 * pool_obs, 1),
