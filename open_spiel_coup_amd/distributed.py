@@ -45,14 +45,15 @@ def init(backend="nccl", gpu=None):
     return dev
 
 
-def collate(t):
-    """All-gather a per-lane tensor ([B, ...]) from every rank; returns the
-    [W*B, ...] concatenation in rank (= global env id) order."""
+def collate(t, dim=0):
+    """All-gather a per-lane tensor from every rank; lanes are along `dim`
+    ([B, ...] by default, dim=1 for [T, B, ...] trajectories).  Returns the
+    concatenation along `dim` in rank (= global env id) order."""
     if not dist.is_initialized() or dist.get_world_size() == 1:
         return t
     parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
     dist.all_gather(parts, t.contiguous())
-    return torch.cat(parts, 0)
+    return torch.cat(parts, dim)
 
 
 def max_over_ranks(x, device):

@@ -167,6 +167,54 @@ class BatchedCoupEnv:
         self._bind_stream()
         return g
 
+    def trajectory_buffers(self, steps):
+        """Device buffers for `steps` recorded env steps: [T, B, ...] versions of
+        the step outputs this env writes (the learner-side replay data of
+        rl_environment time steps, rl_environment.py:282-322)."""
+        T, B, P, dev = int(steps), self.batch, self.num_players, self.device
+        buf = {"actions": torch.empty(T, B, dtype=torch.int8, device=dev),
+               "rewards": torch.empty(T, B, P, dtype=torch.int8, device=dev),
+               "step_type": torch.empty(T, B, dtype=torch.uint8, device=dev),
+               "legal_mask": torch.empty(T, B, dtype=torch.int32, device=dev),
+               "current_player": torch.empty(T, B, dtype=torch.int8, device=dev)}
+        if self.obs is not None:
+            buf["obs"] = torch.empty(T, B, P, self.obs_size, dtype=torch.float32, device=dev)
+        if self.info_state is not None:
+            buf["info_state"] = torch.empty(T, B, 2, INFO_STATE_SIZE, dtype=torch.float32, device=dev)
+        return buf
+
+    def _slice_outputs(self, buf, t):
+        return _native.StepOutputs(*[_addr(buf[k][t]) if k in buf else None for k in
+                                     ("actions", "rewards", "step_type", "legal_mask", "current_player", "obs",
+                                      "info_state")])
+
+    def collect_trajectory(self, steps, buf=None):
+        """`steps` uniform-policy env steps whose outputs land in slice t of
+        [T, B, ...] device buffers (trajectory_buffers); returns them."""
+        buf = buf if buf is not None else self.trajectory_buffers(steps)
+        self._bind_stream()
+        for t in range(int(steps)):
+            out = self._slice_outputs(buf, t)
+            _native.check(self.lib.coup_step(self._h, None, ctypes.byref(out)))
+        return buf
+
+    def capture_trajectory(self, steps, buf=None):
+        """collect_trajectory recorded as one HIP graph: `graph.replay()`
+        steps the env `steps` times and refills the same [T, B, ...] buffers.
+        Returns (graph, buffers).  The env must outlive the graph."""
+        buf = buf if buf is not None else self.trajectory_buffers(steps)
+        self._traj_outs = [self._slice_outputs(buf, t) for t in range(int(steps))]
+        g = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.graph(g, stream=side):
+            self._bind_stream()
+            for out in self._traj_outs:
+                _native.check(self.lib.coup_step(self._h, None, ctypes.byref(out)))
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        self._bind_stream()
+        return g, buf
+
     def rollout(self, steps, stats=None):
         """`steps` uniform-random steps per lane in one launch.  stats: optional
         dict with int32 [B] tensors 'episodes', 'return_sum', 'length_sum'

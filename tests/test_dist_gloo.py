@@ -39,10 +39,12 @@ def _worker(rank, world, port, out_dir):
     rewards = torch.from_numpy(ref["rewards"][-1].astype(np.int64))
     gathered = D.collate(final)
     gathered_rw = D.collate(rewards)
+    traj = D.collate(torch.from_numpy(ref["actions"].astype(np.int64)), dim=1)  # [T, B] trajectories
     t = D.max_over_ranks(float(rank + 1), dev)
     if rank == 0:
         np.save(os.path.join(out_dir, "gathered.npy"), gathered.numpy())
         np.save(os.path.join(out_dir, "gathered_rw.npy"), gathered_rw.numpy())
+        np.save(os.path.join(out_dir, "traj.npy"), traj.numpy())
         with open(os.path.join(out_dir, "tmax.txt"), "w") as f:
             f.write(str(t))
     dist.barrier()
@@ -56,6 +58,7 @@ def test_two_rank_sharding_equals_single_process(tmp_path):
     full = oracle.rollout(seed=SEED, n=world * PER_RANK, steps=STEPS)
     np.testing.assert_array_equal(np.load(tmp_path / "gathered.npy").astype(np.uint32), full["final_state"])
     np.testing.assert_array_equal(np.load(tmp_path / "gathered_rw.npy"), full["rewards"][-1].astype(np.int64))
+    np.testing.assert_array_equal(np.load(tmp_path / "traj.npy"), full["actions"].astype(np.int64))
     assert float(open(tmp_path / "tmax.txt").read()) == 2.0
 
 

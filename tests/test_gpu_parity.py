@@ -381,3 +381,26 @@ def test_query_info_state_equals_step_output(n):
         o = env.step()
     q = env.query(obs=False, info_state=True)
     np.testing.assert_array_equal(_np(q["info_state"]), _np(o["info_state"]))
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_trajectory_collection_matches_stepwise(graph):
+    """[T, B, ...] trajectory buffers (eager collect_trajectory, or one HIP
+    graph replay) == T single steps of an identical env, and the oracle."""
+    n, T, seed = 300, 12, 5
+    ref = oracle.rollout(seed=seed, n=n, steps=T, want_obs=True)
+    env = BatchedCoupEnv(n, seed=seed, obs=True)
+    if graph:
+        g, buf = env.capture_trajectory(T)
+        g.replay()
+        torch.cuda.synchronize()
+    else:
+        buf = env.collect_trajectory(T)
+    twin = BatchedCoupEnv(n, seed=seed, obs=True)
+    for t in range(T):
+        o = twin.step()
+        for k in ("actions", "rewards", "step_type", "legal_mask", "current_player", "obs"):
+            np.testing.assert_array_equal(_np(buf[k][t]), _np(o[k]), err_msg=f"{k} step {t}")
+        np.testing.assert_array_equal(_np(buf["actions"][t]), ref["actions"][t])
+        np.testing.assert_array_equal(_np(buf["obs"][t]), ref["obs"][t])
+    np.testing.assert_array_equal(_np(env.export_state()), _np(twin.export_state()))
