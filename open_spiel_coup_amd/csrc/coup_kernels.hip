@@ -1315,7 +1315,8 @@ struct coup_env {
   uint8_t* hist;  // [B][96] when COUP_FLAG_HISTORY
   uint32_t* err_count;
   hipStream_t stream;
-  uint8_t* slot_scratch;  // device staging of coup_slot_op results (lazy)
+  uint8_t* slot_scratch;  // coup_slot_op results: pinned host memory the kernels write directly (lazy)
+  uint8_t* slot_scratch_dev;  // its device address
 };
 
 namespace {
@@ -1399,7 +1400,7 @@ void release(coup_env* env) {
   (void)hipFree(env->state);
   (void)hipFree(env->hist);
   (void)hipFree(env->err_count);
-  (void)hipFree(env->slot_scratch);
+  if (env->slot_scratch) (void)hipHostFree(env->slot_scratch);
   delete env;
 }
 
@@ -1438,6 +1439,7 @@ int coup_create_ex(int64_t batch, uint64_t seed, uint32_t env_id_base, int flags
   env->hist = nullptr;
   env->err_count = nullptr;
   env->slot_scratch = nullptr;
+  env->slot_scratch_dev = nullptr;
   const size_t lanes = (size_t)(batch > 0 ? batch : 1);
   hipError_t e = hipMalloc(&env->state, lanes * sizeof(uint4) * (generic ? 2 : 1));
   if (e == hipSuccess) e = hipMalloc(&env->err_count, sizeof(uint32_t));
@@ -1681,8 +1683,14 @@ int coup_slot_op(coup_env* env, int64_t lane, const coup_env* src_env, int64_t s
   if (result && !host_out) return fail(COUP_E_INVALID, "coup_slot_op: host_out is null");
   const bool obs = result && (flags & COUP_SLOT_OBS), info = result && (flags & COUP_SLOT_INFO);
   const size_t obs_bytes = 2u * COUP_OBS_SIZE * sizeof(float), info_bytes = 2u * COUP_INFO_STATE_SIZE * sizeof(float);
-  if (result && !env->slot_scratch)
-    COUP_HIP_TRY(hipMalloc(&env->slot_scratch, sizeof(coup_slot_result) + obs_bytes + info_bytes));
+  if (result && !env->slot_scratch) {
+    // the kernels store the result straight into pinned host memory over
+    // PCIe: no copy kernel before the synchronisation
+    COUP_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&env->slot_scratch),
+                               sizeof(coup_slot_result) + obs_bytes + info_bytes,
+                               hipHostMallocMapped | hipHostMallocCoherent));
+    COUP_HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&env->slot_scratch_dev), env->slot_scratch, 0));
+  }
   coup::SlotArgs a;
   a.dst_state = env->state + lane;
   a.dst_hist = env->hist + lane * COUP_HISTORY_BYTES;
@@ -1691,7 +1699,7 @@ int coup_slot_op(coup_env* env, int64_t lane, const coup_env* src_env, int64_t s
   a.action = action;
   a.init = (flags & COUP_SLOT_INIT) ? 1 : 0;
   a.store = (src_env || a.init || action >= 0) ? 1 : 0;
-  uint8_t* sc = env->slot_scratch;
+  uint8_t* sc = env->slot_scratch_dev;
   a.out = result ? reinterpret_cast<coup_slot_result*>(sc) : nullptr;
   a.obs = obs ? reinterpret_cast<float*>(sc + sizeof(coup_slot_result)) : nullptr;
   hipStream_t s = env->stream;
@@ -1710,8 +1718,8 @@ int coup_slot_op(coup_env* env, int64_t lane, const coup_env* src_env, int64_t s
   }
   if (!result) return COUP_OK;
   const size_t n = sizeof(coup_slot_result) + (obs ? obs_bytes : 0) + (info ? info_bytes : 0);
-  COUP_HIP_TRY(hipMemcpyAsync(host_out, sc, n, hipMemcpyDeviceToHost, s));
   COUP_HIP_TRY(hipStreamSynchronize(s));
+  std::memcpy(host_out, env->slot_scratch, n);
   return COUP_OK;
 }
 
