@@ -92,7 +92,9 @@ class BatchedCoupEnv:
     # ------------------------------------------------------------ plumbing
     def _bind_stream(self):
         s = torch.cuda.current_stream(self.device).cuda_stream
-        _native.check(self.lib.coup_set_stream(self._h, ctypes.c_void_p(s)))
+        if s != getattr(self, "_bound_stream", None):
+            _native.check(self.lib.coup_set_stream(self._h, ctypes.c_void_p(s)))
+            self._bound_stream = s
 
     def close(self):
         if self._h:

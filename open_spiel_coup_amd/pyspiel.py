@@ -87,6 +87,13 @@ class GameType:
         self.parameter_specification = {}
 
 
+# coup_slot_result (include/coup_mi355x.h), 128 bytes
+_SLOT_RESULT = np.dtype([("record", "<u4", (4,)), ("history", "u1", (96,)), ("legal_mask", "<u4"),
+                         ("cur_player", "i1"), ("terminal", "u1"), ("ok", "u1"), ("reserved", "u1"),
+                         ("rewards", "i1", (2,)), ("returns", "i1", (2,)), ("pad", "u1", (4,))])
+assert _SLOT_RESULT.itemsize == 128
+
+
 class _Pool:
     """Device-resident lane pool: every live CoupState owns one lane of a
     2-player history env (segments of SEG lanes, grown on demand).  Each
@@ -104,6 +111,8 @@ class _Pool:
         nbytes = _native.SLOT_RESULT_BYTES + 2 * OBS_SIZE * 4 + 2 * INFO_STATE_SIZE * 4
         self.host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
         self.buf = self.host.numpy()
+        self.res = self.buf[:_native.SLOT_RESULT_BYTES].view(_SLOT_RESULT)[0]
+        self.host_ptr = ctypes.c_void_p(self.host.data_ptr())
 
     def alloc(self):
         if not self.free:
@@ -127,20 +136,14 @@ class _Pool:
         env._bind_stream()
         src_h, src_lane = src if src is not None else (None, 0)
         _native.check(self.lib.coup_slot_op(env._h, slot[1], src_h, src_lane, int(action), flags,
-                                            ctypes.c_void_p(self.host.data_ptr()) if result else None))
+                                            self.host_ptr if result else None))
         if not result:
             return None
+        r = self.res.copy()  # one copy of the 128-byte coup_slot_result
+        q = {"record": r["record"], "history": r["history"], "legal_mask": int(r["legal_mask"]),
+             "current_player": int(r["cur_player"]), "terminal": bool(r["terminal"]), "ok": bool(r["ok"]),
+             "rewards": r["rewards"], "returns": r["returns"]}
         b = self.buf
-        q = {
-            "record": b[0:16].view(np.uint32).copy(),
-            "history": b[16:112].copy(),
-            "legal_mask": int(b[112:116].view(np.uint32)[0]),
-            "current_player": int(b[116:117].view(np.int8)[0]),
-            "terminal": bool(b[117]),
-            "ok": bool(b[118]),
-            "rewards": b[120:122].view(np.int8).copy(),
-            "returns": b[122:124].view(np.int8).copy(),
-        }
         off = _native.SLOT_RESULT_BYTES
         if obs:
             q["obs"] = b[off:off + 2 * OBS_SIZE * 4].view(np.float32).reshape(2, OBS_SIZE).copy()
@@ -171,6 +174,11 @@ class CoupGame:
             raise SpielError("coup takes no parameters (coup.cc:51-52)")
         self._type = GameType()
         self._device = device
+        self._pool = None  # the lane pool of `device`, bound on first use
+
+    def _bind_pool(self):
+        self._pool = _pool(self._device)
+        return self._pool
 
     # --- metadata (coup.h:203-220, spiel.h:888-890)
     def get_type(self):
@@ -256,7 +264,7 @@ class CoupState:
 
     def __init__(self, game, _src=None, _history=None, _q=None):
         self._game = game
-        self._pool = _pool(game._device)
+        self._pool = game._pool if game._pool is not None else game._bind_pool()
         self._slot = self._pool.alloc()
         if _src is None:
             self._q = self._pool.op(self._slot, init=True)
