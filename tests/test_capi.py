@@ -90,3 +90,26 @@ def test_packed_roundtrip_of_initial_state():
     assert r["last_action"] == [-1, -1]
     assert r["queue"] == [0, 1, 0, 1]
     assert r["turn_begin"] == 1 and r["move_number"] == 0
+
+
+def test_slot_result_layout_matches_header(tmp_path):
+    """The Python view of coup_slot_result (pyspiel._SLOT_RESULT) has the C
+    struct's field offsets and size (gcc offsetof on include/coup_mi355x.h)."""
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    from open_spiel_coup_amd import pyspiel
+    src = tmp_path / "layout.c"
+    fields = ["record", "history", "legal_mask", "cur_player", "terminal", "ok", "reserved", "rewards", "returns",
+              "pad"]
+    src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "coup_mi355x.h"\nint main(void) {\n'
+                   + "".join(f'  printf("{f} %zu\\n", offsetof(coup_slot_result, {f}));\n' for f in fields)
+                   + '  printf("size %zu\\n", sizeof(coup_slot_result));\n  return 0;\n}\n')
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
+    got = dict(line.split() for line in subprocess.check_output([str(exe)], text=True).splitlines())
+    dt = pyspiel._SLOT_RESULT
+    for f in fields:
+        assert int(got[f]) == dt.fields[f][1], f
+    assert int(got["size"]) == dt.itemsize == _native.SLOT_RESULT_BYTES
