@@ -23,14 +23,22 @@ steps, --settle (default 256) untimed steps run through the fused rollout so
 the lanes are spread over game phases as in a long run (a freshly reset batch
 is in lock-step, and its first steps diverge less).  Multi-GPU: one
 process per GPU (torchrun), global env ids sharded by rank, no collective
-inside the step loop; the timed region ends with one RCCL all-gather of
-the ranks' final per-lane rewards/step types (trajectory collation).
+inside the step loop; every step accumulates, per lane, the episodes that
+end and player 0's Returns() of each (coup.cc:1016-1032), and the timed
+region ends with one RCCL all-gather of those per-lane episode counts and
+return sums (the collation of SURVEY.md 8(e)).
 
 roofline: algorithmic bytes per launch over the step
 kernel's average duration from HIP events on the launch stream; traffic:
 HBM bytes per launch from the rocprofv3 PMC passes recorded in profiles/
-(null if absent).  cpu_baseline: the C oracle (a scalar port of the
-reference rules) on one host core, same per-lane workload.
+(null if absent).  For the 2-player step configs the same process then
+times coup_measure_step_traffic -- the step's loads and stores in the same
+order with no rules -- over the same buffers: roofline.store_ceiling_ms is
+that ceiling on this box, frac_of_store_ceiling = ceiling / kernel time.
+`box` names the GPU box (boxes differ in HBM store rate).
+cpu_baseline: the C oracle (a scalar port of the reference rules, ~14x
+faster than the reference's own C++ on the survey host) on one
+host core, same per-lane workload.
 """
 import argparse
 import json
@@ -162,6 +170,61 @@ def cpu_baseline(target_s, with_obs, with_info, players=2):
     return out
 
 
+def _box_identity(dev):
+    """Which GPU box ran this line (tools/boxinfo.sh fields, best effort)."""
+    import socket
+    import subprocess
+    import torch
+    p = torch.cuda.get_device_properties(dev)
+    box = {"host": socket.gethostname(), "gpu": p.name, "arch": getattr(p, "gcnArchName", None),
+           "cus": p.multi_processor_count, "uuid": str(getattr(p, "uuid", "")) or None}
+    try:
+        out = subprocess.run(["rocm-smi", "--showserial", "--showmemorypartition", "--showcomputepartition",
+                              "--showclocks"], capture_output=True, text=True, timeout=20).stdout
+        for line in out.splitlines():
+            low = line.lower()
+            for key, tag in (("serial", "serial number"), ("mem_partition", "memory partition"),
+                             ("compute_partition", "compute partition"), ("mclk", "mclk"), ("fclk", "fclk"),
+                             ("sclk", "sclk")):
+                if tag in low and key not in box and ":" in line:
+                    box[key] = line.split(":", 2)[-1].strip()
+    except Exception as e:  # noqa: BLE001  (identity is best effort)
+        box["rocm_smi"] = f"unavailable: {type(e).__name__}"
+    return box
+
+
+def _time_traffic_ceiling(env, steps, stream):
+    """Average duration of coup_measure_step_traffic over the env's own
+    buffers (K launches replayed from one HIP graph, like the step)."""
+    import ctypes
+    import torch
+    from open_spiel_coup_amd import _native
+    rec = env.export_state()
+    out = _native.StepOutputs(*[t.data_ptr() if t is not None else None for t in
+                                (env.actions, env.rewards, env.step_type, env.legal_mask, env.cur_player,
+                                 env.obs)])
+
+    def launch(s):
+        _native.check(env.lib.coup_measure_step_traffic(env.batch, ctypes.c_void_p(rec.data_ptr()),
+                                                         ctypes.byref(out), ctypes.c_void_p(s)))
+
+    for _ in range(3):
+        launch(stream.cuda_stream)
+    g = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream(env.device)
+    side.wait_stream(stream)
+    with torch.cuda.graph(g, stream=side):
+        for _ in range(steps):
+            launch(side.cuda_stream)
+    stream.wait_stream(side)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(stream)
+    g.replay()
+    b.record(stream)
+    b.synchronize()
+    return a.elapsed_time(b) / steps
+
+
 def main():
     args = parse()
     import torch
@@ -177,7 +240,11 @@ def main():
     B0, with_obs, with_info, fused, bytes_per_lane, workload, players = CONFIGS[cfg]
     B = args.batch or B0
     env = BatchedCoupEnv(B, seed=args.seed, env_id_base=D.env_id_base(rank, B), auto_reset=True, obs=with_obs,
-                         info_state=with_info, device=dev, num_players=players)
+                         info_state=with_info, device=dev, num_players=players, episode_stats=not fused)
+    # per-lane finished-episode counts and player-0 return sums of the timed
+    # steps: the step kernels accumulate them (coup_step_outputs.episodes /
+    # return_sum), the fused rollout through coup_rollout_stats
+    stats = env.new_stats() if fused else None
 
     def barrier():
         if world > 1:
@@ -201,10 +268,20 @@ def main():
             env.step()
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(args.steps)]
+    def episode_tensors():
+        if fused:
+            return stats["episodes"], stats["return_sum"]
+        return env.episode_stats()
+
     if world > 1:
         # first all-gather outside the timed region (RCCL sets up its
         # all-gather channels lazily on first use)
-        D.collate(torch.cat([env.rewards.view(torch.uint8), env.step_type.view(-1, 1)], 1))
+        D.collate(torch.stack(episode_tensors(), 1))
+    if fused:
+        for t in stats.values():
+            t.zero_()
+    else:
+        env.clear_episode_stats()
     barrier()
     t0 = time.perf_counter()
     if graph is not None:
@@ -213,23 +290,28 @@ def main():
         ev[0][1].record(stream)
     elif fused:
         ev[0][0].record(stream)
-        env.rollout(args.steps)
+        env.rollout(args.steps, stats)
         ev[0][1].record(stream)
     else:
         for k in range(args.steps):
             ev[k][0].record(stream)
             env.step()
             ev[k][1].record(stream)
-    if world > 1:
-        # collate the final step's per-lane outcome over xGMI (RCCL all-gather)
-        D.collate(torch.cat([env.rewards.view(torch.uint8), env.step_type.view(-1, 1)], 1))
+    # collate every lane's finished-episode count and player-0 return sum over
+    # xGMI (RCCL all-gather, [world * B, 2] int32; identity at one rank)
+    gathered = D.collate(torch.stack(episode_tensors(), 1))
     barrier()
     elapsed = time.perf_counter() - t0
+    ep_total = int(gathered[:, 0].sum())
+    ret_total = int(gathered[:, 1].sum())
 
     # per env step; with a graph, the replay's duration / K (launch gaps included)
     kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
     elapsed = D.max_over_ranks(elapsed, dev)
     errors = env.error_count()
+    ceiling_ms = None
+    if players == 2 and not fused and not with_info:
+        ceiling_ms = _time_traffic_ceiling(env, args.steps, stream)
 
     if rank == 0:
         bytes_per_launch = bytes_per_lane * B * (args.steps if fused else 1)
@@ -279,8 +361,14 @@ def main():
                                                                    " [gloo rehearsal, ranks share GPUs]")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kernel,
-                         "kernel_ms": launch_ms, "bytes_per_launch": bytes_per_launch},
+                         "kernel_ms": launch_ms, "bytes_per_launch": bytes_per_launch,
+                         "store_ceiling_ms": ceiling_ms,
+                         "frac_of_store_ceiling": (ceiling_ms / launch_ms) if ceiling_ms else None},
+            "episodes": {"finished": ep_total, "mean_return_p0": ret_total / max(ep_total, 1),
+                         "collective": "all_gather [world*B, 2] int32 (episodes, return sum per lane)"
+                         if world > 1 else None},
             "lane_errors": errors,
+            "box": _box_identity(dev),
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, with_obs, with_info, players)

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define COUP_ABI_VERSION 4
+#define COUP_ABI_VERSION 5
 
 #define COUP_NUM_PLAYERS 2          /* coup.h:42 */
 #define COUP_MAX_PLAYERS 6          /* N-player extension */
@@ -81,6 +81,12 @@ typedef struct {
   int8_t* cur_player;   /* [B]  CurrentPlayer() of the (post-reset) state */
   float* obs;           /* [B][2][98] ObservationTensor(p) for p = 0, 1 */
   float* info_state;    /* [B][2][2492] InformationStateTensor(p) (needs COUP_FLAG_HISTORY) */
+  /* Per-episode accumulators, updated only for lanes whose episode ends in
+   * this step (step type LAST): episodes[i] += 1 and return_sum[i] +=
+   * Returns()[0] of the finished game (coup.cc:1016-1032), read before an
+   * auto-reset.  The multi-GPU bench all-gathers them. */
+  int32_t* episodes;    /* [B] */
+  int32_t* return_sum;  /* [B] */
 } coup_step_outputs;
 
 /* Per-lane query of the current state (State accessors); all optional. */
@@ -129,6 +135,8 @@ const char* coup_last_error(void);
 /* Create an env of `batch` lanes on the current HIP device.  Lane i uses the
  * global env id env_id_base + i for its random streams, so a batch split over
  * ranks by id range reproduces the single-GPU trajectories bit for bit.
+ * Ids are 32-bit: env_id_base + batch must not exceed 2^32 (COUP_E_INVALID
+ * otherwise, instead of lanes silently sharing streams).
  * flags: COUP_FLAG_AUTO_RESET -- SyncVectorEnv(reset_if_done=True) semantics
  * (a finished lane restarts inside the same step); without it rl_environment
  * semantics (LAST, then the next step resets).  COUP_FLAG_HISTORY -- keep a
@@ -208,6 +216,20 @@ int coup_import_history(coup_env* env, const uint8_t* src);
 /* Number of lanes that rejected an action since the last call (resets the
  * counter).  Synchronises the env's stream. */
 int coup_error_count(coup_env* env, int64_t* out);
+
+/* --- measurement ------------------------------------------------------- */
+
+/* The memory traffic of one observation-writing 2-player step over `batch`
+ * lanes with no rules in between: every lane's 16-byte record is loaded and
+ * stored back unchanged, and the action, rewards, step type, legal mask,
+ * current player and [B][2][98] float observation buffers are written in the
+ * step kernel's order (same grid, same XCD-aware block -> lane-group
+ * mapping, same wave-cooperative sc1 buffer stores).  Timing it beside
+ * coup_step in one process gives that step's store-pattern ceiling on the
+ * box at hand (bench.py: roofline.store_ceiling_ms).  `records` is a device
+ * buffer of batch x 16 bytes; the output pointers are as in
+ * coup_step_outputs (any may be NULL).  Asynchronous on `hip_stream`. */
+int coup_measure_step_traffic(int64_t batch, uint32_t* records, const coup_step_outputs* out, void* hip_stream);
 
 #ifdef __cplusplus
 }

@@ -11,10 +11,14 @@
  *                            use (spiel.h:210-1035, coup.h:111-231), one
  *                            game per object.
  *
- * A CoupState keeps its 16-byte lane record and 96 history bytes on the host.
- * Every rules operation (ApplyAction, LegalActions, tensors, ...) uploads
- * them to a one-lane scratch env and runs the HIP kernels; there is no CPU
- * rules engine.  Strings are formatted on the host from the record and the
+ * Every live CoupState owns one lane of a device-resident lane pool
+ * (detail::Pool: 2-player history envs of 4096 lanes, grown on demand, slots
+ * reused).  Each rules operation (ApplyAction, the tensors, ...) is one
+ * coup_slot_op launch on that lane, and the 128-byte coup_slot_result it
+ * returns (record, history, legal mask, player, rewards, returns) answers
+ * the accessors until the next op; a Clone is a device-side lane copy.
+ * There is no CPU rules engine.  The pool is guarded by a mutex, so States
+ * may be used from several threads.  Strings are formatted on the host from the record and the
  * history (coup.cc:60-135, 290-373, 945-987), as open_spiel_coup_amd/strings.py
  * does.  Errors throw coup_amd::SpielError (SpielFatalError,
  * spiel_utils.cc:132-136; pyspiel.SpielError).
@@ -31,6 +35,7 @@
 #include <cstdint>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -215,6 +220,7 @@ class Pool {
   };
 
   Slot Alloc() {
+    std::lock_guard<std::mutex> g(mu_);
     if (free_.empty()) {
       segs_.emplace_back(new BatchedEnv(kSeg, 0, 0, COUP_FLAG_HISTORY));
       const int k = (int)segs_.size() - 1;
@@ -225,10 +231,13 @@ class Pool {
     return s;
   }
   void Release(const Slot& s) {
+    std::lock_guard<std::mutex> g(mu_);
     if (s.seg >= 0) free_.push_back(s);
   }
   // host_out: coup_slot_result followed by the tensors the flags ask for
   void Op(const Slot& s, const Slot* src, int action, int flags, void* host_out) {
+    // one op at a time: each segment answers through one pinned scratch buffer
+    std::lock_guard<std::mutex> g(mu_);
     coup_env* src_env = src ? segs_[src->seg]->get() : nullptr;
     Check(coup_slot_op(segs_[s.seg]->get(), s.lane, src_env, src ? src->lane : 0, action, flags, host_out),
           "coup_slot_op");
@@ -237,6 +246,7 @@ class Pool {
  private:
   std::vector<std::unique_ptr<BatchedEnv>> segs_;
   std::vector<Slot> free_;
+  std::mutex mu_;
 };
 
 inline Pool& ThePool() {

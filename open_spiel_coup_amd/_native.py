@@ -11,7 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # COUP_LIB_PATH: load another build of the same library (A/B timing of two
 # builds, tools/ab_builds.sh); there is still no fallback
 LIB_PATH = os.environ.get("COUP_LIB_PATH") or os.path.join(HERE, "libcoup_mi355x.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 FLAG_AUTO_RESET, FLAG_HISTORY, FLAG_GENERIC = 1, 2, 4
 MAX_PLAYERS = 6
 HISTORY_BYTES = 96
@@ -24,7 +24,7 @@ SYMBOLS = (
     "coup_set_stream", "coup_batch", "coup_num_players", "coup_state_bytes", "coup_reset", "coup_step", "coup_rollout",
     "coup_new_initial_state", "coup_apply_action", "coup_query",
     "coup_export_state", "coup_import_state", "coup_export_history",
-    "coup_import_history", "coup_error_count", "coup_slot_op",
+    "coup_import_history", "coup_error_count", "coup_slot_op", "coup_measure_step_traffic",
 )
 
 # coup_slot_op flags and result layout (coup_slot_result, 128 bytes)
@@ -36,7 +36,8 @@ class StepOutputs(ctypes.Structure):
     _fields_ = [("actions", ctypes.c_void_p), ("rewards", ctypes.c_void_p),
                 ("step_type", ctypes.c_void_p), ("legal_mask", ctypes.c_void_p),
                 ("cur_player", ctypes.c_void_p), ("obs", ctypes.c_void_p),
-                ("info_state", ctypes.c_void_p)]
+                ("info_state", ctypes.c_void_p), ("episodes", ctypes.c_void_p),
+                ("return_sum", ctypes.c_void_p)]
 
 
 class QueryOutputs(ctypes.Structure):
@@ -91,6 +92,7 @@ def load():
         "coup_import_history": ([vp, vp], i32),
         "coup_error_count": ([vp, ctypes.POINTER(i64)], i32),
         "coup_slot_op": ([vp, i64, vp, i64, i32, i32, vp], i32),
+        "coup_measure_step_traffic": ([i64, vp, ctypes.POINTER(StepOutputs), vp], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

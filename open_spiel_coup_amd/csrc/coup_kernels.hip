@@ -513,6 +513,8 @@ struct StepArgs {
   float* obs;
   uint8_t* hist;   // [B][96] history bytes (INFO != kInfoNone)
   float* info;     // [B][2][2492] (INFO == kInfoWrite)
+  int32_t* ep_count;   // [B] per-episode accumulators (coup_step_outputs.episodes)
+  int32_t* ep_return;  // [B] (coup_step_outputs.return_sum)
   uint32_t* err_count;
   int xcd_remap;   // block -> lane group mapping (xcd_group)
 #ifdef COUP_WAVE_TRACE
@@ -576,11 +578,12 @@ constexpr bool is_wave_bits(int m) { return m == kObsWaveBits || m == kObsWaveBi
 constexpr int wave_bits_policy(int m) { return m == kObsWaveBitsPlain ? 0 : (m == kObsWaveBitsSc1 ? 2 : 1); }
 
 // The per-lane part of one env step: returns the decision applied (-1 if
-// none), the step type and player 0's reward; L is updated in place and
-// every applied action is recorded in `hist`.
+// none), the step type, player 0's reward and, at LAST, player 0's return of
+// the finished game; L is updated in place and every applied action is
+// recorded in `hist`.
 template <bool UNIFORM, class H>
 __device__ __forceinline__ void step_lane(const StepArgs& a, int64_t i, Lane& L, int& act, uint32_t& st,
-                                          int32_t& rew, H& hist) {
+                                          int32_t& rew, int32_t& ret, H& hist) {
   Rng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, i), 0u, make_uint4(0, 0, 0, 0)};
   act = -1;
   rew = 0;
@@ -616,6 +619,7 @@ __device__ __forceinline__ void step_lane(const StepArgs& a, int64_t i, Lane& L,
   rew = L.r0;
   if (is_terminal(L)) {
     st = COUP_STEP_LAST;
+    ret = return0(L);
     if (a.auto_reset) {
       // SyncVectorEnv.step(reset_if_done=True) (vector_env.py:62-65)
       L = new_episode(L.episode + 1u, rng, hist);
@@ -731,16 +735,20 @@ __device__ __forceinline__ void step_group_compute(const StepArgs& a, int64_t gr
 #endif
     int act;
     uint32_t st;
-    int32_t rew;
+    int32_t rew, ret = 0;
     if (INFO != kInfoNone) {
       RegHistory rec;
-      step_lane<UNIFORM>(a, i, L, act, st, rew, rec);
+      step_lane<UNIFORM>(a, i, L, act, st, rew, ret, rec);
       rec.flush(lds.hist + threadIdx.x * kHist);
     } else {
       NoHistory none;
-      step_lane<UNIFORM>(a, i, L, act, st, rew, none);
+      step_lane<UNIFORM>(a, i, L, act, st, rew, ret, none);
     }
     a.state[i] = pack(L);
+    if (st == COUP_STEP_LAST && a.ep_count) {
+      a.ep_count[i] += 1;
+      a.ep_return[i] += ret;
+    }
     if (a.actions) a.actions[i] = (int8_t)act;
     if (a.rewards) {
       a.rewards[2 * i] = (int8_t)rew;
@@ -777,6 +785,44 @@ __device__ __forceinline__ void step_group_compute(const StepArgs& a, int64_t gr
     write_obs_block_bits<T, OBS == kObsBlockBitsNT>(a.obs + block0 * (2 * kObsSize), lds.bits, n_valid);
   } else if (kDesc && wave_valid > 0) {
     write_obs_wave<OBS == kObsWaveNT>(a.obs + wave0 * (2 * kObsSize), obs_key(L), wave_valid, lds.desc);
+  }
+}
+
+// coup_measure_step_traffic: the bytes of k_step<*, kObsWaveBitsSc1, 256,
+// kInfoNone> with no rules in between -- the record loaded and stored back,
+// the small outputs stored, the lane's 8 LDS words taken from its record
+// instead of built by obs_bits_to_lds, then the same wave-cooperative sc1
+// store loop over the same XCD-remapped lane groups.  Its duration is the
+// step's store-pattern ceiling on the box that runs it.
+__global__ __launch_bounds__(kThreads, 8) void k_measure_traffic(StepArgs a) {
+  __shared__ uint32_t bits[kThreads * 8];
+  const uint32_t grp = a.xcd_remap ? xcd_group(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int64_t i = (int64_t)grp * kThreads + threadIdx.x;
+  const uint4 rec = i < a.n ? a.state[i] : make_uint4(0u, 0u, 0u, 0u);
+  if (i < a.n) {
+    a.state[i] = rec;
+    if (a.actions) a.actions[i] = (int8_t)(rec.x & 15u);
+    if (a.rewards) {
+      a.rewards[2 * i] = (int8_t)(rec.y & 1u);
+      a.rewards[2 * i + 1] = (int8_t)(rec.y & 2u);
+    }
+    if (a.step_type) a.step_type[i] = (uint8_t)(rec.z & 3u);
+    if (a.legal) a.legal[i] = rec.w;
+    if (a.cur_player) a.cur_player[i] = (int8_t)(rec.x >> 28);
+  }
+  reinterpret_cast<uint4*>(bits + threadIdx.x * 8u)[0] = rec;
+  reinterpret_cast<uint4*>(bits + threadIdx.x * 8u)[1] = make_uint4(rec.w, rec.z, rec.y, rec.x & 0x0F0Fu);
+  wave_sync();
+  if (a.obs) {
+    const uint32_t wl = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x & ~63u));
+    const int64_t wave0 = (int64_t)grp * kThreads + wl;
+    const int64_t wleft = a.n - wave0;
+    const uint32_t wave_valid = wleft >= 64 ? 64u : (wleft > 0 ? (uint32_t)wleft : 0u);
+    float* wave_obs = a.obs + wave0 * (2 * kObsSize);
+    if (wave_valid == 64u)
+      write_obs_wave_bits<2, true>(wave_obs, bits + wl * 8u, 64u);
+    else if (wave_valid > 0u)
+      write_obs_wave_bits<2, false>(wave_obs, bits + wl * 8u, wave_valid);
   }
 }
 
@@ -842,7 +888,7 @@ template <bool UNIFORM>
 __global__ __launch_bounds__(kThreads, 8) void k_step_sorted(StepArgs a) {
   __shared__ uint4 s_rec[kThreads];
   __shared__ uint32_t s_meta[kThreads];   // slot -> owner thread | key << 8 | st << 13
-  __shared__ uint32_t s_out[kThreads];    // slot -> act + 1 | st << 5 | (rew + 2) << 7 | cp << 24
+  __shared__ uint32_t s_out[kThreads];    // slot -> act + 1 | st << 5 | (rew + 2) << 7 | (ret + 2) << 10 | cp << 24
   __shared__ uint32_t s_legal[kThreads];  // slot -> post-step legal mask
   __shared__ uint32_t s_reset[kThreads];  // slots whose lane auto-resets
   __shared__ uint32_t s_bin[32];
@@ -902,6 +948,7 @@ __global__ __launch_bounds__(kThreads, 8) void k_step_sorted(StepArgs a) {
         if (L.err && !err_before) count_error(a.err_count);
         const bool term = is_terminal(L);
         out = (k + 1u) | ((term ? COUP_STEP_LAST : COUP_STEP_MID) << 5) | ((uint32_t)(L.r0 + 2) << 7);
+        if (a.ep_count && term) out |= (uint32_t)(return0(L) + 2) << 10;
         pending = term && a.auto_reset != 0;
         if (pending) s_reset[atomicAdd(&s_nreset, 1u)] = t;
         s_rec[t] = pack(L);
@@ -942,6 +989,10 @@ __global__ __launch_bounds__(kThreads, 8) void k_step_sorted(StepArgs a) {
   if (a.step_type) a.step_type[i] = (uint8_t)((o >> 5) & 3u);
   if (a.legal) a.legal[i] = s_legal[pos];
   if (a.cur_player) a.cur_player[i] = (int8_t)(o >> 24);
+  if (((o >> 5) & 3u) == COUP_STEP_LAST && a.ep_count) {
+    a.ep_count[i] += 1;
+    a.ep_return[i] += (int32_t)((o >> 10) & 7u) - 2;
+  }
 }
 
 // The decision key of a lane at a decision node: the uniform policy's draw,
@@ -1420,6 +1471,8 @@ int coup_create_ex(int64_t batch, uint64_t seed, uint32_t env_id_base, int flags
   if (!out) return fail(COUP_E_INVALID, "coup_create: out is null");
   *out = nullptr;
   if (batch < 0 || batch > (int64_t(1) << 32)) return fail(COUP_E_INVALID, "coup_create: batch out of range");
+  if ((int64_t)env_id_base + batch > (int64_t(1) << 32))
+    return fail(COUP_E_INVALID, "coup_create: env_id_base + batch exceeds 2^32 (lanes would share random streams)");
   if (flags & ~(COUP_FLAG_AUTO_RESET | COUP_FLAG_HISTORY | COUP_FLAG_GENERIC))
     return fail(COUP_E_INVALID, "coup_create: unknown flags");
   if (num_players < 2 || num_players > COUP_MAX_PLAYERS)
@@ -1538,7 +1591,11 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
     a.cur_player = out->cur_player;
     a.obs = out->obs;
     a.info = out->info_state;
+    a.ep_count = out->episodes;
+    a.ep_return = out->return_sum;
   }
+  if ((a.ep_count == nullptr) != (a.ep_return == nullptr))
+    return fail(COUP_E_INVALID, "coup_step: episodes and return_sum go together");
   if (a.info && !a.hist)
     return fail(COUP_E_INVALID, "coup_step: info_state needs an env created with COUP_FLAG_HISTORY");
   const bool uniform = actions == nullptr;
@@ -1767,6 +1824,28 @@ int coup_error_count(coup_env* env, int64_t* out) {
   COUP_HIP_TRY(hipMemsetAsync(env->err_count, 0, sizeof(uint32_t), env->stream));
   COUP_HIP_TRY(hipStreamSynchronize(env->stream));
   *out = (int64_t)h;
+  return COUP_OK;
+}
+
+int coup_measure_step_traffic(int64_t batch, uint32_t* records, const coup_step_outputs* out, void* hip_stream) {
+  if (batch < 0 || batch > (int64_t(1) << 32)) return fail(COUP_E_INVALID, "coup_measure_step_traffic: bad batch");
+  if (!records) return fail(COUP_E_INVALID, "coup_measure_step_traffic: records is null");
+  if (batch == 0) return COUP_OK;
+  coup::StepArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.state = reinterpret_cast<uint4*>(records);
+  a.n = batch;
+  a.xcd_remap = xcd_remap();
+  if (out) {
+    a.actions = out->actions;
+    a.rewards = out->rewards;
+    a.step_type = out->step_type;
+    a.legal = out->legal_mask;
+    a.cur_player = out->cur_player;
+    a.obs = out->obs;
+  }
+  coup::k_measure_traffic<<<grid_for(batch), coup::kThreads, 0, (hipStream_t)hip_stream>>>(a);
+  COUP_HIP_TRY(hipGetLastError());
   return COUP_OK;
 }
 

@@ -673,10 +673,12 @@ __device__ __forceinline__ uint32_t step_lane_pre(NLane<N>& L, NRng& rng, uint32
   return x;
 }
 
-// Second half: apply decision x, resolve the deals, auto-reset.
+// Second half: apply decision x, resolve the deals, auto-reset.  ret0:
+// player 0's return of a game that ends here (read before the reset).
 template <int N>
 __device__ __forceinline__ void step_lane_post(NLane<N>& L, NRng& rng, uint32_t x, bool auto_reset, int& act,
-                                               uint32_t& st, uint32_t& rl, uint32_t& rc, bool& error) {
+                                               uint32_t& st, uint32_t& rl, uint32_t& rc, int32_t& ret0,
+                                               bool& error) {
   const uint32_t err_before = L.err;
   apply_decision(L, x);
   L.move += 1u;
@@ -687,6 +689,7 @@ __device__ __forceinline__ void step_lane_post(NLane<N>& L, NRng& rng, uint32_t 
   rc = L.rcount;
   if (is_terminal(L)) {
     st = 2;  // LAST
+    ret0 = returns(L, 0u);
     if (auto_reset) L = new_episode<N>(L.episode + 1u, rng);
   }
 }
@@ -696,15 +699,17 @@ __device__ __forceinline__ void step_lane_post(NLane<N>& L, NRng& rng, uint32_t 
 // 2-player engine's step_lane with the N-player rules.  x is the decision
 // to apply (the uniform policy's draw when UNIFORM).  Outputs: the applied
 // action (-1 if none), the step type, Rewards() as (loser, count), and
-// whether the lane rejected the action or hit a rules error.
+// whether the lane rejected the action or hit a rules error; at LAST, ret0
+// is player 0's return of the finished game.
 template <int N, bool UNIFORM>
 __device__ __forceinline__ void step_lane(NLane<N>& L, NRng& rng, uint32_t x, bool auto_reset, int& act,
-                                          uint32_t& st, uint32_t& rl, uint32_t& rc, bool& error) {
+                                          uint32_t& st, uint32_t& rl, uint32_t& rc, int32_t& ret0, bool& error) {
   act = -1;
   rl = 0;
   rc = 0;
+  ret0 = 0;
   if (step_lane_pre<N, UNIFORM>(L, rng, x, st, error) != kStepDone)
-    step_lane_post<N>(L, rng, x, auto_reset, act, st, rl, rc, error);
+    step_lane_post<N>(L, rng, x, auto_reset, act, st, rl, rc, ret0, error);
 }
 
 }  // namespace np

@@ -56,8 +56,18 @@ struct StepArgs {
   uint8_t* step_type;
   uint32_t* legal;
   int8_t* cur_player;
+  int32_t* ep_count;   // [B] per-episode accumulators (coup_step_outputs.episodes)
+  int32_t* ep_return;  // [B] (coup_step_outputs.return_sum)
   uint32_t* err_count;
 };
+
+// Episode accumulators of a lane whose game ended in this step (LAST).
+__device__ __forceinline__ void store_episode(const StepArgs& a, int64_t i, uint32_t st, int32_t ret0) {
+  if (st == 2u && a.ep_count) {
+    a.ep_count[i] += 1;
+    a.ep_return[i] += ret0;
+  }
+}
 
 // The per-lane outputs of a step: applied action, Rewards() as (loser,
 // count), step type, post-step legal mask and current player.
@@ -96,10 +106,12 @@ __global__ __launch_bounds__(kThreads) void k_step(StepArgs a) {
   NRng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, i), 0u, make_uint4(0, 0, 0, 0)};
   int act;
   uint32_t st, rl, rc;
+  int32_t ret0;
   bool error;
   step_lane<N, UNIFORM>(L, rng, UNIFORM ? 0u : (uint32_t)(uint8_t)a.actions_in[i], a.auto_reset != 0, act, st, rl,
-                        rc, error);
+                        rc, ret0, error);
   if (error) count_error(a.err_count);
+  store_episode(a, i, st, ret0);
   uint4 wa, wb;
   pack(L, wa, wb);
   a.sa[i] = wa;
@@ -133,7 +145,8 @@ template <int N, bool UNIFORM, bool AHEAD>
 __global__ __launch_bounds__(kThreads) void k_step_sorted(StepArgs a) {
   __shared__ uint4 s_a[kThreads], s_b[kThreads];
   __shared__ uint32_t s_meta[kThreads];   // slot -> owner thread | key << 8 | st << 13 | error << 15
-  __shared__ uint32_t s_out[kThreads];    // slot -> act + 1 | st << 5 | rl << 7 | rc << 10 | error << 13 | cp << 24
+  __shared__ uint32_t s_out[kThreads];    // slot -> act + 1 | st << 5 | rl << 7 | rc << 10 | error << 13 |
+                                          //         (ret0 + 16) << 14 | cp << 24
   __shared__ uint32_t s_legal[kThreads];  // slot -> post-step legal mask
   __shared__ uint32_t s_reset[kThreads];  // slots whose lane auto-resets
   __shared__ uint32_t s_bin[32];
@@ -204,6 +217,7 @@ __global__ __launch_bounds__(kThreads) void k_step_sorted(StepArgs a) {
         if (err) count_error(a.err_count);
         const bool term = is_terminal(L);
         out = (k + 1u) | ((term ? 2u : 1u) << 5) | (L.rloser << 7) | (L.rcount << 10) | ((uint32_t)err << 13);
+        if (a.ep_count && term) out |= (uint32_t)(returns(L, 0u) + 16) << 14;
         pending = term && a.auto_reset != 0;
         if (pending) s_reset[atomicAdd(&s_nreset, 1u)] = t;
         uint4 wa, wb;
@@ -251,6 +265,7 @@ __global__ __launch_bounds__(kThreads) void k_step_sorted(StepArgs a) {
   const uint32_t o = s_out[pos];
   store_step_outputs<N>(a, i, (int)(o & 31u) - 1, (o >> 5) & 3u, (o >> 7) & 7u, (o >> 10) & 7u, s_legal[pos],
                         (int)(int8_t)(o >> 24));
+  store_episode(a, i, (o >> 5) & 3u, (int32_t)((o >> 14) & 31u) - 16);
 }
 
 struct RolloutArgs {
@@ -601,6 +616,8 @@ hipError_t launch_step(const Env& e, const int8_t* actions, const coup_step_outp
     a.step_type = out->step_type;
     a.legal = out->legal_mask;
     a.cur_player = out->cur_player;
+    a.ep_count = out->episodes;
+    a.ep_return = out->return_sum;
     obs = out->obs;
   }
   return dispatch(e.players, [&](auto np) {

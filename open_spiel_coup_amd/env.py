@@ -54,10 +54,15 @@ class BatchedCoupEnv:
       num_players: 2 (the reference game) .. 6.  N > 2 has no history /
         info_state; rewards / returns are [B, N], obs [B, N, 49 N].
       generic: run the N-player engine also at N = 2 (cross-checks).
+      episode_stats: keep per-lane int32 accumulators `episodes` and
+        `return_sum` (player 0's Returns() of every game that ends, coup.cc:
+        1016-1032), updated by every step at the lanes that reach LAST.
     """
 
     def __init__(self, batch, seed=0, env_id_base=0, auto_reset=True, obs=True, info_state=False,
-                 history=False, device=None, num_players=2, generic=False):
+                 history=False, device=None, num_players=2, generic=False, episode_stats=False):
+        if not (0 <= int(env_id_base) and int(env_id_base) + int(batch) <= 1 << 32):
+            raise ValueError("env ids are 32-bit: need 0 <= env_id_base and env_id_base + batch <= 2^32")
         self.lib = _native.load()
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
@@ -85,9 +90,12 @@ class BatchedCoupEnv:
         self.obs = torch.zeros(B, P, self.obs_size, dtype=torch.float32, device=dev) if obs else None
         self.info_state = (torch.zeros(B, 2, INFO_STATE_SIZE, dtype=torch.float32, device=dev)
                            if info_state else None)
+        self.episodes = torch.zeros(B, dtype=torch.int32, device=dev) if episode_stats else None
+        self.return_sum = torch.zeros(B, dtype=torch.int32, device=dev) if episode_stats else None
         self._out = _native.StepOutputs(
             _addr(self.actions), _addr(self.rewards), _addr(self.step_type), _addr(self.legal_mask),
-            _addr(self.cur_player), _addr(self.obs), _addr(self.info_state))
+            _addr(self.cur_player), _addr(self.obs), _addr(self.info_state), _addr(self.episodes),
+            _addr(self.return_sum))
 
     # ------------------------------------------------------------ plumbing
     def _bind_stream(self):
@@ -147,6 +155,18 @@ class BatchedCoupEnv:
             out["info_state"] = self.info_state
         return out
 
+    def episode_stats(self):
+        """(episodes, return_sum) per lane since the last clear_episode_stats
+        (int32 [B] device tensors; needs episode_stats=True)."""
+        if self.episodes is None:
+            raise ValueError("env created without episode_stats=True")
+        return self.episodes, self.return_sum
+
+    def clear_episode_stats(self):
+        if self.episodes is not None:
+            self.episodes.zero_()
+            self.return_sum.zero_()
+
     def capture_steps(self, steps, actions=None):
         """Record `steps` batched env steps (uniform policy, or the fixed
         `actions` tensor every step) as one HIP graph; `graph.replay()` then
@@ -188,7 +208,7 @@ class BatchedCoupEnv:
     def _slice_outputs(self, buf, t):
         return _native.StepOutputs(*[_addr(buf[k][t]) if k in buf else None for k in
                                      ("actions", "rewards", "step_type", "legal_mask", "current_player", "obs",
-                                      "info_state")])
+                                      "info_state")], _addr(self.episodes), _addr(self.return_sum))
 
     def collect_trajectory(self, steps, buf=None):
         """`steps` uniform-policy env steps whose outputs land in slice t of

@@ -19,6 +19,7 @@ This is the compatibility path; batched learners use BatchedCoupEnv.
 """
 import ctypes
 import enum
+import threading
 
 import numpy as np
 import torch
@@ -99,12 +100,19 @@ class _Pool:
     2-player history env (segments of SEG lanes, grown on demand).  Each
     State op is one coup_slot_op launch on its lane, and only ops that need
     an answer copy a 128-byte result back (one synchronisation); a clone is
-    a device-to-device lane copy with no round trip."""
+    a device-to-device lane copy with no round trip.
+
+    Thread-safe: one lock serialises alloc / release / op, because every op
+    answers through the pool's one pinned result buffer (and each segment's
+    one scratch), and ctypes releases the GIL inside coup_slot_op.  States
+    of one pool may therefore be used from several threads, as the
+    reference's independent State objects can."""
 
     SEG = 4096
 
     def __init__(self, device):
         self.device = torch.device(device)
+        self.lock = threading.RLock()
         self.lib = _native.load()
         self.segs = []
         self.free = []
@@ -115,6 +123,10 @@ class _Pool:
         self.host_ptr = ctypes.c_void_p(self.host.data_ptr())
 
     def alloc(self):
+        with self.lock:
+            return self._alloc()
+
+    def _alloc(self):
         if not self.free:
             env = BatchedCoupEnv(self.SEG, seed=0, auto_reset=False, obs=False, history=True, device=self.device)
             k = len(self.segs)
@@ -123,13 +135,18 @@ class _Pool:
         return self.free.pop()
 
     def release(self, slot):
-        self.free.append(slot)
+        with self.lock:
+            self.free.append(slot)
 
     def handle(self, slot):
         return self.segs[slot[0]]._h
 
     def op(self, slot, src=None, action=-1, init=False, obs=False, info=False, result=True):
         """coup_slot_op on `slot`; src = (coup_env handle, lane) or None."""
+        with self.lock:
+            return self._op(slot, src, action, init, obs, info, result)
+
+    def _op(self, slot, src, action, init, obs, info, result):
         flags = ((_native.SLOT_INIT if init else 0) | (_native.SLOT_OBS if obs else 0)
                  | (_native.SLOT_INFO if info else 0) | (0 if result else _native.SLOT_NO_RESULT))
         env = self.segs[slot[0]]
@@ -289,9 +306,10 @@ class CoupState:
     def _copy_to_env(self, env_handle, lane):
         """Write this state into lane `lane` of a 2-player history env."""
         env = self._pool.segs[self._slot[0]]
-        env._bind_stream()
-        _native.check(env.lib.coup_slot_op(env_handle, lane, env._h, self._slot[1], -1,
-                                           _native.SLOT_NO_RESULT, None))
+        with self._pool.lock:
+            env._bind_stream()
+            _native.check(env.lib.coup_slot_op(env_handle, lane, env._h, self._slot[1], -1,
+                                               _native.SLOT_NO_RESULT, None))
 
     # ------------------------------------------------------------- internals
     def _query(self, obs=False, info=False):

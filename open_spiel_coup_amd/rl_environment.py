@@ -15,13 +15,16 @@ and step() after LAST resets (:310-311).  One Environment drives one lane of
 a BatchedCoupEnv; batched learners should use BatchedCoupEnv directly.
 
 Chance sampling: by default the deals come from the build's Philox contract
- inside the kernel, keyed by `seed`.  Passing a
+ inside the kernel, keyed by `seed` (None, the default:
+64 bits of OS entropy, so independent environments deal independent games,
+like the reference's RandomState(None) sampler).  Passing a
 `chance_event_sampler` (an object called with the state, like the
 reference's ChanceEventSampler, :119-131) switches to the State API path:
 decisions and deals are applied one at a time and the sampler picks each
 deal.
 """
 import collections
+import os
 import enum
 
 import numpy as np
@@ -92,12 +95,22 @@ def registered_games():
     return pyspiel.registered_names()
 
 
+def _resolve_seed(seed):
+    """The sampling-contract seed of an Environment.  None draws 64 bits of
+    OS entropy, as the reference's default ChanceEventSampler does with
+    np.random.RandomState(None) (rl_environment.py:119-131): two
+    default-constructed environments deal different games."""
+    if seed is None:
+        return int.from_bytes(os.urandom(8), "little")
+    return int(seed) & ((1 << 64) - 1)
+
+
 class Environment:
     """rl_environment.Environment for Coup on the GPU (one lane)."""
 
     def __init__(self, game="coup", discount=1.0, chance_event_sampler=None, observation_type=None,
                  include_full_state=False, mfg_distribution=None, mfg_population=None,
-                 enable_legality_check=False, seed=0, device=None, **kwargs):
+                 enable_legality_check=False, seed=None, device=None, **kwargs):
         if isinstance(game, str):
             self._game = pyspiel.load_game(game, kwargs or None)
         else:
@@ -113,7 +126,7 @@ class Environment:
             observation_type = ObservationType.INFORMATION_STATE
         self._use_observation = observation_type == ObservationType.OBSERVATION
         self._device = device
-        self._seed = int(seed or 0)
+        self._seed = _resolve_seed(seed)
         self._make_env()
         self._should_reset = True
         self._last = None
@@ -180,7 +193,7 @@ class Environment:
         if self._sampler is not None:
             self._sampler.seed(seed)
             return
-        self._seed = int(seed or 0)
+        self._seed = _resolve_seed(seed)
         self._make_env()
         self._should_reset = True
 

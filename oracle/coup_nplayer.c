@@ -563,6 +563,8 @@ int np_rollout(const np_rollout_args* a) {
           np_returns(&s, ret);
           done++;
           ret_sum += ret[0];
+          if (a->lane_episodes) a->lane_episodes[lane] += 1;
+          if (a->lane_return_sum) a->lane_return_sum[lane] += ret[0];
           st = 2;
           if (a->auto_reset) {
             ep++;

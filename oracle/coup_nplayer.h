@@ -82,6 +82,8 @@ typedef struct {
   uint32_t* final_state; /* [n][8] */
   int64_t* episodes_done;
   int64_t* return_sum_p0;
+  int32_t* lane_episodes;   /* [n] per lane (optional) */
+  int32_t* lane_return_sum; /* [n] per lane (optional) */
 } np_rollout_args;
 int np_rollout(const np_rollout_args* a);
 

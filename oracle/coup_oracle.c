@@ -880,6 +880,8 @@ int oc_rollout(const oc_rollout_args* a) {
           oc_returns(&s, ret);
           done_eps++;
           ret_sum += ret[0];
+          if (a->lane_episodes) a->lane_episodes[lane] += 1;
+          if (a->lane_return_sum) a->lane_return_sum[lane] += ret[0];
           st = 2; /* LAST */
           if (a->auto_reset) {
             /* SyncVectorEnv.step(reset_if_done=True) (vector_env.py:62-65) */

@@ -143,6 +143,8 @@ typedef struct {
   int64_t* decisions;      /* total decisions applied (scalar) */
   int64_t* episodes_done;  /* total finished episodes (scalar) */
   int64_t* return_sum_p0;  /* sum of final returns of player 0 */
+  int32_t* lane_episodes;  /* [n] episodes finished per lane (optional) */
+  int32_t* lane_return_sum; /* [n] per lane: sum of player 0's final returns (optional) */
 } oc_rollout_args;
 int oc_rollout(const oc_rollout_args* a);
 

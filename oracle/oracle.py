@@ -50,7 +50,8 @@ class _RolloutArgs(ctypes.Structure):
                 ("obs", ctypes.c_void_p), ("info", ctypes.c_void_p),
                 ("final_state", ctypes.c_void_p), ("final_hist", ctypes.c_void_p),
                 ("decisions", ctypes.c_void_p), ("episodes_done", ctypes.c_void_p),
-                ("return_sum_p0", ctypes.c_void_p)]
+                ("return_sum_p0", ctypes.c_void_p), ("lane_episodes", ctypes.c_void_p),
+                ("lane_return_sum", ctypes.c_void_p)]
 
 
 class _NpPlayer(ctypes.Structure):
@@ -71,7 +72,8 @@ class _NpRolloutArgs(ctypes.Structure):
                 ("n", ctypes.c_int64), ("steps", ctypes.c_int64), ("auto_reset", ctypes.c_int),
                 ("actions", ctypes.c_void_p), ("rewards", ctypes.c_void_p), ("step_type", ctypes.c_void_p),
                 ("legal", ctypes.c_void_p), ("obs", ctypes.c_void_p), ("final_state", ctypes.c_void_p),
-                ("episodes_done", ctypes.c_void_p), ("return_sum_p0", ctypes.c_void_p)]
+                ("episodes_done", ctypes.c_void_p), ("return_sum_p0", ctypes.c_void_p),
+                ("lane_episodes", ctypes.c_void_p), ("lane_return_sum", ctypes.c_void_p)]
 
 
 _lib = None
@@ -277,6 +279,8 @@ def rollout(seed, n, steps, env_id_base=0, auto_reset=True, want_obs=False,
     a.decisions = buf("decisions", (1,), np.int64)
     a.episodes_done = buf("episodes_done", (1,), np.int64)
     a.return_sum_p0 = buf("return_sum_p0", (1,), np.int64)
+    a.lane_episodes = buf("lane_episodes", (n,), np.int32)
+    a.lane_return_sum = buf("lane_return_sum", (n,), np.int32)
     lib().oc_rollout(ctypes.byref(a))
     return out
 
@@ -359,5 +363,7 @@ def np_rollout(n_players, seed, n, steps, env_id_base=0, auto_reset=True, want_o
     a.final_state = buf("final_state", (n, 8), np.uint32)
     a.episodes_done = buf("episodes_done", (1,), np.int64)
     a.return_sum_p0 = buf("return_sum_p0", (1,), np.int64)
+    a.lane_episodes = buf("lane_episodes", (n,), np.int32)
+    a.lane_return_sum = buf("lane_return_sum", (n,), np.int32)
     lib().np_rollout(ctypes.byref(a))
     return out

@@ -40,11 +40,14 @@ def _worker(rank, world, port, out_dir):
     gathered = D.collate(final)
     gathered_rw = D.collate(rewards)
     traj = D.collate(torch.from_numpy(ref["actions"].astype(np.int64)), dim=1)  # [T, B] trajectories
+    # per-lane finished episodes and player-0 return sums (the bench's collective)
+    eps = D.collate(torch.from_numpy(np.stack([ref["lane_episodes"], ref["lane_return_sum"]], 1)))
     t = D.max_over_ranks(float(rank + 1), dev)
     if rank == 0:
         np.save(os.path.join(out_dir, "gathered.npy"), gathered.numpy())
         np.save(os.path.join(out_dir, "gathered_rw.npy"), gathered_rw.numpy())
         np.save(os.path.join(out_dir, "traj.npy"), traj.numpy())
+        np.save(os.path.join(out_dir, "eps.npy"), eps.numpy())
         with open(os.path.join(out_dir, "tmax.txt"), "w") as f:
             f.write(str(t))
     dist.barrier()
@@ -59,6 +62,10 @@ def test_two_rank_sharding_equals_single_process(tmp_path):
     np.testing.assert_array_equal(np.load(tmp_path / "gathered.npy").astype(np.uint32), full["final_state"])
     np.testing.assert_array_equal(np.load(tmp_path / "gathered_rw.npy"), full["rewards"][-1].astype(np.int64))
     np.testing.assert_array_equal(np.load(tmp_path / "traj.npy"), full["actions"].astype(np.int64))
+    eps = np.load(tmp_path / "eps.npy")
+    np.testing.assert_array_equal(eps[:, 0], full["lane_episodes"])
+    np.testing.assert_array_equal(eps[:, 1], full["lane_return_sum"])
+    assert int(eps[:, 0].sum()) == int(full["episodes_done"][0]) > 0
     assert float(open(tmp_path / "tmax.txt").read()) == 2.0
 
 

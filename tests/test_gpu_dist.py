@@ -1,0 +1,117 @@
+"""C5 on the HIP engine: env-id sharding over 2 processes, per-episode
+returns gathered (BASELINE config 5).
+
+Two fresh child processes (tests/dist_hip_worker.py), each initialising the
+GPU itself, run libcoup_mi355x on their shards of the global env ids and
+all-gather the per-lane finished-episode counts and player-0 return sums
+(Returns(), coup.cc:1016-1032) with open_spiel_coup_amd.distributed.collate
+over gloo -- both ranks on the box's one GPU, since RCCL refuses two ranks
+on one device.  Rank 0's gathered tensors must equal a single-process HIP
+run over all 2B lanes and the oracle's per-lane statistics.
+
+The second test runs bench.py itself under torch.distributed.run with 2
+ranks (--dist-backend gloo): the exact multi-GPU bench code path, whose
+timed region ends with the all-gather of the per-episode returns.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+B, SEED, K_FUSED, K_STEP = 3000, 2024, 200, 96
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _run_ranks(cmd_for_rank, world, timeout):
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(cmd_for_rank(r), env=env, cwd=ROOT, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append(out)
+    for p, out in zip(procs, outs):
+        assert p.returncode == 0, out[-3000:]
+    return outs
+
+
+def test_two_process_hip_shards_gather_episode_returns(tmp_path):
+    import torch
+    from open_spiel_coup_amd import BatchedCoupEnv
+
+    world = 2
+    _run_ranks(lambda r: [sys.executable, "-u", os.path.join(ROOT, "tests", "dist_hip_worker.py"), str(tmp_path),
+                          str(B), str(SEED), str(K_FUSED), str(K_STEP)], world, timeout=100)
+    assert int(np.load(tmp_path / "errors.npy")[0]) == 0
+    fused_stats = np.load(tmp_path / "fused_stats.npy")
+    step_stats = np.load(tmp_path / "step_stats.npy")
+    n = world * B
+    assert fused_stats.shape == (n, 3) and step_stats.shape == (n, 2)
+
+    # one process over all 2B lanes, same engine
+    fused = BatchedCoupEnv(n, seed=SEED, obs=False)
+    stats = fused.new_stats()
+    fused.rollout(K_FUSED, stats)
+    single = torch.stack([stats["episodes"], stats["return_sum"], stats["length_sum"]], 1).cpu().numpy()
+    np.testing.assert_array_equal(fused_stats, single)
+    np.testing.assert_array_equal(np.load(tmp_path / "fused_rec.npy"), fused.export_state().cpu().numpy())
+    stepped = BatchedCoupEnv(n, seed=SEED, obs=False, episode_stats=True)
+    for _ in range(K_STEP):
+        stepped.step()
+    eps, ret = stepped.episode_stats()
+    np.testing.assert_array_equal(step_stats, torch.stack([eps, ret], 1).cpu().numpy())
+    np.testing.assert_array_equal(np.load(tmp_path / "step_rec.npy"), stepped.export_state().cpu().numpy())
+
+    # the oracle, lane by lane
+    ref = oracle.rollout(seed=SEED, n=n, steps=K_FUSED, want_trajectory=False)
+    np.testing.assert_array_equal(fused_stats[:, 0], ref["lane_episodes"])
+    np.testing.assert_array_equal(fused_stats[:, 1], ref["lane_return_sum"])
+    assert int(fused_stats[:, 0].sum()) == int(ref["episodes_done"][0])
+    assert int(fused_stats[:, 1].sum()) == int(ref["return_sum_p0"][0])
+    ref = oracle.rollout(seed=SEED, n=n, steps=K_STEP, want_trajectory=False)
+    np.testing.assert_array_equal(step_stats[:, 0], ref["lane_episodes"])
+    np.testing.assert_array_equal(step_stats[:, 1], ref["lane_return_sum"])
+    np.testing.assert_array_equal(np.load(tmp_path / "step_rec.npy").astype(np.uint32), ref["final_state"])
+
+
+@pytest.mark.parametrize("config", ["c2", "c3"])
+def test_bench_two_ranks_gloo(config):
+    """bench.py's multi-GPU path (torchrun environment, env-id shards,
+    barrier, per-episode all-gather, max over ranks) with 2 ranks sharing the
+    GPU; the line reports the gathered episodes and no lane errors."""
+    batch = 1 << 16 if config == "c3" else 1 << 14
+    outs = _run_ranks(lambda r: [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config",
+                                 config, "--steps", "8", "--warmup", "2", "--settle", "16", "--batch", str(batch),
+                                 "--dist-backend", "gloo"], 2, timeout=110)
+    lines = [ln for ln in outs[0].splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, outs[0][-2000:]
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["global_batch"] == 2 * batch
+    assert rec["lane_errors"] == 0
+    assert rec["episodes"]["finished"] > 0 and rec["episodes"]["collective"].startswith("all_gather")
+    assert -2.0 <= rec["episodes"]["mean_return_p0"] <= 2.0

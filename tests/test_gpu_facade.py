@@ -173,3 +173,25 @@ def test_sync_vector_env():
         for t, d, u in zip(ts, done, unreset):
             assert d == u.last()
             assert t.first() if d else t.mid()
+
+
+def test_default_environments_deal_independent_games():
+    """Environment('coup') without a seed draws its key from OS entropy, like
+    the reference's RandomState(None) chance sampler (rl_environment.py:
+    119-131): default-constructed environments do not replay one stream, and
+    seed(None) re-keys."""
+    envs = [rl_environment.Environment("coup") for _ in range(4)]
+    for e in envs:
+        e.reset()
+    deals = {tuple(e.get_state.history()) for e in envs}
+    keys = {e._seed for e in envs}
+    assert len(keys) == 4
+    # 4 initial deals from 15 cards: four identical deals by chance are ~impossible
+    assert len(deals) > 1
+    k = envs[0]._seed
+    envs[0].seed(None)
+    assert envs[0]._seed != k
+    fixed = [rl_environment.Environment("coup", seed=5) for _ in range(2)]
+    for e in fixed:
+        e.reset()
+    assert fixed[0].get_state.history() == fixed[1].get_state.history()

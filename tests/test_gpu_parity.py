@@ -193,6 +193,73 @@ def test_history_kept_by_apply_and_step():
         assert bytes(h[i, :m]) == st.history_bytes()[:m], s["name"]
 
 
+def test_c2_bench_kernel_matches_oracle_every_step():
+    """BASELINE config 2 exactly as bench.py's c2 runs it: 65,536 lanes,
+    in-kernel uniform policy (random_agent.py:29-42), no observations, so
+    coup_step launches the in-place k_step<true, 0, 256, 0> (regrouping
+    starts at 2^18 lanes).  Every lane's action, rewards, step type and
+    post-step legal mask (LegalActions, coup.cc:824-938) equal the oracle's
+    at each of 160 steps; so do the per-lane episode accumulators and the
+    final records."""
+    from open_spiel_coup_amd import _native  # noqa: F401
+    n, steps, seed = 65536, 160, 1
+    assert n < (1 << 18)  # the in-place kernel, not k_step_sorted
+    ref = oracle.rollout(seed=seed, n=n, steps=steps)
+    env = BatchedCoupEnv(n, seed=seed, obs=False, episode_stats=True)
+    for t in range(steps):
+        o = env.step()
+        np.testing.assert_array_equal(_np(o["actions"]), ref["actions"][t], err_msg=f"step {t}")
+        np.testing.assert_array_equal(_np(o["rewards"]), ref["rewards"][t], err_msg=f"step {t}")
+        np.testing.assert_array_equal(_np(o["step_type"]), ref["step_type"][t], err_msg=f"step {t}")
+        np.testing.assert_array_equal(_np(o["legal_mask"]).astype(np.uint32), ref["legal"][t], err_msg=f"step {t}")
+    np.testing.assert_array_equal(_np(env.export_state()).astype(np.uint32), ref["final_state"])
+    eps, ret = env.episode_stats()
+    np.testing.assert_array_equal(_np(eps), ref["lane_episodes"])
+    np.testing.assert_array_equal(_np(ret), ref["lane_return_sum"])
+    assert env.error_count() == 0
+
+
+@pytest.mark.parametrize("regroup", ["1", "0"], ids=["regrouped", "in-place"])
+@pytest.mark.parametrize("auto_reset", [True, False])
+def test_episode_stats_match_oracle(monkeypatch, regroup, auto_reset):
+    """coup_step's per-episode accumulators (episodes, player-0 return sum
+    per lane) == the oracle's, with the obs writer on and off, in place and
+    regrouped by decision."""
+    monkeypatch.setenv("COUP_REGROUP", regroup)
+    n, steps, seed = 3000, 120, 8
+    ref = oracle.rollout(seed=seed, n=n, steps=steps, auto_reset=auto_reset, want_trajectory=False)
+    for obs in (False, True):
+        env = BatchedCoupEnv(n, seed=seed, auto_reset=auto_reset, obs=obs, episode_stats=True)
+        for _ in range(steps):
+            env.step()
+        eps, ret = env.episode_stats()
+        np.testing.assert_array_equal(_np(eps), ref["lane_episodes"], err_msg=f"obs={obs}")
+        np.testing.assert_array_equal(_np(ret), ref["lane_return_sum"], err_msg=f"obs={obs}")
+        env.clear_episode_stats()
+        assert int(env.episode_stats()[0].sum()) == 0
+
+
+def test_traffic_ceiling_kernel_leaves_records():
+    """coup_measure_step_traffic (bench.py's in-process store ceiling) stores
+    every record back unchanged and writes the full obs buffer, ragged
+    batch included, nothing past it."""
+    import ctypes
+    from open_spiel_coup_amd import _native
+    n = 1000
+    env = BatchedCoupEnv(n, seed=3, obs=True)
+    for _ in range(5):
+        env.step()
+    rec = env.export_state()
+    before = rec.clone()
+    guard = torch.full((n + 64, 2, 98), -7.0, device="cuda")
+    out = _native.StepOutputs(None, None, None, None, None, guard.data_ptr())
+    _native.check(env.lib.coup_measure_step_traffic(n, ctypes.c_void_p(rec.data_ptr()), ctypes.byref(out),
+                                                    ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    torch.cuda.synchronize()
+    assert torch.equal(rec, before)
+    assert torch.all(guard[n:] == -7.0) and not torch.any(guard[:n] == -7.0)
+
+
 def test_external_actions_replay():
     """Feeding the oracle's chosen actions back through coup_step(actions)
     reproduces the same trajectory (chance deals depend only on the env's

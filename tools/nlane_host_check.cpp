@@ -39,17 +39,26 @@ int run(uint64_t seed, int64_t n, int64_t steps, int auto_reset) {
   a.obs = obs.data();
   a.episodes_done = &done;
   a.return_sum_p0 = &ret0;
+  std::vector<int32_t> lane_eps(n, 0), lane_ret(n, 0);
+  a.lane_episodes = lane_eps.data();
+  a.lane_return_sum = lane_ret.data();
   np_rollout(&a);
   int bad = 0;
   for (int64_t i = 0; i < n && bad < 5; ++i) {
     NRng rng{(uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)i, 0u, make_uint4(0, 0, 0, 0)};
     NLane<N> L = initial_lane<N>(0);
     resolve_chance(L, rng);
+    int32_t eps = 0, rsum = 0;
     for (int64_t t = 0; t < steps && bad < 5; ++t) {
       int x;
       uint32_t s, rl, rc;
+      int32_t r0;
       bool err;
-      step_lane<N, true>(L, rng, 0u, auto_reset != 0, x, s, rl, rc, err);
+      step_lane<N, true>(L, rng, 0u, auto_reset != 0, x, s, rl, rc, r0, err);
+      if (s == 2u) {
+        eps += 1;
+        rsum += r0;
+      }
       const int64_t o = t * n + i;
       bool ok = !err && x == act[o] && s == st[o] && legal_mask(L) == legal[o];
       for (int p = 0; p < N; ++p) {
@@ -71,6 +80,10 @@ int run(uint64_t seed, int64_t n, int64_t steps, int auto_reset) {
                     act[o], s, st[o], legal_mask(L), legal[o], (int)err);
         ++bad;
       }
+    }
+    if (eps != lane_eps[i] || rsum != lane_ret[i]) {
+      std::printf("lane %lld episodes %d/%d return sum %d/%d\n", (long long)i, eps, lane_eps[i], rsum, lane_ret[i]);
+      ++bad;
     }
     uint4 wa, wb;
     pack(L, wa, wb);

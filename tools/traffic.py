@@ -97,7 +97,10 @@ def main():
                     bench = json.loads(line)
                     summary["bench_line_of_traced_command"] = {
                         "value": bench["value"], "ms_per_step": bench["ms_per_step"],
-                        "kernel_ms": bench["roofline"]["kernel_ms"], "frac": bench["roofline"]["frac"]}
+                        "kernel_ms": bench["roofline"]["kernel_ms"], "frac": bench["roofline"]["frac"],
+                        "store_ceiling_ms": bench["roofline"].get("store_ceiling_ms"),
+                        "frac_of_store_ceiling": bench["roofline"].get("frac_of_store_ceiling"),
+                        "box": bench.get("box")}
                     tk = summary.get("timed_kernel")
                     if fused:
                         # a fused config launches the same kernel for the settle,
@@ -113,6 +116,25 @@ def main():
                     elif tk and tk in summary.get("kernels", {}):
                         rp = summary["kernels"][tk]["avg_ns"] * 1e-6
                         summary["bench_vs_rocprof_kernel_ms"] = [bench["roofline"]["kernel_ms"], rp]
+
+    # plain bench lines of the same lease, before and after the profiler passes
+    for which in ("before", "after"):
+        path = os.path.join(src, f"bench_{which}.json")
+        if os.path.exists(path):
+            with open(path) as f:
+                for line in f:
+                    if line.startswith("{") and '"metric"' in line:
+                        b = json.loads(line)
+                        summary[f"bench_line_{which}"] = {
+                            "value": b["value"], "kernel_ms": b["roofline"]["kernel_ms"],
+                            "frac": b["roofline"]["frac"], "store_ceiling_ms": b["roofline"].get("store_ceiling_ms"),
+                            "frac_of_store_ceiling": b["roofline"].get("frac_of_store_ceiling")}
+                        shutil.copy(path, os.path.join(dst, f"bench_{which}.json"))
+    if summary.get("bench_vs_rocprof_kernel_ms"):
+        a, b = summary["bench_vs_rocprof_kernel_ms"]
+        summary["rocprof_minus_bench_pct"] = 100.0 * (b - a) / a
+    if os.path.exists(os.path.join(src, "box.txt")):
+        shutil.copy(os.path.join(src, "box.txt"), os.path.join(dst, "box.txt"))
 
     def counter(kind, cname):
         vals = []
