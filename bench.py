@@ -273,10 +273,9 @@ def main():
             return stats["episodes"], stats["return_sum"]
         return env.episode_stats()
 
-    if world > 1:
-        # first all-gather outside the timed region (RCCL sets up its
-        # all-gather channels lazily on first use)
-        D.collate(torch.stack(episode_tensors(), 1))
+    # one collation outside the timed region: RCCL sets up its all-gather
+    # channels lazily, and HIP loads torch's stack kernel on first use
+    D.collate(torch.stack(episode_tensors(), 1))
     if fused:
         for t in stats.values():
             t.zero_()

@@ -81,10 +81,11 @@ typedef struct {
   int8_t* cur_player;   /* [B]  CurrentPlayer() of the (post-reset) state */
   float* obs;           /* [B][2][98] ObservationTensor(p) for p = 0, 1 */
   float* info_state;    /* [B][2][2492] InformationStateTensor(p) (needs COUP_FLAG_HISTORY) */
-  /* Per-episode accumulators, updated only for lanes whose episode ends in
-   * this step (step type LAST): episodes[i] += 1 and return_sum[i] +=
-   * Returns()[0] of the finished game (coup.cc:1016-1032), read before an
-   * auto-reset.  The multi-GPU bench all-gathers them. */
+  /* Per-episode accumulators: for a lane whose episode ends in this step
+   * (step type LAST), episodes[i] += 1 and return_sum[i] += Returns()[0] of
+   * the finished game (coup.cc:1016-1032), read before an auto-reset; other
+   * lanes keep their values.  The multi-GPU bench all-gathers them
+   * (SURVEY.md 8(e)).  Both or neither. */
   int32_t* episodes;    /* [B] */
   int32_t* return_sum;  /* [B] */
 } coup_step_outputs;

@@ -515,6 +515,7 @@ struct StepArgs {
   float* info;     // [B][2][2492] (INFO == kInfoWrite)
   int32_t* ep_count;   // [B] per-episode accumulators (coup_step_outputs.episodes)
   int32_t* ep_return;  // [B] (coup_step_outputs.return_sum)
+  int ep_mode;         // episode accumulators: kEpEarly / kEpEarlyAll / kEpLate (COUP_EP_MODE, A/B)
   uint32_t* err_count;
   int xcd_remap;   // block -> lane group mapping (xcd_group)
 #ifdef COUP_WAVE_TRACE
@@ -628,6 +629,45 @@ __device__ __forceinline__ void step_lane(const StepArgs& a, int64_t i, Lane& L,
   COUP_TRACE_ANY(a, 9);
 }
 
+// How a step updates the per-episode accumulators (coup_step_outputs.
+// episodes / return_sum).  kEpEarlyAll (default): the lane's two words are
+// loaded with its record, before the rules, and every lane stores them back
+// (coalesced, unchanged where no episode ended); kEpEarly: the same load,
+// stores only where an episode ended; kEpLate: load-add-store after the
+// rules at the finished lanes only.  Same-process A/B on the c3 step
+// (2^20 lanes, obs x2; profiles/r02/ab/ab_epstats.jsonl): no accumulators
+// 148.8 us, kEpEarlyAll 153.0, kEpEarly 163.3, kEpLate 163.9 -- the ~7% of
+// lanes that finish scatter 4-byte stores over most lines, and those
+// partial-line writes cost more than 16 MB of full-line ones.
+enum EpMode : int { kEpEarlyAll = 0, kEpEarly = 1, kEpLate = 2 };
+
+struct EpStats {
+  int32_t count = 0, ret = 0;
+};
+
+__device__ __forceinline__ EpStats ep_prefetch(const StepArgs& a, int64_t i, bool active) {
+  EpStats e;
+  if (a.ep_count && a.ep_mode != kEpLate && active) {
+    e.count = a.ep_count[i];
+    e.ret = a.ep_return[i];
+  }
+  return e;
+}
+
+__device__ __forceinline__ void ep_update(const StepArgs& a, int64_t i, const EpStats& e, uint32_t st, int32_t ret) {
+  if (!a.ep_count) return;
+  const bool last = st == COUP_STEP_LAST;
+  if (a.ep_mode == kEpLate) {
+    if (last) {
+      a.ep_count[i] += 1;
+      a.ep_return[i] += ret;
+    }
+  } else if (last || a.ep_mode == kEpEarlyAll) {
+    a.ep_count[i] = e.count + (last ? 1 : 0);
+    a.ep_return[i] = e.ret + (last ? ret : 0);
+  }
+}
+
 // Wave-scope hand-off of LDS data between lanes of one wave.
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -722,6 +762,7 @@ __device__ __forceinline__ void step_group_compute(const StepArgs& a, int64_t gr
   const int64_t wleft = a.n - wave0;
   const uint32_t wave_valid = wleft >= 64 ? 64u : (wleft > 0 ? (uint32_t)wleft : 0u);  // wave-uniform
   uint8_t* hist_wave = lds.hist + wl * kHist;
+  const EpStats eps = ep_prefetch(a, i, active);
   if (INFO != kInfoNone) {
     if (wave_valid) wave_hist_copy<true>(a.hist + wave0 * kHist, hist_wave, wave_valid);
     wave_sync();
@@ -745,10 +786,7 @@ __device__ __forceinline__ void step_group_compute(const StepArgs& a, int64_t gr
       step_lane<UNIFORM>(a, i, L, act, st, rew, ret, none);
     }
     a.state[i] = pack(L);
-    if (st == COUP_STEP_LAST && a.ep_count) {
-      a.ep_count[i] += 1;
-      a.ep_return[i] += ret;
-    }
+    ep_update(a, i, eps, st, ret);
     if (a.actions) a.actions[i] = (int8_t)act;
     if (a.rewards) {
       a.rewards[2 * i] = (int8_t)rew;
@@ -904,6 +942,7 @@ __global__ __launch_bounds__(kThreads, 8) void k_step_sorted(StepArgs a) {
   // phase 1: up to the decision (step_lane)
   Lane L = initial_lane(0u);
   uint32_t key = kKeyDead, st = COUP_STEP_MID;
+  const EpStats eps = ep_prefetch(a, i, live);
   if (live) {
     L = unpack(a.state[i]);
     Rng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, i), 0u, make_uint4(0, 0, 0, 0)};
@@ -989,10 +1028,7 @@ __global__ __launch_bounds__(kThreads, 8) void k_step_sorted(StepArgs a) {
   if (a.step_type) a.step_type[i] = (uint8_t)((o >> 5) & 3u);
   if (a.legal) a.legal[i] = s_legal[pos];
   if (a.cur_player) a.cur_player[i] = (int8_t)(o >> 24);
-  if (((o >> 5) & 3u) == COUP_STEP_LAST && a.ep_count) {
-    a.ep_count[i] += 1;
-    a.ep_return[i] += (int32_t)((o >> 10) & 7u) - 2;
-  }
+  ep_update(a, i, eps, (o >> 5) & 3u, (int32_t)((o >> 10) & 7u) - 2);
 }
 
 // The decision key of a lane at a decision node: the uniform policy's draw,
@@ -1593,6 +1629,10 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
     a.info = out->info_state;
     a.ep_count = out->episodes;
     a.ep_return = out->return_sum;
+  }
+  {
+    const char* em = std::getenv("COUP_EP_MODE");  // A/B of the accumulator update (coup::EpMode)
+    a.ep_mode = em ? std::atoi(em) : coup::kEpEarlyAll;
   }
   if ((a.ep_count == nullptr) != (a.ep_return == nullptr))
     return fail(COUP_E_INVALID, "coup_step: episodes and return_sum go together");

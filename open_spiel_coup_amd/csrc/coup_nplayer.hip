@@ -61,11 +61,20 @@ struct StepArgs {
   uint32_t* err_count;
 };
 
-// Episode accumulators of a lane whose game ended in this step (LAST).
-__device__ __forceinline__ void store_episode(const StepArgs& a, int64_t i, uint32_t st, int32_t ret0) {
-  if (st == 2u && a.ep_count) {
-    a.ep_count[i] += 1;
-    a.ep_return[i] += ret0;
+// Episode accumulators (coup_step_outputs.episodes / return_sum): the
+// lane's two words are loaded with its record, before the rules, and every
+// lane stores them back (coalesced; unchanged unless the episode ended), so
+// no wave waits on a late load and no line is written partially (the
+// 2-player kernels' kEpEarlyAll, coup_kernels.hip).
+__device__ __forceinline__ int2 load_episode(const StepArgs& a, int64_t i) {
+  return a.ep_count ? make_int2(a.ep_count[i], a.ep_return[i]) : make_int2(0, 0);
+}
+
+__device__ __forceinline__ void store_episode(const StepArgs& a, int64_t i, int2 e, uint32_t st, int32_t ret0) {
+  if (a.ep_count) {
+    const bool last = st == 2u;
+    a.ep_count[i] = e.x + (last ? 1 : 0);
+    a.ep_return[i] = e.y + (last ? ret0 : 0);
   }
 }
 
@@ -103,6 +112,7 @@ __global__ __launch_bounds__(kThreads) void k_step(StepArgs a) {
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= a.n) return;
   NLane<N> L = unpack<N>(a.sa[i], a.sb[i]);
+  const int2 eps = load_episode(a, i);
   NRng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, i), 0u, make_uint4(0, 0, 0, 0)};
   int act;
   uint32_t st, rl, rc;
@@ -111,7 +121,7 @@ __global__ __launch_bounds__(kThreads) void k_step(StepArgs a) {
   step_lane<N, UNIFORM>(L, rng, UNIFORM ? 0u : (uint32_t)(uint8_t)a.actions_in[i], a.auto_reset != 0, act, st, rl,
                         rc, ret0, error);
   if (error) count_error(a.err_count);
-  store_episode(a, i, st, ret0);
+  store_episode(a, i, eps, st, ret0);
   uint4 wa, wb;
   pack(L, wa, wb);
   a.sa[i] = wa;
@@ -162,6 +172,7 @@ __global__ __launch_bounds__(kThreads) void k_step_sorted(StepArgs a) {
   NLane<N> L;
   uint32_t key = kKeyDead, st = 0u;
   bool error = false;
+  const int2 eps = live ? load_episode(a, i) : make_int2(0, 0);
   if (live) {
     const uint4 rb = a.sb[i];
     L = unpack<N>(a.sa[i], rb);
@@ -265,7 +276,7 @@ __global__ __launch_bounds__(kThreads) void k_step_sorted(StepArgs a) {
   const uint32_t o = s_out[pos];
   store_step_outputs<N>(a, i, (int)(o & 31u) - 1, (o >> 5) & 3u, (o >> 7) & 7u, (o >> 10) & 7u, s_legal[pos],
                         (int)(int8_t)(o >> 24));
-  store_episode(a, i, (o >> 5) & 3u, (int32_t)((o >> 14) & 31u) - 16);
+  store_episode(a, i, eps, (o >> 5) & 3u, (int32_t)((o >> 14) & 31u) - 16);
 }
 
 struct RolloutArgs {

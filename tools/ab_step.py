@@ -5,7 +5,11 @@ HBM variance is larger than the differences being measured).
 
 Each positional argument is one variant: a comma-separated list of
 environment settings read by coup_step at launch (COUP_OBS_MODE,
-COUP_XCD_REMAP, COUP_STEP_DYN_LDS).  The variants run
+COUP_XCD_REMAP, COUP_STEP_DYN_LDS, COUP_REGROUP, COUP_AHEAD, COUP_EP_MODE),
+plus STATS=0/1 (bind the per-episode accumulators, coup_step_outputs.
+episodes / return_sum; default 1, as bench.py) and CEIL=1 (time
+coup_measure_step_traffic -- the step's traffic with no rules -- instead of
+the step).  The variants run
 round-robin `rounds` times over the same settled batch; prints one JSON line
 per variant with the median and min per-step kernel time (HIP events on the
 launch stream).  Measurement tool only.
@@ -19,7 +23,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-KNOBS = ("COUP_OBS_MODE", "COUP_XCD_REMAP", "COUP_STEP_DYN_LDS", "COUP_REGROUP", "COUP_AHEAD")
+KNOBS = ("COUP_OBS_MODE", "COUP_XCD_REMAP", "COUP_STEP_DYN_LDS", "COUP_REGROUP", "COUP_AHEAD", "COUP_EP_MODE")
 
 
 def main():
@@ -36,8 +40,20 @@ def main():
     import torch
 
     from open_spiel_coup_amd import BatchedCoupEnv
+    import ctypes
+    from open_spiel_coup_amd import _native
     env = BatchedCoupEnv(a.batch, seed=1, auto_reset=True, obs=bool(a.obs) and not a.info, info_state=bool(a.info),
-                         device="cuda:0", num_players=a.players)
+                         device="cuda:0", num_players=a.players, episode_stats=True)
+    stats_ptrs = (env._out.episodes, env._out.return_sum)
+    rec = env.export_state()
+    ceil_out = _native.StepOutputs(*[t.data_ptr() if t is not None else None for t in
+                                     (env.actions, env.rewards, env.step_type, env.legal_mask, env.cur_player,
+                                      env.obs)])
+
+    def ceiling_launch():
+        _native.check(env.lib.coup_measure_step_traffic(a.batch, ctypes.c_void_p(rec.data_ptr()),
+                                                         ctypes.byref(ceil_out),
+                                                         ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)))
     if a.info:
         for _ in range(32):  # histories: no fused rollout
             env.step()
@@ -49,22 +65,28 @@ def main():
         for v in a.variants:
             for k in KNOBS:
                 os.environ.pop(k, None)
+            opts = {"STATS": "1", "CEIL": "0"}
             for kv in v.split(","):
                 if kv:
                     k, val = kv.split("=")
-                    os.environ[k] = val
+                    if k in opts:
+                        opts[k] = val
+                    else:
+                        os.environ[k] = val
+            env._out.episodes, env._out.return_sum = stats_ptrs if opts["STATS"] == "1" else (None, None)
+            step = ceiling_launch if opts["CEIL"] == "1" else env.step
             if a.fused:
                 env.rollout(a.fused)
             else:
                 for _ in range(3):
-                    env.step()
+                    step()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
             if a.fused:
                 env.rollout(a.fused * a.steps)
             else:
                 for _ in range(a.steps):
-                    env.step()
+                    step()
             e1.record(stream)
             e1.synchronize()
             times[v].append(e0.elapsed_time(e1) * 1e3 / (a.steps * max(a.fused, 1)))  # us per env step
