@@ -1,8 +1,15 @@
-"""Build libcoup_mi355x.so in-tree with hipcc for gfx950.
+"""Build the libraries in-tree.
 
     python -m open_spiel_coup_amd.build [--force] [--verbose]
 
-The .so is git-ignored but travels to the GPU box with the gpurun snapshot.
+  libcoup_mi355x.so   the kernels and the C ABI (include/coup_mi355x.h), hipcc
+                      for gfx950;
+  librust_spiel.so    the reference's per-state C ABI (rust_open_spiel.h,
+                      include/coup_rust_abi.h) over it, host C++ (g++), so the
+                      reference's Rust crate links it as `dylib=rust_spiel`.
+
+The .so files are git-ignored but travel to the GPU box with the gpurun
+snapshot.
 """
 import argparse
 import os
@@ -16,6 +23,11 @@ SOURCES = [os.path.join(CSRC, "coup_kernels.hip"), os.path.join(CSRC, "coup_npla
 DEPS = SOURCES + [os.path.join(CSRC, h) for h in ("coup_lane.h", "coup_nlane.h", "coup_np.h", "coup_regroup.h")] + [
     os.path.join(ROOT, "include", "coup_mi355x.h")]
 OUT = os.path.join(HERE, "libcoup_mi355x.so")
+RUST_SRC = os.path.join(CSRC, "rust_spiel.cpp")
+RUST_DEPS = [RUST_SRC, os.path.join(ROOT, "include", "coup_rust_abi.h"), os.path.join(ROOT, "include", "coup_mi355x.hpp"),
+             os.path.join(ROOT, "include", "coup_mi355x.h")]
+RUST_OUT = os.path.join(HERE, "librust_spiel.so")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("COUP_OFFLOAD_ARCH", "gfx950")
 
@@ -28,20 +40,33 @@ def command(resource_usage=False, out=OUT, defines=()):
     return cmd
 
 
-def up_to_date():
-    if not os.path.exists(OUT):
+def rust_command(out=RUST_OUT):
+    """librust_spiel.so: host-only C++ over libcoup_mi355x.so (found next to it
+    through $ORIGIN) and the HIP runtime."""
+    return [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-D__HIP_PLATFORM_AMD__",
+            "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROCM, "include"), RUST_SRC, "-o", out,
+            "-L", HERE, "-lcoup_mi355x", "-L", os.path.join(ROCM, "lib"), "-lamdhip64",
+            "-Wl,-rpath,$ORIGIN:" + os.path.join(ROCM, "lib")]
+
+
+def up_to_date(out=OUT, deps=DEPS):
+    if not os.path.exists(out):
         return False
-    t = os.path.getmtime(OUT)
-    return all(os.path.getmtime(p) <= t for p in DEPS)
+    t = os.path.getmtime(out)
+    return all(os.path.getmtime(p) <= t for p in deps)
 
 
 def build(force=False, verbose=False):
-    if not force and up_to_date():
-        return OUT
-    cmd = command(resource_usage=verbose)
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.check_call(cmd)
+    if force or not up_to_date():
+        cmd = command(resource_usage=verbose)
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.check_call(cmd)
+    if force or not up_to_date(RUST_OUT, RUST_DEPS + [OUT]):
+        cmd = rust_command()
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.check_call(cmd)
     return OUT
 
 
