@@ -121,6 +121,16 @@ typedef struct {
 #define COUP_SLOT_INFO 4       /* append InformationStateTensor [2][2492] float (after obs if both) */
 #define COUP_SLOT_NO_RESULT 8  /* asynchronous: no result, host_out may be NULL */
 
+/* One request of coup_slot_ops (24 bytes): the op coup_slot_op would run on
+ * lane `lane` with src_lane (< 0: no copy), action (< 0: none) and flags
+ * (COUP_SLOT_INIT only; the output flags are per call). */
+typedef struct {
+  int64_t lane;
+  int64_t src_lane;
+  int32_t action;
+  int32_t flags;
+} coup_slot_req;
+
 /* Per-lane rollout statistics accumulated by coup_rollout (device, [B]). */
 typedef struct {
   int32_t* episodes;    /* [B] episodes finished */
@@ -205,6 +215,20 @@ int coup_query(coup_env* env, const coup_query_outputs* out);
  * StateObservationTensor, StateInformationStateTensor) with one round trip. */
 int coup_slot_op(coup_env* env, int64_t lane, const coup_env* src_env, int64_t src_lane, int action, int flags,
                  void* host_out);
+
+/* n independent coup_slot_op requests (host array `reqs`) in one launch --
+ * e.g. all children of a Deep CFR traverser node (deep_cfr.py:440-471:
+ * state.child(a) for every legal a) or one action on each state of a
+ * frontier.  Copies read src_env (may be env; NULL only if no request
+ * copies).  Requests must be independent: destination lanes distinct, and
+ * no destination lane the source of another request when src_env == env
+ * (COUP_E_INVALID otherwise).  flags: COUP_SLOT_OBS / COUP_SLOT_INFO /
+ * COUP_SLOT_NO_RESULT for every request.  Unless COUP_SLOT_NO_RESULT,
+ * host_out receives n coup_slot_result, then (COUP_SLOT_OBS) n x [2][98]
+ * floats, then (COUP_SLOT_INFO) n x [2][2492] floats, and the call
+ * synchronises the env's stream. */
+int coup_slot_ops(coup_env* env, int64_t n, const coup_slot_req* reqs, const coup_env* src_env, int flags,
+                  void* host_out);
 
 /* Copy the packed lane records ([B][coup_state_bytes / 4] uint32, device)
  * out of / into the env. */

@@ -31,6 +31,7 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
 #include <array>
 #include <cstdint>
 #include <cstring>
@@ -234,6 +235,14 @@ class Pool {
     std::lock_guard<std::mutex> g(mu_);
     if (s.seg >= 0) free_.push_back(s);
   }
+  // n requests on segment `seg` in one launch (coup_slot_ops); copies read
+  // segment src_seg (-1: none); host_out: n results (+ tensors per flags)
+  void Ops(int seg, const std::vector<coup_slot_req>& reqs, int src_seg, int flags, void* host_out) {
+    std::lock_guard<std::mutex> g(mu_);
+    coup_env* src_env = src_seg >= 0 ? segs_[src_seg]->get() : nullptr;
+    Check(coup_slot_ops(segs_[seg]->get(), (int64_t)reqs.size(), reqs.data(), src_env, flags, host_out),
+          "coup_slot_ops");
+  }
   // host_out: coup_slot_result followed by the tensors the flags ask for
   void Op(const Slot& s, const Slot* src, int action, int flags, void* host_out) {
     // one op at a time: each segment answers through one pinned scratch buffer
@@ -336,6 +345,48 @@ class CoupState {
     return c;
   }
   std::unique_ptr<CoupState> Clone() const { return std::unique_ptr<CoupState>(new CoupState(*this)); }
+  // Child(a) for every a in `actions`, one coup_slot_ops launch per pool
+  // segment: the expansion of a Deep CFR traverser node (deep_cfr.py:440-471)
+  std::vector<std::unique_ptr<CoupState>> Children(const std::vector<Action>& actions) const {
+    const Player p = CurrentPlayer();
+    for (Action a : actions)
+      if (a < 0 || a >= COUP_NUM_ACTIONS || !((Q().legal_mask >> a) & 1u) || p == kTerminalPlayerId)
+        throw SpielError("Children: illegal action " + std::to_string(a));
+    detail::Pool& pool = detail::ThePool();
+    std::vector<detail::Pool::Slot> slots;
+    for (size_t k = 0; k < actions.size(); ++k) slots.push_back(pool.Alloc());
+    std::vector<coup_slot_result> res(actions.size());
+    try {
+      std::vector<size_t> done;
+      for (size_t k = 0; k < slots.size(); ++k) {  // group the requests by destination segment
+        if (std::find(done.begin(), done.end(), k) != done.end()) continue;
+        std::vector<coup_slot_req> reqs;
+        std::vector<size_t> ks;
+        for (size_t j = k; j < slots.size(); ++j)
+          if (slots[j].seg == slots[k].seg) {
+            reqs.push_back({slots[j].lane, slot_.lane, (int32_t)actions[j], 0});
+            ks.push_back(j);
+            done.push_back(j);
+          }
+        std::vector<coup_slot_result> part(reqs.size());
+        pool.Ops(slots[k].seg, reqs, slot_.seg, 0, part.data());
+        for (size_t j = 0; j < ks.size(); ++j) {
+          if (!part[j].ok) throw SpielError("Children: illegal action " + std::to_string(actions[ks[j]]));
+          res[ks[j]] = part[j];
+        }
+      }
+    } catch (...) {
+      for (const auto& s : slots) pool.Release(s);
+      throw;
+    }
+    std::vector<std::unique_ptr<CoupState>> out;
+    for (size_t k = 0; k < actions.size(); ++k) {
+      std::vector<PlayerAction> h = history_;
+      h.push_back({p, actions[k]});
+      out.emplace_back(new CoupState(game_, slots[k], std::move(h), res[k]));
+    }
+    return out;
+  }
 
   std::vector<double> Rewards() const { return {(double)Q().rewards[0], (double)Q().rewards[1]}; }
   std::vector<double> Returns() const { return {(double)Q().returns[0], (double)Q().returns[1]}; }
@@ -379,6 +430,9 @@ class CoupState {
   std::array<uint32_t, 4> PackedRecord() const { return Rec(); }
 
  private:
+  CoupState(const CoupGame* game, detail::Pool::Slot slot, std::vector<PlayerAction> history,
+            const coup_slot_result& q)
+      : game_(game), slot_(slot), history_(std::move(history)), q_(q) {}
   // the result of the last op on this lane (every op refreshes it)
   const coup_slot_result& Q() const { return q_; }
   std::array<uint32_t, 4> Rec() const { return {q_.record[0], q_.record[1], q_.record[2], q_.record[3]}; }

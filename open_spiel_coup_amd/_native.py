@@ -24,7 +24,7 @@ SYMBOLS = (
     "coup_set_stream", "coup_batch", "coup_num_players", "coup_state_bytes", "coup_reset", "coup_step", "coup_rollout",
     "coup_new_initial_state", "coup_apply_action", "coup_query",
     "coup_export_state", "coup_import_state", "coup_export_history",
-    "coup_import_history", "coup_error_count", "coup_slot_op", "coup_measure_step_traffic",
+    "coup_import_history", "coup_error_count", "coup_slot_op", "coup_slot_ops", "coup_measure_step_traffic",
 )
 
 # coup_slot_op flags and result layout (coup_slot_result, 128 bytes)
@@ -50,6 +50,12 @@ class QueryOutputs(ctypes.Structure):
 class RolloutStats(ctypes.Structure):
     _fields_ = [("episodes", ctypes.c_void_p), ("return_sum", ctypes.c_void_p),
                 ("length_sum", ctypes.c_void_p)]
+
+
+class SlotReq(ctypes.Structure):
+    """coup_slot_req (24 bytes)."""
+    _fields_ = [("lane", ctypes.c_int64), ("src_lane", ctypes.c_int64), ("action", ctypes.c_int32),
+                ("flags", ctypes.c_int32)]
 
 
 class CoupError(RuntimeError):
@@ -92,6 +98,7 @@ def load():
         "coup_import_history": ([vp, vp], i32),
         "coup_error_count": ([vp, ctypes.POINTER(i64)], i32),
         "coup_slot_op": ([vp, i64, vp, i64, i32, i32, vp], i32),
+        "coup_slot_ops": ([vp, i64, ctypes.POINTER(SlotReq), vp, i32, vp], i32),
         "coup_measure_step_traffic": ([i64, vp, ctypes.POINTER(StepOutputs), vp], i32),
     }
     for name, (args, res) in sig.items():

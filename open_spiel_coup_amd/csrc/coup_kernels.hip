@@ -8,10 +8,12 @@
 // the optional ObservationTensor write-out (784 B per lane and step).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #ifdef COUP_COUNT_PHILOX
 // Measurement builds: [0] wave-level Philox evaluations, [1] lanes active in
@@ -1237,14 +1239,17 @@ __global__ __launch_bounds__(kThreads) void k_query(QueryArgs a) {
 // facade, rl_environment) that is one wave storing alone, ~150 us.  Here the
 // 1246 float4 of a lane are spread over 1246 threads; each thread decodes its
 // lane's record and history bytes itself (L2-resident).
+// reqs (coup_slot_ops): output row l is the lane of request l.
 __global__ __launch_bounds__(kThreads) void k_info_elems(const uint4* __restrict__ state,
                                                         const uint8_t* __restrict__ hist, int64_t n,
-                                                        float* __restrict__ info) {
+                                                        float* __restrict__ info,
+                                                        const coup_slot_req* __restrict__ reqs = nullptr) {
   typedef float v4f __attribute__((ext_vector_type(4)));
   const int64_t g = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (g >= n * kInfoF4) return;
-  const int64_t lane = g / kInfoF4;
-  const uint32_t c = (uint32_t)(g - lane * kInfoF4);
+  const int64_t row = g / kInfoF4;
+  const uint32_t c = (uint32_t)(g - row * kInfoF4);
+  const int64_t lane = reqs ? reqs[row].lane : row;
   const uint32_t p = c >= (uint32_t)kInfoHalfF4 ? 1u : 0u;
   const int f0 = 4 * (int)(c - p * (uint32_t)kInfoHalfF4);
   const Lane L = unpack(state[lane]);
@@ -1346,10 +1351,10 @@ __device__ __noinline__ void slot_result(uint4 w, uint32_t ok, coup_slot_result*
   out->returns[1] = (int8_t)(-r0);
 }
 
+// One State op on one lane by one wave (k_slot: one op per launch;
+// k_slot_batch: one op per block).  hist / bits: the wave's LDS.
 template <bool OBS>
-__global__ __launch_bounds__(64) void k_slot(SlotArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t hist[kHist];
-  __shared__ __attribute__((aligned(16))) uint32_t bits[OBS ? 64 * 8 : 1];
+__device__ __forceinline__ void slot_op(const SlotArgs& a, uint8_t* __restrict__ hist, uint32_t* __restrict__ bits) {
   const uint32_t t = threadIdx.x;
   const uint4* rs = a.src_state ? a.src_state : a.dst_state;
   const uint8_t* hs = a.src_state ? a.src_hist : a.dst_hist;
@@ -1387,6 +1392,45 @@ __global__ __launch_bounds__(64) void k_slot(SlotArgs a) {
     write_obs_wave_bits<0, false>(a.obs, bits, 1u);
   }
 }
+
+template <bool OBS>
+__global__ __launch_bounds__(64) void k_slot(SlotArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t hist[kHist];
+  __shared__ __attribute__((aligned(16))) uint32_t bits[OBS ? 64 * 8 : 1];
+  slot_op<OBS>(a, hist, bits);
+}
+
+// coup_slot_ops: n independent State ops in one launch, block b = request b
+// (a Deep CFR node's children, a frontier of states).  The requests sit in
+// mapped pinned host memory next to the results; the host has checked that
+// no destination lane repeats or is another request's source.
+struct SlotBatchArgs {
+  uint4* state;               // the env's records / histories (destinations)
+  uint8_t* hist;
+  const uint4* src_state;     // the source env's (copies)
+  const uint8_t* src_hist;
+  const coup_slot_req* reqs;  // [n]
+  coup_slot_result* out;      // [n] or null
+  float* obs;                 // [n][2][98] or null
+};
+
+template <bool OBS>
+__global__ __launch_bounds__(64) void k_slot_batch(SlotBatchArgs b) {
+  __shared__ __attribute__((aligned(16))) uint8_t hist[kHist];
+  __shared__ __attribute__((aligned(16))) uint32_t bits[OBS ? 64 * 8 : 1];
+  const coup_slot_req r = b.reqs[blockIdx.x];
+  SlotArgs a;
+  a.dst_state = b.state + r.lane;
+  a.dst_hist = b.hist + r.lane * kHist;
+  a.src_state = r.src_lane >= 0 ? b.src_state + r.src_lane : nullptr;
+  a.src_hist = r.src_lane >= 0 ? b.src_hist + r.src_lane * kHist : nullptr;
+  a.action = r.action;
+  a.init = (r.flags & COUP_SLOT_INIT) ? 1 : 0;
+  a.store = (r.src_lane >= 0 || a.init || r.action >= 0) ? 1 : 0;
+  a.out = b.out ? b.out + blockIdx.x : nullptr;
+  a.obs = OBS ? b.obs + (size_t)blockIdx.x * (2 * kObsSize) : nullptr;
+  slot_op<OBS>(a, hist, bits);
+}
 }  // namespace coup
 
 // ====================================================================== C ABI
@@ -1404,6 +1448,10 @@ struct coup_env {
   hipStream_t stream;
   uint8_t* slot_scratch;  // coup_slot_op results: pinned host memory the kernels write directly (lazy)
   uint8_t* slot_scratch_dev;  // its device address
+  uint8_t* batch_scratch;     // coup_slot_ops: requests + results (mapped pinned, grown on demand)
+  uint8_t* batch_scratch_dev;
+  size_t batch_cap;
+  bool batch_pending;         // an asynchronous coup_slot_ops may still read the requests
 };
 
 namespace {
@@ -1488,6 +1536,7 @@ void release(coup_env* env) {
   (void)hipFree(env->hist);
   (void)hipFree(env->err_count);
   if (env->slot_scratch) (void)hipHostFree(env->slot_scratch);
+  if (env->batch_scratch) (void)hipHostFree(env->batch_scratch);
   delete env;
 }
 
@@ -1529,6 +1578,10 @@ int coup_create_ex(int64_t batch, uint64_t seed, uint32_t env_id_base, int flags
   env->err_count = nullptr;
   env->slot_scratch = nullptr;
   env->slot_scratch_dev = nullptr;
+  env->batch_scratch = nullptr;
+  env->batch_scratch_dev = nullptr;
+  env->batch_cap = 0;
+  env->batch_pending = false;
   const size_t lanes = (size_t)(batch > 0 ? batch : 1);
   hipError_t e = hipMalloc(&env->state, lanes * sizeof(uint4) * (generic ? 2 : 1));
   if (e == hipSuccess) e = hipMalloc(&env->err_count, sizeof(uint32_t));
@@ -1817,6 +1870,96 @@ int coup_slot_op(coup_env* env, int64_t lane, const coup_env* src_env, int64_t s
   const size_t n = sizeof(coup_slot_result) + (obs ? obs_bytes : 0) + (info ? info_bytes : 0);
   COUP_HIP_TRY(hipStreamSynchronize(s));
   std::memcpy(host_out, env->slot_scratch, n);
+  return COUP_OK;
+}
+
+int coup_slot_ops(coup_env* env, int64_t n, const coup_slot_req* reqs, const coup_env* src_env, int flags,
+                  void* host_out) {
+  COUP_CHECK_ENV(env);
+  if (env->generic || !env->hist)
+    return fail(COUP_E_INVALID, "coup_slot_ops: needs a 2-player env created with COUP_FLAG_HISTORY");
+  if (flags & ~(COUP_SLOT_OBS | COUP_SLOT_INFO | COUP_SLOT_NO_RESULT))
+    return fail(COUP_E_INVALID, "coup_slot_ops: unknown flags");
+  if (n < 0 || n > (int64_t(1) << 20)) return fail(COUP_E_INVALID, "coup_slot_ops: n out of range");
+  if (n == 0) return COUP_OK;
+  if (!reqs) return fail(COUP_E_INVALID, "coup_slot_ops: reqs is null");
+  if (src_env && (src_env->generic || !src_env->hist))
+    return fail(COUP_E_INVALID, "coup_slot_ops: src_env needs COUP_FLAG_HISTORY (2 players)");
+  const bool result = !(flags & COUP_SLOT_NO_RESULT);
+  if (result && !host_out) return fail(COUP_E_INVALID, "coup_slot_ops: host_out is null");
+  // every request in range; destinations distinct and not a source of
+  // another request of the same env (the blocks run in any order)
+  std::vector<int64_t> dst((size_t)n), srcs;
+  for (int64_t k = 0; k < n; ++k) {
+    const coup_slot_req& r = reqs[k];
+    if (r.lane < 0 || r.lane >= env->batch) return fail(COUP_E_INVALID, "coup_slot_ops: lane out of range");
+    if (r.flags & ~COUP_SLOT_INIT) return fail(COUP_E_INVALID, "coup_slot_ops: request flags other than INIT");
+    if (r.action < -1 || r.action >= COUP_NUM_ACTIONS) return fail(COUP_E_INVALID, "coup_slot_ops: action out of range");
+    if (r.src_lane >= 0) {
+      if (!src_env) return fail(COUP_E_INVALID, "coup_slot_ops: a request copies but src_env is null");
+      if (r.src_lane >= src_env->batch) return fail(COUP_E_INVALID, "coup_slot_ops: src_lane out of range");
+      if (src_env == env) srcs.push_back(r.src_lane);
+    }
+    dst[(size_t)k] = r.lane;
+  }
+  std::sort(dst.begin(), dst.end());
+  if (std::adjacent_find(dst.begin(), dst.end()) != dst.end())
+    return fail(COUP_E_INVALID, "coup_slot_ops: a destination lane repeats");
+  for (int64_t s : srcs)
+    if (std::binary_search(dst.begin(), dst.end(), s))
+      return fail(COUP_E_INVALID, "coup_slot_ops: a source lane is also a destination");
+  const bool obs = result && (flags & COUP_SLOT_OBS), info = result && (flags & COUP_SLOT_INFO);
+  const size_t obs_bytes = 2u * COUP_OBS_SIZE * sizeof(float), info_bytes = 2u * COUP_INFO_STATE_SIZE * sizeof(float);
+  const size_t req_bytes = ((size_t)n * sizeof(coup_slot_req) + 127u) & ~(size_t)127u;
+  const size_t out_bytes = result ? (size_t)n * (sizeof(coup_slot_result) + (obs ? obs_bytes : 0) +
+                                                  (info ? info_bytes : 0)) : 0;
+  if (env->batch_pending) {
+    // the last (asynchronous) batch may still be reading its requests
+    COUP_HIP_TRY(hipStreamSynchronize(env->stream));
+    env->batch_pending = false;
+  }
+  if (req_bytes + out_bytes > env->batch_cap) {
+    if (env->batch_scratch) (void)hipHostFree(env->batch_scratch);
+    env->batch_scratch = nullptr;
+    env->batch_cap = 0;
+    const size_t cap = std::max<size_t>(req_bytes + out_bytes, 64u << 10);
+    COUP_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&env->batch_scratch), cap,
+                               hipHostMallocMapped | hipHostMallocCoherent));
+    COUP_HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&env->batch_scratch_dev), env->batch_scratch, 0));
+    env->batch_cap = cap;
+  }
+  std::memcpy(env->batch_scratch, reqs, (size_t)n * sizeof(coup_slot_req));
+  uint8_t* dev = env->batch_scratch_dev;
+  coup::SlotBatchArgs b;
+  b.state = env->state;
+  b.hist = env->hist;
+  b.src_state = src_env ? src_env->state : nullptr;
+  b.src_hist = src_env ? src_env->hist : nullptr;
+  b.reqs = reinterpret_cast<const coup_slot_req*>(dev);
+  b.out = result ? reinterpret_cast<coup_slot_result*>(dev + req_bytes) : nullptr;
+  float* obs_out = obs ? reinterpret_cast<float*>(dev + req_bytes + (size_t)n * sizeof(coup_slot_result)) : nullptr;
+  float* info_out = info ? reinterpret_cast<float*>(dev + req_bytes + (size_t)n * (sizeof(coup_slot_result) +
+                                                                                    (obs ? obs_bytes : 0)))
+                         : nullptr;
+  b.obs = obs_out;
+  hipStream_t s = env->stream;
+  if (obs)
+    coup::k_slot_batch<true><<<(unsigned)n, 64, 0, s>>>(b);
+  else
+    coup::k_slot_batch<false><<<(unsigned)n, 64, 0, s>>>(b);
+  COUP_HIP_TRY(hipGetLastError());
+  if (info_out) {
+    const int64_t nf4 = n * coup::kInfoF4;
+    coup::k_info_elems<<<(unsigned)((nf4 + coup::kThreads - 1) / coup::kThreads), coup::kThreads, 0, s>>>(
+        env->state, env->hist, n, info_out, b.reqs);
+    COUP_HIP_TRY(hipGetLastError());
+  }
+  if (!result) {
+    env->batch_pending = true;
+    return COUP_OK;
+  }
+  COUP_HIP_TRY(hipStreamSynchronize(s));
+  std::memcpy(host_out, env->batch_scratch + req_bytes, out_bytes);
   return COUP_OK;
 }
 

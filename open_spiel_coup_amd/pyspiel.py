@@ -146,6 +146,46 @@ class _Pool:
         with self.lock:
             return self._op(slot, src, action, init, obs, info, result)
 
+    def ops(self, seg, reqs, src_seg=None, obs=False, info=False):
+        """coup_slot_ops: the (lane, src_lane, action) requests on segment
+        `seg` (copies from segment `src_seg`) in one launch; returns one
+        result dict per request, like op()."""
+        with self.lock:
+            n = len(reqs)
+            arr = (_native.SlotReq * n)(*[_native.SlotReq(lane, src, action, 0) for lane, src, action in reqs])
+            per = _native.SLOT_RESULT_BYTES
+            nbytes = n * (per + (2 * OBS_SIZE * 4 if obs else 0) + (2 * INFO_STATE_SIZE * 4 if info else 0))
+            if getattr(self, "_batch_host", None) is None or self._batch_host.numel() < nbytes:
+                self._batch_host = torch.empty(max(nbytes, 1 << 16), dtype=torch.uint8, pin_memory=True)
+            env = self.segs[seg]
+            env._bind_stream()
+            flags = (_native.SLOT_OBS if obs else 0) | (_native.SLOT_INFO if info else 0)
+            src_h = self.segs[src_seg]._h if src_seg is not None else None
+            _native.check(self.lib.coup_slot_ops(env._h, n, arr, src_h, flags,
+                                                 ctypes.c_void_p(self._batch_host.data_ptr())))
+            buf = self._batch_host.numpy()[:nbytes]
+            res = buf[:n * per].view(_SLOT_RESULT).copy()
+            off = n * per
+            obs_t = info_t = None
+            if obs:
+                obs_t = buf[off:off + n * 2 * OBS_SIZE * 4].view(np.float32).reshape(n, 2, OBS_SIZE).copy()
+                off += n * 2 * OBS_SIZE * 4
+            if info:
+                info_t = buf[off:off + n * 2 * INFO_STATE_SIZE * 4].view(np.float32).reshape(
+                    n, 2, INFO_STATE_SIZE).copy()
+            out = []
+            for k in range(n):
+                r = res[k]
+                q = {"record": r["record"], "history": r["history"], "legal_mask": int(r["legal_mask"]),
+                     "current_player": int(r["cur_player"]), "terminal": bool(r["terminal"]), "ok": bool(r["ok"]),
+                     "rewards": r["rewards"], "returns": r["returns"]}
+                if obs:
+                    q["obs"] = obs_t[k]
+                if info:
+                    q["info_state"] = info_t[k]
+                out.append(q)
+            return out
+
     def _op(self, slot, src, action, init, obs, info, result):
         flags = ((_native.SLOT_INIT if init else 0) | (_native.SLOT_OBS if obs else 0)
                  | (_native.SLOT_INFO if info else 0) | (0 if result else _native.SLOT_NO_RESULT))
@@ -279,9 +319,12 @@ class CoupGame:
 class CoupState:
     """open_spiel::coup::CoupState (coup.h:111-197) over the GPU engine."""
 
-    def __init__(self, game, _src=None, _history=None, _q=None):
+    def __init__(self, game, _src=None, _history=None, _q=None, _slot=None):
         self._game = game
         self._pool = game._pool if game._pool is not None else game._bind_pool()
+        if _slot is not None:  # filled by a batched op (children / apply_actions)
+            self._slot, self._q, self._history = _slot, _q, _history
+            return
         self._slot = self._pool.alloc()
         if _src is None:
             self._q = self._pool.op(self._slot, init=True)
@@ -418,6 +461,48 @@ class CoupState:
         c.apply_action(action)
         return c
 
+    def children(self, actions, obs=False, info_state=False):
+        """[self.child(a) for a in actions] in one launch per pool segment
+        (coup_slot_ops: each child is a device-side copy of this lane plus
+        ApplyAction).  Deep CFR expands every legal action of a traverser
+        node this way (deep_cfr.py:440-471).  With obs / info_state the
+        children's tensors come back with the same round trip."""
+        actions = [int(a) for a in actions]
+        player, mask = self.current_player(), self._mask()
+        for a in actions:
+            if not 0 <= a < 18 or not (mask >> a) & 1 or player == PlayerId.TERMINAL:
+                raise SpielError(f"illegal action {a}")
+        if not actions:
+            return []
+        pool = self._pool
+        slots = [pool.alloc() for _ in actions]
+        out = [None] * len(actions)
+        try:
+            by_seg = {}
+            for k, s in enumerate(slots):
+                by_seg.setdefault(s[0], []).append(k)
+            for seg, ks in by_seg.items():
+                res = pool.ops(seg, [(slots[k][1], self._slot[1], actions[k]) for k in ks], src_seg=self._slot[0],
+                               obs=obs, info=info_state)
+                for k, q in zip(ks, res):
+                    if not q["ok"]:
+                        raise SpielError(f"illegal action {actions[k]}")
+                    out[k] = CoupState(self._game, _slot=slots[k], _q=q,
+                                       _history=self._history + [(player, actions[k])])
+        except Exception:
+            for k, s in enumerate(slots):
+                if out[k] is None:
+                    pool.release(s)
+            raise
+        return out
+
+    def legal_children(self, obs=False, info_state=False):
+        """[(a, self.child(a)) for a in self.legal_actions()] in one launch:
+        the frontier of a traverser node (deep_cfr.py:440-471) or of a chance
+        node (the chance outcomes, in ascending order)."""
+        acts = self.legal_actions()
+        return list(zip(acts, self.children(acts, obs=obs, info_state=info_state)))
+
     def clone(self):
         return CoupState(self._game, _src=(self._pool.handle(self._slot), self._slot[1]),
                          _history=list(self._history), _q=self._q)
@@ -489,6 +574,37 @@ class CoupState:
 
     def history_bytes(self):
         return self._hist.copy()
+
+
+def apply_actions(states, actions):
+    """states[k].apply_action(actions[k]) for every k, one launch per pool
+    segment (coup_slot_ops): a frontier of independent games advanced
+    together (MCCFR walkers, many rl_environment-style games).  The states
+    must be distinct objects.  Raises SpielError before launching if any
+    action is illegal."""
+    states, actions = list(states), [int(a) for a in actions]
+    if len(states) != len(actions):
+        raise ValueError("one action per state")
+    if len({id(s) for s in states}) != len(states):
+        raise ValueError("apply_actions needs distinct states")
+    players = []
+    for st, a in zip(states, actions):
+        p = st.current_player()
+        if not 0 <= a < 18 or not (st._mask() >> a) & 1 or p == PlayerId.TERMINAL:
+            raise SpielError(f"illegal action {a}")
+        players.append(p)
+    by_pool = {}
+    for k, st in enumerate(states):
+        by_pool.setdefault((id(st._pool), st._slot[0]), []).append(k)
+    for (_, seg), ks in by_pool.items():
+        pool = states[ks[0]]._pool
+        res = pool.ops(seg, [(states[k]._slot[1], -1, actions[k]) for k in ks])
+        for k, q in zip(ks, res):
+            if not q["ok"]:
+                states[k]._q = pool.op(states[k]._slot)
+                raise SpielError(f"illegal action {actions[k]}")
+            states[k]._q = q
+            states[k]._history = states[k]._history + [(players[k], actions[k])]
 
 
 def load_game(name, params=None):

@@ -3,8 +3,10 @@
 // it with the reference's golden transcript.  Test tooling.
 //   state_driver <action> <action> ...      (the history to replay)
 //   state_driver --illegal                  (error behaviour check)
+//   state_driver --children                 (batched Children == Child one by one)
 #include <cstdio>
 #include <cstdlib>
+#include <random>
 #include <string>
 
 #include "coup_mi355x.hpp"
@@ -78,6 +80,29 @@ int main(int argc, char** argv) {
   try {
     auto game = LoadGame("coup");
     auto state = game->NewInitialState();
+    if (argc == 2 && std::string(argv[1]) == "--children") {
+      std::mt19937 rng(5);
+      int checked = 0;
+      for (int game_no = 0; game_no < 6; ++game_no) {
+        auto st = game->NewInitialState();
+        for (int d = 0; d < 100 && !st->IsTerminal(); ++d) {
+          const auto legal = st->LegalActions();
+          auto kids = st->Children(legal);
+          for (size_t k = 0; k < legal.size(); ++k) {
+            auto c = st->Child(legal[k]);
+            if (c->PackedRecord() != kids[k]->PackedRecord() || c->History() != kids[k]->History() ||
+                c->LegalActions() != kids[k]->LegalActions() || c->ToString() != kids[k]->ToString()) {
+              std::printf("{\"mismatch\":%s}\n", List(c->History()).c_str());
+              return 1;
+            }
+            ++checked;
+          }
+          st = std::move(kids[rng() % kids.size()]);
+        }
+      }
+      std::printf("{\"children_checked\":%d}\n", checked);
+      return 0;
+    }
     if (argc == 2 && std::string(argv[1]) == "--illegal") {
       for (int a : {4, 3, 2, 0}) state->ApplyAction(a);
       const auto before = state->History();

@@ -79,3 +79,12 @@ def test_cpp_state_errors_clone_child(driver):
     assert r["illegal"] == "rejected"
     assert r["history"] == [4, 3, 2, 0] and r["clone"] == [4, 3, 2, 0]
     assert r["child"] == [4, 3, 2, 0, 0] and r["roundtrip"] == [4, 3, 2, 0, 0]
+
+
+@pytest.mark.gpu
+def test_cpp_batched_children_equal_child(driver):
+    """coup_amd::CoupState::Children (one coup_slot_ops launch for all legal
+    actions) == Child(a) one by one, along six random games."""
+    out = subprocess.run([driver, "--children"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert json.loads(out.stdout)["children_checked"] > 100

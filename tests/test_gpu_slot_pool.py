@@ -131,3 +131,85 @@ def test_facade_op_latency_report():
         st.clone()
     t2 = time.perf_counter()
     print(f"\nfacade: child+legal_actions {1e6 * (t1 - t0) / n:.1f} us, clone {1e6 * (t2 - t1) / n:.1f} us")
+
+
+def test_tree_walk_through_batched_children_matches_oracle():
+    """The Deep CFR-shaped walk with every node's expansion done by ONE
+    batched call (CoupState.legal_children -> coup_slot_ops: all legal
+    children of a traverser node, deep_cfr.py:440-471), recursing into up
+    to 3 of them, to depth 8; every node against the oracle, tensors
+    (returned by the same batched call) on a sample.  The parent is
+    untouched."""
+    rng = np.random.default_rng(11)
+    game = pyspiel.load_game("coup")
+    nodes = [0]
+
+    def walk(st, ref, depth):
+        nodes[0] += 1
+        if st.is_terminal() or depth == 0:
+            return
+        want_tensors = nodes[0] % 7 == 0
+        kids = st.legal_children(obs=want_tensors, info_state=want_tensors)
+        assert [a for a, _ in kids] == ref.legal_actions()
+        for a, ch in kids:
+            r2 = ref.clone()
+            r2.apply_action(a)
+            _same(ch, r2, tensors=want_tensors)
+        for k in rng.permutation(len(kids))[:3 if not st.is_chance_node() else 2]:
+            a, ch = kids[k]
+            r2 = ref.clone()
+            r2.apply_action(a)
+            walk(ch, r2, depth - 1)
+        _same(st, ref)
+
+    root, r0 = game.new_initial_state(), oracle.OracleState()
+    _same(root, r0)
+    walk(root, r0, 8)
+    assert nodes[0] > 200
+
+
+def test_apply_actions_advances_a_frontier():
+    """pyspiel.apply_actions: one action on each of 600 independent states in
+    one launch per segment == the oracle, and illegal actions are refused
+    before anything is applied."""
+    rng = np.random.default_rng(3)
+    game = pyspiel.load_game("coup")
+    states = [game.new_initial_state() for _ in range(600)]
+    refs = [oracle.OracleState() for _ in states]
+    for _ in range(40):
+        live = [k for k, r in enumerate(refs) if not r.is_terminal()]
+        if not live:
+            break
+        acts = [int(rng.choice(refs[k].legal_actions())) for k in live]
+        pyspiel.apply_actions([states[k] for k in live], acts)
+        for k, a in zip(live, acts):
+            refs[k].apply_action(a)
+    for st, ref in zip(states, refs):
+        _same(st, ref)
+    st = states[0]
+    before = st.packed_record().tolist()
+    if not st.is_terminal():
+        with pytest.raises(pyspiel.SpielError):
+            pyspiel.apply_actions([st], [17 if 17 not in st.legal_actions() else 18])
+    assert st.packed_record().tolist() == before
+    with pytest.raises(ValueError):
+        pyspiel.apply_actions([st, st], [0, 0])
+
+
+def test_slot_ops_rejects_dependent_requests():
+    """coup_slot_ops requires independent requests: a repeated destination
+    lane, or a destination that is another request's source, is refused
+    before any launch (COUP_E_INVALID)."""
+    import ctypes
+    from open_spiel_coup_amd import _native
+    game = pyspiel.load_game("coup")
+    st = game.new_initial_state()
+    pool = st._pool
+    env = pool.segs[st._slot[0]]
+    R = _native.SlotReq
+    host = (ctypes.c_uint8 * (128 * 4))()
+    for reqs in ([R(5, -1, -1, 0), R(5, -1, -1, 0)], [R(6, 7, -1, 0), R(7, -1, -1, 0)],
+                 [R(1 << 20, -1, -1, 0)], [R(3, -1, 18, 0)]):
+        arr = (R * len(reqs))(*reqs)
+        rc = pool.lib.coup_slot_ops(env._h, len(reqs), arr, env._h, 0, host)
+        assert rc == _native.COUP_E_INVALID, pool.lib.coup_last_error()

@@ -1,7 +1,9 @@
 """Per-op latency of the per-game State facade: the lane pool (coup_slot_op,
 one launch + one 128-byte read-back per answered op) against the previous
 design (one-lane scratch env: import record + history, apply, error count,
-export record + history), timed in one process.  Measurement tool only."""
+export record + history), and the batched ops (coup_slot_ops: n children of
+one node, or one action on each of n states, per launch), timed in one
+process.  Measurement tool only."""
 import json
 import os
 import sys
@@ -60,6 +62,29 @@ def main(n=2000):
         r2, h2 = scratch_apply(env, rec, hist, 0)
         scratch_query(env, r2, h2)
     scratch_child = (time.perf_counter() - t0) / n
+    # batched: all children of one node in one call, per child
+    batched = {}
+    for k in (1, 7, 64, 1024):
+        acts = [0] * k
+        for _ in range(5):
+            st.children(acts)
+        reps = max(20, n // k)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            st.children(acts)
+        batched[f"children_n{k}_us_per_child"] = round(1e6 * (time.perf_counter() - t0) / (reps * k), 2)
+        t0 = time.perf_counter()
+        for _ in range(max(5, reps // 4)):
+            st.children(acts, info_state=True)
+        batched[f"children_n{k}_with_info_state_us_per_child"] = round(
+            1e6 * (time.perf_counter() - t0) / (max(5, reps // 4) * k), 2)
+    frontier = [st.clone() for _ in range(1024)]
+    for _ in range(3):
+        pyspiel.apply_actions(frontier, [0] * 1024)
+        frontier = [st.clone() for _ in range(1024)]
+    t0 = time.perf_counter()
+    pyspiel.apply_actions(frontier, [0] * 1024)
+    batched["apply_actions_n1024_us_per_state"] = round(1e6 * (time.perf_counter() - t0) / 1024, 2)
     from open_spiel_coup_amd import rl_environment
     renv = rl_environment.Environment("coup", seed=3)
     ts = renv.reset()
@@ -85,7 +110,7 @@ def main(n=2000):
                       "pool_child_plus_legal_us": round(1e6 * pool_child, 1),
                       "pool_clone_us": round(1e6 * pool_clone, 1),
                       "pool_observation_tensor_us": round(1e6 * pool_obs, 1),
-                      "scratch_env_child_plus_legal_us": round(1e6 * scratch_child, 1)}))
+                      "scratch_env_child_plus_legal_us": round(1e6 * scratch_child, 1), **batched}))
 
 
 if __name__ == "__main__":
