@@ -83,8 +83,9 @@ static void dump(const void* st, const long* hist, int nhist) {
   StateReturns(st, ret);
   printf(",\"returns\":[%g,%g],\"player_return1\":%g", ret[0], ret[1], StatePlayerReturn(st, 1));
   free(ret);
+  char* str = StateToString(st, &n); /* n is set by the call: never read it in the same expression */
   printf(",\"to_string\":");
-  put_string(StateToString(st, &n), n);
+  put_string(str, n);
   const int osz = StateObservationTensorSize(st), isz = StateInformationStateTensorSize(st);
   float* obs = (float*)malloc(sizeof(float) * osz);
   float* info = (float*)malloc(sizeof(float) * isz);
@@ -99,10 +100,12 @@ static void dump(const void* st, const long* hist, int nhist) {
   free(obs);
   free(info);
   if (cur >= 0) { /* the no-argument strings are for the current player (spiel.h:484-486, 543-545) */
+    str = StateObservationString(st, &n);
     printf(",\"obs_str\":");
-    put_string(StateObservationString(st, &n), n);
+    put_string(str, n);
+    str = StateInformationStateString(st, &n);
     printf(",\"info_str\":");
-    put_string(StateInformationStateString(st, &n), n);
+    put_string(str, n);
   }
   printf("}\n");
 }
