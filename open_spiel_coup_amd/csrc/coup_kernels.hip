@@ -1136,6 +1136,7 @@ __global__ __launch_bounds__(kThreads) void k_reset(uint4* state, int64_t n, con
   if (mask && mask[i] == 0) return;
   const uint32_t ep = mode == 0 ? 0u : unpack(state[i]).episode + 1u;
   Lane L = initial_lane(ep);
+  L.err = (mode != 0 && L.episode == 0u) ? 1u : 0u;  // counter wrap (coup_lane.h kEpisodeMask)
   if (deal) {
     Rng rng{seed_lo, seed_hi, lane_stream_id(env_id_base, i), 0u, make_uint4(0, 0, 0, 0)};
     if (hist) {

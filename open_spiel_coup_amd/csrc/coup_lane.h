@@ -35,7 +35,11 @@ constexpr uint32_t kEmptyHand = 0xFFFFu;
 constexpr uint32_t kInitialDeck = 0x33333u;  // kNumEachCardInDeck = 3 of each type
 constexpr uint32_t kMaxGameLength = 90;      // coup.h:219
 constexpr uint32_t kChanceFlag = 1u << 31;
-constexpr uint32_t kEpisodeMask = 0x1FFFFFFu;  // 25-bit episode counter
+// 28-bit episode counter: w3 [31:7] holds bits 24..0, w2 [31:29] bits 27..25.
+// It keys the lane's Philox counter, so past 2^28 episodes a lane would
+// replay its first games: the wrap sets the record's error flag instead of
+// passing silently (new_episode).
+constexpr uint32_t kEpisodeMask = 0xFFFFFFFu;
 
 struct Lane {
   uint32_t h0, h1;      // hands of P1 / P2 (16-bit nibble strings)
@@ -73,7 +77,7 @@ __device__ __forceinline__ Lane unpack(uint4 w) {
   L.begin = (w.z >> 21) & 1u;
   L.move = (w.z >> 22) & 0x7Fu;
   L.turn = w.w & 0x7Fu;
-  L.episode = w.w >> 7;
+  L.episode = (w.w >> 7) | ((w.z >> 29) << 25);
   return L;
 }
 
@@ -82,8 +86,8 @@ __device__ __forceinline__ uint4 pack(const Lane& L) {
   w.x = L.h0 | (L.h1 << 16);
   w.y = L.deck | (L.c0 << 20) | (L.c1 << 24) | ((uint32_t)(L.r0 + 2) << 28) | (L.err << 31);
   w.z = L.l0 | (L.l1 << 5) | (L.lost0 << 10) | (L.lost1 << 11) | (L.qlen << 12) | (L.qids << 15) |
-        (L.T << 19) | (L.M << 20) | (L.begin << 21) | (L.move << 22);
-  w.w = L.turn | ((L.episode & kEpisodeMask) << 7);
+        (L.T << 19) | (L.M << 20) | (L.begin << 21) | (L.move << 22) | (((L.episode >> 25) & 7u) << 29);
+  w.w = L.turn | (L.episode << 7);
   return w;
 }
 
@@ -684,6 +688,7 @@ __device__ __forceinline__ void resolve_chance(Lane& L, Rng& rng) {
 template <class H>
 __device__ __forceinline__ Lane new_episode(uint32_t episode, Rng& rng, H& hist) {
   Lane L = initial_lane(episode);
+  L.err = L.episode == 0u ? 1u : 0u;  // the counter wrapped: this stream repeats episode 0's
   uint32_t t[4];
 #pragma unroll
   for (uint32_t k = 0; k < 4u; ++k) {

@@ -14,8 +14,9 @@
 //   w5      deck [19:0] | initial deals left [23:20] | queue length [25:24] |
 //           queue player [28:26] | turn player T [31:29]
 //   w6      move [8:0] | turn [17:9] | mover M [20:18] | counterpart O [23:21] |
-//           reward loser [26:24]
-//   w7      episode [24:0]
+//           reward loser [26:24] | episode bits 29..25 [31:27]
+//   w7      episode bits 24..0 [24:0] (30-bit counter; [29:25] park the
+//           regrouped step's next decision, coup_nplayer.hip)
 // Rewards() is (loser, count): one decision makes at most one player lose
 // cards, -(N-1) per card to the loser and +1 to everybody else.  Deals
 // queued after the initial ones always go to one player (replacement card
@@ -30,6 +31,15 @@
 
 namespace coup {
 namespace np {
+
+// 30-bit episode counter (the Philox counter word of the lane's draws);
+// past 2^30 episodes a lane would replay its first games, so the wrap sets
+// the record's error flag (new_episode).  kNpEpisodeLo: its bits in w7.
+constexpr uint32_t kNpEpisodeMask = 0x3FFFFFFFu;
+constexpr uint32_t kNpEpisodeLo = 0x1FFFFFFu;
+
+// episode of a packed record's second plane
+__device__ __forceinline__ uint32_t plane_episode(const uint4& b) { return (b.w & kNpEpisodeLo) | ((b.z >> 27) << 25); }
 
 constexpr uint32_t kMaxSeats = 6;
 
@@ -67,7 +77,7 @@ __device__ __forceinline__ NLane<N> unpack(uint4 a, uint4 b) {
   L.M = (b.z >> 18) & 7u;
   L.O = (b.z >> 21) & 7u;
   L.rloser = (b.z >> 24) & 7u;
-  L.episode = b.w & kEpisodeMask;
+  L.episode = plane_episode(b);
   return L;
 }
 
@@ -79,8 +89,8 @@ __device__ __forceinline__ void pack(const NLane<N>& L, uint4& a, uint4& b) {
   a.w = L.coins | (L.lost << 24) | (L.begin << 30) | (L.err << 31);
   b.x = L.last | (L.rcount << 30);
   b.y = L.deck | (L.init_left << 20) | (L.qlen << 24) | ((L.qlen ? L.qp : 0u) << 26) | (L.T << 29);
-  b.z = L.move | (L.turn << 9) | (L.M << 18) | (L.O << 21) | (L.rloser << 24);
-  b.w = L.episode & kEpisodeMask;
+  b.z = L.move | (L.turn << 9) | (L.M << 18) | (L.O << 21) | (L.rloser << 24) | (((L.episode >> 25) & 31u) << 27);
+  b.w = L.episode & kNpEpisodeLo;
 }
 
 // NewInitialState: deck 3 of each, no cards dealt yet (2N initial deals go
@@ -106,7 +116,7 @@ __device__ __forceinline__ NLane<N> initial_lane(uint32_t episode) {
   L.err = 0;
   L.move = 0;
   L.turn = 0;
-  L.episode = episode & kEpisodeMask;
+  L.episode = episode & kNpEpisodeMask;
   L.rloser = 0;
   L.rcount = 0;
   return L;
@@ -598,6 +608,7 @@ __device__ __forceinline__ void resolve_chance(NLane<N>& L, NRng& rng) {
 template <int N>
 __device__ __forceinline__ NLane<N> new_episode(uint32_t episode, NRng& rng) {
   NLane<N> L = initial_lane<N>(episode);
+  L.err = L.episode == 0u ? 1u : 0u;  // the counter wrapped: this stream repeats episode 0's
   uint32_t t[2 * N];
 #pragma unroll
   for (int k = 0; k < 2 * N; ++k) {

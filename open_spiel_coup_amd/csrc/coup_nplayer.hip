@@ -257,7 +257,7 @@ __global__ __launch_bounds__(kThreads) void k_step_sorted(StepArgs a) {
     const uint32_t slot = s_reset[j];
     NRng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, base + (s_meta[slot] & 255u)), 0u,
              make_uint4(0, 0, 0, 0)};
-    const NLane<N> R = new_episode<N>((s_b[slot].w & kEpisodeMask) + 1u, rng);
+    const NLane<N> R = new_episode<N>(plane_episode(s_b[slot]) + 1u, rng);
     uint4 wa, wb;
     pack(R, wa, wb);
     s_a[slot] = wa;
@@ -446,8 +446,9 @@ __global__ __launch_bounds__(kThreads) void k_reset(uint4* sa, uint4* sb, int64_
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= n) return;
   if (mask && mask[i] == 0) return;
-  const uint32_t ep = mode == 0 ? 0u : (sb[i].w & kEpisodeMask) + 1u;
+  const uint32_t ep = mode == 0 ? 0u : plane_episode(sb[i]) + 1u;
   NLane<N> L = initial_lane<N>(ep);
+  L.err = (mode != 0 && L.episode == 0u) ? 1u : 0u;  // counter wrap (coup_nlane.h kNpEpisodeMask)
   if (deal) {
     NRng rng{seed_lo, seed_hi, lane_stream_id(env_id_base, i), 0u, make_uint4(0, 0, 0, 0)};
     resolve_chance(L, rng);
@@ -564,7 +565,7 @@ __global__ __launch_bounds__(kThreads) void k_export(const uint4* sa, const uint
   if (i >= n) return;
   dst[2 * i] = sa[i];
   uint4 b = sb[i];
-  b.w &= kEpisodeMask;  // a parked decision (k_step_sorted) is not state
+  b.w &= kNpEpisodeLo;  // a parked decision (k_step_sorted) is not state
   dst[2 * i + 1] = b;
 }
 
@@ -573,7 +574,7 @@ __global__ __launch_bounds__(kThreads) void k_import(uint4* sa, uint4* sb, int64
   if (i >= n) return;
   sa[i] = src[2 * i];
   uint4 b = src[2 * i + 1];
-  b.w &= kEpisodeMask;
+  b.w &= kNpEpisodeLo;
   sb[i] = b;
 }
 

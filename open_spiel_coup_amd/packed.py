@@ -10,8 +10,9 @@ the HIP kernels.
   w2  [4:0] P1 last action (31 = None), [9:5] P2 last action, [10] P1 lost
       challenge, [11] P2 lost challenge, [14:12] deal-queue length,
       [18:15] deal-queue players (entry j = bit 15+j, front first),
-      [19] turn player, [20] move player, [21] turn begin, [28:22] move number
-  w3  [6:0] turn number, [31:7] episode (25 bits)
+      [19] turn player, [20] move player, [21] turn begin, [28:22] move number,
+      [31:29] episode bits 27..25
+  w3  [6:0] turn number, [31:7] episode bits 24..0 (28-bit episode counter)
 """
 import numpy as np
 
@@ -45,7 +46,7 @@ def decode(words):
         "turn_begin": (z >> 21) & 1,
         "move_number": (z >> 22) & 0x7F,
         "turn_number": v & 0x7F,
-        "episode": v >> 7,
+        "episode": (v >> 7) | ((z >> 29) << 25),
     }
     return d
 

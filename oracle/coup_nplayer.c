@@ -507,15 +507,15 @@ void np_pack(const np_state* s, uint32_t episode, uint32_t* w) {
   w[4] = last | (rcount << 30);
   w[5] = deck | ((uint32_t)s->init_left << 20) | ((uint32_t)s->qlen << 24) | (qp << 26) | ((uint32_t)s->T << 29);
   w[6] = (uint32_t)s->move | ((uint32_t)s->turn << 9) | ((uint32_t)s->M << 18) | ((uint32_t)s->O << 21) |
-         (rloser << 24);
-  w[7] = episode & 0x1FFFFFFu;
+         (rloser << 24) | (((episode >> 25) & 31u) << 27);
+  w[7] = episode & 0x1FFFFFFu; /* 30-bit episode: bits 24..0 here, 29..25 in w[6] */
 }
 
 /* ------------------------------------------------------------- rollouts */
 
 static void resolve(np_state* s, uint64_t seed, uint32_t env, uint32_t ep) {
   while (np_current_player(s) == -1) {
-    uint32_t u = oc_draw(seed, env, ep, (uint32_t)s->move);
+    uint32_t u = oc_draw(seed, env, ep & NP_EPISODE_MASK, (uint32_t)s->move);
     int total = 0;
     for (int t = 0; t < 5; ++t) total += s->deck[t];
     uint32_t r = (uint32_t)(((uint64_t)u * (uint32_t)total) >> 32), cum = 0;
@@ -551,7 +551,7 @@ int np_rollout(const np_rollout_args* a) {
         st = 0;
       } else {
         uint32_t m = np_legal_mask(&s);
-        uint32_t u = oc_draw(a->seed, env, ep, (uint32_t)s.move);
+        uint32_t u = oc_draw(a->seed, env, ep & NP_EPISODE_MASK, (uint32_t)s.move);
         uint32_t idx = (uint32_t)(((uint64_t)u * (uint32_t)__builtin_popcount(m)) >> 32);
         for (uint32_t k = 0; k < idx; ++k) m &= m - 1;
         act = __builtin_ctz(m);

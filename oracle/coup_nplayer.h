@@ -35,6 +35,7 @@ extern "C" {
 
 #define NP_MAX_PLAYERS 6
 #define NP_MAX_HIST 300
+#define NP_EPISODE_MASK 0x3FFFFFFFu /* 30-bit episode counter of the N-player record */
 
 typedef struct {
   int value, state;

@@ -769,8 +769,8 @@ void oc_pack(const oc_state* s, uint32_t episode, uint32_t err, uint32_t* w) {
   w[2] = last0 | (last1 << 5) | ((uint32_t)s->pl[0].lost_challenge << 10) |
          ((uint32_t)s->pl[1].lost_challenge << 11) | ((uint32_t)s->qlen << 12) | (q << 15) |
          ((uint32_t)s->turn_player << 19) | ((uint32_t)s->move_player << 20) |
-         ((uint32_t)s->turn_begin << 21) | ((uint32_t)s->move_number << 22);
-  w[3] = (uint32_t)s->turn_number | ((episode & 0x1FFFFFFu) << 7);
+         ((uint32_t)s->turn_begin << 21) | ((uint32_t)s->move_number << 22) | (((episode >> 25) & 7u) << 29);
+  w[3] = (uint32_t)s->turn_number | ((episode & 0x1FFFFFFu) << 7); /* 28-bit episode: bits 24..0 here */
 }
 
 void oc_history_bytes(const oc_state* s, uint8_t* out) {
@@ -813,7 +813,7 @@ uint32_t oc_draw(uint64_t seed, uint32_t env_id, uint32_t episode, uint32_t draw
   /* One 32-bit draw per history slot: key = (env id, seed lo),
    * counter = (slot / 4, episode, seed hi, 'Coup'), word = slot % 4. */
   uint32_t key[2] = {env_id, (uint32_t)seed};
-  uint32_t ctr[4] = {draw_idx >> 2, episode & 0x1FFFFFFu, (uint32_t)(seed >> 32), 0x436F7570u};
+  uint32_t ctr[4] = {draw_idx >> 2, episode, (uint32_t)(seed >> 32), 0x436F7570u}; /* episode as stored */
   uint32_t out[4];
   oc_philox4x32_10(ctr, key, out);
   return out[draw_idx & 3];
@@ -842,7 +842,7 @@ static int sample_uniform(const oc_state* s, uint32_t u) {
 static void resolve_chance(oc_state* s, uint64_t seed, uint32_t env_id, uint32_t episode) {
   /* rl_environment._sample_external_events (rl_environment.py:369-382) */
   while (oc_current_player(s) == -1) {
-    uint32_t u = oc_draw(seed, env_id, episode, (uint32_t)s->move_number);
+    uint32_t u = oc_draw(seed, env_id, episode & OC_EPISODE_MASK, (uint32_t)s->move_number);
     oc_apply_action(s, sample_chance(s, u));
   }
 }
@@ -868,7 +868,7 @@ int oc_rollout(const oc_rollout_args* a) {
         pending_reset = 0;
         st = 0; /* FIRST */
       } else {
-        uint32_t u = oc_draw(a->seed, env_id, episode, (uint32_t)s.move_number);
+        uint32_t u = oc_draw(a->seed, env_id, episode & OC_EPISODE_MASK, (uint32_t)s.move_number);
         int action = sample_uniform(&s, u);
         act = (int8_t)action;
         oc_apply_action(&s, action);

@@ -114,7 +114,11 @@ void oc_history_bytes(const oc_state* s, uint8_t* out96);
 
 /* --- Sampling contract --------------------------------------------------- */
 void oc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+/* `episode` enters the counter as given; callers pass it masked to the
+ * record's width (OC_EPISODE_MASK: 28 bits for 2 players; the N-player
+ * record keeps 30, NP_EPISODE_MASK) */
 uint32_t oc_draw(uint64_t seed, uint32_t env_id, uint32_t episode, uint32_t draw_idx);
+#define OC_EPISODE_MASK 0xFFFFFFFu
 
 /* --- Batched rollout driver (uniform random policy) ----------------------
  * Mirrors the batched step of the product: per lane and per step, sample a

@@ -113,3 +113,17 @@ def test_slot_result_layout_matches_header(tmp_path):
     for f in fields:
         assert int(got[f]) == dt.fields[f][1], f
     assert int(got["size"]) == dt.itemsize == _native.SLOT_RESULT_BYTES
+
+
+def test_episode_counter_is_28_bits_in_the_record():
+    """The 2-player record keeps a 28-bit episode (w3 [31:7] + w2 [31:29]):
+    the oracle's packing and the host decoder agree up to 2^28 - 1 and the
+    other fields are untouched."""
+    st = oracle.OracleState()
+    for a in (0, 1, 2, 3, 0):
+        st.apply_action(a)
+    base = packed.lane(np.array([st.pack(0)], np.uint32))
+    for ep in (1, (1 << 25) - 1, 1 << 25, (1 << 28) - 1):
+        r = packed.lane(np.array([st.pack(ep)], np.uint32))
+        assert r["episode"] == ep
+        assert {k: v for k, v in r.items() if k != "episode"} == {k: v for k, v in base.items() if k != "episode"}

@@ -471,3 +471,39 @@ def test_trajectory_collection_matches_stepwise(graph):
         np.testing.assert_array_equal(_np(buf["actions"][t]), ref["actions"][t])
         np.testing.assert_array_equal(_np(buf["obs"][t]), ref["obs"][t])
     np.testing.assert_array_equal(_np(env.export_state()), _np(twin.export_state()))
+
+
+@pytest.mark.parametrize("players", [2, 6])
+def test_episode_counter_wrap_is_flagged(players):
+    """Each lane's episode number keys its Philox counter (DESIGN.md section
+    4).  Near the top of the counter (2^28 for 2 players, 2^30 for N) the
+    lanes keep stepping; the episode that wraps to 0 -- whose stream would
+    repeat the lane's first game -- carries the record's error flag, and
+    the episodes before and after it do not."""
+    n = 512
+    env = BatchedCoupEnv(n, seed=9, obs=False, num_players=players, episode_stats=True)
+    w = env.export_state().cpu().numpy().view(np.uint32).copy()
+    top = (1 << 28) - 2 if players == 2 else (1 << 30) - 2
+    if players == 2:  # w3 [31:7] bits 24..0, w2 [31:29] bits 27..25
+        w[:, 3] = (w[:, 3] & 0x7F) | ((top & 0x1FFFFFF) << 7)
+        w[:, 2] = (w[:, 2] & 0x1FFFFFFF) | (((top >> 25) & 7) << 29)
+    else:  # w7 bits 24..0, w6 [31:27] bits 29..25
+        w[:, 7] = top & 0x1FFFFFF
+        w[:, 6] = (w[:, 6] & 0x07FFFFFF) | (((top >> 25) & 31) << 27)
+    env.import_state(torch.from_numpy(w.view(np.int32)))
+
+    def episode_and_err(words):
+        if players == 2:
+            d = packed.decode(words)
+            return d["episode"], d["error"]
+        ww = words.astype(np.int64)
+        return (ww[:, 7] & 0x1FFFFFF) | ((ww[:, 6] >> 27) << 25), (ww[:, 3] >> 31) & 1
+
+    seen_zero = np.zeros(n, bool)
+    for _ in range(80):
+        env.step()
+        ep, err = episode_and_err(env.export_state().cpu().numpy().view(np.uint32))
+        assert np.all(err[ep == 0] == 1)
+        assert np.all(err[ep != 0] == 0)
+        seen_zero |= ep == 0
+    assert seen_zero.sum() > n // 2

@@ -50,14 +50,15 @@ def _to_2p_record(w8):
     last, rcount = w[4] & 0x3FFFFFFF, w[4] >> 30
     deck, qlen, qp, T = w[5] & 0xFFFFF, (w[5] >> 24) & 3, (w[5] >> 26) & 7, w[5] >> 29
     move, turn, M, rloser = w[6] & 0x1FF, (w[6] >> 9) & 0x1FF, (w[6] >> 18) & 7, (w[6] >> 24) & 7
-    ep = w[7] & 0x1FFFFFF
+    ep = (w[7] & 0x1FFFFFF) | ((w[6] >> 27) << 25)  # 30-bit N-player episode
     r0 = -rcount if rloser == 0 else rcount
     qids = (1 << qlen) - 1 if qp == 1 else 0
     return [w[0],
             deck | ((coins & 0xF) << 20) | (((coins >> 4) & 0xF) << 24) | ((r0 + 2) << 28) | (err << 31),
             (last & 31) | (((last >> 5) & 31) << 5) | ((lost & 1) << 10) | (((lost >> 1) & 1) << 11) |
-            (qlen << 12) | (qids << 15) | (T << 19) | (M << 20) | (begin << 21) | (move << 22),
-            turn | (ep << 7)]
+            (qlen << 12) | (qids << 15) | (T << 19) | (M << 20) | (begin << 21) | (move << 22) |
+            (((ep >> 25) & 7) << 29),
+            turn | ((ep & 0x1FFFFFF) << 7)]
 
 
 @pytest.mark.parametrize("auto_reset", [True, False])
