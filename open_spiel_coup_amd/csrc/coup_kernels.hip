@@ -1314,11 +1314,20 @@ struct SlotArgs {
   float* obs;              // [2][98] or null
 };
 
+// -DCOUP_SLOT_INLINE (measurement / investigation builds, DESIGN.md section
+// 12): the two pieces below inlined into the wave-uniform k_slot, the form
+// that produced wrong records.
+#ifdef COUP_SLOT_INLINE
+#define COUP_SLOT_FN __forceinline__
+#else
+#define COUP_SLOT_FN __noinline__
+#endif
+
 // Out-of-line pieces of k_slot.  slot_transition applies action x to the
 // packed record `w` (State::ApplyAction with its legality check) into *out
 // and returns bit 0 = accepted without a new error, bit 1 = history entry to
 // store, bits 8..15 its index, bits 16..23 the entry byte.
-__device__ __noinline__ uint32_t slot_transition(uint4 w, uint32_t x, uint4* out) {
+__device__ COUP_SLOT_FN uint32_t slot_transition(uint4 w, uint32_t x, uint4* out) {
   Lane L = unpack(w);
   const uint32_t idx = L.move;
   const uint32_t entry = is_chance(L) ? hist_deal(x, L.qids & 1u) : hist_decision(x, L.M);
@@ -1334,7 +1343,7 @@ __device__ __noinline__ uint32_t slot_transition(uint4 w, uint32_t x, uint4* out
   return ok | store | (idx << 8) | (entry << 16);
 }
 
-__device__ __noinline__ void slot_result(uint4 w, uint32_t ok, coup_slot_result* out) {
+__device__ COUP_SLOT_FN void slot_result(uint4 w, uint32_t ok, coup_slot_result* out) {
   const Lane L = unpack(w);
   out->record[0] = w.x;
   out->record[1] = w.y;

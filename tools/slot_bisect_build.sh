@@ -1,0 +1,16 @@
+#!/bin/bash
+# Build the k_slot reproducer (tools/slot_inline_repro.hip) with LLVM's
+# -opt-bisect-limit=N for each N given: passes past N are skipped (in the
+# device and the host compilations alike; the host code only gets slower).
+# Running the binaries on a GPU finds the first device pass after which
+# the inline k_slot miscompiles.
+#   tools/slot_bisect_build.sh N1 N2 ...   -> build/bisect/repro_N
+set -euo pipefail
+R=$(cd "$(dirname "$0")/.." && pwd)
+mkdir -p "$R/build/bisect"
+for n in "$@"; do
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -I "$R/include" -I "$R/open_spiel_coup_amd/csrc" \
+    -mllvm -opt-bisect-limit="$n" "$R/tools/slot_inline_repro.hip" "$R/open_spiel_coup_amd/csrc/coup_nplayer.hip" \
+    -o "$R/build/bisect/repro_$n" 2>/dev/null &
+done
+wait
