@@ -49,6 +49,22 @@ def rust_command(out=RUST_OUT):
             "-Wl,-rpath,$ORIGIN:" + os.path.join(ROCM, "lib")]
 
 
+REPRO_SRC = os.path.join(ROOT, "tools", "slot_inline_repro.hip")
+REPRO_OUT = os.path.join(ROOT, "build", "slot_inline_repro")
+
+
+def build_repro(force=False):
+    """The k_slot miscompile reproducer (investigation tool, DESIGN.md
+    section 12; tests/test_gpu_codegen_hazard.py runs it on the GPU)."""
+    deps = [REPRO_SRC] + DEPS
+    if not force and up_to_date(REPRO_OUT, deps):
+        return REPRO_OUT
+    os.makedirs(os.path.dirname(REPRO_OUT), exist_ok=True)
+    subprocess.check_call([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-I", os.path.join(ROOT, "include"),
+                           "-I", CSRC, REPRO_SRC, os.path.join(CSRC, "coup_nplayer.hip"), "-o", REPRO_OUT])
+    return REPRO_OUT
+
+
 def up_to_date(out=OUT, deps=DEPS):
     if not os.path.exists(out):
         return False

@@ -1314,9 +1314,14 @@ struct SlotArgs {
   float* obs;              // [2][98] or null
 };
 
-// -DCOUP_SLOT_INLINE (measurement / investigation builds, DESIGN.md section
-// 12): the two pieces below inlined into the wave-uniform k_slot, the form
-// that produced wrong records.
+// -DCOUP_SLOT_INLINE (investigation builds only): the
+// two pieces below inlined into the wave-uniform k_slot, the form the ROCm 7.2
+// compiler miscompiles at -O2/-O3 (word 3 of the record after a next_move
+// transition; reproducer: tools/slot_inline_repro.hip, k_min<0>).  The
+// product must never be built this way.
+#if defined(COUP_SLOT_INLINE) && !defined(COUP_INVESTIGATION_BUILD)
+#error "COUP_SLOT_INLINE reproduces a miscompile (DESIGN.md section 12); only tools/slot_inline_repro.hip may set it"
+#endif
 #ifdef COUP_SLOT_INLINE
 #define COUP_SLOT_FN __forceinline__
 #else

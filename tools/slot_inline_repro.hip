@@ -31,6 +31,7 @@
 #ifndef COUP_SLOT_INLINE
 #define COUP_SLOT_INLINE 1  // k_slot's rules inlined (the hazard under study)
 #endif
+#define COUP_INVESTIGATION_BUILD 1  // allows COUP_SLOT_INLINE (coup_kernels.hip refuses it otherwise)
 #include "coup_kernels.hip"  // the product's k_slot, slot_transition, slot_result
 
 using namespace coup;
