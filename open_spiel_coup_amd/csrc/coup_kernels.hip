@@ -583,8 +583,14 @@ constexpr int wave_bits_policy(int m) { return m == kObsWaveBitsPlain ? 0 : (m =
 // The per-lane part of one env step: returns the decision applied (-1 if
 // none), the step type, player 0's reward and, at LAST, player 0's return of
 // the finished game; L is updated in place and every applied action is
-// recorded in `hist`.
-template <bool UNIFORM, class H>
+// recorded in `hist`.  FLOW: the decision through apply_decision_v1 (the
+// reference's branches) instead of the effect form -- the kernels that write
+// observations are bound by their stores, and there the effect form's extra
+// VALU work and registers cost more than its shorter divergent paths save
+// (same-process A/B, profiles/r02/ab/ab_rules_c3.txt: 160.6 vs 165.6 us per
+// 2^20-lane step); the rules-bound kernels take the effect form (c2 8.4 ->
+// 7.7 us, c2r 3.61 -> 3.20 us per step, profiles/r02/ab/ab_rules_c2*.txt).
+template <bool UNIFORM, bool FLOW, class H>
 __device__ __forceinline__ void step_lane(const StepArgs& a, int64_t i, Lane& L, int& act, uint32_t& st,
                                           int32_t& rew, int32_t& ret, H& hist) {
   Rng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, i), 0u, make_uint4(0, 0, 0, 0)};
@@ -612,7 +618,10 @@ __device__ __forceinline__ void step_lane(const StepArgs& a, int64_t i, Lane& L,
   }
   const uint32_t err_before = L.err;
   hist.record(L.move, hist_decision(x, L.M));
-  apply_decision(L, x);
+  if (FLOW)
+    apply_decision_v1(L, x);
+  else
+    apply_decision(L, x);
   L.move += 1u;
   COUP_TRACE_ANY(a, 7);
   resolve_chance(L, rng, hist);
@@ -779,13 +788,14 @@ __device__ __forceinline__ void step_group_compute(const StepArgs& a, int64_t gr
     int act;
     uint32_t st;
     int32_t rew, ret = 0;
+    constexpr bool kFlow = OBS != kObsNone || INFO != kInfoNone;  // store-bound kernels (step_lane)
     if (INFO != kInfoNone) {
       RegHistory rec;
-      step_lane<UNIFORM>(a, i, L, act, st, rew, ret, rec);
+      step_lane<UNIFORM, kFlow>(a, i, L, act, st, rew, ret, rec);
       rec.flush(lds.hist + threadIdx.x * kHist);
     } else {
       NoHistory none;
-      step_lane<UNIFORM>(a, i, L, act, st, rew, ret, none);
+      step_lane<UNIFORM, kFlow>(a, i, L, act, st, rew, ret, none);
     }
     a.state[i] = pack(L);
     ep_update(a, i, eps, st, ret);

@@ -435,10 +435,11 @@ __device__ __forceinline__ void apply_challenge(Lane& L) {
   }
 }
 
-// Decision branch of DoApplyAction (coup.cc:522-808) for a LEGAL action.
-// Claims (FA / Tax / Exchange / Steal) are only legal at turn begin, so the
-// direct call always takes their "announce" half.
-__device__ __forceinline__ void apply_decision(Lane& L, uint32_t a) {
+// Decision branch of DoApplyAction (coup.cc:522-808) for a LEGAL action,
+// written as the reference's control flow (kept for A/B builds:
+// -DCOUP_RULES_V1).  Claims (FA / Tax / Exchange / Steal) are only legal at
+// turn begin, so the direct call always takes their "announce" half.
+__device__ __forceinline__ void apply_decision_v1(Lane& L, uint32_t a) {
   const uint32_t M = L.M, O = M ^ 1u;
   L.r0 = 0;  // cur_rewards_ = {0, 0} (coup.cc:527)
   if (a == kChallenge) {
@@ -504,6 +505,159 @@ __device__ __forceinline__ void apply_decision(Lane& L, uint32_t a) {
       break;
   }
 }
+
+// The same transition as apply_decision_v1, computed as one set of effects
+// per lane instead of the reference's nested branches.  A wave holds lanes
+// taking many different paths through DoApplyAction, so it executes the
+// union of them; here every lane evaluates the same straight-line effect
+// formulas (coin deltas, a coin transfer, lost flags, queue pushes, the
+// turn transition) and at most one hand operation of each kind, so the
+// eight ChallengeFailReplaceCard sites of coup.cc:635-771 become one.
+//
+// Effects, by action (M mover, O = M ^ 1; citations as in v1):
+//   Income (531-534)      +1 coin to M, NextPlayerTurn
+//   Coup/Assassinate      -7 / -3 coins to M, NextPlayerMove (548-553, 567-573)
+//   FA/Tax/Exch/Steal/Block announce: NextPlayerMove (536-603, 631-633)
+//   LoseCard (605-616)    flip slot, re-sort, lost cleared, -1 reward to M, NextPlayerTurn
+//   ExchangeReturn (773-804) erase two slots, credit the slot INDICES to the deck,
+//                         O lost a challenge ? NextPlayerMove : NextPlayerTurn
+//   Pass (618-629)        pending Block: NextPlayerTurn; else the claim completes for O
+//                         (FA +2, Tax +3, Steal: k from M to O, then NextPlayerTurn --
+//                         NextPlayerMove followed by NextPlayerTurn is NextPlayerTurn;
+//                         Exchange: two deals to O, NextPlayerMove)
+//   Challenge (635-771)   claim = M's own last action if O blocked it, else O's claim;
+//                         the claimed card t1 (and the Ambassador for a blocked Steal);
+//                         O holds it face down ("has") or not:
+//                           has: M loses the challenge and O's card is replaced
+//                                (one deal to O), except a claimed Assassinate: M's two
+//                                cards flip (-1 each); Tax +3 to O; Steal: k from M to O;
+//                                Exchange: NextPlayerMove and two more deals to O
+//                           not: O loses the challenge and NextPlayerMove, except a
+//                                blocked Assassinate: O's two cards flip (+1 each to M);
+//                                blocked FA +2 to M; blocked Steal: k from O to M;
+//                                claimed Assassinate: +3 refund to O
+//   k = the giver's coins > 1 ? 2 : 1.
+__device__ __forceinline__ void apply_decision_v2(Lane& L, uint32_t a) {
+  const uint32_t M = L.M, O = M ^ 1u;
+  uint32_t cp_h = COUP_PGET(L, h, M), op_h = COUP_PGET(L, h, O);
+  const uint32_t cp_c = COUP_PGET(L, c, M), op_c = COUP_PGET(L, c, O);
+  const uint32_t cp_l = COUP_PGET(L, l, M), op_l = COUP_PGET(L, l, O);
+  const uint32_t cp_lost = COUP_PGET(L, lost, M), op_lost = COUP_PGET(L, lost, O);
+
+  const bool is_chal = a == kChallenge;
+  const bool is_pass = a == kPass;
+  const bool is_lose = a == kLoseCard1 || a == kLoseCard2;
+  const bool is_xret = a >= kExchangeReturn12;
+
+  // --- the challenged claim
+  const bool blk = op_l == kBlock;
+  const uint32_t claim = blk ? cp_l : op_l;
+  // claimed card by claim id, 3 bits per action id (7 = cannot be challenged):
+  // blocked FA -> Duke, blocked Assassinate -> Contessa, blocked Steal ->
+  // Captain; Tax -> Duke, Exchange -> Ambassador, Assassinate -> Assassin,
+  // Steal -> Captain
+  constexpr uint64_t kBlockCard = (0x3FFFFFFFFFFFFFFFull & ~((7ull << 3) | (7ull << 12) | (7ull << 18))) |
+                                  ((uint64_t)kDuke << 3) | ((uint64_t)kContessa << 12) | ((uint64_t)kCaptain << 18);
+  constexpr uint64_t kClaimCard = (0x3FFFFFFFFFFFFFFFull & ~((7ull << 9) | (7ull << 15) | (7ull << 12) | (7ull << 18))) |
+                                  ((uint64_t)kDuke << 9) | ((uint64_t)kAmbassador << 15) |
+                                  ((uint64_t)kAssassin << 12) | ((uint64_t)kCaptain << 18);
+  const uint32_t cidx = claim < 18u ? claim : 19u;  // None (31) -> a field of 7s
+  const uint32_t t1 = (uint32_t)(((blk ? kBlockCard : kClaimCard) >> (3u * cidx)) & 7u);
+  const bool valid = t1 != 7u;
+  const bool h1 = valid && nib_eq(op_h, 2u * t1) != 0u;
+  const bool h2 = blk && claim == kSteal && nib_eq(op_h, 2u * kAmbassador) != 0u;
+  const bool has = h1 || h2;
+  const bool ass = claim == kAssassinate;
+  const bool flip_o = is_chal && blk && ass && !has;
+  const bool flip_m = is_chal && !blk && ass && has;
+  const bool do_replace = is_chal && has && !(!blk && ass);
+  const bool lose_op = is_chal && valid && !has && !(blk && ass);
+  const bool exch_more = (is_pass && op_l == kExchange) || (is_chal && !blk && claim == kExchange && has);
+  const bool pass_ok = op_l == kBlock || op_l == kForeignAid || op_l == kTax || op_l == kExchange || op_l == kSteal;
+
+  // --- coins: fixed deltas and one transfer of k
+  uint32_t dcp = 0u, dop = 0u;
+  dcp = a == kIncome ? 1u : dcp;
+  dcp = a == kCoup ? (uint32_t)-7 : dcp;
+  dcp = a == kAssassinate ? (uint32_t)-3 : dcp;
+  dcp = (is_chal && blk && claim == kForeignAid && !has) ? 2u : dcp;
+  dop = (is_pass && op_l == kForeignAid) ? 2u : dop;
+  dop = (is_pass && op_l == kTax) ? 3u : dop;
+  dop = (is_chal && !blk && ((claim == kTax && has) || (ass && !has))) ? 3u : dop;
+  const bool give_cp = (is_pass && op_l == kSteal) || (is_chal && !blk && claim == kSteal && has);
+  const bool give_op = is_chal && blk && claim == kSteal && !has;
+  const uint32_t k_cp = cp_c > 1u ? 2u : 1u, k_op = op_c > 1u ? 2u : 1u;
+  const uint32_t k = give_cp ? k_cp : (give_op ? k_op : 0u);
+  const uint32_t new_cp_c = cp_c + dcp + (give_op ? k : 0u) - (give_cp ? k : 0u);
+  const uint32_t new_op_c = op_c + dop + (give_cp ? k : 0u) - (give_op ? k : 0u);
+
+  // --- hands
+  int32_t rew = 0;  // cur_rewards_ of the mover (O gets -rew)
+  if (is_lose) {
+    const uint32_t slot = a - kLoseCard1;
+    cp_h = hand_insert(hand_remove(cp_h, slot), nib(cp_h, slot) | 1u);
+    rew = -1;
+  } else if (is_xret) {
+    const uint32_t kk = a - kExchangeReturn12;
+    const uint32_t lo = (0x211000u >> (4u * kk)) & 0xFu, hi = (0x332321u >> (4u * kk)) & 0xFu;
+    cp_h = hand_remove(hand_remove(cp_h, hi), lo);
+    L.deck += (1u << (4u * hi)) + (1u << (4u * lo));  // the slot INDEX (coup.cc:794 quirk)
+  }
+  if (do_replace) {
+    const uint32_t rtype = h1 ? t1 : kAmbassador;
+    op_h = hand_remove(op_h, (uint32_t)__builtin_ctz(nib_eq(op_h, 2u * rtype)) >> 2);
+    L.deck += 1u << (4u * rtype);
+  }
+  if (flip_o || flip_m) {  // no re-sort (coup.cc:660-669, 733-742)
+    uint32_t h = flip_o ? op_h : cp_h;
+    const uint32_t down = ~h & 0x11u;  // slots 0 and 1 face down
+    h |= down;
+    const int32_t n = (int32_t)__popc(down);
+    rew = flip_o ? n : -n;
+    op_h = flip_o ? h : op_h;
+    cp_h = flip_o ? cp_h : h;
+  }
+
+  // --- write back by seat
+  const uint32_t new_cp_l = (is_chal && !valid) ? cp_l : (is_chal ? (uint32_t)kChallenge : a);
+  const uint32_t new_cp_lost = is_lose ? 0u : (do_replace ? 1u : cp_lost);
+  const uint32_t new_op_lost = lose_op ? 1u : op_lost;
+  L.h0 = M ? op_h : cp_h;
+  L.h1 = M ? cp_h : op_h;
+  L.c0 = M ? new_op_c : new_cp_c;
+  L.c1 = M ? new_cp_c : new_op_c;
+  L.l0 = M ? op_l : new_cp_l;
+  L.l1 = M ? new_cp_l : op_l;
+  L.lost0 = M ? new_op_lost : new_cp_lost;
+  L.lost1 = M ? new_cp_lost : new_op_lost;
+  L.r0 = M ? -rew : rew;  // cur_rewards_ = {0, 0} first (coup.cc:527)
+  L.err |= ((is_chal && !valid) || (is_pass && !pass_ok)) ? 1u : 0u;
+
+  // --- deals queued for O: the replacement, then two Exchange draws
+  const uint32_t npush = (do_replace ? 1u : 0u) + (exch_more ? 2u : 0u);
+  L.qids |= (O ? (1u << npush) - 1u : 0u) << L.qlen;
+  L.qlen += npush;
+
+  // --- turn transition
+  const bool nt = a == kIncome || is_lose || (is_xret && !op_lost) || (is_pass && pass_ok && op_l != kExchange);
+  const bool nm = (a >= kForeignAid && a <= kSteal) || a == kBlock || (is_xret && op_lost) ||
+                  (is_pass && !(pass_ok && op_l != kExchange)) || lose_op || (is_chal && exch_more);
+  if (nt) {
+    L.T ^= 1u;
+    L.M = L.T;
+    L.turn += 1u;
+    L.begin = 1u;
+  } else if (nm) {
+    L.M ^= 1u;
+    L.begin = 0u;
+  }
+}
+
+#ifdef COUP_RULES_V1
+__device__ __forceinline__ void apply_decision(Lane& L, uint32_t a) { apply_decision_v1(L, a); }
+#else
+__device__ __forceinline__ void apply_decision(Lane& L, uint32_t a) { apply_decision_v2(L, a); }
+#endif
 
 // Chance branch of DoApplyAction (coup.cc:491-520): deal card `type` to the
 // queue front, keep the hand sorted.

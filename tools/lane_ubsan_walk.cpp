@@ -1,4 +1,5 @@
-// Host build of the lane rules under UBSan: random legal-action walks
+// Host build of the lane rules under UBSan (apply_decision = the effect
+// form apply_decision_v2 by default, -DCOUP_RULES_V1 for the branch form): random legal-action walks
 // (decisions and chance outcomes) against the oracle, every step.
 //   g++ -O2 -g -fsanitize=undefined -fno-sanitize-recover=all -I tools/hoststub \
 //       -I open_spiel_coup_amd/csrc -I oracle tools/lane_ubsan_walk.cpp oracle/coup_oracle.c -o /tmp/lane_ubsan_walk
