@@ -168,19 +168,24 @@ __global__ __launch_bounds__(kThreads) void k_step_sorted(StepArgs a) {
   if (t < 32u) s_bin[t] = 0u;
   if (t == 0u) s_nreset = 0u;
 
-  // phase 1: up to the decision
+  // phase 1: up to the decision.  A lane with a parked decision needs
+  // nothing else here, so its record goes to LDS as loaded (phase 2's unpack
+  // ignores the parked bits): no unpack / pack round trip for it.
   NLane<N> L;
   uint32_t key = kKeyDead, st = 0u;
-  bool error = false;
+  bool error = false, raw = false;
   const int2 eps = live ? load_episode(a, i) : make_int2(0, 0);
+  uint4 ra = make_uint4(0u, 0u, 0u, 0u), rb = ra;
   if (live) {
-    const uint4 rb = a.sb[i];
-    L = unpack<N>(a.sa[i], rb);
+    ra = a.sa[i];
+    rb = a.sb[i];
     const uint32_t parked = (rb.w >> kAheadShift) & 31u;
     if (UNIFORM && AHEAD && parked != 0u) {
       key = parked - 1u;  // drawn by the last step for this state: a decision node
       st = 1u;            // MID
+      raw = true;
     } else {
+      L = unpack<N>(ra, rb);
       NRng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, i), 0u, make_uint4(0, 0, 0, 0)};
       uint32_t x = UNIFORM ? 0u : (uint32_t)(uint8_t)a.actions_in[i];
       key = step_lane_pre<N, UNIFORM>(L, rng, x, st, error);
@@ -202,7 +207,10 @@ __global__ __launch_bounds__(kThreads) void k_step_sorted(StepArgs a) {
   }
   __syncthreads();
   const uint32_t pos = s_bin[key] + rank;
-  if (live) {
+  if (raw) {
+    s_a[pos] = ra;
+    s_b[pos] = rb;
+  } else if (live) {
     uint4 wa, wb;
     pack(L, wa, wb);
     s_a[pos] = wa;
