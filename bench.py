@@ -226,30 +226,33 @@ def _time_traffic_ceiling(env, steps, stream):
 
 
 def _calibrate_gate(env, stream):
-    """GPU spin length (torch.cuda._sleep cycles) that covers the host's
-    enqueue latency for one fused rollout (event record + ctypes launch), so
-    the start event of the timed launch fires when the rollout is already
-    queued.  Sized to 1.25x the measured latency: the spin's tail beyond
-    the enqueue adds at most a quarter of that latency to the wall time."""
+    """Steps of an untimed rollout (the gate) that keep the GPU busy for
+    twice the host's enqueue latency of one fused rollout (event record +
+    ctypes launch), so the timed launch's start event fires with the rollout
+    already queued behind it and the GPU never idles between them.  Each
+    step's duration is measured behind such a gate too."""
+    import math
     import time
     import torch
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    cycles = 200000
-    torch.cuda._sleep(cycles)  # load the spin kernel
-    a.record(stream)
-    torch.cuda._sleep(cycles)
-    b.record(stream)
-    b.synchronize()
-    cycles_per_us = cycles / max(a.elapsed_time(b) * 1e3, 1e-3)
+    one = env.rollout_launcher(1)
     lat = []
-    for _ in range(5):
+    for _ in range(7):
         torch.cuda.synchronize()
         t = time.perf_counter()
         a.record(stream)
-        env.rollout(1)
+        one()
         lat.append(time.perf_counter() - t)
     torch.cuda.synchronize()
-    return int(1.25 * min(lat) * 1e6 * cycles_per_us)
+    probe = 64
+    env.rollout(probe)  # busy while the measured launch is enqueued
+    a.record(stream)
+    env.rollout(probe)
+    b.record(stream)
+    b.synchronize()
+    step_s = a.elapsed_time(b) * 1e-3 / probe
+    # 3x the median: a launch right after a barrier is slower than a warm one
+    return max(1, math.ceil(3.0 * sorted(lat)[len(lat) // 2] / max(step_s, 1e-9)))
 
 
 def main():
@@ -290,12 +293,17 @@ def main():
     elif fused:
         env.rollout(args.warmup)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))]
-        gate_cycles = _calibrate_gate(env, stream)
+        gate_steps = _calibrate_gate(env, stream)
+        gate, timed = env.rollout_launcher(gate_steps), env.rollout_launcher(args.steps, stats)
     else:
         for _ in range(args.warmup):
             env.step()
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(args.steps)]
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))]
+        if with_info:  # no rollout on a history env; a c3i step is ~1 ms, its launch latency noise
+            gate = lambda: None  # noqa: E731
+            gate.steps = 0
+        else:
+            gate = env.rollout_launcher(_calibrate_gate(env, stream))
     def episode_tensors():
         if fused:
             return stats["episodes"], stats["return_sum"]
@@ -310,12 +318,13 @@ def main():
     else:
         env.clear_episode_stats()
     barrier()
-    if fused:
-        # a GPU-side spin ahead of the start event keeps the queue busy while
-        # the host enqueues the rollout, so the event pair brackets the
-        # kernel and not the host's launch latency (~50 us, 40% of a
-        # 20-step c2r launch); enqueued before t0, it overlaps that latency
-        torch.cuda._sleep(gate_cycles)
+    if graph is None:
+        # an untimed rollout ahead of the start event keeps the GPU busy
+        # while the host enqueues the timed launch(es), so the event pair
+        # brackets the kernels and not the host's launch latency and an idle
+        # GPU's wake-up (~60 us: half of a 20-step c2r launch); enqueued
+        # before t0, it overlaps that latency in the wall time too
+        gate()
     t0 = time.perf_counter()
     if graph is not None:
         ev[0][0].record(stream)
@@ -323,13 +332,14 @@ def main():
         ev[0][1].record(stream)
     elif fused:
         ev[0][0].record(stream)
-        env.rollout(args.steps, stats)
+        timed()
         ev[0][1].record(stream)
     else:
+        # K eager launches back to back: the span / K, like the graph replay
+        ev[0][0].record(stream)
         for k in range(args.steps):
-            ev[k][0].record(stream)
             env.step()
-            ev[k][1].record(stream)
+        ev[0][1].record(stream)
     # collate every lane's finished-episode count and player-0 return sum over
     # xGMI (RCCL all-gather, [world * B, 2] int32; identity at one rank)
     gathered = D.collate(torch.stack(episode_tensors(), 1))
@@ -338,7 +348,8 @@ def main():
     ep_total = int(gathered[:, 0].sum())
     ret_total = int(gathered[:, 1].sum())
 
-    # per env step; with a graph, the replay's duration / K (launch gaps included)
+    # per env step: the span of the K steps (one replay, one fused launch or K
+    # eager launches) / K, launch gaps included
     kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
     elapsed = D.max_over_ranks(elapsed, dev)
     errors = env.error_count()
@@ -390,6 +401,7 @@ def main():
             "config": {"workload": workload, "batch_per_gpu": B, "global_batch": world * B, "players": players,
                        "outputs": outputs, "auto_reset": True, "fused_steps_per_launch": args.steps if fused else 1,
                        "hip_graph": graph is not None,
+                       "gate_steps": 0 if graph is not None else gate.steps,
                        "parallelism": f"dp{world} (env-id sharding)" + ("" if args.dist_backend == "nccl" else
                                                                    " [gloo rehearsal, ranks share GPUs]")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -1670,6 +1670,8 @@ int coup_debug_set_trace(uint64_t* buf) {
   g_trace = buf;
   return COUP_OK;
 }
+// the buffer for the N-player step (coup_nplayer.hip)
+uint64_t* coup_debug_get_trace() { return g_trace; }
 #endif
 
 int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out) {

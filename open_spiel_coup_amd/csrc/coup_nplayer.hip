@@ -26,6 +26,10 @@ __device__ __forceinline__ void count_philox_eval() {
 #include "coup_np.h"
 #include "coup_regroup.h"
 
+#ifdef COUP_WAVE_TRACE
+extern "C" uint64_t* coup_debug_get_trace();  // coup_kernels.hip
+#endif
+
 namespace coup {
 namespace np {
 
@@ -59,7 +63,33 @@ struct StepArgs {
   int32_t* ep_count;   // [B] per-episode accumulators (coup_step_outputs.episodes)
   int32_t* ep_return;  // [B] (coup_step_outputs.return_sum)
   uint32_t* err_count;
+#ifdef COUP_WAVE_TRACE
+  // measurement builds only (tools/np_wave_trace.py): per wave of
+  // k_step_sorted, 10 s_memrealtime (100 MHz) stamps at the phase edges
+  uint64_t* trace;
+#endif
 };
+
+#ifdef COUP_WAVE_TRACE
+#define NP_TRACE(a, k)                                                                             \
+  do {                                                                                             \
+    if ((a).trace && (threadIdx.x & 63u) == 0u)                                                    \
+      (a).trace[((size_t)blockIdx.x * (blockDim.x / 64u) + threadIdx.x / 64u) * 10u + (k)] =      \
+          __builtin_amdgcn_s_memrealtime();                                                        \
+  } while (0)
+#define NP_TRACE_WAIT(a, k)                                                                        \
+  do {                                                                                             \
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                               \
+    NP_TRACE(a, k);                                                                                \
+  } while (0)
+#else
+#define NP_TRACE(a, k) \
+  do {                 \
+  } while (0)
+#define NP_TRACE_WAIT(a, k) \
+  do {                      \
+  } while (0)
+#endif
 
 // Episode accumulators (coup_step_outputs.episodes / return_sum): the
 // lane's two words are loaded with its record, before the rules, and every
@@ -151,20 +181,29 @@ __global__ __launch_bounds__(kThreads) void k_step(StepArgs a) {
 // drawn for.
 constexpr uint32_t kAheadShift = 25u;
 
-template <int N, bool UNIFORM, bool AHEAD>
-__global__ __launch_bounds__(kThreads) void k_step_sorted(StepArgs a) {
-  __shared__ uint4 s_a[kThreads], s_b[kThreads];
-  __shared__ uint32_t s_meta[kThreads];   // slot -> owner thread | key << 8 | st << 13 | error << 15
-  __shared__ uint32_t s_out[kThreads];    // slot -> act + 1 | st << 5 | rl << 7 | rc << 10 | error << 13 |
+template <int N, bool UNIFORM, bool AHEAD, int T = kThreads>
+#ifdef COUP_WAVE_TRACE
+// the stamps' registers must not cost the traced kernel its 8 blocks per CU
+#define NP_STEP_SORTED_BOUNDS __launch_bounds__(T, 8)
+#else
+#define NP_STEP_SORTED_BOUNDS __launch_bounds__(T)
+#endif
+__global__ NP_STEP_SORTED_BOUNDS void k_step_sorted(StepArgs a) {
+  __shared__ uint4 s_a[T], s_b[T];
+  __shared__ uint32_t s_meta[T];   // slot -> owner thread | key << kO | st << kO + 5 | error << kO + 7
+  __shared__ uint32_t s_out[T];    // slot -> act + 1 | st << 5 | rl << 7 | rc << 10 | error << 13 |
                                           //         (ret0 + 16) << 14 | cp << 24
-  __shared__ uint32_t s_legal[kThreads];  // slot -> post-step legal mask
-  __shared__ uint32_t s_reset[kThreads];  // slots whose lane auto-resets
+  __shared__ uint32_t s_legal[T];  // slot -> post-step legal mask
+  __shared__ uint32_t s_reset[T];  // slots whose lane auto-resets
   __shared__ uint32_t s_bin[32];
   __shared__ uint32_t s_nreset;
+  static_assert((T & (T - 1)) == 0 && T >= 64 && T <= 1024, "power-of-two block of whole waves");
+  constexpr uint32_t kO = T <= 256 ? 8u : 10u;  // owner-thread bits of s_meta
   const uint32_t t = threadIdx.x;
-  const int64_t base = (int64_t)blockIdx.x * kThreads;
+  const int64_t base = (int64_t)blockIdx.x * T;
   const int64_t i = base + t;
   const bool live = i < a.n;
+  NP_TRACE(a, 0);
   if (t < 32u) s_bin[t] = 0u;
   if (t == 0u) s_nreset = 0u;
 
@@ -179,6 +218,9 @@ __global__ __launch_bounds__(kThreads) void k_step_sorted(StepArgs a) {
   if (live) {
     ra = a.sa[i];
     rb = a.sb[i];
+  }
+  NP_TRACE_WAIT(a, 1);
+  if (live) {
     const uint32_t parked = (rb.w >> kAheadShift) & 31u;
     if (UNIFORM && AHEAD && parked != 0u) {
       key = parked - 1u;  // drawn by the last step for this state: a decision node
@@ -192,6 +234,7 @@ __global__ __launch_bounds__(kThreads) void k_step_sorted(StepArgs a) {
       if (error) count_error(a.err_count);
     }
   }
+  NP_TRACE(a, 2);
   __syncthreads();
   const uint32_t rank = atomicAdd(&s_bin[key], 1u);
   __syncthreads();
@@ -216,17 +259,18 @@ __global__ __launch_bounds__(kThreads) void k_step_sorted(StepArgs a) {
     s_a[pos] = wa;
     s_b[pos] = wb;
   }
-  s_meta[pos] = t | (key << 8) | (st << 13) | ((uint32_t)error << 15);
+  s_meta[pos] = t | (key << kO) | (st << (kO + 5)) | ((uint32_t)error << (kO + 7));
   __syncthreads();
+  NP_TRACE(a, 3);
 
   // phase 2: thread t runs slot t's decision
   {
-    const uint32_t m = s_meta[t], k = (m >> 8) & 31u;
+    const uint32_t m = s_meta[t], k = (m >> kO) & 31u;
     if (k <= kStepDone) {
       L = unpack<N>(s_a[t], s_b[t]);
-      uint32_t out = (m >> 13) & 3u, legal = 0u;  // a lane finished in phase 1: no action, its st
+      uint32_t out = (m >> (kO + 5)) & 3u, legal = 0u;  // a lane finished in phase 1: no action, its st
       bool pending = false;
-      NRng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, base + (m & 255u)), 0u, make_uint4(0, 0, 0, 0)};
+      NRng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, base + (m & (T - 1u))), 0u, make_uint4(0, 0, 0, 0)};
       if (k < kStepDone) {
         const uint32_t err_before = L.err;
         apply_decision(L, k);
@@ -244,7 +288,7 @@ __global__ __launch_bounds__(kThreads) void k_step_sorted(StepArgs a) {
         s_a[t] = wa;
         s_b[t] = wb;
       } else {
-        out = 0u | (((m >> 13) & 3u) << 5);
+        out = 0u | (((m >> (kO + 5)) & 3u) << 5);
       }
       if (!pending) {
         legal = legal_mask(L);
@@ -257,13 +301,15 @@ __global__ __launch_bounds__(kThreads) void k_step_sorted(StepArgs a) {
       s_legal[t] = legal;
     }
   }
+  NP_TRACE(a, 4);
   __syncthreads();
+  NP_TRACE(a, 5);
 
   // the auto-resets, packed onto the first threads
   const uint32_t nreset = s_nreset;
-  for (uint32_t j = t; j < nreset; j += kThreads) {
+  for (uint32_t j = t; j < nreset; j += T) {
     const uint32_t slot = s_reset[j];
-    NRng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, base + (s_meta[slot] & 255u)), 0u,
+    NRng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, base + (s_meta[slot] & (T - 1u))), 0u,
              make_uint4(0, 0, 0, 0)};
     const NLane<N> R = new_episode<N>(plane_episode(s_b[slot]) + 1u, rng);
     uint4 wa, wb;
@@ -275,7 +321,9 @@ __global__ __launch_bounds__(kThreads) void k_step_sorted(StepArgs a) {
     s_out[slot] = (s_out[slot] & 0x00FFFFFFu) | (((uint32_t)current_player(R) & 0xFFu) << 24);
     if (UNIFORM && AHEAD) s_b[slot].w |= (sample_action(legal, rng.draw(R.episode, R.move)) + 1u) << kAheadShift;
   }
+  NP_TRACE(a, 6);
   __syncthreads();
+  NP_TRACE(a, 7);
 
   // phase 3: each thread stores its own lane
   if (!live) return;
@@ -285,6 +333,8 @@ __global__ __launch_bounds__(kThreads) void k_step_sorted(StepArgs a) {
   store_step_outputs<N>(a, i, (int)(o & 31u) - 1, (o >> 5) & 3u, (o >> 7) & 7u, (o >> 10) & 7u, s_legal[pos],
                         (int)(int8_t)(o >> 24));
   store_episode(a, i, eps, (o >> 5) & 3u, (int32_t)((o >> 14) & 31u) - 16);
+  NP_TRACE(a, 8);
+  NP_TRACE_WAIT(a, 9);
 }
 
 struct RolloutArgs {
@@ -365,14 +415,16 @@ __device__ __forceinline__ uint32_t draw_key(const NLane<N>& L, NRng& rng, uint3
 // 8 waves per SIMD (64 VGPRs, a few spilled): 29.1 vs 30.3 us per step at
 // 6 waves.  Carrying each lane's cached Philox block through LDS with the
 // record measured no faster (30.2 us) and was dropped.
-template <int N>
-__global__ __launch_bounds__(kThreads, 8) void k_rollout_sorted(RolloutArgs a) {
-  __shared__ uint4 s_a[kThreads], s_b[kThreads];
-  __shared__ uint32_t s_meta[kThreads];  // slot -> lane | key << 8 | decisions this episode << 13
-  __shared__ int32_t s_eps[kThreads], s_ret[kThreads], s_len[kThreads];  // by lane
+template <int N, int T = kThreads>
+__global__ __launch_bounds__(T, 8) void k_rollout_sorted(RolloutArgs a) {
+  static_assert((T & (T - 1)) == 0 && T >= 64 && T <= 1024, "power-of-two block of whole waves");
+  constexpr uint32_t kO = T <= 256 ? 8u : 10u;  // lane bits of s_meta
+  __shared__ uint4 s_a[T], s_b[T];
+  __shared__ uint32_t s_meta[T];  // slot -> lane | key << kO | decisions this episode << kO + 5
+  __shared__ int32_t s_eps[T], s_ret[T], s_len[T];  // by lane
   __shared__ __attribute__((aligned(16))) uint32_t s_bin[2][32];
   const uint32_t t = threadIdx.x;
-  const int64_t base = (int64_t)blockIdx.x * kThreads;
+  const int64_t base = (int64_t)blockIdx.x * T;
   const bool live = base + t < a.n;
   if (t < 64u) s_bin[t >> 5][t & 31u] = 0u;
   s_eps[t] = 0;
@@ -398,12 +450,12 @@ __global__ __launch_bounds__(kThreads, 8) void k_rollout_sorted(RolloutArgs a) {
     pack(L, wa, wb);
     s_a[pos] = wa;
     s_b[pos] = wb;
-    s_meta[pos] = lane | (key << 8) | (cur << 13);
+    s_meta[pos] = lane | (key << kO) | (cur << (kO + 5));
     __syncthreads();
     const uint32_t m = s_meta[t];
-    lane = m & 255u;
-    key = (m >> 8) & 31u;
-    cur = m >> 13;
+    lane = m & (T - 1u);
+    key = (m >> kO) & 31u;
+    cur = m >> (kO + 5);
     L = unpack<N>(s_a[t], s_b[t]);
     if (key == kKeyDead) continue;
     rng.env_id = lane_stream_id(a.env_id_base, base + lane);
@@ -617,6 +669,25 @@ hipError_t launch_reset(const Env& e, const uint8_t* mask, int mode, int deal) {
   });
 }
 
+// Lanes per regrouping block.  Larger blocks give each wave of the rules
+// phase lanes with fewer distinct decisions, at the price of longer
+// barrier waits: the 6-player uniform step measured 39.5 / 35.9 / 36.4 us
+// per 2^20-lane step at 256 / 512 / 1024 lanes, the 6-player rollout 29.3 /
+// 25.7 / 22.7 us per step (3 and 4 players: 512 best for the step;
+// profiles/r02/ab/np_sort_block_size.log).  The step keeps its auto-resets
+// on one wave behind a barrier, which 1024-lane blocks make the longer
+// wait; the rollout sorts its resets like a decision.  COUP_NP_SORT_THREADS
+// = 256 / 512 / 1024 overrides both (A/B runs; 128 measured 47.4 us; every size gives the
+// same results, test_regrouped_*_block_size_invariant).
+constexpr int kStepSortLanes = 512;
+constexpr int kRolloutSortLanes = 1024;
+
+int sort_threads(int dflt) {
+  const char* s = std::getenv("COUP_NP_SORT_THREADS");
+  const int v = s ? std::atoi(s) : dflt;
+  return (v == 256 || v == 512 || v == 1024) ? v : dflt;
+}
+
 hipError_t launch_step(const Env& e, const int8_t* actions, const coup_step_outputs* out) {
   if (e.n == 0) return hipSuccess;
   StepArgs a{};
@@ -629,6 +700,9 @@ hipError_t launch_step(const Env& e, const int8_t* actions, const coup_step_outp
   a.auto_reset = e.auto_reset;
   a.actions_in = actions;
   a.err_count = e.err_count;
+#ifdef COUP_WAVE_TRACE
+  a.trace = coup_debug_get_trace();
+#endif
   float* obs = nullptr;
   if (out) {
     a.actions = out->actions;
@@ -646,12 +720,21 @@ hipError_t launch_step(const Env& e, const int8_t* actions, const coup_step_outp
     if (regroup_lanes(e.n)) {
       const char* ah = std::getenv("COUP_AHEAD");  // 0: no decision drawn ahead (A/B)
       const bool ahead = ah ? std::atoi(ah) != 0 : true;
-      if (actions)
-        k_step_sorted<N, false, false><<<grid, kThreads, 0, e.stream>>>(a);
-      else if (ahead)
-        k_step_sorted<N, true, true><<<grid, kThreads, 0, e.stream>>>(a);
-      else
-        k_step_sorted<N, true, false><<<grid, kThreads, 0, e.stream>>>(a);
+      auto go = [&](auto lanes) {
+        constexpr int TB = decltype(lanes)::value;
+        const unsigned g = grid_for(e.n, TB);
+        if (actions)
+          k_step_sorted<N, false, false, TB><<<g, TB, 0, e.stream>>>(a);
+        else if (ahead)
+          k_step_sorted<N, true, true, TB><<<g, TB, 0, e.stream>>>(a);
+        else
+          k_step_sorted<N, true, false, TB><<<g, TB, 0, e.stream>>>(a);
+      };
+      switch (sort_threads(kStepSortLanes)) {
+        case 256: go(std::integral_constant<int, 256>()); break;
+        case 1024: go(std::integral_constant<int, 1024>()); break;
+        default: go(std::integral_constant<int, 512>()); break;
+      }
     } else if (actions) {
       k_step<N, false><<<grid, kThreads, 0, e.stream>>>(a);
     } else {
@@ -680,10 +763,15 @@ hipError_t launch_rollout(const Env& e, int64_t steps, const coup_rollout_stats*
   return dispatch(e.players, [&](auto np) {
     constexpr int N = decltype(np)::value;
     const unsigned grid = grid_for(e.n, kThreads);
-    if (regroup_lanes(e.n))
-      k_rollout_sorted<N><<<grid, kThreads, 0, e.stream>>>(a);
-    else
+    if (regroup_lanes(e.n)) {
+      switch (sort_threads(kRolloutSortLanes)) {
+        case 512: k_rollout_sorted<N, 512><<<grid_for(e.n, 512), 512, 0, e.stream>>>(a); break;
+        case 256: k_rollout_sorted<N, 256><<<grid, 256, 0, e.stream>>>(a); break;
+        default: k_rollout_sorted<N, 1024><<<grid_for(e.n, 1024), 1024, 0, e.stream>>>(a); break;
+      }
+    } else {
       k_rollout<N><<<grid, kThreads, 0, e.stream>>>(a);
+    }
   });
 }
 

@@ -241,12 +241,24 @@ class BatchedCoupEnv:
         """`steps` uniform-random steps per lane in one launch.  stats: optional
         dict with int32 [B] tensors 'episodes', 'return_sum', 'length_sum'
         (accumulated)."""
+        self.rollout_launcher(steps, stats)()
+
+    def rollout_launcher(self, steps, stats=None):
+        """rollout(steps, stats) with its arguments bound up front: a
+        zero-argument callable that only enqueues the launch (on the stream
+        current when it was made), for timing loops."""
         self._bind_stream()
         s = None
         if stats is not None:
             s = _native.RolloutStats(_addr(stats["episodes"]), _addr(stats["return_sum"]),
                                      _addr(stats["length_sum"]))
-        _native.check(self.lib.coup_rollout(self._h, int(steps), ctypes.byref(s) if s else None))
+        fn, h, k, ref = self.lib.coup_rollout, self._h, int(steps), ctypes.byref(s) if s else None
+
+        def launch():
+            _native.check(fn(h, k, ref))
+        launch.stats = s  # keeps the struct alive with the callable
+        launch.steps = k
+        return launch
 
     def new_stats(self):
         z = lambda: torch.zeros(self.batch, dtype=torch.int32, device=self.device)  # noqa: E731

@@ -186,6 +186,64 @@ def test_regrouped_step_equals_in_place_step(monkeypatch, n_players, auto_reset,
     assert envs["0"].error_count() == envs["1"].error_count()
 
 
+@pytest.mark.parametrize("n_players", [3, 6])
+def test_regrouped_step_block_size_invariant(monkeypatch, n_players):
+    """The uniform regrouped step sorting 256-, 512- or 1024-lane blocks
+    (COUP_NP_SORT_THREADS, A/B variants) == the default 256-lane blocks: the
+    sort only changes which wave runs a lane, never its result.  Ragged
+    batch, auto-reset, episode accumulators."""
+    n, steps, seed = 1000, 150, 5 + n_players
+    knobs = ("256", "512", "1024")
+    envs = {}
+    monkeypatch.setenv("COUP_REGROUP", "1")
+    for knob in knobs:
+        monkeypatch.setenv("COUP_NP_SORT_THREADS", knob)
+        envs[knob] = BatchedCoupEnv(n, seed=seed, env_id_base=7 << 20, auto_reset=True, obs=False,
+                                    num_players=n_players, generic=True, episode_stats=True)
+    for t in range(steps):
+        outs = {}
+        for knob, env in envs.items():
+            monkeypatch.setenv("COUP_NP_SORT_THREADS", knob)
+            outs[knob] = {k: v.clone() for k, v in env.step().items()}
+        for knob in knobs[1:]:
+            for k in ("actions", "rewards", "step_type", "legal_mask", "current_player"):
+                assert torch.equal(outs["256"][k], outs[knob][k]), (knob, t, k)
+            assert torch.equal(envs["256"].export_state(), envs[knob].export_state()), (knob, t)
+    for knob in knobs[1:]:
+        for a, b in zip(envs["256"].episode_stats(), envs[knob].episode_stats()):
+            assert torch.equal(a, b), knob
+        assert envs[knob].error_count() == 0
+    assert int(envs["256"].episode_stats()[0].sum()) > 0
+    assert envs["256"].error_count() == 0
+
+
+@pytest.mark.parametrize("n_players", [2, 6])
+def test_regrouped_rollout_block_size_invariant(monkeypatch, n_players):
+    """k_rollout_sorted over 256-, 512- and 1024-lane blocks (1024 the
+    default) agree: records and per-lane statistics, ragged batch, launches of 1, 9
+    and 140 steps, starting mid-game."""
+    n, seed = 3000, 61 + n_players
+    knobs = ("256", "512", "1024")
+    monkeypatch.setenv("COUP_REGROUP", "1")
+    envs, stats = {}, {}
+    for knob in knobs:
+        monkeypatch.setenv("COUP_NP_SORT_THREADS", knob)
+        env = BatchedCoupEnv(n, seed=seed, auto_reset=True, obs=False, num_players=n_players, generic=True)
+        for _ in range(25):
+            env.step()
+        envs[knob], stats[knob] = env, env.new_stats()
+    for k in (1, 9, 140):
+        for knob, env in envs.items():
+            monkeypatch.setenv("COUP_NP_SORT_THREADS", knob)
+            env.rollout(k, stats[knob])
+        for knob in knobs[1:]:
+            assert torch.equal(envs["256"].export_state(), envs[knob].export_state()), (knob, k)
+            for key in ("episodes", "return_sum", "length_sum"):
+                assert torch.equal(stats["256"][key], stats[knob][key]), (knob, k, key)
+    assert int(stats["256"]["episodes"].sum()) > 0
+    assert all(env.error_count() == 0 for env in envs.values())
+
+
 @pytest.mark.parametrize("n_players", [2, 5, 6])
 def test_regrouped_rollout_equals_in_place_rollout(monkeypatch, n_players):
     """k_rollout_sorted (lanes re-sorted by their next decision every step,
