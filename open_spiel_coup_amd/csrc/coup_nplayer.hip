@@ -181,6 +181,20 @@ __global__ __launch_bounds__(kThreads) void k_step(StepArgs a) {
 // drawn for.
 constexpr uint32_t kAheadShift = 25u;
 
+// The regrouping key of decision x at L: its refined key (coup_nlane.h
+// refine_key: 6-player step 37.1 -> 36.4 us per 2^20-lane step,
+// profiles/r02/ab/np_refined_keys.log), or x itself in -DCOUP_NP_PLAIN_KEYS
+// builds (A/B).
+template <int N>
+__device__ __forceinline__ uint32_t ahead_key(const NLane<N>& L, uint32_t x) {
+#ifdef COUP_NP_PLAIN_KEYS
+  (void)L;
+  return x;
+#else
+  return refine_key(L, x);
+#endif
+}
+
 template <int N, bool UNIFORM, bool AHEAD, int T = kThreads>
 #ifdef COUP_WAVE_TRACE
 // the stamps' registers must not cost the traced kernel its 8 blocks per CU
@@ -266,20 +280,21 @@ __global__ NP_STEP_SORTED_BOUNDS void k_step_sorted(StepArgs a) {
   // phase 2: thread t runs slot t's decision
   {
     const uint32_t m = s_meta[t], k = (m >> kO) & 31u;
-    if (k <= kStepDone) {
+    if (k != kKeyDead) {
       L = unpack<N>(s_a[t], s_b[t]);
       uint32_t out = (m >> (kO + 5)) & 3u, legal = 0u;  // a lane finished in phase 1: no action, its st
       bool pending = false;
       NRng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, base + (m & (T - 1u))), 0u, make_uint4(0, 0, 0, 0)};
-      if (k < kStepDone) {
+      if (k != kStepDone) {
+        const uint32_t x = key_action(k);
         const uint32_t err_before = L.err;
-        apply_decision(L, k);
+        apply_decision(L, x);
         L.move += 1u;
         resolve_chance(L, rng);
         const bool err = L.err && !err_before;
         if (err) count_error(a.err_count);
         const bool term = is_terminal(L);
-        out = (k + 1u) | ((term ? 2u : 1u) << 5) | (L.rloser << 7) | (L.rcount << 10) | ((uint32_t)err << 13);
+        out = (x + 1u) | ((term ? 2u : 1u) << 5) | (L.rloser << 7) | (L.rcount << 10) | ((uint32_t)err << 13);
         if (a.ep_count && term) out |= (uint32_t)(returns(L, 0u) + 16) << 14;
         pending = term && a.auto_reset != 0;
         if (pending) s_reset[atomicAdd(&s_nreset, 1u)] = t;
@@ -294,8 +309,8 @@ __global__ NP_STEP_SORTED_BOUNDS void k_step_sorted(StepArgs a) {
         legal = legal_mask(L);
         const int cp = current_player(L);
         out |= ((uint32_t)cp & 0xFFu) << 24;
-        if (UNIFORM && AHEAD && k < kStepDone && cp >= 0)
-          s_b[t].w |= (sample_action(legal, rng.draw(L.episode, L.move)) + 1u) << kAheadShift;
+        if (UNIFORM && AHEAD && k != kStepDone && cp >= 0)
+          s_b[t].w |= (ahead_key(L, sample_action(legal, rng.draw(L.episode, L.move))) + 1u) << kAheadShift;
       }
       s_out[t] = out;
       s_legal[t] = legal;
@@ -319,7 +334,7 @@ __global__ NP_STEP_SORTED_BOUNDS void k_step_sorted(StepArgs a) {
     const uint32_t legal = legal_mask(R);
     s_legal[slot] = legal;
     s_out[slot] = (s_out[slot] & 0x00FFFFFFu) | (((uint32_t)current_player(R) & 0xFFu) << 24);
-    if (UNIFORM && AHEAD) s_b[slot].w |= (sample_action(legal, rng.draw(R.episode, R.move)) + 1u) << kAheadShift;
+    if (UNIFORM && AHEAD) s_b[slot].w |= (ahead_key(R, sample_action(legal, rng.draw(R.episode, R.move))) + 1u) << kAheadShift;
   }
   NP_TRACE(a, 6);
   __syncthreads();
@@ -409,7 +424,7 @@ __device__ __forceinline__ uint32_t draw_key(const NLane<N>& L, NRng& rng, uint3
     errs += 1u;
     return kKeyDead;
   }
-  return sample_action(m, rng.draw(L.episode, L.move));
+  return ahead_key(L, sample_action(m, rng.draw(L.episode, L.move)));
 }
 
 // 8 waves per SIMD (64 VGPRs, a few spilled): 29.1 vs 30.3 us per step at
@@ -444,7 +459,7 @@ __global__ __launch_bounds__(T, 8) void k_rollout_sorted(RolloutArgs a) {
     __syncthreads();  // this step's bins are zero; last step's slots are read
     const uint32_t rank = atomicAdd(&bin[key], 1u);
     __syncthreads();
-    const uint32_t pos = bins_below(bin, key) + rank;
+    const uint32_t pos = bins_below<7>(bin, key) + rank;  // keys up to kKeyChallengeLost = 25
     if (t < 32u) s_bin[(s + 1) & 1][t] = 0u;  // read for the last time in step s - 1
     uint4 wa, wb;
     pack(L, wa, wb);
@@ -466,7 +481,7 @@ __global__ __launch_bounds__(T, 8) void k_rollout_sorted(RolloutArgs a) {
       if (key == kKeyDead) continue;
     }
     const uint32_t err_before = L.err;
-    apply_decision(L, key);
+    apply_decision(L, key_action(key));
     L.move += 1u;
     resolve_chance(L, rng);
     errs += (L.err && !err_before) ? 1u : 0u;

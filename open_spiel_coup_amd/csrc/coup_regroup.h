@@ -20,12 +20,14 @@ constexpr uint32_t kKeyReset = 18u;  // the lane finished: deal its next episode
 constexpr uint32_t kKeyDead = 19u;   // no decision to play (errored lane, or past the batch)
 constexpr uint32_t kKeyCount = 20u;
 
-// Exclusive prefix of the key counts below `key`: five broadcast 16-byte
-// LDS reads (every lane reads the same addresses, no bank conflicts).
+// Exclusive prefix of the key counts below `key`: Q broadcast 16-byte LDS
+// reads (every lane reads the same addresses, no bank conflicts); Q = 5 for
+// the 20 decision keys, 7 with the N-player refined keys (coup_nlane.h).
+template <int Q = 5>
 __device__ __forceinline__ uint32_t bins_below(const uint32_t* bin, uint32_t key) {
   uint32_t below = 0u;
 #pragma unroll
-  for (int q = 0; q < 5; ++q) {
+  for (int q = 0; q < Q; ++q) {
     const uint4 b = reinterpret_cast<const uint4*>(bin)[q];
     below += (4u * q + 0u < key ? b.x : 0u) + (4u * q + 1u < key ? b.y : 0u) + (4u * q + 2u < key ? b.z : 0u) +
              (4u * q + 3u < key ? b.w : 0u);
