@@ -36,6 +36,10 @@ __device__ __forceinline__ void count_philox_eval() {
 namespace coup {
 
 constexpr int kThreads = 256;
+// lanes per regrouping block of the 2-player sorted step / rollout
+// (profiles/r02/ab/sort_block_size_2p.log)
+constexpr int kStepSortLanes = 512;
+constexpr int kRolloutSortLanes = 1024;
 constexpr int kObsSize = COUP_OBS_SIZE;
 
 // The RNG key of lane i (global env id).  A measurement
@@ -926,6 +930,21 @@ __global__ __launch_bounds__(kThreads) void k_rollout(RolloutArgs a) {
   if (errs) atomicAdd(a.err_count, errs);
 }
 
+// The regrouping key of decision x at L: x itself, or refine_key
+// (coup_lane.h) in -DCOUP_REFINE_KEYS builds.  Unlike the 6-player kernels,
+// the 2-player ones lose with refined keys (step 27.9 -> 30.9 us, rollout
+// 15.9 -> 16.4 us per 2^20-lane step, profiles/r02/ab/refined_keys_2p.log):
+// the step computes them in the unsorted phase 1, and a 2-player Pass has
+// no next responder to tell apart.
+__device__ __forceinline__ uint32_t regroup_key(const Lane& L, uint32_t x) {
+#ifdef COUP_REFINE_KEYS
+  return refine_key(L, x);
+#else
+  (void)L;
+  return x;
+#endif
+}
+
 // The bare step (no observations, no history) with the block's lanes
 // regrouped by decision (batches of 2^18 lanes and more: coup_regroup.h),
 // the 2-player form of np::k_step_sorted.  Phase 1: each thread takes its
@@ -934,17 +953,19 @@ __global__ __launch_bounds__(kThreads) void k_rollout(RolloutArgs a) {
 // decision and resolves the deals; finished lanes are listed and dealt their
 // next episode by the block's first threads.  Phase 3: each thread stores
 // its own lane's record and outputs, coalesced.  Same results as k_step.
-template <bool UNIFORM>
-__global__ __launch_bounds__(kThreads, 8) void k_step_sorted(StepArgs a) {
-  __shared__ uint4 s_rec[kThreads];
-  __shared__ uint32_t s_meta[kThreads];   // slot -> owner thread | key << 8 | st << 13
-  __shared__ uint32_t s_out[kThreads];    // slot -> act + 1 | st << 5 | (rew + 2) << 7 | (ret + 2) << 10 | cp << 24
-  __shared__ uint32_t s_legal[kThreads];  // slot -> post-step legal mask
-  __shared__ uint32_t s_reset[kThreads];  // slots whose lane auto-resets
+template <bool UNIFORM, int T = kThreads>
+__global__ __launch_bounds__(T, 8) void k_step_sorted(StepArgs a) {
+  static_assert((T & (T - 1)) == 0 && T >= 64 && T <= 1024, "power-of-two block of whole waves");
+  constexpr uint32_t kO = T <= 256 ? 8u : 10u;  // owner-thread bits of s_meta
+  __shared__ uint4 s_rec[T];
+  __shared__ uint32_t s_meta[T];   // slot -> owner thread | key << kO | st << kO + 5
+  __shared__ uint32_t s_out[T];    // slot -> act + 1 | st << 5 | (rew + 2) << 7 | (ret + 2) << 10 | cp << 24
+  __shared__ uint32_t s_legal[T];  // slot -> post-step legal mask
+  __shared__ uint32_t s_reset[T];  // slots whose lane auto-resets
   __shared__ uint32_t s_bin[32];
   __shared__ uint32_t s_nreset;
   const uint32_t t = threadIdx.x;
-  const int64_t base = (int64_t)blockIdx.x * kThreads;
+  const int64_t base = (int64_t)blockIdx.x * T;
   const int64_t i = base + t;
   const bool live = i < a.n;
   if (t < 32u) s_bin[t] = 0u;
@@ -971,34 +992,35 @@ __global__ __launch_bounds__(kThreads, 8) void k_step_sorted(StepArgs a) {
         count_error(a.err_count);
         key = kKeyReset;  // rejected: nothing to apply either
       } else {
-        key = x;
+        key = regroup_key(L, x);
       }
     }
   }
   __syncthreads();
   const uint32_t rank = atomicAdd(&s_bin[key], 1u);
   __syncthreads();
-  const uint32_t pos = bins_below(s_bin, key) + rank;
+  const uint32_t pos = bins_below<7>(s_bin, key) + rank;  // keys up to kKeyChallengeLost = 25
   s_rec[pos] = pack(L);
-  s_meta[pos] = t | (key << 8) | (st << 13);
+  s_meta[pos] = t | (key << kO) | (st << (kO + 5));
   __syncthreads();
 
   // phase 2: thread t runs slot t's decision
   {
-    const uint32_t m = s_meta[t], k = (m >> 8) & 31u;
+    const uint32_t m = s_meta[t], k = (m >> kO) & 31u;
     if (k != kKeyDead) {
       L = unpack(s_rec[t]);
-      uint32_t out = ((m >> 13) & 3u) << 5 | (2u << 7), legal = 0u;  // no action, reward 0
+      uint32_t out = ((m >> (kO + 5)) & 3u) << 5 | (2u << 7), legal = 0u;  // no action, reward 0
       bool pending = false;
-      if (k < kKeyReset) {
-        Rng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, base + (m & 255u)), 0u, make_uint4(0, 0, 0, 0)};
+      if (is_decision_key(k)) {
+        Rng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, base + (m & (T - 1u))), 0u, make_uint4(0, 0, 0, 0)};
+        const uint32_t x = key_action(k);
         const uint32_t err_before = L.err;
-        apply_decision_v1(L, k);  // regrouped lanes diverge little: the branch form (coup_lane.h)
+        apply_decision_v1(L, x);  // regrouped lanes diverge little: the branch form (coup_lane.h)
         L.move += 1u;
         resolve_chance(L, rng);
         if (L.err && !err_before) count_error(a.err_count);
         const bool term = is_terminal(L);
-        out = (k + 1u) | ((term ? COUP_STEP_LAST : COUP_STEP_MID) << 5) | ((uint32_t)(L.r0 + 2) << 7);
+        out = (x + 1u) | ((term ? COUP_STEP_LAST : COUP_STEP_MID) << 5) | ((uint32_t)(L.r0 + 2) << 7);
         if (a.ep_count && term) out |= (uint32_t)(return0(L) + 2) << 10;
         pending = term && a.auto_reset != 0;
         if (pending) s_reset[atomicAdd(&s_nreset, 1u)] = t;
@@ -1016,9 +1038,9 @@ __global__ __launch_bounds__(kThreads, 8) void k_step_sorted(StepArgs a) {
 
   // the auto-resets (vector_env.py:62-65), packed onto the first threads
   const uint32_t nreset = s_nreset;
-  for (uint32_t j = t; j < nreset; j += kThreads) {
+  for (uint32_t j = t; j < nreset; j += T) {
     const uint32_t slot = s_reset[j];
-    Rng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, base + (s_meta[slot] & 255u)), 0u,
+    Rng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, base + (s_meta[slot] & (T - 1u))), 0u,
             make_uint4(0, 0, 0, 0)};
     const Lane R = new_episode(unpack(s_rec[slot]).episode + 1u, rng, none);
     s_rec[slot] = pack(R);
@@ -1051,7 +1073,7 @@ __device__ __forceinline__ uint32_t draw_key(const Lane& L, Rng& rng, uint32_t& 
     errs += 1u;
     return kKeyDead;
   }
-  return sample_action(m, rng.draw(L.episode, L.move));
+  return regroup_key(L, sample_action(m, rng.draw(L.episode, L.move)));
 }
 
 // k_rollout with the block's lanes regrouped by decision every step
@@ -1061,13 +1083,16 @@ __device__ __forceinline__ uint32_t draw_key(const Lane& L, Rng& rng, uint32_t& 
 // lanes get kKeyReset and are dealt their next episode together, in one
 // wave.  Per-lane statistics live in LDS by lane; the lanes go home at the
 // end.  Same results as k_rollout.
-__global__ __launch_bounds__(kThreads, 8) void k_rollout_sorted(RolloutArgs a) {
-  __shared__ uint4 s_rec[kThreads];
-  __shared__ uint32_t s_meta[kThreads];  // slot -> lane | key << 8 | decisions this episode << 13
-  __shared__ int32_t s_eps[kThreads], s_ret[kThreads], s_len[kThreads];  // by lane
+template <int T = kThreads>
+__global__ __launch_bounds__(T, 8) void k_rollout_sorted(RolloutArgs a) {
+  static_assert((T & (T - 1)) == 0 && T >= 64 && T <= 1024, "power-of-two block of whole waves");
+  constexpr uint32_t kO = T <= 256 ? 8u : 10u;  // lane bits of s_meta
+  __shared__ uint4 s_rec[T];
+  __shared__ uint32_t s_meta[T];  // slot -> lane | key << kO | decisions this episode << kO + 5
+  __shared__ int32_t s_eps[T], s_ret[T], s_len[T];  // by lane
   __shared__ __attribute__((aligned(16))) uint32_t s_bin[2][32];
   const uint32_t t = threadIdx.x;
-  const int64_t base = (int64_t)blockIdx.x * kThreads;
+  const int64_t base = (int64_t)blockIdx.x * T;
   const bool live = base + t < a.n;
   if (t < 64u) s_bin[t >> 5][t & 31u] = 0u;
   s_eps[t] = 0;
@@ -1088,15 +1113,15 @@ __global__ __launch_bounds__(kThreads, 8) void k_rollout_sorted(RolloutArgs a) {
     __syncthreads();  // this step's bins are zero; last step's slots are read
     const uint32_t rank = atomicAdd(&bin[key], 1u);
     __syncthreads();
-    const uint32_t pos = bins_below(bin, key) + rank;
+    const uint32_t pos = bins_below<7>(bin, key) + rank;  // keys up to kKeyChallengeLost = 25
     if (t < 32u) s_bin[(s + 1) & 1][t] = 0u;  // read for the last time in step s - 1
     s_rec[pos] = pack(L);
-    s_meta[pos] = lane | (key << 8) | (cur << 13);
+    s_meta[pos] = lane | (key << kO) | (cur << (kO + 5));
     __syncthreads();
     const uint32_t m = s_meta[t];
-    lane = m & 255u;
-    key = (m >> 8) & 31u;
-    cur = m >> 13;
+    lane = m & (T - 1u);
+    key = (m >> kO) & 31u;
+    cur = m >> (kO + 5);
     L = unpack(s_rec[t]);
     if (key == kKeyDead) continue;
     rng.env_id = lane_stream_id(a.env_id_base, base + lane);
@@ -1107,7 +1132,7 @@ __global__ __launch_bounds__(kThreads, 8) void k_rollout_sorted(RolloutArgs a) {
       if (key == kKeyDead) continue;
     }
     const uint32_t err_before = L.err;
-    apply_decision_v1(L, key);  // regrouped: the branch form (2^20 lanes: 18.4 vs 19.4 us, profiles/r02/ab)
+    apply_decision_v1(L, key_action(key));  // regrouped: the branch form (2^20 lanes: 18.4 vs 19.4 us, profiles/r02/ab)
     L.move += 1u;
     resolve_chance(L, rng);
     errs += (L.err && !err_before) ? 1u : 0u;
@@ -1725,10 +1750,22 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
   hipStream_t s = env->stream;
   const int64_t n = env->batch;
   if (info == coup::kInfoNone && mode == coup::kObsNone && coup::regroup_lanes(n)) {
-    if (uniform)
-      coup::k_step_sorted<true><<<grid_for(n), coup::kThreads, 0, s>>>(a);
+    // COUP_SORT_THREADS: lanes per regrouping block (A/B; coup_regroup.h)
+    const int lanes = coup::sort_lanes("COUP_SORT_THREADS", coup::kStepSortLanes);
+    auto go = [&](auto tb) {
+      constexpr int TB = decltype(tb)::value;
+      const unsigned g = (unsigned)((n + TB - 1) / TB);
+      if (uniform)
+        coup::k_step_sorted<true, TB><<<g, TB, 0, s>>>(a);
+      else
+        coup::k_step_sorted<false, TB><<<g, TB, 0, s>>>(a);
+    };
+    if (lanes == 512)
+      go(std::integral_constant<int, 512>());
+    else if (lanes == 1024)
+      go(std::integral_constant<int, 1024>());
     else
-      coup::k_step_sorted<false><<<grid_for(n), coup::kThreads, 0, s>>>(a);
+      go(std::integral_constant<int, 256>());
     COUP_HIP_TRY(hipGetLastError());
     return COUP_OK;
   }
@@ -1785,9 +1822,14 @@ int coup_rollout(coup_env* env, int64_t steps, const coup_rollout_stats* stats) 
     a.return_sum = stats->return_sum;
     a.length_sum = stats->length_sum;
   }
-  if (coup::regroup_lanes(env->batch))
-    coup::k_rollout_sorted<<<grid_for(env->batch), coup::kThreads, 0, env->stream>>>(a);
-  else
+  if (coup::regroup_lanes(env->batch)) {
+    const int64_t n = env->batch;
+    switch (coup::sort_lanes("COUP_SORT_THREADS", coup::kRolloutSortLanes)) {
+      case 256: coup::k_rollout_sorted<256><<<grid_for(n), 256, 0, env->stream>>>(a); break;
+      case 512: coup::k_rollout_sorted<512><<<(unsigned)((n + 511) / 512), 512, 0, env->stream>>>(a); break;
+      default: coup::k_rollout_sorted<1024><<<(unsigned)((n + 1023) / 1024), 1024, 0, env->stream>>>(a); break;
+    }
+  } else
     coup::k_rollout<<<grid_for(env->batch), coup::kThreads, 0, env->stream>>>(a);
   COUP_HIP_TRY(hipGetLastError());
   return COUP_OK;

@@ -18,6 +18,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include "coup_regroup.h"
 
 namespace coup {
 
@@ -433,6 +434,44 @@ __device__ __forceinline__ void apply_challenge(Lane& L) {
       COUP_PSET(L, l, M, cp_last);
       L.err = 1u;
   }
+}
+
+// The decision of a regrouping key (coup_regroup.h).
+__device__ __forceinline__ uint32_t key_action(uint32_t k) {
+  return k < kKeyPassBlock ? k : (k < kKeyChallengeLost ? (uint32_t)kPass : (uint32_t)kChallenge);
+}
+
+// The claimed card a Challenge tests: does the challenged player (O) hold
+// it?  apply_challenge's first branch (coup.cc:635-771).
+__device__ __forceinline__ bool challenge_holds(uint32_t op_last, uint32_t cp_last, uint32_t h) {
+  if (op_last == kBlock)
+    return cp_last == kForeignAid    ? has_face_down(h, kDuke)
+           : cp_last == kAssassinate ? has_face_down(h, kContessa)
+                                     : has_face_down(h, kCaptain) || has_face_down(h, kAmbassador);
+  return op_last == kTax        ? has_face_down(h, kDuke)
+         : op_last == kExchange ? has_face_down(h, kAmbassador)
+         : op_last == kAssassinate ? has_face_down(h, kAssassin)
+                                    : has_face_down(h, kCaptain);
+}
+
+// Regrouping key of decision x at L: Pass split by what it ends, Challenge
+// by its outcome (the 2-player sorted kernels).
+__device__ __forceinline__ uint32_t refine_key(const Lane& L, uint32_t x) {
+  const uint32_t O = L.M ^ 1u;
+  if (x == kPass) {
+    switch (COUP_PGET(L, l, O)) {
+      case kBlock: return kKeyPassBlock;
+      case kForeignAid: return kKeyPassComplete + 0u;
+      case kTax: return kKeyPassComplete + 1u;
+      case kExchange: return kKeyPassComplete + 2u;
+      case kSteal: return kKeyPassComplete + 3u;
+      default: return kPass;
+    }
+  }
+  if (x == kChallenge)
+    return challenge_holds(COUP_PGET(L, l, O), COUP_PGET(L, l, L.M), COUP_PGET(L, h, O)) ? kKeyChallengeLost
+                                                                                        : (uint32_t)kChallenge;
+  return x;
 }
 
 // Decision branch of DoApplyAction (coup.cc:522-808) for a LEGAL action,

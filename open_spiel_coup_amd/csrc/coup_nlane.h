@@ -538,20 +538,8 @@ __device__ __forceinline__ void apply_decision(NLane<N>& L, uint32_t a) {
   }
 }
 
-// Regrouping keys finer than the decision (the sorted step and rollout):
-// a Pass that ends a block, completes a claim (one key per claim) or hands
-// the claim to the next responder, and a Challenge the challenged player
-// wins, each get their own key so a wave of the rules runs one branch of
-// apply_decision.  Keys 20..25 sit above kKeyReset / kKeyDead (18, 19);
-// key_action maps a key back to its decision.
-constexpr uint32_t kKeyPassBlock = 20u;     // Pass after a Block: next turn
-constexpr uint32_t kKeyPassComplete = 21u;  // + 0..3: Pass completing Foreign Aid / Tax / Exchange / Steal
-constexpr uint32_t kKeyChallengeLost = 25u; // Challenge of a player who holds the claimed card
-
-__device__ __forceinline__ uint32_t key_action(uint32_t k) {
-  return k < 20u ? k : (k < kKeyChallengeLost ? (uint32_t)kPass : (uint32_t)kChallenge);
-}
-
+// Regrouping key of decision x at L (coup_regroup.h, the sorted step and
+// rollout): Pass split by what it ends, Challenge by its outcome.
 template <int N>
 __device__ __forceinline__ uint32_t refine_key(const NLane<N>& L, uint32_t x) {
   if (x == kPass) {
@@ -566,20 +554,8 @@ __device__ __forceinline__ uint32_t refine_key(const NLane<N>& L, uint32_t x) {
       default: return kPass;
     }
   }
-  if (x == kChallenge) {
-    const uint32_t op_last = last(L, L.O), cp_last = last(L, L.M), h = hand(L, L.O);
-    bool holds;
-    if (op_last == kBlock)
-      holds = cp_last == kForeignAid    ? has_face_down(h, kDuke)
-              : cp_last == kAssassinate ? has_face_down(h, kContessa)
-                                        : has_face_down(h, kCaptain) || has_face_down(h, kAmbassador);
-    else
-      holds = op_last == kTax        ? has_face_down(h, kDuke)
-              : op_last == kExchange ? has_face_down(h, kAmbassador)
-              : op_last == kAssassinate ? has_face_down(h, kAssassin)
-                                         : has_face_down(h, kCaptain);
-    return holds ? kKeyChallengeLost : (uint32_t)kChallenge;
-  }
+  if (x == kChallenge)
+    return challenge_holds(last(L, L.O), last(L, L.M), hand(L, L.O)) ? kKeyChallengeLost : (uint32_t)kChallenge;
   return x;
 }
 

@@ -697,12 +697,6 @@ hipError_t launch_reset(const Env& e, const uint8_t* mask, int mode, int deal) {
 constexpr int kStepSortLanes = 512;
 constexpr int kRolloutSortLanes = 1024;
 
-int sort_threads(int dflt) {
-  const char* s = std::getenv("COUP_NP_SORT_THREADS");
-  const int v = s ? std::atoi(s) : dflt;
-  return (v == 256 || v == 512 || v == 1024) ? v : dflt;
-}
-
 hipError_t launch_step(const Env& e, const int8_t* actions, const coup_step_outputs* out) {
   if (e.n == 0) return hipSuccess;
   StepArgs a{};
@@ -745,7 +739,7 @@ hipError_t launch_step(const Env& e, const int8_t* actions, const coup_step_outp
         else
           k_step_sorted<N, true, false, TB><<<g, TB, 0, e.stream>>>(a);
       };
-      switch (sort_threads(kStepSortLanes)) {
+      switch (sort_lanes("COUP_NP_SORT_THREADS", kStepSortLanes)) {
         case 256: go(std::integral_constant<int, 256>()); break;
         case 1024: go(std::integral_constant<int, 1024>()); break;
         default: go(std::integral_constant<int, 512>()); break;
@@ -779,7 +773,7 @@ hipError_t launch_rollout(const Env& e, int64_t steps, const coup_rollout_stats*
     constexpr int N = decltype(np)::value;
     const unsigned grid = grid_for(e.n, kThreads);
     if (regroup_lanes(e.n)) {
-      switch (sort_threads(kRolloutSortLanes)) {
+      switch (sort_lanes("COUP_NP_SORT_THREADS", kRolloutSortLanes)) {
         case 512: k_rollout_sorted<N, 512><<<grid_for(e.n, 512), 512, 0, e.stream>>>(a); break;
         case 256: k_rollout_sorted<N, 256><<<grid, 256, 0, e.stream>>>(a); break;
         default: k_rollout_sorted<N, 1024><<<grid_for(e.n, 1024), 1024, 0, e.stream>>>(a); break;

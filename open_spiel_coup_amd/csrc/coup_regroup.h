@@ -20,6 +20,18 @@ constexpr uint32_t kKeyReset = 18u;  // the lane finished: deal its next episode
 constexpr uint32_t kKeyDead = 19u;   // no decision to play (errored lane, or past the batch)
 constexpr uint32_t kKeyCount = 20u;
 
+// Keys finer than the decision (refine_key in coup_lane.h / coup_nlane.h):
+// a Pass that ends a block or completes a claim (one key per claim), and a
+// Challenge the challenged player wins, get their own keys so a wave of the
+// rules runs one branch of apply_decision.  They sit above kKeyReset /
+// kKeyDead; key_action (coup_lane.h) maps a key back to its decision.
+constexpr uint32_t kKeyPassBlock = 20u;      // Pass after a Block: next turn
+constexpr uint32_t kKeyPassComplete = 21u;   // + 0..3: Pass completing Foreign Aid / Tax / Exchange / Steal
+constexpr uint32_t kKeyChallengeLost = 25u;  // Challenge of a player who holds the claimed card
+
+// a key that carries a decision to apply (not kKeyReset / kKeyDead)
+__host__ __device__ __forceinline__ bool is_decision_key(uint32_t k) { return k < kKeyReset || k >= kKeyPassBlock; }
+
 // Exclusive prefix of the key counts below `key`: Q broadcast 16-byte LDS
 // reads (every lane reads the same addresses, no bank conflicts); Q = 5 for
 // the 20 decision keys, 7 with the N-player refined keys (coup_nlane.h).
@@ -47,6 +59,14 @@ inline bool regroup_lanes(int64_t n) {
   const char* e = std::getenv("COUP_REGROUP");
   if (e) return std::atoi(e) != 0;
   return n >= kRegroupMinLanes;
+}
+
+// Lanes per regrouping block: `dflt`, or 256 / 512 / 1024 from environment
+// variable `var` (A/B runs; every size gives the same results).
+inline int sort_lanes(const char* var, int dflt) {
+  const char* s = std::getenv(var);
+  const int v = s ? std::atoi(s) : dflt;
+  return (v == 256 || v == 512 || v == 1024) ? v : dflt;
 }
 
 }  // namespace coup

@@ -348,6 +348,48 @@ def test_regrouped_step_equals_in_place_step(monkeypatch, auto_reset):
     assert envs["0"].error_count() == envs["1"].error_count()
 
 
+def test_regrouped_block_size_invariant(monkeypatch):
+    """2-player k_step_sorted (uniform and caller actions) and
+    k_rollout_sorted over 256-, 512- and 1024-lane blocks
+    (COUP_SORT_THREADS) agree lane by lane: records, outputs, statistics."""
+    n, seed = 3000, 53
+    knobs = ("256", "512", "1024")
+    monkeypatch.setenv("COUP_REGROUP", "1")
+    envs, stats = {}, {}
+    for knob in knobs:
+        monkeypatch.setenv("COUP_SORT_THREADS", knob)
+        envs[knob] = BatchedCoupEnv(n, seed=seed, env_id_base=99, auto_reset=True, obs=False, episode_stats=True)
+        stats[knob] = envs[knob].new_stats()
+    g = torch.Generator().manual_seed(seed)
+    for t in range(90):
+        acts = None
+        if t % 4 == 3:
+            legal = envs["256"].query(obs=False)["legal_mask"].cpu().to(torch.int64)
+            first = torch.where(legal != 0, (legal & -legal).float().log2().to(torch.int64), torch.zeros_like(legal))
+            acts = first.to(torch.int8)
+        outs = {}
+        for knob, env in envs.items():
+            monkeypatch.setenv("COUP_SORT_THREADS", knob)
+            outs[knob] = {k: v.clone() for k, v in env.step(acts).items()}
+        for knob in knobs[1:]:
+            for k in outs["256"]:
+                assert torch.equal(outs["256"][k], outs[knob][k]), (knob, t, k)
+            assert torch.equal(envs["256"].export_state(), envs[knob].export_state()), (knob, t)
+    for steps in (1, 40):
+        for knob, env in envs.items():
+            monkeypatch.setenv("COUP_SORT_THREADS", knob)
+            env.rollout(steps, stats[knob])
+        for knob in knobs[1:]:
+            assert torch.equal(envs["256"].export_state(), envs[knob].export_state()), (knob, steps)
+            for key in stats["256"]:
+                assert torch.equal(stats["256"][key], stats[knob][key]), (knob, key)
+    for knob in knobs[1:]:
+        for a, b in zip(envs["256"].episode_stats(), envs[knob].episode_stats()):
+            assert torch.equal(a, b)
+    assert int(stats["256"]["episodes"].sum()) > 0
+    assert all(env.error_count() == 0 for env in envs.values())
+
+
 def test_illegal_action_rejected():
     env = BatchedCoupEnv(4, seed=0, obs=False)
     before = _np(env.export_state()).copy()
