@@ -610,7 +610,9 @@ __device__ __forceinline__ void step_lane(const StepArgs& a, int64_t i, Lane& L,
   const uint32_t m = decision_mask(L);
   uint32_t x;
   if (UNIFORM) {
-    x = m ? sample_action(m, rng.draw(L.episode, L.move)) : 32u;
+    // in place, the rules-bound kernels mix every draw in a wave: no loop
+    x = m ? (FLOW ? sample_action(m, rng.draw(L.episode, L.move)) : sample_action_select(m, rng.draw(L.episode, L.move)))
+          : 32u;
   } else {
     x = (uint32_t)(uint8_t)a.actions_in[i];
   }
@@ -910,7 +912,7 @@ __global__ __launch_bounds__(kThreads) void k_rollout(RolloutArgs a) {
       break;
     }
     const uint32_t err_before = L.err;
-    apply_decision(L, sample_action(m, rng.draw(L.episode, L.move)));
+    apply_decision(L, sample_action_select(m, rng.draw(L.episode, L.move)));
     L.move += 1u;
     resolve_chance(L, rng);
     errs += (L.err && !err_before) ? 1u : 0u;
@@ -986,7 +988,7 @@ __global__ __launch_bounds__(T, 8) void k_step_sorted(StepArgs a) {
     } else {
       resolve_chance(L, rng);
       const uint32_t m = decision_mask(L);
-      const uint32_t x = UNIFORM ? (m ? sample_action(m, rng.draw(L.episode, L.move)) : 32u)
+      const uint32_t x = UNIFORM ? (m ? sample_action_select(m, rng.draw(L.episode, L.move)) : 32u)  // unsorted lanes
                                  : (uint32_t)(uint8_t)a.actions_in[i];
       if (x > 17u || ((m >> x) & 1u) == 0u || is_terminal(L)) {
         count_error(a.err_count);

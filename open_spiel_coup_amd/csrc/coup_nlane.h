@@ -696,7 +696,7 @@ __device__ __forceinline__ uint32_t step_lane_pre(NLane<N>& L, NRng& rng, uint32
   }
   resolve_chance(L, rng);
   const uint32_t m = decision_mask(L);
-  if (UNIFORM) x = m ? sample_action(m, rng.draw(L.episode, L.move)) : 32u;
+  if (UNIFORM) x = m ? sample_action_select(m, rng.draw(L.episode, L.move)) : 32u;  // lanes in place
   st = 1;  // MID
   if (x > 17u || ((m >> x) & 1u) == 0u || is_terminal(L)) {
     error = true;

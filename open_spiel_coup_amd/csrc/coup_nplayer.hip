@@ -382,7 +382,7 @@ __global__ __launch_bounds__(kThreads) void k_rollout(RolloutArgs a) {
       break;
     }
     const uint32_t err_before = L.err;
-    apply_decision(L, sample_action(m, rng.draw(L.episode, L.move)));
+    apply_decision(L, sample_action_select(m, rng.draw(L.episode, L.move)));
     L.move += 1u;
     resolve_chance(L, rng);
     errs += (L.err && !err_before) ? 1u : 0u;
