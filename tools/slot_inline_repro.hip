@@ -21,6 +21,8 @@
 // 5. the product's own k_slot<false> built with COUP_SLOT_INLINE, one launch
 //    per case, and stripped copies of it (variants below), to find the
 //    construct that breaks it.
+// 6. k_apply_bytehist: round 1's k_apply with the history byte stored from
+//    inside the rules, batched and one lane per launch.
 // Prints mismatches per action id, and the first few cases.
 #include <hip/hip_runtime.h>
 
@@ -174,6 +176,26 @@ __global__ __launch_bounds__(64) void k_min(SlotArgs a) {
   if (W >= 4) wave_sync();
 }
 
+// The round-1 k_apply form: the history byte stored
+// from INSIDE the inlined rules through a per-lane pointer, one thread per
+// lane.  Launched over all cases (a batch) and one case per launch (the
+// 1-lane env of a per-game State then, only thread 0 active).
+struct ByteHistory {
+  uint8_t* bytes;
+  __device__ __forceinline__ void record(uint32_t idx, uint32_t entry) {
+    if (idx < (uint32_t)kHist) bytes[idx] = (uint8_t)entry;
+  }
+};
+
+__global__ __launch_bounds__(256) void k_apply_bytehist(int n, uint4* state, const uint32_t* acts, uint8_t* hist) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Lane L = unpack(state[i]);
+  ByteHistory h{hist + (size_t)i * kHist};
+  if (!apply_action(L, acts[i], h)) return;
+  state[i] = pack(L);
+}
+
 #define CHECK(x)                                                               \
   do {                                                                         \
     hipError_t e_ = (x);                                                       \
@@ -221,10 +243,11 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&slot_hist, (size_t)m * kHist));
   CHECK(hipMalloc(&slot_out, m * sizeof(coup_slot_result)));
   std::printf("{\"slot_variants\":{");
-  for (int v = 0; v < 14; ++v) {
+  for (int v = 0; v < 16; ++v) {
     CHECK(hipMemcpy(slot_recs, recs, m * sizeof(uint4), hipMemcpyDeviceToDevice));
     CHECK(hipMemset(slot_hist, 0xFF, (size_t)m * kHist));
-    for (int i = 0; i < m; ++i) {
+    if (v == 14) k_apply_bytehist<<<(m + 255) / 256, 256>>>(m, slot_recs, acts, slot_hist);
+    for (int i = 0; v < 14 && i < m; ++i) {
       SlotArgs sa;
       sa.dst_state = slot_recs + i;
       sa.dst_hist = slot_hist + (size_t)i * kHist;
@@ -252,14 +275,26 @@ int main(int argc, char** argv) {
         default: k_min<4><<<1, 64>>>(sa); break;
       }
     }
+    if (v == 15)
+      for (int i = 0; i < m; ++i) k_apply_bytehist<<<1, 256>>>(1, slot_recs + i, acts + i, slot_hist + (size_t)i * kHist);
     CHECK(hipDeviceSynchronize());
     std::vector<uint4> got(m);
     CHECK(hipMemcpy(got.data(), slot_recs, m * sizeof(uint4), hipMemcpyDeviceToHost));
+    std::vector<uint8_t> gh;
+    if (v >= 14) {  // the history byte too: entry at index move_number_
+      gh.resize((size_t)m * kHist);
+      CHECK(hipMemcpy(gh.data(), slot_hist, gh.size(), hipMemcpyDeviceToHost));
+    }
     int bad = 0, first = -1;
     int by[18] = {0};
     for (int i = 0; i < m; ++i) {
       const uint4 e = a[i].rec, g = got[i];
-      if (e.x != g.x || e.y != g.y || e.z != g.z || e.w != g.w) {
+      bool hist_bad = false;
+      if (v >= 14 && (a[i].code & 1u)) {
+        const uint32_t idx = (a[i].code >> 8) & 0xFFu;
+        hist_bad = idx < (uint32_t)kHist && gh[(size_t)i * kHist + idx] != (uint8_t)(a[i].code >> 16);
+      }
+      if (hist_bad || e.x != g.x || e.y != g.y || e.z != g.z || e.w != g.w) {
         ++bad;
         by[ha[i] < 18u ? ha[i] : 0]++;
         if (first < 0) first = i;
@@ -270,7 +305,7 @@ int main(int argc, char** argv) {
                 v == 4 ? "no_slot_result" : v == 5 ? "no_unpack_after" : v == 6 ? "always_load" :
                 v == 7 ? "always_load_expr" : v == 8 ? "always_apply" : v == 9 ? "min0_load_apply_store" :
                 v == 10 ? "min1_if_action" : v == 11 ? "min2_if_store" : v == 12 ? "min3_slot_result" :
-                "min4_barriers", bad);
+                v == 13 ? "min4_barriers" : v == 14 ? "apply_bytehist_batch" : "apply_bytehist_1lane", bad);
     for (int x = 0; x < 18; ++x) std::printf("%s%d", x ? "," : "", by[x]);
     std::printf("]");
     if (first >= 0)
