@@ -23,6 +23,7 @@ SOURCES = [os.path.join(CSRC, "coup_kernels.hip"), os.path.join(CSRC, "coup_npla
 DEPS = SOURCES + [os.path.join(CSRC, h) for h in ("coup_lane.h", "coup_nlane.h", "coup_np.h", "coup_regroup.h")] + [
     os.path.join(ROOT, "include", "coup_mi355x.h")]
 OUT = os.path.join(HERE, "libcoup_mi355x.so")
+OBJ_DIR = os.path.join(ROOT, "build", "obj")  # git-ignored (build/)
 RUST_SRC = os.path.join(CSRC, "rust_spiel.cpp")
 RUST_DEPS = [RUST_SRC, os.path.join(ROOT, "include", "coup_rust_abi.h"), os.path.join(ROOT, "include", "coup_mi355x.hpp"),
              os.path.join(ROOT, "include", "coup_mi355x.h")]
@@ -60,9 +61,16 @@ def build_repro(force=False):
     if not force and up_to_date(REPRO_OUT, deps):
         return REPRO_OUT
     os.makedirs(os.path.dirname(REPRO_OUT), exist_ok=True)
-    subprocess.check_call([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-I", os.path.join(ROOT, "include"),
-                           "-I", CSRC, REPRO_SRC, os.path.join(CSRC, "coup_nplayer.hip"), "-o", REPRO_OUT])
+    subprocess.check_call(repro_command())
     return REPRO_OUT
+
+
+def repro_command():
+    # COUP_RULES_V1: the branch-form decision transition, the form the inlined
+    # k_slot miscompiles (the effect form, default since round 2, happens to
+    # compile correctly inline: DESIGN.md section 12)
+    return [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-DCOUP_RULES_V1", "-I", os.path.join(ROOT, "include"),
+            "-I", CSRC, REPRO_SRC, os.path.join(CSRC, "coup_nplayer.hip"), "-o", REPRO_OUT]
 
 
 def up_to_date(out=OUT, deps=DEPS):
@@ -72,12 +80,40 @@ def up_to_date(out=OUT, deps=DEPS):
     return all(os.path.getmtime(p) <= t for p in deps)
 
 
-def build(force=False, verbose=False):
-    if force or not up_to_date():
-        cmd = command(resource_usage=verbose)
+def _run_all(cmds, verbose=False):
+    """Run compiler commands concurrently (one process each); raise if any fails."""
+    procs = []
+    for cmd in cmds:
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
-        subprocess.check_call(cmd)
+        procs.append((cmd, subprocess.Popen(cmd)))
+    failed = [cmd for cmd, p in procs if p.wait() != 0]
+    if failed:
+        raise subprocess.CalledProcessError(1, failed[0])
+
+
+def build(force=False, verbose=False, repro=False):
+    """libcoup_mi355x.so (its two HIP sources compiled concurrently, then
+    linked), librust_spiel.so, and with `repro` the section-12 reproducer in
+    the same batch of compiler processes."""
+    jobs, objs = [], []
+    lib_stale = force or not up_to_date()
+    if lib_stale:
+        os.makedirs(OBJ_DIR, exist_ok=True)
+        for src in SOURCES:
+            obj = os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
+            objs.append(obj)
+            cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-I",
+                   os.path.join(ROOT, "include"), "-c", src, "-o", obj]
+            if verbose:
+                cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
+            jobs.append(cmd)
+    if repro and (force or not up_to_date(REPRO_OUT, [REPRO_SRC] + DEPS)):
+        os.makedirs(os.path.dirname(REPRO_OUT), exist_ok=True)
+        jobs.append(repro_command())
+    _run_all(jobs, verbose)
+    if lib_stale:
+        _run_all([[HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT] + objs], verbose)
     if force or not up_to_date(RUST_OUT, RUST_DEPS + [OUT]):
         cmd = rust_command()
         if verbose:

@@ -8,7 +8,10 @@ the rules behind __noinline__ functions (the shipped k_slot's form), and
 through copies of k_slot built with the rules inlined (COUP_SLOT_INLINE).
 The shipped form must agree with the per-lane form on every case; the
 inlined k_slot copies are reported (ROCm 7.2 at -O2/-O3 gets word 3 of the
-record wrong after Tax / Exchange / Steal / Block announcements)."""
+record wrong after Tax / Exchange / Steal / Block announcements).  The
+reproducer is built with the branch-form rules (-DCOUP_RULES_V1), the form
+that triggers it; it also reports round 1's k_apply with the history byte
+stored from inside the rules (apply_bytehist_*)."""
 import json
 import os
 import subprocess
