@@ -44,11 +44,14 @@ def main():
     tag = os.path.basename(os.path.dirname(os.path.normpath(src)))
     cfg = "c3"
     batch = None
+    steps = 20
     for i, a in enumerate(args):
         if a == "--config":
             cfg = args[i + 1]
         if a == "--batch":
             batch = int(args[i + 1])
+        if a == "--steps":
+            steps = int(args[i + 1])
     sys.path.insert(0, ROOT)
     from bench import CONFIGS
     batch = batch or CONFIGS[cfg][0]
@@ -62,10 +65,10 @@ def main():
         """Is `kn` the kernel bench.py times for this config?"""
         if players != 2:
             if fused:
-                return bool(re.search(r"np::k_rollout(_sorted)?<%d>|2np(9k_rollout|16k_rollout_sorted)ILi%dE"
+                return bool(re.search(r"np::k_rollout(_sorted)?<%d(, \d+)?>|2np(9k_rollout|16k_rollout_sorted)ILi%dE"
                                       % (players, players), kn))
-            return bool(re.search(r"np::k_step(_sorted)?<%d, true(, (true|false))?>|2np(6k_step|13k_step_sorted)ILi%dELb1E"
-                                  % (players, players), kn))
+            return bool(re.search(r"np::k_step(_sorted)?<%d, true(, (true|false))?(, \d+)?>|"
+                                  r"2np(6k_step|13k_step_sorted)ILi%dELb1E" % (players, players), kn))
         if "np::" in kn or "2np" in kn:
             return False
         if fused:
@@ -114,7 +117,20 @@ def main():
                             summary["bench_vs_rocprof_kernel_ms"] = [bench["roofline"]["kernel_ms"], rp]
                             summary["rocprof_compared_dispatch"] = "the timed (last) rollout launch"
                     elif tk and tk in summary.get("kernels", {}):
-                        rp = summary["kernels"][tk]["avg_ns"] * 1e-6
+                        # the timed window: the last `steps` dispatches of the
+                        # timed kernel (after the warm-up launches, which
+                        # include the first, cold one)
+                        disp = sorted((r for r in rows(os.path.join(src, "trace", "**", "*kernel_trace.csv"))
+                                       if r[col(r, "kernel", "name")] == tk),
+                                      key=lambda r: int(r[col(r, "start", "timestamp")]))
+                        window = disp[-steps:]
+                        if window:
+                            rp = sum(int(r[col(r, "end", "timestamp")]) - int(r[col(r, "start", "timestamp")])
+                                     for r in window) / len(window) * 1e-6
+                            summary["rocprof_compared_dispatch"] = f"mean of the last {len(window)} dispatches (the timed steps)"
+                        else:
+                            rp = summary["kernels"][tk]["avg_ns"] * 1e-6
+                        summary["rocprof_all_dispatch_avg_ms"] = summary["kernels"][tk]["avg_ns"] * 1e-6
                         summary["bench_vs_rocprof_kernel_ms"] = [bench["roofline"]["kernel_ms"], rp]
 
     # plain bench lines of the same lease, before and after the profiler passes
