@@ -53,7 +53,7 @@ sys.path.insert(0, ROOT)
 # step kernels (9 us, 60 us) are shorter than the host's per-step launch
 # cost, and c3, where the graph removes the ~6 us gap per step that eager
 # launches leave between kernels
-GRAPH_AUTO = ("c2", "c3", "c4")
+GRAPH_AUTO = ("c2", "c3")  # c4: K eager launches measured 38.1 vs 39.2 us per step (profiles/r02/ab/graph_vs_eager.log)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
 
