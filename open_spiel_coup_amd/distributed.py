@@ -51,6 +51,11 @@ def collate(t, dim=0):
     concatenation along `dim` in rank (= global env id) order."""
     if not dist.is_initialized() or dist.get_world_size() == 1:
         return t
+    if dim == 0 and dist.get_backend() == "nccl":
+        # RCCL writes the rank-ordered concatenation in place: no gather list, no cat
+        out = torch.empty((dist.get_world_size() * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t.contiguous())
+        return out
     parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
     dist.all_gather(parts, t.contiguous())
     return torch.cat(parts, dim)
