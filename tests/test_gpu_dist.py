@@ -115,3 +115,13 @@ def test_bench_two_ranks_gloo(config):
     assert rec["lane_errors"] == 0
     assert rec["episodes"]["finished"] > 0 and rec["episodes"]["collective"].startswith("all_gather")
     assert -2.0 <= rec["episodes"]["mean_return_p0"] <= 2.0
+    # the same 2B env ids in one process (a graph config: no timing-calibrated
+    # gate steps, so the runs play identical games): the gathered totals match
+    one = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "1", "--config", config,
+                          "--steps", "8", "--warmup", "2", "--settle", "16", "--batch", str(2 * batch),
+                          "--no-cpu-baseline"], capture_output=True, text=True, timeout=110, cwd=ROOT)
+    assert one.returncode == 0, one.stderr[-2000:]
+    single = json.loads([ln for ln in one.stdout.splitlines() if ln.startswith("{")][-1])
+    assert single["config"]["hip_graph"] and rec["config"]["hip_graph"]
+    assert single["episodes"]["finished"] == rec["episodes"]["finished"]
+    assert single["episodes"]["mean_return_p0"] == rec["episodes"]["mean_return_p0"]
