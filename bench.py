@@ -154,6 +154,12 @@ def cpu_baseline(target_s, with_obs, with_info, players=2):
     src = "oracle/coup_nplayer.c" if players != 2 else "oracle/coup_oracle.c"
     out = {"value": n * steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
            "sample": f"{n} lanes x {steps} uniform-random {players}-player steps{what}, {dt:.1f} s, {src} -O2"}
+    if players == 2:
+        # the port runs the rules on the packed record; the reference C++ is slower
+        # (it cannot be built here: coup.cc needs abseil)
+        out["note"] = ("bit-exact scalar C port of the reference rules on the packed 16-B record; SURVEY.md section 6 "
+                       "timed the reference C++ at 3.43e6 (bare) / 0.89e6 (obs x2) env-steps/s on 1 core of the "
+                       "survey host, so this baseline overstates the reference's CPU speed by roughly 5-14x")
     k = _cpu_threads()
     if k > 1:
         # same total work per thread as the 1-core sample, k lane ranges
