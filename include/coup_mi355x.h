@@ -49,6 +49,7 @@ extern "C" {
 #define COUP_STEP_FIRST 0
 #define COUP_STEP_MID 1
 #define COUP_STEP_LAST 2
+#define COUP_STEP_SKIPPED 3        /* coup_step with actions[i] < 0: lane i left untouched */
 
 /* open_spiel player ids (spiel_globals.h:28,34) */
 #define COUP_CHANCE_PLAYER (-1)
@@ -180,7 +181,11 @@ int coup_reset(coup_env* env, const uint8_t* lane_mask);
  * follow (rl_environment.py:369-382), report rewards / step type, reset a
  * finished lane (see auto_reset) and write the post-step legal mask and
  * observations.  An illegal action leaves the lane unchanged and counts in
- * coup_error_count. */
+ * coup_error_count.  A negative action skips the lane: it is left untouched
+ * (no reset, no deals, no error), reports action -1, rewards 0 and step type
+ * COUP_STEP_SKIPPED, and its legal mask / observations describe its current
+ * state -- so one launch steps any subset of the lanes (SyncVectorEnv over
+ * per-game environments, vector_env.py:40-67). */
 int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out);
 
 /* `steps` uniform-random env steps per lane in one launch, state kept in

@@ -600,6 +600,12 @@ __device__ __forceinline__ void step_lane(const StepArgs& a, int64_t i, Lane& L,
   Rng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, i), 0u, make_uint4(0, 0, 0, 0)};
   act = -1;
   rew = 0;
+  if (!UNIFORM && (int8_t)a.actions_in[i] < 0) {
+    // a negative action skips the lane: untouched, no error (SyncVectorEnv
+    // stepping a subset of its envs in one launch)
+    st = COUP_STEP_SKIPPED;
+    return;
+  }
   if (is_terminal(L)) {
     // step() after LAST starts a new episode (rl_environment.py:310-311)
     L = new_episode(L.episode + 1u, rng, hist);
@@ -981,7 +987,10 @@ __global__ __launch_bounds__(T, 8) void k_step_sorted(StepArgs a) {
   if (live) {
     L = unpack(a.state[i]);
     Rng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, i), 0u, make_uint4(0, 0, 0, 0)};
-    if (is_terminal(L)) {
+    if (!UNIFORM && (int8_t)a.actions_in[i] < 0) {
+      st = COUP_STEP_SKIPPED;  // a negative action skips the lane (coup_step)
+      key = kKeyReset;         // nothing to apply
+    } else if (is_terminal(L)) {
       L = new_episode(L.episode + 1u, rng, none);  // step() after LAST (rl_environment.py:310-311)
       st = COUP_STEP_FIRST;
       key = kKeyReset;  // nothing left to apply

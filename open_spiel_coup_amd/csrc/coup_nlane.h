@@ -689,6 +689,10 @@ constexpr uint32_t kStepDone = 18u;
 template <int N, bool UNIFORM>
 __device__ __forceinline__ uint32_t step_lane_pre(NLane<N>& L, NRng& rng, uint32_t& x, uint32_t& st, bool& error) {
   error = false;
+  if (!UNIFORM && x > 127u) {  // a negative int8 action skips the lane (coup_step)
+    st = 3;                    // COUP_STEP_SKIPPED
+    return kStepDone;
+  }
   if (is_terminal(L)) {
     L = new_episode<N>(L.episode + 1u, rng);
     st = 0;  // FIRST

@@ -12,7 +12,10 @@ INFORMATION_STATE (rl_environment.py:195-200), chance events are sampled
 until a decision node (:369-382), every time step carries both players'
 tensors and legal actions (:219-268), discounts are 0 at LAST (:252-254),
 and step() after LAST resets (:310-311).  One Environment drives one lane of
-a BatchedCoupEnv; batched learners should use BatchedCoupEnv directly.
+a BatchedCoupEnv: its own one-lane env, or -- once a vector_env.SyncVectorEnv
+adopts it -- lane i of the vector env's shared N-lane env, so that the
+vector env steps all of its games with one launch.  Batched learners that do
+not need per-game time steps should use BatchedCoupEnv directly.
 
 Chance sampling: by default the deals come from the build's Philox contract
  inside the kernel, keyed by `seed` (None, the default:
@@ -127,6 +130,7 @@ class Environment:
         self._use_observation = observation_type == ObservationType.OBSERVATION
         self._device = device
         self._seed = _resolve_seed(seed)
+        self._owner = None  # the SyncVectorEnv whose shared env holds this game, if any
         self._make_env()
         self._should_reset = True
         self._last = None
@@ -137,12 +141,41 @@ class Environment:
         # (and everything else) with one query_host round trip
         self._env = BatchedCoupEnv(1, seed=self._seed, auto_reset=False, obs=False, info_state=False,
                                    history=True, device=self._device)
+        self._lane = 0
+        self._owner = None
         self._act = torch.empty(1, dtype=torch.int8, pin_memory=True)
         self._last = None
 
+    def _bind_lane(self, env, lane, owner):
+        """Play on lane `lane` of `env` (a SyncVectorEnv's shared env, which
+        already holds this game's record and history) from now on."""
+        self._env, self._lane, self._owner = env, int(lane), owner
+
+    def _batchable(self):
+        """Whether a SyncVectorEnv may adopt this env: in-kernel chance
+        sampling (no caller sampler), on no other vector env."""
+        return self._sampler is None and self._owner is None
+
+    def _lane_actions(self, action):
+        """[B] int8 actions: `action` on this env's lane, -1 (skip) elsewhere."""
+        if self._env.batch == 1:
+            self._act[0] = int(action)
+            return self._act.to(self._env.device, non_blocking=True)
+        a = torch.full((self._env.batch,), -1, dtype=torch.int8)
+        a[self._lane] = int(action)
+        return a.to(self._env.device)
+
+    def _lane_mask(self):
+        if self._env.batch == 1:
+            return None
+        m = torch.zeros(self._env.batch, dtype=torch.uint8)
+        m[self._lane] = 1
+        return m
+
     def _state_view(self):
-        words = self._env.export_state().cpu().numpy().view(np.uint32).reshape(4).copy()
-        hist = self._env.export_history().cpu().numpy().reshape(HISTORY_BYTES).copy()
+        j = self._lane
+        words = self._env.export_state()[j].cpu().numpy().view(np.uint32).reshape(4).copy()
+        hist = self._env.export_history()[j].cpu().numpy().reshape(HISTORY_BYTES).copy()
         return words, hist
 
     def _history_list(self, words, hist):
@@ -176,7 +209,7 @@ class Environment:
 
     def _query(self):
         q = self._env.query_host(obs=self._use_observation, info_state=not self._use_observation)
-        return {k: v[0] for k, v in q.items()}
+        return {k: v[self._lane] for k, v in q.items()}
 
     def _sample_external_events(self):
         """rl_environment.py:369-382 with a caller-supplied sampler."""
@@ -189,12 +222,18 @@ class Environment:
 
     # ------------------------------------------------------------ public API
     def seed(self, seed=None):
-        """Re-key the env's chance stream (ChanceEventSampler.seed)."""
+        """Re-key the env's chance stream (ChanceEventSampler.seed).  On an
+        env a SyncVectorEnv has adopted this re-keys the vector env's shared
+        stream (every lane keeps its game); this env restarts on its next step
+        either way."""
         if self._sampler is not None:
             self._sampler.seed(seed)
             return
         self._seed = _resolve_seed(seed)
-        self._make_env()
+        if self._owner is not None:
+            self._owner._rekey(self._seed)
+        else:
+            self._make_env()
         self._should_reset = True
 
     def get_time_step(self):
@@ -217,8 +256,9 @@ class Environment:
         # skipped
         cur = self._last["current_player"] if self._last else -1
         known_legal = cur >= 0 and int(actions[0]) in self._last["legal_actions"][cur]
-        self._act[0] = int(actions[0])
-        a = self._act.to(self._env.device, non_blocking=True)
+        if not 0 <= int(actions[0]) < 128:
+            raise pyspiel.SpielError(f"illegal action {actions[0]}")  # not an int8 action id
+        a = self._lane_actions(actions[0])
         if self._sampler is None:
             self._env.step(a)
         else:
@@ -231,7 +271,7 @@ class Environment:
     def reset(self):
         self._should_reset = False
         if self._sampler is None:
-            self._env.reset()
+            self._env.reset(self._lane_mask())
             q = self._query()
         else:
             self._env.new_initial_state()
@@ -287,12 +327,12 @@ class Environment:
     def get_state(self):
         """A pyspiel-shaped CoupState snapshot of the env's lane."""
         words, hist = self._state_view()
-        return pyspiel.CoupState._from_env(self._game, self._env._h, 0, self._history_list(words, hist))
+        return pyspiel.CoupState._from_env(self._game, self._env._h, self._lane, self._history_list(words, hist))
 
     def set_state(self, new_state):
         assert new_state.get_game() == self.game, "State must have been created by the same game."
         self._env._bind_stream()
-        new_state._copy_to_env(self._env._h, 0)
+        new_state._copy_to_env(self._env._h, self._lane)
         self._last = None  # the cached legal actions no longer describe the lane
 
     @property

@@ -1,17 +1,45 @@
-"""`vector_env.SyncVectorEnv` (open_spiel/python/vector_env.py:17-78) with the
-reference's semantics, over a list of rl_environment.Environment facades.
+"""`vector_env.SyncVectorEnv` (open_spiel/python/vector_env.py:17-78) over
+rl_environment.Environment facades, stepped as one batch.
 
-This is the compatibility surface.  The vectorised path the reference's
-SyncVectorEnv stands in for is BatchedCoupEnv: one kernel steps every game,
-and observations stay on the GPU as [B, 2, 98] / [B, 2, 2492] tensors.
+The reference steps its envs one after another in a Python loop
+(vector_env.py:54-57).  Here the vector env adopts its envs' games: their
+lane records and histories move into lane i of one shared N-lane
+BatchedCoupEnv, and each Environment keeps working on its lane (its own
+step / reset / get_state / set_state still apply to that game).  A vector
+step is then one reset launch for the envs that restart, one step launch
+for the rest (lanes not stepped take action -1, which the kernel skips), and
+one device-to-host copy of every env's tensors, legal mask, player, rewards
+and terminal flag -- instead of N round trips.
+
+Chance streams: env i draws its deals from global env id i under the first
+env's seed; the envs' own seeds no longer apply once
+adopted.  The reference's envs sample from independent RandomState(None)
+streams (rl_environment.py:119-131), which no caller can replay either.
+
+Envs with a caller-supplied chance sampler (the State API path), envs of
+different games / observation types / devices, or envs already adopted by
+another vector env are stepped in the reference's loop instead.
+
+Errors: an action outside 0..127 raises SpielError before anything is
+applied; an illegal action is rejected by its lane (the other envs' actions
+are applied) and raises SpielError after the launch, as Environment.step does.
 """
+import numpy as np
+import torch
+
+from . import pyspiel
+from .env import BatchedCoupEnv
 
 
 class SyncVectorEnv:
-    def __init__(self, envs):
+    def __init__(self, envs, batched=True):
+        """batched=False keeps the reference's one-env-at-a-time loop."""
         if not isinstance(envs, list):
             raise ValueError("Need to call this with a list of rl_environment.Environment objects")
         self.envs = envs
+        self._shared = None
+        if batched and self._can_batch():
+            self._adopt(self.envs[0]._seed)
 
     def __len__(self):
         return len(self.envs)
@@ -23,19 +51,140 @@ class SyncVectorEnv:
     def num_players(self):
         return self.envs[0].num_players
 
+    @property
+    def batched(self):
+        """True when one shared env steps every game (see the module doc)."""
+        return self._shared is not None
+
+    # ------------------------------------------------------------ adoption
+    def _can_batch(self):
+        from .rl_environment import Environment
+        envs = self.envs
+        if not envs or not all(isinstance(e, Environment) and e._batchable() for e in envs):
+            return False
+        if len({id(e) for e in envs}) != len(envs):
+            return False
+        e0 = envs[0]
+        return all(e._use_observation == e0._use_observation and e._device == e0._device
+                   and e.num_players == e0.num_players == 2
+                   and str(e.game) == str(e0.game) for e in envs)
+
+    def _adopt(self, seed):
+        """Move every env's game into lane i of a new shared env keyed by
+        `seed` (records, histories and each env's pending-reset flag carry
+        over), and bind the envs to their lanes."""
+        envs = self.envs
+        records = torch.cat([e._env.export_state()[e._lane:e._lane + 1] for e in envs])
+        hist = torch.cat([e._env.export_history()[e._lane:e._lane + 1] for e in envs])
+        shared = BatchedCoupEnv(len(envs), seed=seed, auto_reset=False, obs=False, info_state=False, history=True,
+                                device=envs[0]._device)
+        shared.import_state(records)
+        shared.import_history(hist)
+        self._shared = shared
+        for i, e in enumerate(envs):
+            e._bind_lane(shared, i, self)
+
+    def _rekey(self, seed):
+        """Environment.seed() of an adopted env: the shared stream takes the
+        new seed, every lane keeps its game."""
+        for e in self.envs:
+            e._owner = None
+        self._adopt(seed)
+
+    # ------------------------------------------------------------ batched ops
+    def _query(self):
+        e0 = self.envs[0]
+        return self._shared.query_host(obs=e0._use_observation, info_state=not e0._use_observation)
+
+    def _time_steps(self, q, firsts, prev_q=None, prev=None):
+        """Time steps from one query of every lane: FIRST where firsts[i] (a
+        lane reset this call), else what Environment.get_time_step reports --
+        from prev_q when given (lanes unchanged since that query), or prev[i]
+        itself when that was already such a time step (MID or LAST)."""
+        from .rl_environment import StepType
+        out = []
+        for i, (e, first) in enumerate(zip(self.envs, firsts)):
+            if not first and prev is not None and not prev[i].first():
+                out.append(prev[i])  # the tensors are host lists: reuse, do not rebuild
+                continue
+            src = q if first or prev_q is None else prev_q
+            row = {k: v[i] for k, v in src.items()}
+            if first:
+                out.append(e._time_step(row, StepType.FIRST, None))
+            else:
+                st = StepType.LAST if int(row["terminal"]) else StepType.MID
+                e._should_reset = st == StepType.LAST
+                out.append(e._time_step(row, st, [float(x) for x in row["rewards"]]))
+        return out
+
+    def _reset_lanes(self, resets):
+        mask = torch.tensor(np.asarray(resets, dtype=np.uint8))
+        sh = self._shared
+        sh._bind_stream()
+        from . import _native
+        _native.check(sh.lib.coup_reset(sh._h, sh._mask_ptr(mask)))
+        for e, r in zip(self.envs, resets):
+            if r:
+                e._should_reset = False
+
+    def _step_batched(self, step_outputs):
+        envs = self.envs
+        n = len(envs)
+        resets = [bool(e._should_reset) for e in envs]
+        acts = np.full(n, -1, dtype=np.int8)
+        unknown = []  # envs whose action the last time step did not list as legal
+        for i, e in enumerate(envs):
+            if resets[i]:
+                continue
+            a = int(step_outputs[i].action)
+            if e._enable_legality_check:
+                legal = e._last["legal_actions"][e._last["current_player"]] if e._last else []
+                if a not in legal:
+                    raise RuntimeError(f"step() called on illegal action {a}")
+            if not 0 <= a < 128:
+                raise pyspiel.SpielError(f"illegal action {a}")  # not an int8 action id
+            cur = e._last["current_player"] if e._last else -1
+            if not (cur >= 0 and a in e._last["legal_actions"][cur]):
+                unknown.append(i)
+            acts[i] = a
+        if any(resets):
+            self._reset_lanes(resets)
+        if not all(resets):
+            self._shared.step(torch.from_numpy(acts))
+            if unknown and self._shared.error_count():
+                raise pyspiel.SpielError(f"illegal action among envs {unknown}")
+        self._q_step = self._query()
+        return self._time_steps(self._q_step, resets)
+
+    # ------------------------------------------------------------ public API
     def step(self, step_outputs, reset_if_done=False):
         """vector_env.py:40-67: returns (time_steps, reward, done, unreset_time_steps)."""
-        time_steps = [self.envs[i].step([step_outputs[i].action]) for i in range(len(self.envs))]
+        if self._shared is None:
+            time_steps = [self.envs[i].step([step_outputs[i].action]) for i in range(len(self.envs))]
+        else:
+            time_steps = self._step_batched(step_outputs)
         reward = [step.rewards for step in time_steps]
         done = [step.last() for step in time_steps]
         unreset_time_steps = time_steps
         if reset_if_done:
-            time_steps = self.reset(envs_to_reset=done)
+            if self._shared is None:
+                time_steps = self.reset(envs_to_reset=done)
+            elif any(done):
+                # the envs that go on are unchanged since the step's query
+                self._reset_lanes(done)
+                time_steps = self._time_steps(self._query(), done, prev_q=self._q_step, prev=time_steps)
+            else:
+                time_steps = self._time_steps(self._q_step, done, prev=time_steps)
         return time_steps, reward, done, unreset_time_steps
 
     def reset(self, envs_to_reset=None):
         """vector_env.py:69-78"""
         if envs_to_reset is None:
             envs_to_reset = [True for _ in range(len(self.envs))]
-        return [self.envs[i].reset() if envs_to_reset[i] else self.envs[i].get_time_step()
-                for i in range(len(self.envs))]
+        if self._shared is None:
+            return [self.envs[i].reset() if envs_to_reset[i] else self.envs[i].get_time_step()
+                    for i in range(len(self.envs))]
+        resets = [bool(r) for r in envs_to_reset]
+        if any(resets):
+            self._reset_lanes(resets)
+        return self._time_steps(self._query(), resets)

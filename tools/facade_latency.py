@@ -33,6 +33,42 @@ def scratch_query(env, rec, hist):
     return {k: v.cpu().numpy()[0] for k, v in q.items()}
 
 
+class _Out:
+    def __init__(self, a):
+        self.action = a
+
+
+def vector_env_rows(steps=40):
+    """SyncVectorEnv.step(reset_if_done=True) per env step: one shared env
+    (batched) against the reference's loop over the envs, for both
+    observation types."""
+    from open_spiel_coup_amd import rl_environment, vector_env
+    rows = {}
+    rng = np.random.default_rng(1)
+    for otype, tag in ((rl_environment.ObservationType.INFORMATION_STATE, "info"),
+                       (rl_environment.ObservationType.OBSERVATION, "obs")):
+        for k in (1, 8, 64, 256):
+            for batched in (True, False):
+                if not batched and k > 64:
+                    continue
+                envs = [rl_environment.Environment("coup", seed=k, observation_type=otype) for _ in range(k)]
+                venv = vector_env.SyncVectorEnv(envs, batched=batched)
+                ts = venv.reset()
+
+                def run(m, ts):
+                    for _ in range(m):
+                        outs = [_Out(int(rng.choice(t.observations["legal_actions"][t.current_player()])))
+                                for t in ts]
+                        ts, _, _, _ = venv.step(outs, reset_if_done=True)
+                    return ts
+                ts = run(3, ts)
+                t0 = time.perf_counter()
+                run(steps, ts)
+                us = 1e6 * (time.perf_counter() - t0) / (steps * k)
+                rows[f"vector_env_{tag}_n{k}_{'batched' if batched else 'loop'}_us_per_env_step"] = round(us, 1)
+    return rows
+
+
 def main(n=2000):
     game = pyspiel.load_game("coup")
     st = game.new_initial_state()
@@ -103,6 +139,7 @@ def main(n=2000):
     for _ in range(n):
         e1.query_host(obs=False, info_state=True)
     query_one_copy = (time.perf_counter() - t0) / n
+    vector = vector_env_rows()
     print(json.dumps({"tool": "facade_latency", "ops": n,
                       "rl_environment_step_us": round(1e6 * rl_step, 1),
                       "query_info_per_tensor_copies_us": round(1e6 * query_per_tensor, 1),
@@ -110,7 +147,7 @@ def main(n=2000):
                       "pool_child_plus_legal_us": round(1e6 * pool_child, 1),
                       "pool_clone_us": round(1e6 * pool_clone, 1),
                       "pool_observation_tensor_us": round(1e6 * pool_obs, 1),
-                      "scratch_env_child_plus_legal_us": round(1e6 * scratch_child, 1), **batched}))
+                      "scratch_env_child_plus_legal_us": round(1e6 * scratch_child, 1), **batched, **vector}))
 
 
 if __name__ == "__main__":
