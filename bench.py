@@ -1,6 +1,6 @@
 """Coup env-steps/sec on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c3i|c2|c2r|c4|c4r]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c3i|c2|c2r|c2t|c4|c4r|c4t]
 
 Workload (default c3 = configs[2] of BASELINE.json, the batch-2^20 config the
 metric is quoted on): 2-player Coup, B = 2^20 lanes per GPU, uniform-random
@@ -16,6 +16,9 @@ Other configs (secondary lines, not the headline):
   c4   configs[3]: 6-player extension, B = 2^20, no observations (parity
        unpinned w.r.t. the 2-player reference; pinned to oracle/coup_nplayer.c)
   c4r  c4 fused: `steps` 6-player env steps in ONE launch
+  c2t, c4t  c2 / c4 as ONE coup_step_trajectory launch of `steps` env steps
+       with every step's outputs (actions, rewards, step types, legal masks,
+       players) stored to [K][B] trajectory buffers; lanes in place
 
 A "step" is one batched env step over all B lanes; value = env-steps/s of
 the whole job (N x B x K / max-over-ranks wall time).  Before the W warmup
@@ -57,15 +60,19 @@ GRAPH_AUTO = ("c2", "c3")  # c4: K eager launches measured 38.1 vs 39.2 us per s
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
 
-# config -> (default batch, obs, info_state, fused, algorithmic bytes per lane-step, workload name, players)
+# config -> (default batch, obs, info_state, fused, algorithmic bytes per lane-step, workload name, players);
+# fused: False (one coup_step per step), "rollout" (coup_rollout: statistics
+# only) or "traj" (coup_step_trajectory: every step's outputs)
 CONFIGS = {
     "c3": (1 << 20, True, False, False, 824, "coup-2p-uniform-b2^20-obs", 2),
     "c3i": (1 << 18, False, True, False, 40 + 2 * 2492 * 4 + 96 + 96, "coup-2p-uniform-b2^18-infostate", 2),
     "c2": (65536, False, False, False, 40, "coup-2p-uniform-b65536", 2),
-    "c2r": (65536, False, False, True, 32, "coup-2p-uniform-b65536-fused-rollout", 2),
+    "c2r": (65536, False, False, "rollout", 32, "coup-2p-uniform-b65536-fused-rollout", 2),
+    "c2t": (65536, False, False, "traj", 40, "coup-2p-uniform-b65536-fused-trajectory", 2),
     # 2 x 48 B state + mask 4 + action 1 + rewards 6 + 1
     "c4": (1 << 20, False, False, False, 108, "coup-6p-uniform-b2^20", 6),
-    "c4r": (1 << 20, False, False, True, 96, "coup-6p-uniform-b2^20-fused-rollout", 6),
+    "c4r": (1 << 20, False, False, "rollout", 96, "coup-6p-uniform-b2^20-fused-rollout", 6),
+    "c4t": (1 << 20, False, False, "traj", 108, "coup-6p-uniform-b2^20-fused-trajectory", 6),
 }
 
 
@@ -276,11 +283,11 @@ def main():
     B0, with_obs, with_info, fused, bytes_per_lane, workload, players = CONFIGS[cfg]
     B = args.batch or B0
     env = BatchedCoupEnv(B, seed=args.seed, env_id_base=D.env_id_base(rank, B), auto_reset=True, obs=with_obs,
-                         info_state=with_info, device=dev, num_players=players, episode_stats=not fused)
+                         info_state=with_info, device=dev, num_players=players, episode_stats=fused != "rollout")
     # per-lane finished-episode counts and player-0 return sums of the timed
     # steps: the step kernels accumulate them (coup_step_outputs.episodes /
     # return_sum), the fused rollout through coup_rollout_stats
-    stats = env.new_stats() if fused else None
+    stats = env.new_stats() if fused == "rollout" else None
 
     def barrier():
         if world > 1:
@@ -300,7 +307,11 @@ def main():
         env.rollout(args.warmup)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))]
         gate_steps = _calibrate_gate(env, stream)
-        gate, timed = env.rollout_launcher(gate_steps), env.rollout_launcher(args.steps, stats)
+        gate = env.rollout_launcher(gate_steps)
+        if fused == "traj":
+            timed = env.step_trajectory_launcher(args.steps, env.trajectory_buffers(args.steps))
+        else:
+            timed = env.rollout_launcher(args.steps, stats)
     else:
         for _ in range(args.warmup):
             env.step()
@@ -311,7 +322,7 @@ def main():
         else:
             gate = env.rollout_launcher(_calibrate_gate(env, stream))
     def episode_tensors():
-        if fused:
+        if stats is not None:
             return stats["episodes"], stats["return_sum"]
         return env.episode_stats()
 
@@ -333,7 +344,7 @@ def main():
     # one collation outside the timed region: RCCL sets up its all-gather
     # channels lazily, and HIP loads torch's stack kernel on first use
     D.collate(episode_payload())
-    if fused:
+    if stats is not None:
         for t in stats.values():
             t.zero_()
     else:
@@ -393,9 +404,12 @@ def main():
         sorted_ = "_sorted" if _regrouped(B) else ""
         if players != 2:
             ahead = os.environ.get("COUP_AHEAD", "1") != "0"
-            kernel = ("coup::np::k_rollout%s<%d>" % (sorted_, players) if fused else
+            kernel = ("coup::np::k_step_trajectory<%d>" % players if fused == "traj" else
+                      "coup::np::k_rollout%s<%d>" % (sorted_, players) if fused else
                       "coup::np::k_step_sorted<%d, true, %s>" % (players, "true" if ahead else "false") if sorted_ else
                       "coup::np::k_step<%d, true>" % players)
+        elif fused == "traj":
+            kernel = "coup::k_step_trajectory"
         elif fused:
             kernel = "coup::k_rollout" + sorted_
         elif with_info:
@@ -405,7 +419,10 @@ def main():
         else:
             kernel = "coup::k_step<true, 0, 256, 0>"
         outputs = ("ObservationTensor fp32 [B][2][98] per step" if with_obs else
-                   "InformationStateTensor fp32 [B][2][2492] per step" if with_info else "none")
+                   "InformationStateTensor fp32 [B][2][2492] per step" if with_info else
+                   "per-episode statistics only" if fused == "rollout" else
+                   "actions, rewards, step types, legal masks, players: [K][B] trajectory buffers" if fused else
+                   "actions, rewards, step types, legal masks, players per step")
         line = {
             "metric": "Coup env-steps/sec at batch 2^20, 1/2/4/8 MI355X; HBM GB/s vs peak",
             "value": world * B * args.steps / elapsed,

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define COUP_ABI_VERSION 5
+#define COUP_ABI_VERSION 6
 
 #define COUP_NUM_PLAYERS 2          /* coup.h:42 */
 #define COUP_MAX_PLAYERS 6          /* N-player extension */
@@ -187,6 +187,18 @@ int coup_reset(coup_env* env, const uint8_t* lane_mask);
  * state -- so one launch steps any subset of the lanes (SyncVectorEnv over
  * per-game environments, vector_env.py:40-67). */
 int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out);
+
+/* `steps` uniform-random env steps per lane (the coup_step of actions ==
+ * NULL, with the env's auto-reset setting) in ONE launch, the state kept in
+ * registers, every step's outputs stored: out's actions / rewards /
+ * step_type / legal_mask / cur_player point to [steps][B][...] buffers
+ * (slice t = step t, laid out as coup_step's [B][...]); episodes /
+ * return_sum are [B] accumulators as in coup_step.  obs / info_state must
+ * be NULL, and the env must not keep histories (COUP_E_INVALID).  Results
+ * equal `steps` coup_step calls -- the trajectory a learner collects
+ * (rl_environment.py:282-322 per step), without the per-step launch and
+ * record round trip.  Lanes stay in place (no regrouping by decision). */
+int coup_step_trajectory(coup_env* env, int64_t steps, const coup_step_outputs* out);
 
 /* `steps` uniform-random env steps per lane in one launch, state kept in
  * registers (auto-reset always on); per-lane statistics are accumulated

@@ -5,7 +5,7 @@ BStarcheus/open_spiel_coup, bit-exact), HIP kernels behind a C ABI.
     env = BatchedCoupEnv(batch=1 << 20, seed=1)
     ts = env.step()          # uniform random policy, obs for both players
 """
-from .env import BatchedCoupEnv, FIRST, MID, LAST, NUM_ACTIONS, OBS_SIZE, INFO_STATE_SIZE  # noqa: F401
+from .env import BatchedCoupEnv, FIRST, MID, LAST, SKIPPED, NUM_ACTIONS, OBS_SIZE, INFO_STATE_SIZE  # noqa: F401
 from . import packed  # noqa: F401
 
-__all__ = ["BatchedCoupEnv", "FIRST", "MID", "LAST", "NUM_ACTIONS", "OBS_SIZE", "INFO_STATE_SIZE", "packed"]
+__all__ = ["BatchedCoupEnv", "FIRST", "MID", "LAST", "SKIPPED", "NUM_ACTIONS", "OBS_SIZE", "INFO_STATE_SIZE", "packed"]

@@ -938,6 +938,44 @@ __global__ __launch_bounds__(kThreads) void k_rollout(RolloutArgs a) {
   if (errs) atomicAdd(a.err_count, errs);
 }
 
+// coup_step_trajectory: `steps` uniform-policy env steps per lane in ONE
+// launch, the state held in registers, step t's outputs stored to slice t
+// of the caller's [steps][B] buffers.  The step is k_step's own step_lane
+// (effect form, no history), so the outputs, records and accumulators equal
+// those of `steps` coup_step launches; what goes is the per-step record
+// round trip and launch.
+__global__ __launch_bounds__(kThreads) void k_step_trajectory(StepArgs a, int64_t steps) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= a.n) return;
+  Lane L = unpack(a.state[i]);
+  NoHistory none;
+  int32_t eps = 0, ret_sum = 0;
+  for (int64_t t = 0; t < steps; ++t) {
+    int act;
+    uint32_t st;
+    int32_t rew, ret = 0;
+    step_lane<true, false>(a, i, L, act, st, rew, ret, none);
+    const int64_t o = t * a.n + i;
+    if (a.actions) a.actions[o] = (int8_t)act;
+    if (a.rewards) {
+      a.rewards[2 * o] = (int8_t)rew;
+      a.rewards[2 * o + 1] = (int8_t)(-rew);
+    }
+    if (a.step_type) a.step_type[o] = (uint8_t)st;
+    if (a.legal) a.legal[o] = legal_mask(L);
+    if (a.cur_player) a.cur_player[o] = (int8_t)current_player(L);
+    if (st == COUP_STEP_LAST) {
+      eps += 1;
+      ret_sum += ret;
+    }
+  }
+  a.state[i] = pack(L);
+  if (a.ep_count) {
+    a.ep_count[i] += eps;
+    a.ep_return[i] += ret_sum;
+  }
+}
+
 // The regrouping key of decision x at L: x itself, or refine_key
 // (coup_lane.h) in -DCOUP_REFINE_KEYS builds.  Unlike the 6-player kernels,
 // the 2-player ones lose with refined keys (step 27.9 -> 30.9 us, rollout
@@ -1842,6 +1880,39 @@ int coup_rollout(coup_env* env, int64_t steps, const coup_rollout_stats* stats) 
     }
   } else
     coup::k_rollout<<<grid_for(env->batch), coup::kThreads, 0, env->stream>>>(a);
+  COUP_HIP_TRY(hipGetLastError());
+  return COUP_OK;
+}
+
+int coup_step_trajectory(coup_env* env, int64_t steps, const coup_step_outputs* out) {
+  COUP_CHECK_ENV(env);
+  if (steps < 0) return fail(COUP_E_INVALID, "coup_step_trajectory: negative steps");
+  if (env->hist) return fail(COUP_E_INVALID, "coup_step_trajectory: not available on an env with COUP_FLAG_HISTORY");
+  if (out && (out->obs || out->info_state))
+    return fail(COUP_E_INVALID, "coup_step_trajectory: obs / info_state are written by coup_step only");
+  if (out && (out->episodes == nullptr) != (out->return_sum == nullptr))
+    return fail(COUP_E_INVALID, "coup_step_trajectory: episodes and return_sum go together");
+  if (env->batch == 0 || steps == 0) return COUP_OK;
+  if (env->generic) return np_result(coup::np::launch_trajectory(np_env(env), steps, out), "coup_step_trajectory");
+  coup::StepArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.state = env->state;
+  a.n = env->batch;
+  a.seed_lo = (uint32_t)env->seed;
+  a.seed_hi = (uint32_t)(env->seed >> 32);
+  a.env_id_base = env->env_id_base;
+  a.auto_reset = (env->flags & COUP_FLAG_AUTO_RESET) ? 1 : 0;
+  a.err_count = env->err_count;
+  if (out) {
+    a.actions = out->actions;
+    a.rewards = out->rewards;
+    a.step_type = out->step_type;
+    a.legal = out->legal_mask;
+    a.cur_player = out->cur_player;
+    a.ep_count = out->episodes;
+    a.ep_return = out->return_sum;
+  }
+  coup::k_step_trajectory<<<grid_for(env->batch), coup::kThreads, 0, env->stream>>>(a, steps);
   COUP_HIP_TRY(hipGetLastError());
   return COUP_OK;
 }

@@ -112,7 +112,7 @@ __device__ __forceinline__ void store_episode(const StepArgs& a, int64_t i, int2
 // count), step type, post-step legal mask and current player.
 template <int N>
 __device__ __forceinline__ void store_step_outputs(const StepArgs& a, int64_t i, int act, uint32_t st, uint32_t rl,
-                                                   uint32_t rc, uint32_t legal, int cp) {
+                                                   uint32_t rc, uint32_t legal, int cp, bool legal_cp = true) {
   if (a.actions) a.actions[i] = (int8_t)act;
   if (a.rewards) {
     // Rewards(): rc to everybody, -(N-1) rc to the loser; an even-N row
@@ -131,8 +131,8 @@ __device__ __forceinline__ void store_step_outputs(const StepArgs& a, int64_t i,
     }
   }
   if (a.step_type) a.step_type[i] = (uint8_t)st;
-  if (a.legal) a.legal[i] = legal;
-  if (a.cur_player) a.cur_player[i] = (int8_t)cp;
+  if (legal_cp && a.legal) a.legal[i] = legal;
+  if (legal_cp && a.cur_player) a.cur_player[i] = (int8_t)cp;
 }
 
 // One rl_environment step per lane (step_lane, coup_nlane.h), lanes in
@@ -195,7 +195,11 @@ __device__ __forceinline__ uint32_t ahead_key(const NLane<N>& L, uint32_t x) {
 #endif
 }
 
-template <int N, bool UNIFORM, bool AHEAD, int T = kThreads>
+// RS: the threads that deal the block's auto-resets store those lanes'
+// records, legal masks and players themselves, and every other lane is
+// stored right after phase 2 -- one barrier fewer, and no wave of the block
+// waits for the resets (COUP_NP_RESET_STORE=0/1 for A/B runs).
+template <int N, bool UNIFORM, bool AHEAD, int T = kThreads, bool RS = false>
 #ifdef COUP_WAVE_TRACE
 // the stamps' registers must not cost the traced kernel its 8 blocks per CU
 #define NP_STEP_SORTED_BOUNDS __launch_bounds__(T, 8)
@@ -206,7 +210,7 @@ __global__ NP_STEP_SORTED_BOUNDS void k_step_sorted(StepArgs a) {
   __shared__ uint4 s_a[T], s_b[T];
   __shared__ uint32_t s_meta[T];   // slot -> owner thread | key << kO | st << kO + 5 | error << kO + 7
   __shared__ uint32_t s_out[T];    // slot -> act + 1 | st << 5 | rl << 7 | rc << 10 | error << 13 |
-                                          //         (ret0 + 16) << 14 | cp << 24
+                                          //         (ret0 + 16) << 14 | reset pending << 19 | cp << 24
   __shared__ uint32_t s_legal[T];  // slot -> post-step legal mask
   __shared__ uint32_t s_reset[T];  // slots whose lane auto-resets
   __shared__ uint32_t s_bin[32];
@@ -297,7 +301,10 @@ __global__ NP_STEP_SORTED_BOUNDS void k_step_sorted(StepArgs a) {
         out = (x + 1u) | ((term ? 2u : 1u) << 5) | (L.rloser << 7) | (L.rcount << 10) | ((uint32_t)err << 13);
         if (a.ep_count && term) out |= (uint32_t)(returns(L, 0u) + 16) << 14;
         pending = term && a.auto_reset != 0;
-        if (pending) s_reset[atomicAdd(&s_nreset, 1u)] = t;
+        if (pending) {
+          s_reset[atomicAdd(&s_nreset, 1u)] = t;
+          out |= 1u << 19;
+        }
         uint4 wa, wb;
         pack(L, wa, wb);
         s_a[t] = wa;
@@ -319,6 +326,41 @@ __global__ NP_STEP_SORTED_BOUNDS void k_step_sorted(StepArgs a) {
   NP_TRACE(a, 4);
   __syncthreads();
   NP_TRACE(a, 5);
+
+  if (RS) {
+    // phase 3 first: each thread stores its own lane, except the record,
+    // legal mask and player of a lane that resets (written below)
+    const uint32_t nreset = s_nreset;
+    if (live) {
+      const uint32_t o = s_out[pos];
+      const bool pend = (o >> 19) & 1u;
+      if (!pend) {
+        a.sa[i] = s_a[pos];
+        a.sb[i] = s_b[pos];
+      }
+      store_step_outputs<N>(a, i, (int)(o & 31u) - 1, (o >> 5) & 3u, (o >> 7) & 7u, (o >> 10) & 7u, s_legal[pos],
+                            (int)(int8_t)(o >> 24), !pend);
+      store_episode(a, i, eps, (o >> 5) & 3u, (int32_t)((o >> 14) & 31u) - 16);
+    }
+    // the auto-resets, packed onto the first threads, stored to their lanes
+    for (uint32_t j = t; j < nreset; j += T) {
+      const uint32_t slot = s_reset[j];
+      const int64_t li = base + (s_meta[slot] & (T - 1u));
+      NRng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, li), 0u, make_uint4(0, 0, 0, 0)};
+      const NLane<N> R = new_episode<N>(plane_episode(s_b[slot]) + 1u, rng);
+      uint4 wa, wb;
+      pack(R, wa, wb);
+      const uint32_t legal = legal_mask(R);
+      if (UNIFORM && AHEAD) wb.w |= (ahead_key(R, sample_action(legal, rng.draw(R.episode, R.move))) + 1u) << kAheadShift;
+      a.sa[li] = wa;
+      a.sb[li] = wb;
+      if (a.legal) a.legal[li] = legal;
+      if (a.cur_player) a.cur_player[li] = (int8_t)current_player(R);
+    }
+    NP_TRACE(a, 8);
+    NP_TRACE_WAIT(a, 9);
+    return;
+  }
 
   // the auto-resets, packed onto the first threads
   const uint32_t nreset = s_nreset;
@@ -350,6 +392,43 @@ __global__ NP_STEP_SORTED_BOUNDS void k_step_sorted(StepArgs a) {
   store_episode(a, i, eps, (o >> 5) & 3u, (int32_t)((o >> 14) & 31u) - 16);
   NP_TRACE(a, 8);
   NP_TRACE_WAIT(a, 9);
+}
+
+// coup_step_trajectory for N players: `steps` uniform steps per lane in one
+// launch (lanes in place), step t's outputs to slice t of the [steps][B]
+// buffers; k_step's step_lane, so the results equal `steps` coup_step
+// launches of the in-place kernel (and of the regrouped one, which the GPU
+// tests hold equal).
+template <int N>
+__global__ __launch_bounds__(kThreads) void k_step_trajectory(StepArgs a, int64_t steps) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= a.n) return;
+  NLane<N> L = unpack<N>(a.sa[i], a.sb[i]);
+  NRng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, i), 0u, make_uint4(0, 0, 0, 0)};
+  int32_t eps = 0, ret_sum = 0;
+  uint32_t errs = 0;
+  for (int64_t t = 0; t < steps; ++t) {
+    int act;
+    uint32_t st, rl, rc;
+    int32_t ret0;
+    bool error;
+    step_lane<N, true>(L, rng, 0u, a.auto_reset != 0, act, st, rl, rc, ret0, error);
+    errs += error ? 1u : 0u;
+    store_step_outputs<N>(a, t * a.n + i, act, st, rl, rc, legal_mask(L), current_player(L));
+    if (st == 2u) {
+      eps += 1;
+      ret_sum += ret0;
+    }
+  }
+  uint4 wa, wb;
+  pack(L, wa, wb);
+  a.sa[i] = wa;
+  a.sb[i] = wb;
+  if (a.ep_count) {
+    a.ep_count[i] += eps;
+    a.ep_return[i] += ret_sum;
+  }
+  if (errs) atomicAdd(a.err_count, errs);
 }
 
 struct RolloutArgs {
@@ -732,8 +811,11 @@ hipError_t launch_step(const Env& e, const int8_t* actions, const coup_step_outp
       auto go = [&](auto lanes) {
         constexpr int TB = decltype(lanes)::value;
         const unsigned g = grid_for(e.n, TB);
+        const char* rs = std::getenv("COUP_NP_RESET_STORE");  // 1: resets stored by their dealers (A/B)
         if (actions)
           k_step_sorted<N, false, false, TB><<<g, TB, 0, e.stream>>>(a);
+        else if (ahead && rs && std::atoi(rs) != 0)
+          k_step_sorted<N, true, true, TB, true><<<g, TB, 0, e.stream>>>(a);
         else if (ahead)
           k_step_sorted<N, true, true, TB><<<g, TB, 0, e.stream>>>(a);
         else
@@ -750,6 +832,31 @@ hipError_t launch_step(const Env& e, const int8_t* actions, const coup_step_outp
       k_step<N, true><<<grid, kThreads, 0, e.stream>>>(a);
     }
     if (obs) k_obs<N><<<grid_for(e.n, kObsLanes), kThreads, 0, e.stream>>>(e.sa, e.sb, e.n, obs);
+  });
+}
+
+hipError_t launch_trajectory(const Env& e, int64_t steps, const coup_step_outputs* out) {
+  StepArgs a{};
+  a.sa = e.sa;
+  a.sb = e.sb;
+  a.n = e.n;
+  a.seed_lo = e.seed_lo;
+  a.seed_hi = e.seed_hi;
+  a.env_id_base = e.env_id_base;
+  a.auto_reset = e.auto_reset;
+  a.err_count = e.err_count;
+  if (out) {
+    a.actions = out->actions;
+    a.rewards = out->rewards;
+    a.step_type = out->step_type;
+    a.legal = out->legal_mask;
+    a.cur_player = out->cur_player;
+    a.ep_count = out->episodes;
+    a.ep_return = out->return_sum;
+  }
+  return dispatch(e.players, [&](auto np) {
+    constexpr int N = decltype(np)::value;
+    k_step_trajectory<N><<<grid_for(e.n, kThreads), kThreads, 0, e.stream>>>(a, steps);
   });
 }
 

@@ -14,6 +14,7 @@ import torch
 from . import _native
 
 FIRST, MID, LAST = 0, 1, 2
+SKIPPED = 3  # coup_step with a negative action: the lane was left untouched
 NUM_ACTIONS = 18
 OBS_SIZE = 98
 INFO_STATE_SIZE = 2492
@@ -210,28 +211,64 @@ class BatchedCoupEnv:
                                      ("actions", "rewards", "step_type", "legal_mask", "current_player", "obs",
                                       "info_state")], _addr(self.episodes), _addr(self.return_sum))
 
+    def _fused_trajectory(self, buf):
+        """Whether coup_step_trajectory can write `buf` in one launch: no
+        observation / info-state tensors, no history."""
+        return not self.history and "obs" not in buf and "info_state" not in buf
+
+    def _trajectory_outputs(self, buf):
+        return _native.StepOutputs(*[_addr(buf[k]) if k in buf else None for k in
+                                     ("actions", "rewards", "step_type", "legal_mask", "current_player", "obs",
+                                      "info_state")], _addr(self.episodes), _addr(self.return_sum))
+
     def collect_trajectory(self, steps, buf=None):
         """`steps` uniform-policy env steps whose outputs land in slice t of
-        [T, B, ...] device buffers (trajectory_buffers); returns them."""
+        [T, B, ...] device buffers (trajectory_buffers); returns them.  Without
+        observation tensors or history the T steps run as ONE launch
+        (coup_step_trajectory, state in registers); otherwise one coup_step
+        per slice.  Same results either way."""
         buf = buf if buf is not None else self.trajectory_buffers(steps)
         self._bind_stream()
+        if self._fused_trajectory(buf):
+            out = self._trajectory_outputs(buf)
+            _native.check(self.lib.coup_step_trajectory(self._h, int(steps), ctypes.byref(out)))
+            return buf
         for t in range(int(steps)):
             out = self._slice_outputs(buf, t)
             _native.check(self.lib.coup_step(self._h, None, ctypes.byref(out)))
         return buf
+
+    def step_trajectory_launcher(self, steps, buf):
+        """collect_trajectory(steps, buf) as a zero-argument callable that only
+        enqueues the one coup_step_trajectory launch (timing loops)."""
+        if not self._fused_trajectory(buf):
+            raise ValueError("coup_step_trajectory writes no obs / info_state and needs an env without history")
+        self._bind_stream()
+        out = self._trajectory_outputs(buf)
+        fn, h, k, ref = self.lib.coup_step_trajectory, self._h, int(steps), ctypes.byref(out)
+
+        def launch():
+            _native.check(fn(h, k, ref))
+        launch.out = out  # keeps the struct alive with the callable
+        launch.buf = buf
+        return launch
 
     def capture_trajectory(self, steps, buf=None):
         """collect_trajectory recorded as one HIP graph: `graph.replay()`
         steps the env `steps` times and refills the same [T, B, ...] buffers.
         Returns (graph, buffers).  The env must outlive the graph."""
         buf = buf if buf is not None else self.trajectory_buffers(steps)
-        self._traj_outs = [self._slice_outputs(buf, t) for t in range(int(steps))]
+        fused = self._fused_trajectory(buf)
+        self._traj_outs = ([self._trajectory_outputs(buf)] if fused else
+                           [self._slice_outputs(buf, t) for t in range(int(steps))])
         g = torch.cuda.CUDAGraph()
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.graph(g, stream=side):
             self._bind_stream()
-            for out in self._traj_outs:
+            if fused:
+                _native.check(self.lib.coup_step_trajectory(self._h, int(steps), ctypes.byref(self._traj_outs[0])))
+            for out in ([] if fused else self._traj_outs):
                 _native.check(self.lib.coup_step(self._h, None, ctypes.byref(out)))
         torch.cuda.current_stream(self.device).wait_stream(side)
         self._bind_stream()

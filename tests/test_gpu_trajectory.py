@@ -1,0 +1,81 @@
+"""coup_step_trajectory: `steps` uniform env steps in one launch with every
+step's outputs in [T][B] buffers, against `steps` coup_step launches."""
+import ctypes
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from open_spiel_coup_amd import BatchedCoupEnv, _native  # noqa: E402
+
+KEYS = ("actions", "rewards", "step_type", "legal_mask", "current_player")
+
+
+def _stepped(env, steps, buf):
+    """The same trajectory through one coup_step per slice."""
+    env._bind_stream()
+    for t in range(steps):
+        _native.check(env.lib.coup_step(env._h, None, ctypes.byref(env._slice_outputs(buf, t))))
+    return buf
+
+
+@pytest.mark.parametrize("regroup", ["0", "1"], ids=["steps-in-place", "steps-regrouped"])
+@pytest.mark.parametrize("auto_reset", [True, False])
+@pytest.mark.parametrize("players,generic", [(2, False), (2, True), (3, False), (6, False)],
+                         ids=["2p", "2p-generic", "3p", "6p"])
+def test_trajectory_equals_steps(monkeypatch, regroup, auto_reset, players, generic):
+    """Every output of every step, the final records and the per-episode
+    accumulators equal those of coup_step launched once per step (in place
+    or regrouped by decision), over three consecutive collections."""
+    monkeypatch.setenv("COUP_REGROUP", regroup)
+    n, T, seed = 1500, 48, 31 + players
+    kw = dict(seed=seed, env_id_base=1 << 20, auto_reset=auto_reset, obs=False, num_players=players,
+              generic=generic, episode_stats=True)
+    fused, ref = BatchedCoupEnv(n, **kw), BatchedCoupEnv(n, **kw)
+    bf, br = fused.trajectory_buffers(T), ref.trajectory_buffers(T)
+    assert fused._fused_trajectory(bf)
+    last = 0
+    for rep in range(3):
+        fused.collect_trajectory(T, bf)
+        _stepped(ref, T, br)
+        for k in KEYS:
+            assert torch.equal(bf[k], br[k]), (rep, k)
+        assert torch.equal(fused.export_state(), ref.export_state()), rep
+        for a, b in zip(fused.episode_stats(), ref.episode_stats()):
+            assert torch.equal(a, b), rep
+        last += int((bf["step_type"] == 2).sum())
+    assert last > 0
+    assert fused.error_count() == ref.error_count() == 0
+
+
+def test_trajectory_graph_and_full_batch():
+    """capture_trajectory records the single launch in a HIP graph; at the
+    2^20 benchmark batch the fused trajectory (lanes in place) equals the
+    regrouped per-step kernels on sampled lanes."""
+    n, T = 1 << 20, 16
+    a = BatchedCoupEnv(n, seed=3, auto_reset=True, obs=False, episode_stats=True)
+    b = BatchedCoupEnv(n, seed=3, auto_reset=True, obs=False, episode_stats=True)
+    g, buf = a.capture_trajectory(T)
+    g.replay()
+    rb = _stepped(b, T, b.trajectory_buffers(T))
+    lanes = torch.arange(0, n, 4099, device=buf["actions"].device)
+    for k in KEYS:
+        assert torch.equal(buf[k][:, lanes], rb[k][:, lanes]), k
+    assert torch.equal(a.export_state(), b.export_state())
+    assert torch.equal(a.episodes, b.episodes) and torch.equal(a.return_sum, b.return_sum)
+
+
+def test_trajectory_rejects_what_it_cannot_write():
+    env = BatchedCoupEnv(64, seed=1, obs=True)
+    buf = env.trajectory_buffers(4)
+    out = _native.StepOutputs(*[buf[k].data_ptr() if k in buf else None for k in
+                                ("actions", "rewards", "step_type", "legal_mask", "current_player", "obs",
+                                 "info_state")], None, None)
+    assert env.lib.coup_step_trajectory(env._h, 4, ctypes.byref(out)) == _native.COUP_E_INVALID
+    hist = BatchedCoupEnv(64, seed=1, obs=False, history=True)
+    assert hist.lib.coup_step_trajectory(hist._h, 4, None) == _native.COUP_E_INVALID
+    assert env.lib.coup_step_trajectory(env._h, -1, None) == _native.COUP_E_INVALID
+    # with obs the Python API falls back to one coup_step per slice
+    env.collect_trajectory(4, buf)
+    assert (buf["step_type"] <= 2).all()
