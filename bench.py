@@ -404,7 +404,8 @@ def main():
         sorted_ = "_sorted" if _regrouped(B) else ""
         if players != 2:
             ahead = os.environ.get("COUP_AHEAD", "1") != "0"
-            kernel = ("coup::np::k_step_trajectory<%d>" % players if fused == "traj" else
+            kernel = (("coup::np::k_trajectory_sorted<%d>" if sorted_ else "coup::np::k_step_trajectory<%d>") % players
+                      if fused == "traj" else
                       "coup::np::k_rollout%s<%d>" % (sorted_, players) if fused else
                       "coup::np::k_step_sorted<%d, true, %s>" % (players, "true" if ahead else "false") if sorted_ else
                       "coup::np::k_step<%d, true>" % players)

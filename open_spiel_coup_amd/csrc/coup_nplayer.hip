@@ -111,8 +111,8 @@ __device__ __forceinline__ void store_episode(const StepArgs& a, int64_t i, int2
 // The per-lane outputs of a step: applied action, Rewards() as (loser,
 // count), step type, post-step legal mask and current player.
 template <int N>
-__device__ __forceinline__ void store_step_outputs(const StepArgs& a, int64_t i, int act, uint32_t st, uint32_t rl,
-                                                   uint32_t rc, uint32_t legal, int cp, bool legal_cp = true) {
+__device__ __forceinline__ void store_step_head(const StepArgs& a, int64_t i, int act, uint32_t st, uint32_t rl,
+                                                uint32_t rc) {
   if (a.actions) a.actions[i] = (int8_t)act;
   if (a.rewards) {
     // Rewards(): rc to everybody, -(N-1) rc to the loser; an even-N row
@@ -131,8 +131,18 @@ __device__ __forceinline__ void store_step_outputs(const StepArgs& a, int64_t i,
     }
   }
   if (a.step_type) a.step_type[i] = (uint8_t)st;
-  if (legal_cp && a.legal) a.legal[i] = legal;
-  if (legal_cp && a.cur_player) a.cur_player[i] = (int8_t)cp;
+}
+
+__device__ __forceinline__ void store_legal_player(const StepArgs& a, int64_t i, uint32_t legal, int cp) {
+  if (a.legal) a.legal[i] = legal;
+  if (a.cur_player) a.cur_player[i] = (int8_t)cp;
+}
+
+template <int N>
+__device__ __forceinline__ void store_step_outputs(const StepArgs& a, int64_t i, int act, uint32_t st, uint32_t rl,
+                                                   uint32_t rc, uint32_t legal, int cp) {
+  store_step_head<N>(a, i, act, st, rl, rc);
+  store_legal_player(a, i, legal, cp);
 }
 
 // One rl_environment step per lane (step_lane, coup_nlane.h), lanes in
@@ -195,11 +205,7 @@ __device__ __forceinline__ uint32_t ahead_key(const NLane<N>& L, uint32_t x) {
 #endif
 }
 
-// RS: the threads that deal the block's auto-resets store those lanes'
-// records, legal masks and players themselves, and every other lane is
-// stored right after phase 2 -- one barrier fewer, and no wave of the block
-// waits for the resets (COUP_NP_RESET_STORE=0/1 for A/B runs).
-template <int N, bool UNIFORM, bool AHEAD, int T = kThreads, bool RS = false>
+template <int N, bool UNIFORM, bool AHEAD, int T = kThreads>
 #ifdef COUP_WAVE_TRACE
 // the stamps' registers must not cost the traced kernel its 8 blocks per CU
 #define NP_STEP_SORTED_BOUNDS __launch_bounds__(T, 8)
@@ -210,7 +216,7 @@ __global__ NP_STEP_SORTED_BOUNDS void k_step_sorted(StepArgs a) {
   __shared__ uint4 s_a[T], s_b[T];
   __shared__ uint32_t s_meta[T];   // slot -> owner thread | key << kO | st << kO + 5 | error << kO + 7
   __shared__ uint32_t s_out[T];    // slot -> act + 1 | st << 5 | rl << 7 | rc << 10 | error << 13 |
-                                          //         (ret0 + 16) << 14 | reset pending << 19 | cp << 24
+                                          //         (ret0 + 16) << 14 | cp << 24
   __shared__ uint32_t s_legal[T];  // slot -> post-step legal mask
   __shared__ uint32_t s_reset[T];  // slots whose lane auto-resets
   __shared__ uint32_t s_bin[32];
@@ -287,7 +293,7 @@ __global__ NP_STEP_SORTED_BOUNDS void k_step_sorted(StepArgs a) {
     if (k != kKeyDead) {
       L = unpack<N>(s_a[t], s_b[t]);
       uint32_t out = (m >> (kO + 5)) & 3u, legal = 0u;  // a lane finished in phase 1: no action, its st
-      bool pending = false;
+      bool pending = false, decision_node = false;
       NRng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, base + (m & (T - 1u))), 0u, make_uint4(0, 0, 0, 0)};
       if (k != kStepDone) {
         const uint32_t x = key_action(k);
@@ -301,10 +307,8 @@ __global__ NP_STEP_SORTED_BOUNDS void k_step_sorted(StepArgs a) {
         out = (x + 1u) | ((term ? 2u : 1u) << 5) | (L.rloser << 7) | (L.rcount << 10) | ((uint32_t)err << 13);
         if (a.ep_count && term) out |= (uint32_t)(returns(L, 0u) + 16) << 14;
         pending = term && a.auto_reset != 0;
-        if (pending) {
-          s_reset[atomicAdd(&s_nreset, 1u)] = t;
-          out |= 1u << 19;
-        }
+        decision_node = !term;  // resolve_chance leaves a live lane at a decision node
+        if (pending) s_reset[atomicAdd(&s_nreset, 1u)] = t;
         uint4 wa, wb;
         pack(L, wa, wb);
         s_a[t] = wa;
@@ -313,8 +317,10 @@ __global__ NP_STEP_SORTED_BOUNDS void k_step_sorted(StepArgs a) {
         out = 0u | (((m >> (kO + 5)) & 3u) << 5);
       }
       if (!pending) {
-        legal = legal_mask(L);
-        const int cp = current_player(L);
+        // at a decision node LegalActionsMask is decision_mask and the player
+        // L.M, without legal_mask's / current_player's terminal and chance tests
+        legal = decision_node ? decision_mask(L) : legal_mask(L);
+        const int cp = decision_node ? (int)L.M : current_player(L);
         out |= ((uint32_t)cp & 0xFFu) << 24;
         if (UNIFORM && AHEAD && k != kStepDone && cp >= 0)
           s_b[t].w |= (ahead_key(L, sample_action(legal, rng.draw(L.episode, L.move))) + 1u) << kAheadShift;
@@ -327,41 +333,6 @@ __global__ NP_STEP_SORTED_BOUNDS void k_step_sorted(StepArgs a) {
   __syncthreads();
   NP_TRACE(a, 5);
 
-  if (RS) {
-    // phase 3 first: each thread stores its own lane, except the record,
-    // legal mask and player of a lane that resets (written below)
-    const uint32_t nreset = s_nreset;
-    if (live) {
-      const uint32_t o = s_out[pos];
-      const bool pend = (o >> 19) & 1u;
-      if (!pend) {
-        a.sa[i] = s_a[pos];
-        a.sb[i] = s_b[pos];
-      }
-      store_step_outputs<N>(a, i, (int)(o & 31u) - 1, (o >> 5) & 3u, (o >> 7) & 7u, (o >> 10) & 7u, s_legal[pos],
-                            (int)(int8_t)(o >> 24), !pend);
-      store_episode(a, i, eps, (o >> 5) & 3u, (int32_t)((o >> 14) & 31u) - 16);
-    }
-    // the auto-resets, packed onto the first threads, stored to their lanes
-    for (uint32_t j = t; j < nreset; j += T) {
-      const uint32_t slot = s_reset[j];
-      const int64_t li = base + (s_meta[slot] & (T - 1u));
-      NRng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, li), 0u, make_uint4(0, 0, 0, 0)};
-      const NLane<N> R = new_episode<N>(plane_episode(s_b[slot]) + 1u, rng);
-      uint4 wa, wb;
-      pack(R, wa, wb);
-      const uint32_t legal = legal_mask(R);
-      if (UNIFORM && AHEAD) wb.w |= (ahead_key(R, sample_action(legal, rng.draw(R.episode, R.move))) + 1u) << kAheadShift;
-      a.sa[li] = wa;
-      a.sb[li] = wb;
-      if (a.legal) a.legal[li] = legal;
-      if (a.cur_player) a.cur_player[li] = (int8_t)current_player(R);
-    }
-    NP_TRACE(a, 8);
-    NP_TRACE_WAIT(a, 9);
-    return;
-  }
-
   // the auto-resets, packed onto the first threads
   const uint32_t nreset = s_nreset;
   for (uint32_t j = t; j < nreset; j += T) {
@@ -373,9 +344,9 @@ __global__ NP_STEP_SORTED_BOUNDS void k_step_sorted(StepArgs a) {
     pack(R, wa, wb);
     s_a[slot] = wa;
     s_b[slot] = wb;
-    const uint32_t legal = legal_mask(R);
+    const uint32_t legal = decision_mask(R);  // a new episode is at a decision node
     s_legal[slot] = legal;
-    s_out[slot] = (s_out[slot] & 0x00FFFFFFu) | (((uint32_t)current_player(R) & 0xFFu) << 24);
+    s_out[slot] = (s_out[slot] & 0x00FFFFFFu) | ((R.M & 0xFFu) << 24);
     if (UNIFORM && AHEAD) s_b[slot].w |= (ahead_key(R, sample_action(legal, rng.draw(R.episode, R.move))) + 1u) << kAheadShift;
   }
   NP_TRACE(a, 6);
@@ -589,6 +560,133 @@ __global__ __launch_bounds__(T, 8) void k_rollout_sorted(RolloutArgs a) {
     if (a.episodes) a.episodes[i] += s_eps[t];
     if (a.return_sum) a.return_sum[i] += s_ret[t];
     if (a.length_sum) a.length_sum[i] += s_len[t];
+  }
+  if (errs) atomicAdd(a.err_count, errs);
+}
+
+// coup_step_trajectory with the block's lanes regrouped by decision every
+// step (N players, batches of 2^18 lanes and more): k_rollout_sorted's
+// schedule with coup_step's outputs, stored to slice s of the [steps][B]
+// buffers by lane (each step the block writes all of its lanes' range).
+// Keys: a decision; kKeyFirst -- the lane is terminal as the step starts
+// (no auto-reset, or a terminal record at launch): it restarts, FIRST;
+// kKeyReset -- it finished the step before with auto-reset: coup_step
+// reports that step's legal mask and player after the new deal, so the
+// block's reset group deals the new episode, completes the finished step's
+// outputs, then decides (the resets of a block sort into one wave instead
+// of diverging every wave).  Results equal coup_step's, step for step.
+constexpr uint32_t kKeyFirst = 26u;
+
+template <int N, int T = kThreads>
+__global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t steps) {
+  static_assert((T & (T - 1)) == 0 && T >= 64 && T <= 1024, "power-of-two block of whole waves");
+  constexpr uint32_t kO = T <= 256 ? 8u : 10u;  // lane bits of s_meta
+  __shared__ uint4 s_a[T], s_b[T];
+  __shared__ uint32_t s_meta[T];            // slot -> lane | key << kO
+  __shared__ int32_t s_eps[T], s_ret[T];    // by lane
+  __shared__ __attribute__((aligned(16))) uint32_t s_bin[2][32];
+  const uint32_t t = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * T;
+  const bool ar = a.auto_reset != 0;
+  if (t < 64u) s_bin[t >> 5][t & 31u] = 0u;
+  s_eps[t] = 0;
+  s_ret[t] = 0;
+  NRng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, base + t), 0u, make_uint4(0, 0, 0, 0)};
+  NLane<N> L = initial_lane<N>(0u);
+  uint32_t lane = t, key = kKeyDead, errs = 0u;
+  if (base + t < a.n) {
+    L = unpack<N>(a.sa[base + t], a.sb[base + t]);
+    if (is_terminal(L)) {
+      key = kKeyFirst;
+    } else {
+      resolve_chance(L, rng);  // a lane left at a chance node
+      const uint32_t m = decision_mask(L);
+      key = m ? ahead_key(L, sample_action(m, rng.draw(L.episode, L.move))) : kKeyDead;
+    }
+  }
+  for (int64_t s = 0; s < steps; ++s) {
+    uint32_t* bin = s_bin[s & 1];
+    __syncthreads();  // this step's bins are zero; last step's slots are read
+    const uint32_t rank = atomicAdd(&bin[key], 1u);
+    __syncthreads();
+    const uint32_t pos = bins_below<7>(bin, key) + rank;  // keys up to kKeyFirst = 26
+    if (t < 32u) s_bin[(s + 1) & 1][t] = 0u;  // read for the last time in step s - 1
+    uint4 wa, wb;
+    pack(L, wa, wb);
+    s_a[pos] = wa;
+    s_b[pos] = wb;
+    s_meta[pos] = lane | (key << kO);
+    __syncthreads();
+    const uint32_t m = s_meta[t];
+    lane = m & (T - 1u);
+    key = (m >> kO) & 31u;
+    L = unpack<N>(s_a[t], s_b[t]);
+    const int64_t li = base + lane;
+    if (li >= a.n) continue;  // past the batch
+    const int64_t o = s * a.n + li;
+    rng.env_id = lane_stream_id(a.env_id_base, li);
+    rng.blk_tag = 0u;
+    // a new episode and a non-terminal state after resolve_chance are
+    // decision nodes: LegalActionsMask is decision_mask, the player L.M
+    if (key == kKeyFirst) {  // step() after LAST (rl_environment.py:310-311)
+      L = new_episode<N>(L.episode + 1u, rng);
+      const uint32_t legal = decision_mask(L);
+      store_step_outputs<N>(a, o, -1, 0u, 0u, 0u, legal, (int)L.M);
+      key = ahead_key(L, sample_action(legal, rng.draw(L.episode, L.move)));
+      continue;
+    }
+    if (key == kKeyReset) {  // finished in step s - 1 with auto-reset (vector_env.py:62-65)
+      L = new_episode<N>(L.episode + 1u, rng);
+      const uint32_t legal = decision_mask(L);
+      store_legal_player(a, o - a.n, legal, (int)L.M);
+      key = ahead_key(L, sample_action(legal, rng.draw(L.episode, L.move)));
+    }
+    if (key == kKeyDead) {  // no legal decision: coup_step's rejected step
+      errs += 1u;
+      store_step_outputs<N>(a, o, -1, 1u, 0u, 0u, legal_mask(L), current_player(L));
+      continue;
+    }
+    const uint32_t x = key_action(key);
+    const uint32_t err_before = L.err;
+    apply_decision(L, x);
+    L.move += 1u;
+    resolve_chance(L, rng);
+    errs += (L.err && !err_before) ? 1u : 0u;
+    const bool term = is_terminal(L);
+    store_step_head<N>(a, o, (int)x, term ? 2u : 1u, L.rloser, L.rcount);
+    if (term) {
+      s_eps[lane] += 1;
+      s_ret[lane] += returns(L, 0u);
+      if (ar) {
+        key = kKeyReset;  // legal mask and player once the next episode is dealt
+        continue;
+      }
+      key = kKeyFirst;
+      store_legal_player(a, o, 0u, -4);  // terminal: no legal actions, kTerminalPlayerId
+      continue;
+    }
+    const uint32_t legal = decision_mask(L);
+    store_legal_player(a, o, legal, (int)L.M);
+    if (s + 1 < steps) key = ahead_key(L, sample_action(legal, rng.draw(L.episode, L.move)));
+  }
+  if (key == kKeyReset && base + lane < a.n) {  // finished on the last step
+    L = new_episode<N>(L.episode + 1u, rng);
+    store_legal_player(a, (steps - 1) * a.n + base + lane, decision_mask(L), (int)L.M);
+  }
+  __syncthreads();
+  uint4 wa, wb;
+  pack(L, wa, wb);
+  s_a[lane] = wa;
+  s_b[lane] = wb;
+  __syncthreads();
+  if (base + t < a.n) {
+    const int64_t i = base + t;
+    a.sa[i] = s_a[t];
+    a.sb[i] = s_b[t];
+    if (a.ep_count) {
+      a.ep_count[i] += s_eps[t];
+      a.ep_return[i] += s_ret[t];
+    }
   }
   if (errs) atomicAdd(a.err_count, errs);
 }
@@ -811,11 +909,8 @@ hipError_t launch_step(const Env& e, const int8_t* actions, const coup_step_outp
       auto go = [&](auto lanes) {
         constexpr int TB = decltype(lanes)::value;
         const unsigned g = grid_for(e.n, TB);
-        const char* rs = std::getenv("COUP_NP_RESET_STORE");  // 1: resets stored by their dealers (A/B)
         if (actions)
           k_step_sorted<N, false, false, TB><<<g, TB, 0, e.stream>>>(a);
-        else if (ahead && rs && std::atoi(rs) != 0)
-          k_step_sorted<N, true, true, TB, true><<<g, TB, 0, e.stream>>>(a);
         else if (ahead)
           k_step_sorted<N, true, true, TB><<<g, TB, 0, e.stream>>>(a);
         else
@@ -856,7 +951,15 @@ hipError_t launch_trajectory(const Env& e, int64_t steps, const coup_step_output
   }
   return dispatch(e.players, [&](auto np) {
     constexpr int N = decltype(np)::value;
-    k_step_trajectory<N><<<grid_for(e.n, kThreads), kThreads, 0, e.stream>>>(a, steps);
+    if (regroup_lanes(e.n)) {
+      switch (sort_lanes("COUP_NP_SORT_THREADS", kRolloutSortLanes)) {
+        case 256: k_trajectory_sorted<N, 256><<<grid_for(e.n, 256), 256, 0, e.stream>>>(a, steps); break;
+        case 512: k_trajectory_sorted<N, 512><<<grid_for(e.n, 512), 512, 0, e.stream>>>(a, steps); break;
+        default: k_trajectory_sorted<N, 1024><<<grid_for(e.n, 1024), 1024, 0, e.stream>>>(a, steps); break;
+      }
+    } else {
+      k_step_trajectory<N><<<grid_for(e.n, kThreads), kThreads, 0, e.stream>>>(a, steps);
+    }
   });
 }
 

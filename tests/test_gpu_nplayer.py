@@ -292,31 +292,3 @@ def test_six_player_full_batch_sampled_lanes_match_spec(fused):
         np.testing.assert_array_equal(words[k:k + 256], ref["final_state"], err_msg=f"slice {k}")
     assert env.error_count() == 0
 
-
-@pytest.mark.parametrize("block", ["512", "1024"])
-@pytest.mark.parametrize("n_players", [2, 3, 6])
-def test_regrouped_step_reset_store_equals_in_place(monkeypatch, n_players, block):
-    """The regrouped uniform step whose reset dealers store the reset lanes
-    themselves (COUP_NP_RESET_STORE=1: one barrier fewer) == the in-place
-    step, lane by lane: outputs, records, episode accumulators.  Ragged
-    batch, auto-reset."""
-    monkeypatch.setenv("COUP_NP_SORT_THREADS", block)
-    monkeypatch.setenv("COUP_NP_RESET_STORE", "1")
-    n, steps, seed = 3000, 150, 17 + n_players
-    envs = {}
-    for knob in ("0", "1"):
-        monkeypatch.setenv("COUP_REGROUP", knob)
-        envs[knob] = BatchedCoupEnv(n, seed=seed, env_id_base=9 << 20, auto_reset=True, obs=False,
-                                    num_players=n_players, generic=True, episode_stats=True)
-    for t in range(steps):
-        outs = {}
-        for knob, env in envs.items():
-            monkeypatch.setenv("COUP_REGROUP", knob)
-            outs[knob] = {k: v.clone() for k, v in env.step().items()}
-        for k in ("actions", "rewards", "step_type", "legal_mask", "current_player"):
-            assert torch.equal(outs["0"][k], outs["1"][k]), (t, k)
-        assert torch.equal(envs["0"].export_state(), envs["1"].export_state()), t
-    for a, b in zip(envs["0"].episode_stats(), envs["1"].episode_stats()):
-        assert torch.equal(a, b)
-    assert int(envs["0"].episode_stats()[0].sum()) > 0
-    assert envs["0"].error_count() == envs["1"].error_count() == 0

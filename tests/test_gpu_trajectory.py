@@ -49,13 +49,17 @@ def test_trajectory_equals_steps(monkeypatch, regroup, auto_reset, players, gene
     assert fused.error_count() == ref.error_count() == 0
 
 
-def test_trajectory_graph_and_full_batch():
+@pytest.mark.parametrize("players", [2, 6])
+def test_trajectory_graph_and_full_batch(players):
     """capture_trajectory records the single launch in a HIP graph; at the
-    2^20 benchmark batch the fused trajectory (lanes in place) equals the
-    regrouped per-step kernels on sampled lanes."""
-    n, T = 1 << 20, 16
-    a = BatchedCoupEnv(n, seed=3, auto_reset=True, obs=False, episode_stats=True)
-    b = BatchedCoupEnv(n, seed=3, auto_reset=True, obs=False, episode_stats=True)
+    2^20 benchmark batch the fused trajectory (2 players: lanes in place;
+    6: regrouped by decision every step) equals the regrouped per-step
+    kernels on sampled lanes, after settling into mixed game phases."""
+    n, T = 1 << 20, 24
+    a = BatchedCoupEnv(n, seed=3, auto_reset=True, obs=False, episode_stats=True, num_players=players)
+    b = BatchedCoupEnv(n, seed=3, auto_reset=True, obs=False, episode_stats=True, num_players=players)
+    a.rollout(40)
+    b.rollout(40)
     g, buf = a.capture_trajectory(T)
     g.replay()
     rb = _stepped(b, T, b.trajectory_buffers(T))

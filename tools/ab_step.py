@@ -25,7 +25,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 KNOBS = ("COUP_OBS_MODE", "COUP_XCD_REMAP", "COUP_STEP_DYN_LDS", "COUP_REGROUP", "COUP_AHEAD", "COUP_EP_MODE",
-         "COUP_NP_SORT_THREADS", "COUP_SORT_THREADS", "COUP_NP_RESET_STORE")
+         "COUP_NP_SORT_THREADS", "COUP_SORT_THREADS")
 
 
 def main():
