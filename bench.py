@@ -183,26 +183,42 @@ def cpu_baseline(target_s, with_obs, with_info, players=2):
     return out
 
 
+def _read(path):
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
 def _box_identity(dev):
-    """Which GPU box ran this line (tools/boxinfo.sh fields, best effort)."""
+    """Which GPU box ran this line (tools/boxinfo.sh fields, best effort).
+    Read from sysfs, with no child process: a process that has initialised
+    the GPU must not exec another program (rocm-smi is one)."""
+    import glob
     import socket
-    import subprocess
     import torch
     p = torch.cuda.get_device_properties(dev)
     box = {"host": socket.gethostname(), "gpu": p.name, "arch": getattr(p, "gcnArchName", None),
            "cus": p.multi_processor_count, "uuid": str(getattr(p, "uuid", "")) or None}
-    try:
-        out = subprocess.run(["rocm-smi", "--showserial", "--showmemorypartition", "--showcomputepartition",
-                              "--showclocks"], capture_output=True, text=True, timeout=20).stdout
-        for line in out.splitlines():
-            low = line.lower()
-            for key, tag in (("serial", "serial number"), ("mem_partition", "memory partition"),
-                             ("compute_partition", "compute partition"), ("mclk", "mclk"), ("fclk", "fclk"),
-                             ("sclk", "sclk")):
-                if tag in low and key not in box and ":" in line:
-                    box[key] = line.split(":", 2)[-1].strip()
-    except Exception as e:  # noqa: BLE001  (identity is best effort)
-        box["rocm_smi"] = f"unavailable: {type(e).__name__}"
+    bus = getattr(p, "pci_bus_id", None)
+    dom = getattr(p, "pci_domain_id", 0) or 0
+    devno = getattr(p, "pci_device_id", 0) or 0
+    cands = glob.glob("/sys/bus/pci/devices/%04x:%02x:%02x.*" % (dom, bus, devno)) if bus is not None else []
+    if not cands:
+        return box
+    d = cands[0]
+    box["pci"] = os.path.basename(d)
+    for key, fname in (("serial", "serial_number"), ("compute_partition", "current_compute_partition"),
+                       ("mem_partition", "current_memory_partition")):
+        v = _read(os.path.join(d, fname))
+        if v:
+            box[key] = v
+    for key, fname in (("sclk", "pp_dpm_sclk"), ("mclk", "pp_dpm_mclk"), ("fclk", "pp_dpm_fclk")):
+        v = _read(os.path.join(d, fname))
+        if v:
+            cur = [ln for ln in v.splitlines() if ln.rstrip().endswith("*")]
+            box[key] = (cur[0] if cur else v.splitlines()[0]).rstrip(" *")
     return box
 
 
