@@ -18,7 +18,7 @@ Other configs (secondary lines, not the headline):
   c4r  c4 fused: `steps` 6-player env steps in ONE launch
   c2t, c4t  c2 / c4 as ONE coup_step_trajectory launch of `steps` env steps
        with every step's outputs (actions, rewards, step types, legal masks,
-       players) stored to [K][B] trajectory buffers; lanes in place
+       players) stored to [K][B] trajectory buffers
 
 A "step" is one batched env step over all B lanes; value = env-steps/s of
 the whole job (N x B x K / max-over-ranks wall time).  Before the W warmup

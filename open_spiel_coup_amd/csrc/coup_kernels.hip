@@ -1888,6 +1888,8 @@ int coup_step_trajectory(coup_env* env, int64_t steps, const coup_step_outputs* 
   COUP_CHECK_ENV(env);
   if (steps < 0) return fail(COUP_E_INVALID, "coup_step_trajectory: negative steps");
   if (env->hist) return fail(COUP_E_INVALID, "coup_step_trajectory: not available on an env with COUP_FLAG_HISTORY");
+  // (a 2-player form writing obs every step measured slower than per-step
+  // launches: 196 vs 162 us per 2^20-lane step)
   if (out && (out->obs || out->info_state))
     return fail(COUP_E_INVALID, "coup_step_trajectory: obs / info_state are written by coup_step only");
   if (out && (out->episodes == nullptr) != (out->return_sum == nullptr))

@@ -77,7 +77,9 @@ def test_trajectory_rejects_what_it_cannot_write():
                                 ("actions", "rewards", "step_type", "legal_mask", "current_player", "obs",
                                  "info_state")], None, None)
     assert env.lib.coup_step_trajectory(env._h, 4, ctypes.byref(out)) == _native.COUP_E_INVALID
-    hist = BatchedCoupEnv(64, seed=1, obs=False, history=True)
+    hist = BatchedCoupEnv(64, seed=1, obs=False, info_state=True)
+    hb = hist.trajectory_buffers(4)
+    assert "info_state" in hb and not hist._fused_trajectory(hb)
     assert hist.lib.coup_step_trajectory(hist._h, 4, None) == _native.COUP_E_INVALID
     assert env.lib.coup_step_trajectory(env._h, -1, None) == _native.COUP_E_INVALID
     # with obs the Python API falls back to one coup_step per slice
