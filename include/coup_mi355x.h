@@ -197,7 +197,8 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
  * be NULL, and the env must not keep histories (COUP_E_INVALID).  Results
  * equal `steps` coup_step calls -- the trajectory a learner collects
  * (rl_environment.py:282-322 per step), without the per-step launch and
- * record round trip.  Lanes stay in place (no regrouping by decision). */
+ * record round trip.  From 2^18 lanes the lanes are regrouped by decision
+ * every step, with the same results. */
 int coup_step_trajectory(coup_env* env, int64_t steps, const coup_step_outputs* out);
 
 /* `steps` uniform-random env steps per lane in one launch, state kept in

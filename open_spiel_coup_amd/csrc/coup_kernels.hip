@@ -1210,6 +1210,137 @@ __global__ __launch_bounds__(T, 8) void k_rollout_sorted(RolloutArgs a) {
   if (errs) atomicAdd(a.err_count, errs);
 }
 
+// coup_step_trajectory for 2 players with the block's lanes regrouped by
+// decision every step (batches of 2^18 lanes and more): k_rollout_sorted's
+// schedule with coup_step's outputs, the 2-player form of
+// np::k_trajectory_sorted (coup_nplayer.hip has the key protocol: a lane
+// that finished with auto-reset keeps kKeyReset, and the next step's reset
+// group deals its new episode and completes the finished step's legal mask
+// and player; kKeyFirst restarts a lane that is terminal as a step starts).
+// Results equal coup_step's, step for step.
+template <int T>
+__global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t steps) {
+  static_assert((T & (T - 1)) == 0 && T >= 64 && T <= 1024, "power-of-two block of whole waves");
+  constexpr uint32_t kO = T <= 256 ? 8u : 10u;  // lane bits of s_meta
+  __shared__ uint4 s_rec[T];
+  __shared__ uint32_t s_meta[T];          // slot -> lane | key << kO
+  __shared__ int32_t s_eps[T], s_ret[T];  // by lane
+  __shared__ __attribute__((aligned(16))) uint32_t s_bin[2][32];
+  const uint32_t t = threadIdx.x;
+  const int64_t base = (int64_t)blockIdx.x * T;
+  const bool ar = a.auto_reset != 0;
+  if (t < 64u) s_bin[t >> 5][t & 31u] = 0u;
+  s_eps[t] = 0;
+  s_ret[t] = 0;
+  Rng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, base + t), 0u, make_uint4(0, 0, 0, 0)};
+  NoHistory none;
+  Lane L = initial_lane(0u);
+  uint32_t lane = t, key = kKeyDead, errs = 0u;
+  if (base + t < a.n) {
+    L = unpack(a.state[base + t]);
+    if (is_terminal(L)) {
+      key = kKeyFirst;
+    } else {
+      resolve_chance(L, rng);  // a lane left at a chance node
+      const uint32_t m = decision_mask(L);
+      key = m ? regroup_key(L, sample_action(m, rng.draw(L.episode, L.move))) : kKeyDead;
+    }
+  }
+  for (int64_t s = 0; s < steps; ++s) {
+    uint32_t* bin = s_bin[s & 1];
+    __syncthreads();  // this step's bins are zero; last step's slots are read
+    const uint32_t rank = atomicAdd(&bin[key], 1u);
+    __syncthreads();
+    const uint32_t pos = bins_below<7>(bin, key) + rank;  // keys up to kKeyFirst = 26
+    if (t < 32u) s_bin[(s + 1) & 1][t] = 0u;  // read for the last time in step s - 1
+    s_rec[pos] = pack(L);
+    s_meta[pos] = lane | (key << kO);
+    __syncthreads();
+    const uint32_t m = s_meta[t];
+    lane = m & (T - 1u);
+    key = (m >> kO) & 31u;
+    L = unpack(s_rec[t]);
+    const int64_t li = base + lane;
+    if (li >= a.n) continue;  // past the batch
+    const int64_t o = s * a.n + li;
+    rng.env_id = lane_stream_id(a.env_id_base, li);
+    rng.blk_tag = 0u;
+    // a new episode and a live lane after resolve_chance are at decision
+    // nodes: LegalActionsMask is decision_mask, the player L.M
+    if (key == kKeyFirst) {  // step() after LAST (rl_environment.py:310-311)
+      L = new_episode(L.episode + 1u, rng, none);
+      const uint32_t legal = decision_mask(L);
+      if (a.actions) a.actions[o] = -1;
+      if (a.rewards) reinterpret_cast<uint16_t*>(a.rewards)[o] = 0u;
+      if (a.step_type) a.step_type[o] = (uint8_t)COUP_STEP_FIRST;
+      if (a.legal) a.legal[o] = legal;
+      if (a.cur_player) a.cur_player[o] = (int8_t)L.M;
+      key = regroup_key(L, sample_action(legal, rng.draw(L.episode, L.move)));
+      continue;
+    }
+    if (key == kKeyReset) {  // finished in step s - 1 with auto-reset (vector_env.py:62-65)
+      L = new_episode(L.episode + 1u, rng, none);
+      const uint32_t legal = decision_mask(L);
+      if (a.legal) a.legal[o - a.n] = legal;
+      if (a.cur_player) a.cur_player[o - a.n] = (int8_t)L.M;
+      key = regroup_key(L, sample_action(legal, rng.draw(L.episode, L.move)));
+    }
+    if (key == kKeyDead) {  // no legal decision: coup_step's rejected step
+      errs += 1u;
+      if (a.actions) a.actions[o] = -1;
+      if (a.rewards) reinterpret_cast<uint16_t*>(a.rewards)[o] = 0u;
+      if (a.step_type) a.step_type[o] = (uint8_t)COUP_STEP_MID;
+      if (a.legal) a.legal[o] = legal_mask(L);
+      if (a.cur_player) a.cur_player[o] = (int8_t)current_player(L);
+      continue;
+    }
+    const uint32_t x = key_action(key);
+    const uint32_t err_before = L.err;
+    apply_decision_v1(L, x);  // regrouped: the branch form, as k_rollout_sorted
+    L.move += 1u;
+    resolve_chance(L, rng);
+    errs += (L.err && !err_before) ? 1u : 0u;
+    const bool term = is_terminal(L);
+    if (a.actions) a.actions[o] = (int8_t)x;
+    if (a.rewards) reinterpret_cast<uint16_t*>(a.rewards)[o] = (uint16_t)((uint8_t)L.r0 | ((uint8_t)(-L.r0) << 8));
+    if (a.step_type) a.step_type[o] = (uint8_t)(term ? COUP_STEP_LAST : COUP_STEP_MID);
+    if (term) {
+      s_eps[lane] += 1;
+      s_ret[lane] += return0(L);
+      if (ar) {
+        key = kKeyReset;  // legal mask and player once the next episode is dealt
+        continue;
+      }
+      key = kKeyFirst;
+      if (a.legal) a.legal[o] = 0u;  // terminal: no legal actions, kTerminalPlayerId
+      if (a.cur_player) a.cur_player[o] = (int8_t)-4;
+      continue;
+    }
+    const uint32_t legal = decision_mask(L);
+    if (a.legal) a.legal[o] = legal;
+    if (a.cur_player) a.cur_player[o] = (int8_t)L.M;
+    if (s + 1 < steps) key = regroup_key(L, sample_action(legal, rng.draw(L.episode, L.move)));
+  }
+  if (key == kKeyReset && base + lane < a.n) {  // finished on the last step
+    L = new_episode(L.episode + 1u, rng, none);
+    const int64_t o = (steps - 1) * a.n + base + lane;
+    if (a.legal) a.legal[o] = decision_mask(L);
+    if (a.cur_player) a.cur_player[o] = (int8_t)L.M;
+  }
+  __syncthreads();
+  s_rec[lane] = pack(L);
+  __syncthreads();
+  if (base + t < a.n) {
+    const int64_t i = base + t;
+    a.state[i] = s_rec[t];
+    if (a.ep_count) {
+      a.ep_count[i] += s_eps[t];
+      a.ep_return[i] += s_ret[t];
+    }
+  }
+  if (errs) atomicAdd(a.err_count, errs);
+}
+
 // NewInitialState / reset of selected lanes.  mode 0: fresh env (episode 0);
 // mode 1: next episode.  deal: resolve the four initial deals.
 __global__ __launch_bounds__(kThreads) void k_reset(uint4* state, int64_t n, const uint8_t* mask, int mode, int deal,
@@ -1914,7 +2045,18 @@ int coup_step_trajectory(coup_env* env, int64_t steps, const coup_step_outputs* 
     a.ep_count = out->episodes;
     a.ep_return = out->return_sum;
   }
-  coup::k_step_trajectory<<<grid_for(env->batch), coup::kThreads, 0, env->stream>>>(a, steps);
+  const int64_t n = env->batch;
+  if (coup::regroup_lanes(n)) {
+    switch (coup::sort_lanes("COUP_SORT_THREADS", coup::kRolloutSortLanes)) {
+      case 256: coup::k_trajectory_sorted<256><<<grid_for(n), 256, 0, env->stream>>>(a, steps); break;
+      case 512: coup::k_trajectory_sorted<512><<<(unsigned)((n + 511) / 512), 512, 0, env->stream>>>(a, steps); break;
+      default:
+        coup::k_trajectory_sorted<1024><<<(unsigned)((n + 1023) / 1024), 1024, 0, env->stream>>>(a, steps);
+        break;
+    }
+  } else {
+    coup::k_step_trajectory<<<grid_for(n), coup::kThreads, 0, env->stream>>>(a, steps);
+  }
   COUP_HIP_TRY(hipGetLastError());
   return COUP_OK;
 }

@@ -575,7 +575,6 @@ __global__ __launch_bounds__(T, 8) void k_rollout_sorted(RolloutArgs a) {
 // block's reset group deals the new episode, completes the finished step's
 // outputs, then decides (the resets of a block sort into one wave instead
 // of diverging every wave).  Results equal coup_step's, step for step.
-constexpr uint32_t kKeyFirst = 26u;
 
 template <int N, int T = kThreads>
 __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t steps) {

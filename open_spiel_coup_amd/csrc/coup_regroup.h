@@ -29,6 +29,11 @@ constexpr uint32_t kKeyPassBlock = 20u;      // Pass after a Block: next turn
 constexpr uint32_t kKeyPassComplete = 21u;   // + 0..3: Pass completing Foreign Aid / Tax / Exchange / Steal
 constexpr uint32_t kKeyChallengeLost = 25u;  // Challenge of a player who holds the claimed card
 
+// Trajectory kernels only (k_trajectory_sorted): the lane is terminal as the
+// step starts (no auto-reset, or a terminal record at launch): it restarts
+// and reports FIRST, with no decision.  Never passed to is_decision_key.
+constexpr uint32_t kKeyFirst = 26u;
+
 // a key that carries a decision to apply (not kKeyReset / kKeyDead)
 __host__ __device__ __forceinline__ bool is_decision_key(uint32_t k) { return k < kKeyReset || k >= kKeyPassBlock; }
 
