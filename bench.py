@@ -426,7 +426,7 @@ def main():
                       "coup::np::k_step_sorted<%d, true, %s>" % (players, "true" if ahead else "false") if sorted_ else
                       "coup::np::k_step<%d, true>" % players)
         elif fused == "traj":
-            kernel = "coup::k_step_trajectory"
+            kernel = "coup::k_trajectory_sorted" if sorted_ else "coup::k_step_trajectory"
         elif fused:
             kernel = "coup::k_rollout" + sorted_
         elif with_info:

@@ -67,7 +67,8 @@ def main():
             if players != 2:
                 return bool(re.search(r"np::k_(step_trajectory|trajectory_sorted)<%d(, \d+)?>|"
                                       r"2np(17k_step_trajectory|19k_trajectory_sorted)ILi%dE" % (players, players), kn))
-            return "k_step_trajectory" in kn and "np::" not in kn and "2np" not in kn
+            return (("k_step_trajectory" in kn or "k_trajectory_sorted" in kn or "19k_trajectory_sorted" in kn)
+                    and "np::" not in kn and "2np" not in kn)
         if players != 2:
             if fused:
                 return bool(re.search(r"np::k_rollout(_sorted)?<%d(, \d+)?>|2np(9k_rollout|16k_rollout_sorted)ILi%dE"
