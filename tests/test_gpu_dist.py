@@ -125,3 +125,22 @@ def test_bench_two_ranks_gloo(config):
     assert single["config"]["hip_graph"] and rec["config"]["hip_graph"]
     assert single["episodes"]["finished"] == rec["episodes"]["finished"]
     assert single["episodes"]["mean_return_p0"] == rec["episodes"]["mean_return_p0"]
+
+
+@pytest.mark.parametrize("config", ["c2t", "c4t"])
+def test_bench_two_ranks_gloo_trajectory(config):
+    """The fused-trajectory configs through bench.py's multi-rank path: one
+    coup_step_trajectory launch per rank, every step's outputs stored, the
+    per-episode accumulators all-gathered."""
+    batch = 1 << 14
+    outs = _run_ranks(lambda r: [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config",
+                                 config, "--steps", "16", "--warmup", "2", "--settle", "64", "--batch", str(batch),
+                                 "--dist-backend", "gloo"], 2, timeout=110)
+    lines = [ln for ln in outs[0].splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, outs[0][-2000:]
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["global_batch"] == 2 * batch
+    assert rec["config"]["fused_steps_per_launch"] == 16 and "trajectory" in rec["config"]["outputs"]
+    assert rec["lane_errors"] == 0
+    assert rec["episodes"]["finished"] > 0 and rec["episodes"]["collective"].startswith("all_gather")
+    assert "trajectory" in rec["roofline"]["kernel"]
