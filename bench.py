@@ -343,18 +343,26 @@ def main():
         return env.episode_stats()
 
     # The collective's payload: per lane, the finished-episode count and the
-    # player-0 return sum.  While they fit 16 bits each (K <= 1000 steps: at
-    # most K episodes and |return| <= 2(N-1) per episode) they travel packed in
-    # one int32 (return << 16 | episodes), 4 B per lane instead of 8.
-    packed = args.steps <= 1000
+    # player-0 return sum (at most K episodes, |return| <= 2(N-1) per episode).
+    # While they fit 8 bits each (2(N-1) K <= 127: K <= 63 steps for 2 players,
+    # the driver's K = 20 among them) they travel as one int16 per lane
+    # (return << 8 | episodes), pairs of lanes viewed as int32 for the
+    # collective (RCCL has no int16); while they fit 16 bits (K <= 1000) as one
+    # int32 (return << 16 | episodes); else as [B, 2] int32.
+    width = 2 if 2 * (players - 1) * args.steps <= 127 and B % 2 == 0 else (4 if args.steps <= 1000 else 8)
 
     def episode_payload():
         eps, ret = episode_tensors()
-        return (ret << 16) | eps if packed else torch.stack((eps, ret), 1)
+        if width == 2:
+            return ((ret.to(torch.int16) << 8) | eps.to(torch.int16)).view(torch.int32)
+        return (ret << 16) | eps if width == 4 else torch.stack((eps, ret), 1)
 
     def unpack_payload(g):
-        if packed:
-            return g & 0xFFFF, g >> 16  # arithmetic shift: signed return sums
+        if width == 2:
+            h = g.view(torch.int16)
+            return (h & 0xFF).to(torch.int32), (h >> 8).to(torch.int32)  # arithmetic shift: signed sums
+        if width == 4:
+            return g & 0xFFFF, g >> 16
         return g[:, 0], g[:, 1]
 
     # one collation outside the timed region: RCCL sets up its all-gather
@@ -466,8 +474,11 @@ def main():
                          "store_ceiling_ms": ceiling_ms,
                          "frac_of_store_ceiling": (ceiling_ms / launch_ms) if ceiling_ms else None},
             "episodes": {"finished": ep_total, "mean_return_p0": ret_total / max(ep_total, 1),
-                         "collective": ("all_gather [world*B] int32 (return sum << 16 | episodes per lane)" if packed
-                                        else "all_gather [world*B, 2] int32 (episodes, return sum per lane)")
+                         "collective": ("all_gather [world*B] int16 (return sum << 8 | episodes per lane)"
+                                        if width == 2 else
+                                        "all_gather [world*B] int32 (return sum << 16 | episodes per lane)"
+                                        if width == 4 else
+                                        "all_gather [world*B, 2] int32 (episodes, return sum per lane)")
                          if world > 1 else None},
             "lane_errors": errors,
             "box": _box_identity(dev),

@@ -114,6 +114,7 @@ def test_bench_two_ranks_gloo(config):
     assert rec["n_gpus"] == 2 and rec["config"]["global_batch"] == 2 * batch
     assert rec["lane_errors"] == 0
     assert rec["episodes"]["finished"] > 0 and rec["episodes"]["collective"].startswith("all_gather")
+    assert "int16" in rec["episodes"]["collective"]  # K = 8: 2 bytes per lane
     assert -2.0 <= rec["episodes"]["mean_return_p0"] <= 2.0
     # the same 2B env ids in one process (a graph config: no timing-calibrated
     # gate steps, so the runs play identical games): the gathered totals match
