@@ -76,6 +76,42 @@ CONFIGS = {
 }
 
 
+def payload_width(players, steps, batch):
+    """Bytes per lane of the collective's payload: per lane, the finished-
+    episode count and the player-0 return sum of `steps` steps (at most
+    `steps` episodes, |return| <= 2(N-1) per episode).  While both fit 8 bits
+    (2(N-1) K <= 127: K <= 63 steps for 2 players, the driver's K = 20 among
+    them) one int16 per lane; while they fit 16 bits (K <= 1000) one int32;
+    else two int32."""
+    if 2 * (players - 1) * steps <= 127 and batch % 2 == 0:
+        return 2
+    return 4 if steps <= 1000 else 8
+
+
+def pack_episodes(eps, ret, width):
+    """[B] int32 episode counts and return sums -> the collective's payload:
+    int16 (return << 8 | episodes) with lane pairs viewed as int32 (RCCL has
+    no int16 type), int32 (return << 16 | episodes), or [B, 2] int32."""
+    import torch
+    if width == 2:
+        return ((ret.to(torch.int16) << 8) | eps.to(torch.int16)).view(torch.int32)
+    if width == 4:
+        return (ret << 16) | eps
+    return torch.stack((eps, ret), 1)
+
+
+def unpack_episodes(g, width):
+    """Inverse of pack_episodes over the gathered payload: (episodes, return
+    sums) as int32 [world * B]."""
+    import torch
+    if width == 2:
+        h = g.view(torch.int16)
+        return (h & 0xFF).to(torch.int32), (h >> 8).to(torch.int32)  # arithmetic shift: signed sums
+    if width == 4:
+        return g & 0xFFFF, g >> 16
+    return g[:, 0], g[:, 1]
+
+
 def _regrouped(batch):
     """Does the library regroup lanes by decision for a launch of `batch`
     lanes (the *_sorted step / rollout kernels)?  Mirrors
@@ -342,28 +378,13 @@ def main():
             return stats["episodes"], stats["return_sum"]
         return env.episode_stats()
 
-    # The collective's payload: per lane, the finished-episode count and the
-    # player-0 return sum (at most K episodes, |return| <= 2(N-1) per episode).
-    # While they fit 8 bits each (2(N-1) K <= 127: K <= 63 steps for 2 players,
-    # the driver's K = 20 among them) they travel as one int16 per lane
-    # (return << 8 | episodes), pairs of lanes viewed as int32 for the
-    # collective (RCCL has no int16); while they fit 16 bits (K <= 1000) as one
-    # int32 (return << 16 | episodes); else as [B, 2] int32.
-    width = 2 if 2 * (players - 1) * args.steps <= 127 and B % 2 == 0 else (4 if args.steps <= 1000 else 8)
+    width = payload_width(players, args.steps, B)
 
     def episode_payload():
-        eps, ret = episode_tensors()
-        if width == 2:
-            return ((ret.to(torch.int16) << 8) | eps.to(torch.int16)).view(torch.int32)
-        return (ret << 16) | eps if width == 4 else torch.stack((eps, ret), 1)
+        return pack_episodes(*episode_tensors(), width)
 
     def unpack_payload(g):
-        if width == 2:
-            h = g.view(torch.int16)
-            return (h & 0xFF).to(torch.int32), (h >> 8).to(torch.int32)  # arithmetic shift: signed sums
-        if width == 4:
-            return g & 0xFFFF, g >> 16
-        return g[:, 0], g[:, 1]
+        return unpack_episodes(g, width)
 
     # one collation outside the timed region: RCCL sets up its all-gather
     # channels lazily, and HIP loads torch's stack kernel on first use
