@@ -90,6 +90,11 @@ class BatchedEnv {
   void Step(const int8_t* actions, const coup_step_outputs& out) {
     Check(coup_step(env_, actions, &out), "coup_step");
   }
+  // `steps` uniform steps in one launch, step t's outputs in slice t of
+  // out's [steps][B] buffers (coup_step_trajectory; no obs / info_state)
+  void StepTrajectory(int64_t steps, const coup_step_outputs& out) {
+    Check(coup_step_trajectory(env_, steps, &out), "coup_step_trajectory");
+  }
   void Rollout(int64_t steps, const coup_rollout_stats* stats = nullptr) {
     Check(coup_rollout(env_, steps, stats), "coup_rollout");
   }
