@@ -137,8 +137,9 @@ class BatchedCoupEnv:
 
     def step(self, actions=None):
         """One batched env step.  actions: int8/long tensor [B] of decision
-        actions, or None for the in-kernel uniform random policy.  Returns a
-        dict of tensors (views of the env's output buffers)."""
+        actions, or None for the in-kernel uniform random policy; a negative
+        action skips its lane (left untouched, step type SKIPPED, no error).
+        Returns a dict of tensors (views of the env's output buffers)."""
         self._bind_stream()
         a = None
         if actions is not None:
