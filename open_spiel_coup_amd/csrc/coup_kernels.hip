@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1527,6 +1528,8 @@ struct SlotArgs {
   int store;               // write the lane back (copy, init or action)
   coup_slot_result* out;   // null: no result
   float* obs;              // [2][98] or null
+  uint32_t* done = nullptr;  // k_slot: completion flag in mapped host memory (null: none)
+  uint32_t seq = 0;          // the value k_slot stores there once its results are visible
 };
 
 // -DCOUP_SLOT_INLINE (investigation builds only): the
@@ -1628,6 +1631,13 @@ __global__ __launch_bounds__(64) void k_slot(SlotArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t hist[kHist];
   __shared__ __attribute__((aligned(16))) uint32_t bits[OBS ? 64 * 8 : 1];
   slot_op<OBS>(a, hist, bits);
+  if (a.done) {
+    // the host polls this flag instead of synchronising the stream: every
+    // thread's result / tensor stores reach system scope first
+    __threadfence_system();
+    wave_sync();
+    if (threadIdx.x == 0u) __hip_atomic_store(a.done, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // coup_slot_ops: n independent State ops in one launch, block b = request b
@@ -1642,6 +1652,8 @@ struct SlotBatchArgs {
   const coup_slot_req* reqs;  // [n]
   coup_slot_result* out;      // [n] or null
   float* obs;                 // [n][2][98] or null
+  uint32_t* done = nullptr;   // [n] completion flags in mapped host memory (null: none)
+  uint32_t seq = 0;           // the value block b stores in done[b] once its results are visible
 };
 
 template <bool OBS>
@@ -1660,10 +1672,21 @@ __global__ __launch_bounds__(64) void k_slot_batch(SlotBatchArgs b) {
   a.out = b.out ? b.out + blockIdx.x : nullptr;
   a.obs = OBS ? b.obs + (size_t)blockIdx.x * (2 * kObsSize) : nullptr;
   slot_op<OBS>(a, hist, bits);
+  if (b.done) {  // as k_slot: the host polls the flags instead of synchronising
+    __threadfence_system();
+    wave_sync();
+    if (threadIdx.x == 0u) __hip_atomic_store(b.done + blockIdx.x, b.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 }  // namespace coup
 
 // ====================================================================== C ABI
+
+// coup_slot_op's mapped scratch: result, obs, info state, then (64-byte
+// aligned) the completion flag k_slot raises
+constexpr size_t kSlotFlagOffset =
+    (sizeof(coup_slot_result) + 2u * COUP_OBS_SIZE * sizeof(float) + 2u * COUP_INFO_STATE_SIZE * sizeof(float) + 63u) &
+    ~size_t(63);
 
 struct coup_env {
   int64_t batch;
@@ -1678,9 +1701,11 @@ struct coup_env {
   hipStream_t stream;
   uint8_t* slot_scratch;  // coup_slot_op results: pinned host memory the kernels write directly (lazy)
   uint8_t* slot_scratch_dev;  // its device address
+  uint32_t slot_seq;          // last completion value k_slot stored in the scratch's flag word
   uint8_t* batch_scratch;     // coup_slot_ops: requests + results (mapped pinned, grown on demand)
   uint8_t* batch_scratch_dev;
   size_t batch_cap;
+  uint32_t batch_seq;         // last completion value k_slot_batch stored in the batch flags
   bool batch_pending;         // an asynchronous coup_slot_ops may still read the requests
 };
 
@@ -1693,6 +1718,11 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
+#define COUP_TRY(expr)   \
+  do {                   \
+    const int _r = (expr); \
+    if (_r != COUP_OK) return _r; \
+  } while (0)
 #define COUP_HIP_TRY(expr)                                                                    \
   do {                                                                                        \
     hipError_t _e = (expr);                                                                   \
@@ -1808,10 +1838,12 @@ int coup_create_ex(int64_t batch, uint64_t seed, uint32_t env_id_base, int flags
   env->err_count = nullptr;
   env->slot_scratch = nullptr;
   env->slot_scratch_dev = nullptr;
+  env->slot_seq = 0;
   env->batch_scratch = nullptr;
   env->batch_scratch_dev = nullptr;
   env->batch_cap = 0;
   env->batch_pending = false;
+  env->batch_seq = 0;
   const size_t lanes = (size_t)(batch > 0 ? batch : 1);
   hipError_t e = hipMalloc(&env->state, lanes * sizeof(uint4) * (generic ? 2 : 1));
   if (e == hipSuccess) e = hipMalloc(&env->err_count, sizeof(uint32_t));
@@ -2110,6 +2142,36 @@ int coup_query(coup_env* env, const coup_query_outputs* out) {
   return COUP_OK;
 }
 
+// Wait on the host until the n completion flags in mapped host memory hold
+// `seq` (k_slot / k_slot_batch raise them after their results), instead of
+// synchronising the stream.  A kernel that never gets there (a HIP error) is
+// caught by a stream synchronisation after a bounded wait.
+// COUP_SLOT_SYNC=1: synchronise the stream instead (A/B of the two waits).
+static bool slot_poll() {
+  static const bool poll = [] {
+    const char* e = std::getenv("COUP_SLOT_SYNC");
+    return !(e && std::atoi(e) != 0);
+  }();
+  return poll;
+}
+
+static int wait_flags(const uint32_t* flags, int64_t n, uint32_t seq, hipStream_t s, const char* what) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int64_t i = 0; i < n; ++i) {
+    for (uint32_t k = 1; __atomic_load_n(flags + i, __ATOMIC_ACQUIRE) != seq; ++k) {
+      if ((k & 4095u) == 0u && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+        COUP_HIP_TRY(hipStreamSynchronize(s));
+        for (int64_t j = i; j < n; ++j)
+          if (__atomic_load_n(flags + j, __ATOMIC_ACQUIRE) != seq)
+            return fail(COUP_E_HIP, std::string(what) + ": a request raised no completion flag");
+        return COUP_OK;
+      }
+      __builtin_ia32_pause();
+    }
+  }
+  return COUP_OK;
+}
+
 int coup_slot_op(coup_env* env, int64_t lane, const coup_env* src_env, int64_t src_lane, int action, int flags,
                  void* host_out) {
   COUP_CHECK_ENV(env);
@@ -2131,10 +2193,10 @@ int coup_slot_op(coup_env* env, int64_t lane, const coup_env* src_env, int64_t s
   if (result && !env->slot_scratch) {
     // the kernels store the result straight into pinned host memory over
     // PCIe: no copy kernel before the synchronisation
-    COUP_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&env->slot_scratch),
-                               sizeof(coup_slot_result) + obs_bytes + info_bytes,
+    COUP_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&env->slot_scratch), kSlotFlagOffset + 64,
                                hipHostMallocMapped | hipHostMallocCoherent));
     COUP_HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&env->slot_scratch_dev), env->slot_scratch, 0));
+    std::memset(env->slot_scratch + kSlotFlagOffset, 0, 64);  // no completion raised yet
   }
   coup::SlotArgs a;
   a.dst_state = env->state + lane;
@@ -2147,6 +2209,16 @@ int coup_slot_op(coup_env* env, int64_t lane, const coup_env* src_env, int64_t s
   uint8_t* sc = env->slot_scratch_dev;
   a.out = result ? reinterpret_cast<coup_slot_result*>(sc) : nullptr;
   a.obs = obs ? reinterpret_cast<float*>(sc + sizeof(coup_slot_result)) : nullptr;
+  // an answered op without the InformationStateTensor (one kernel) raises a
+  // completion flag the host polls; with it, k_info_elems follows and the
+  // stream is synchronised
+  const bool poll = result && !info && slot_poll();
+  a.done = poll ? reinterpret_cast<uint32_t*>(sc + kSlotFlagOffset) : nullptr;
+  a.seq = 0u;
+  if (poll) {
+    a.seq = env->slot_seq + 1u == 0u ? 1u : env->slot_seq + 1u;  // 0 is the flag's initial value
+    env->slot_seq = a.seq;
+  }
   hipStream_t s = env->stream;
   // the InformationStateTensor is written by k_info_elems after the op
   // (1246 threads instead of one wave)
@@ -2163,7 +2235,12 @@ int coup_slot_op(coup_env* env, int64_t lane, const coup_env* src_env, int64_t s
   }
   if (!result) return COUP_OK;
   const size_t n = sizeof(coup_slot_result) + (obs ? obs_bytes : 0) + (info ? info_bytes : 0);
-  COUP_HIP_TRY(hipStreamSynchronize(s));
+  if (poll) {
+    COUP_TRY(wait_flags(reinterpret_cast<const uint32_t*>(env->slot_scratch + kSlotFlagOffset), 1, a.seq, s,
+                        "coup_slot_op"));
+  } else {
+    COUP_HIP_TRY(hipStreamSynchronize(s));
+  }
   std::memcpy(host_out, env->slot_scratch, n);
   return COUP_OK;
 }
@@ -2208,19 +2285,25 @@ int coup_slot_ops(coup_env* env, int64_t n, const coup_slot_req* reqs, const cou
   const size_t req_bytes = ((size_t)n * sizeof(coup_slot_req) + 127u) & ~(size_t)127u;
   const size_t out_bytes = result ? (size_t)n * (sizeof(coup_slot_result) + (obs ? obs_bytes : 0) +
                                                   (info ? info_bytes : 0)) : 0;
+  // answered batches without the InformationStateTensor raise one completion
+  // flag per request (after the results, 128-byte aligned) that the host polls
+  const bool poll = result && !info && slot_poll();
+  const size_t flag_off = (req_bytes + out_bytes + 127u) & ~(size_t)127u;
+  const size_t flag_bytes = poll ? (size_t)n * sizeof(uint32_t) : 0;
   if (env->batch_pending) {
     // the last (asynchronous) batch may still be reading its requests
     COUP_HIP_TRY(hipStreamSynchronize(env->stream));
     env->batch_pending = false;
   }
-  if (req_bytes + out_bytes > env->batch_cap) {
+  if (flag_off + flag_bytes > env->batch_cap) {
     if (env->batch_scratch) (void)hipHostFree(env->batch_scratch);
     env->batch_scratch = nullptr;
     env->batch_cap = 0;
-    const size_t cap = std::max<size_t>(req_bytes + out_bytes, 64u << 10);
+    const size_t cap = std::max<size_t>(flag_off + flag_bytes, 64u << 10);
     COUP_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&env->batch_scratch), cap,
                                hipHostMallocMapped | hipHostMallocCoherent));
     COUP_HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&env->batch_scratch_dev), env->batch_scratch, 0));
+    std::memset(env->batch_scratch, 0, cap);  // no completion flag raised yet
     env->batch_cap = cap;
   }
   std::memcpy(env->batch_scratch, reqs, (size_t)n * sizeof(coup_slot_req));
@@ -2237,6 +2320,11 @@ int coup_slot_ops(coup_env* env, int64_t n, const coup_slot_req* reqs, const cou
                                                                                     (obs ? obs_bytes : 0)))
                          : nullptr;
   b.obs = obs_out;
+  if (poll) {
+    b.done = reinterpret_cast<uint32_t*>(dev + flag_off);
+    b.seq = env->batch_seq + 1u == 0u ? 1u : env->batch_seq + 1u;  // 0: a fresh buffer's value
+    env->batch_seq = b.seq;
+  }
   hipStream_t s = env->stream;
   if (obs)
     coup::k_slot_batch<true><<<(unsigned)n, 64, 0, s>>>(b);
@@ -2253,7 +2341,12 @@ int coup_slot_ops(coup_env* env, int64_t n, const coup_slot_req* reqs, const cou
     env->batch_pending = true;
     return COUP_OK;
   }
-  COUP_HIP_TRY(hipStreamSynchronize(s));
+  if (poll) {
+    COUP_TRY(wait_flags(reinterpret_cast<const uint32_t*>(env->batch_scratch + flag_off), n, b.seq, s,
+                        "coup_slot_ops"));
+  } else {
+    COUP_HIP_TRY(hipStreamSynchronize(s));
+  }
   std::memcpy(host_out, env->batch_scratch + req_bytes, out_bytes);
   return COUP_OK;
 }

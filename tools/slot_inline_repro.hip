@@ -258,6 +258,8 @@ int main(int argc, char** argv) {
       sa.store = 1;
       sa.out = slot_out + i;
       sa.obs = nullptr;
+      sa.done = nullptr;  // no completion flag: the launches are synchronised below
+      sa.seq = 0;
       switch (v) {
         case 0: k_slot<false><<<1, 64>>>(sa); break;
         case 1: k_slot_var<0><<<1, 64>>>(sa); break;
