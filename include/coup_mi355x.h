@@ -21,13 +21,14 @@
 #ifndef COUP_MI355X_H_
 #define COUP_MI355X_H_
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
 extern "C" {
 #endif
 
-#define COUP_ABI_VERSION 6
+#define COUP_ABI_VERSION 7
 
 #define COUP_NUM_PLAYERS 2          /* coup.h:42 */
 #define COUP_MAX_PLAYERS 6          /* N-player extension */
@@ -187,6 +188,25 @@ int coup_reset(coup_env* env, const uint8_t* lane_mask);
  * state -- so one launch steps any subset of the lanes (SyncVectorEnv over
  * per-game environments, vector_env.py:40-67). */
 int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out);
+
+/* coup_step_host flags */
+#define COUP_HOST_OBS 1   /* also return ObservationTensor [B][P][49P] */
+#define COUP_HOST_INFO 2  /* also return InformationStateTensor [B][2][2492] (COUP_FLAG_HISTORY) */
+
+/* coup_step for small batches that want the answers on the host (the
+ * per-game rl_environment.Environment and SyncVectorEnv, rl_environment.py:
+ * 282-322): `actions` is a HOST [B] int8 array (or NULL: uniform policy;
+ * negative entries skip lanes as in coup_step).  The step kernel writes its
+ * outputs straight into mapped pinned host memory and the call synchronises
+ * the env's stream -- one launch, no query kernel, no copy kernel.  host_out
+ * receives, in sections starting at the offsets coup_step_host_layout
+ * returns (16-byte aligned): legal_mask uint32 [B], cur_player int8 [B],
+ * step_type uint8 [B], rewards int8 [B][P], actions int8 [B], then the
+ * tensors `want` asks for (obs before info_state). */
+int coup_step_host(coup_env* env, const int8_t* actions, int want, void* host_out);
+/* Section offsets off[0..5] of coup_step_host's output and its total size in
+ * bytes, for `batch` lanes of `num_players` players. */
+size_t coup_step_host_layout(int64_t batch, int num_players, int want, size_t* off);
 
 /* `steps` uniform-random env steps per lane (the coup_step of actions ==
  * NULL, with the env's auto-reset setting) in ONE launch, the state kept in

@@ -1706,6 +1706,9 @@ struct coup_env {
   uint8_t* batch_scratch_dev;
   size_t batch_cap;
   uint32_t batch_seq;         // last completion value k_slot_batch stored in the batch flags
+  uint8_t* host_scratch;      // coup_step_host: input actions + outputs (mapped pinned, grown on demand)
+  uint8_t* host_scratch_dev;
+  size_t host_cap;
   bool batch_pending;         // an asynchronous coup_slot_ops may still read the requests
 };
 
@@ -1791,12 +1794,40 @@ int launch_reset(coup_env* env, const uint8_t* mask, int mode, int deal) {
   return COUP_OK;
 }
 
+size_t align16(size_t n) { return (n + 15u) & ~size_t(15); }
+
+}  // namespace
+
+// coup_step_host's output layout (coup_mi355x.h): section offsets of legal
+// mask, player, step type, rewards, actions and the tensors; returns the size.
+extern "C" size_t coup_step_host_layout(int64_t batch, int num_players, int want, size_t* off) {
+  const size_t B = (size_t)(batch > 0 ? batch : 0), P = (size_t)num_players;
+  size_t o = 0;
+  off[0] = o;
+  o += align16(4 * B);
+  off[1] = o;
+  o += align16(B);
+  off[2] = o;
+  o += align16(B);
+  off[3] = o;
+  o += align16(B * P);
+  off[4] = o;
+  o += align16(B);
+  off[5] = o;
+  if (want & COUP_HOST_OBS) o += align16(B * P * 49u * P * 4u);
+  if (want & COUP_HOST_INFO) o += B * 2u * COUP_INFO_STATE_SIZE * 4u;
+  return o;
+}
+
+namespace {
+
 void release(coup_env* env) {
   (void)hipFree(env->state);
   (void)hipFree(env->hist);
   (void)hipFree(env->err_count);
   if (env->slot_scratch) (void)hipHostFree(env->slot_scratch);
   if (env->batch_scratch) (void)hipHostFree(env->batch_scratch);
+  if (env->host_scratch) (void)hipHostFree(env->host_scratch);
   delete env;
 }
 
@@ -1844,6 +1875,9 @@ int coup_create_ex(int64_t batch, uint64_t seed, uint32_t env_id_base, int flags
   env->batch_cap = 0;
   env->batch_pending = false;
   env->batch_seq = 0;
+  env->host_scratch = nullptr;
+  env->host_scratch_dev = nullptr;
+  env->host_cap = 0;
   const size_t lanes = (size_t)(batch > 0 ? batch : 1);
   hipError_t e = hipMalloc(&env->state, lanes * sizeof(uint4) * (generic ? 2 : 1));
   if (e == hipSuccess) e = hipMalloc(&env->err_count, sizeof(uint32_t));
@@ -2044,6 +2078,46 @@ int coup_rollout(coup_env* env, int64_t steps, const coup_rollout_stats* stats) 
   } else
     coup::k_rollout<<<grid_for(env->batch), coup::kThreads, 0, env->stream>>>(a);
   COUP_HIP_TRY(hipGetLastError());
+  return COUP_OK;
+}
+
+int coup_step_host(coup_env* env, const int8_t* actions, int want, void* host_out) {
+  COUP_CHECK_ENV(env);
+  if (!host_out) return fail(COUP_E_INVALID, "coup_step_host: host_out is null");
+  if (want & ~(COUP_HOST_OBS | COUP_HOST_INFO)) return fail(COUP_E_INVALID, "coup_step_host: unknown flags");
+  if ((want & COUP_HOST_INFO) && !env->hist)
+    return fail(COUP_E_INVALID, "coup_step_host: info_state needs an env created with COUP_FLAG_HISTORY");
+  const int64_t B = env->batch;
+  if (B == 0) return COUP_OK;
+  const size_t in_bytes = align16((size_t)B);
+  size_t off[6];
+  const size_t total = coup_step_host_layout(B, env->players, want, off);
+  if (in_bytes + total > env->host_cap) {
+    if (env->host_scratch) (void)hipHostFree(env->host_scratch);
+    env->host_scratch = nullptr;
+    env->host_cap = 0;
+    COUP_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&env->host_scratch), in_bytes + total,
+                               hipHostMallocMapped | hipHostMallocCoherent));
+    COUP_HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&env->host_scratch_dev), env->host_scratch, 0));
+    env->host_cap = in_bytes + total;
+  }
+  if (actions) std::memcpy(env->host_scratch, actions, (size_t)B);
+  uint8_t* dev = env->host_scratch_dev + in_bytes;
+  coup_step_outputs o;
+  std::memset(&o, 0, sizeof(o));
+  o.legal_mask = reinterpret_cast<uint32_t*>(dev + off[0]);
+  o.cur_player = reinterpret_cast<int8_t*>(dev + off[1]);
+  o.step_type = dev + off[2];
+  o.rewards = reinterpret_cast<int8_t*>(dev + off[3]);
+  o.actions = reinterpret_cast<int8_t*>(dev + off[4]);
+  if (want & COUP_HOST_OBS) o.obs = reinterpret_cast<float*>(dev + off[5]);
+  if (want & COUP_HOST_INFO)
+    o.info_state = reinterpret_cast<float*>(dev + off[5] +
+                                            ((want & COUP_HOST_OBS) ? align16((size_t)B * env->players * 49u * env->players * 4u) : 0u));
+  const int r = coup_step(env, actions ? reinterpret_cast<const int8_t*>(env->host_scratch_dev) : nullptr, &o);
+  if (r != COUP_OK) return r;
+  COUP_HIP_TRY(hipStreamSynchronize(env->stream));
+  std::memcpy(host_out, env->host_scratch + in_bytes, total);
   return COUP_OK;
 }
 

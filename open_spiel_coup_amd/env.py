@@ -157,6 +157,46 @@ class BatchedCoupEnv:
             out["info_state"] = self.info_state
         return out
 
+    def step_host(self, actions=None, obs=False, info_state=False):
+        """`step` for small batches that want the answers on the host
+        (coup_step_host: the kernel writes into mapped pinned memory, one
+        launch and one synchronisation).  actions: host int8-convertible [B]
+        (negative entries skip lanes) or None for the uniform policy.
+        Returns numpy arrays: legal_mask, current_player, step_type, rewards,
+        actions, terminal (step type LAST), and obs / info_state if asked."""
+        self._bind_stream()
+        B, P = self.batch, self.num_players
+        want = (_native.HOST_OBS if obs else 0) | (_native.HOST_INFO if info_state else 0)
+        key = (want,)
+        if getattr(self, "_sh_key", None) != key:
+            off = (ctypes.c_size_t * 6)()
+            total = self.lib.coup_step_host_layout(B, P, want, off)
+            self._sh_off = list(off)
+            self._sh_buf = np.empty(max(total, 1), dtype=np.uint8)
+            self._sh_key = key
+        a = None
+        if actions is not None:
+            acts = np.ascontiguousarray(np.asarray(actions, dtype=np.int8).reshape(B))
+            self._sh_acts = acts
+            a = ctypes.c_void_p(acts.ctypes.data)
+        _native.check(self.lib.coup_step_host(self._h, a, want, ctypes.c_void_p(self._sh_buf.ctypes.data)))
+        h, off = self._sh_buf, self._sh_off
+        out = {"legal_mask": h[off[0]:off[0] + 4 * B].view(np.int32).copy(),
+               "current_player": h[off[1]:off[1] + B].view(np.int8).copy(),
+               "step_type": h[off[2]:off[2] + B].copy(),
+               "rewards": h[off[3]:off[3] + B * P].view(np.int8).reshape(B, P).copy(),
+               "actions": h[off[4]:off[4] + B].view(np.int8).copy()}
+        out["terminal"] = (out["step_type"] == LAST).astype(np.uint8)
+        o = off[5]
+        if obs:
+            n = B * P * self.obs_size * 4
+            out["obs"] = h[o:o + n].view(np.float32).reshape(B, P, self.obs_size).copy()
+            o += (n + 15) // 16 * 16
+        if info_state:
+            n = B * 2 * INFO_STATE_SIZE * 4
+            out["info_state"] = h[o:o + n].view(np.float32).reshape(B, 2, INFO_STATE_SIZE).copy()
+        return out
+
     def episode_stats(self):
         """(episodes, return_sum) per lane since the last clear_episode_stats
         (int32 [B] device tensors; needs episode_stats=True)."""

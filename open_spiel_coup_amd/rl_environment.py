@@ -165,6 +165,12 @@ class Environment:
         a[self._lane] = int(action)
         return a.to(self._env.device)
 
+    def _lane_actions_host(self, action):
+        """[B] int8 host actions: `action` on this env's lane, -1 (skip) elsewhere."""
+        a = np.full(self._env.batch, -1, dtype=np.int8)
+        a[self._lane] = int(action)
+        return a
+
     def _lane_mask(self):
         if self._env.batch == 1:
             return None
@@ -258,12 +264,18 @@ class Environment:
         known_legal = cur >= 0 and int(actions[0]) in self._last["legal_actions"][cur]
         if not 0 <= int(actions[0]) < 128:
             raise pyspiel.SpielError(f"illegal action {actions[0]}")  # not an int8 action id
-        a = self._lane_actions(actions[0])
         if self._sampler is None:
-            self._env.step(a)
-        else:
-            self._env.apply_action(a)
-            self._sample_external_events()
+            # one launch whose outputs land in mapped host memory (coup_step_host)
+            q = self._env.step_host(self._lane_actions_host(actions[0]), obs=self._use_observation,
+                                    info_state=not self._use_observation)
+            if not known_legal and self._env.error_count():
+                raise pyspiel.SpielError(f"illegal action {actions[0]}")
+            row = {k: v[self._lane] for k, v in q.items()}
+            step_type = StepType.LAST if int(row["terminal"]) else StepType.MID
+            self._should_reset = step_type == StepType.LAST
+            return self._time_step(row, step_type, [float(x) for x in row["rewards"]])
+        self._env.apply_action(self._lane_actions(actions[0]))
+        self._sample_external_events()
         if not known_legal and self._env.error_count():
             raise pyspiel.SpielError(f"illegal action {actions[0]}")
         return self.get_time_step()

@@ -6,10 +6,11 @@ The reference steps its envs one after another in a Python loop
 lane records and histories move into lane i of one shared N-lane
 BatchedCoupEnv, and each Environment keeps working on its lane (its own
 step / reset / get_state / set_state still apply to that game).  A vector
-step is then one reset launch for the envs that restart, one step launch
-for the rest (lanes not stepped take action -1, which the kernel skips), and
-one device-to-host copy of every env's tensors, legal mask, player, rewards
-and terminal flag -- instead of N round trips.
+step is then one reset launch for the envs that restart and one step launch
+for the rest (lanes not stepped take action -1, which the kernel skips) that
+writes every env's tensors, legal mask, player, rewards and step type
+straight into mapped host memory (coup_step_host) -- instead of N round
+trips.
 
 Chance streams: env i draws its deals from global env id i under the first
 env's seed; the envs' own seeds no longer apply once
@@ -150,10 +151,14 @@ class SyncVectorEnv:
         if any(resets):
             self._reset_lanes(resets)
         if not all(resets):
-            self._shared.step(torch.from_numpy(acts))
+            # one launch whose outputs (skipped lanes: their current state) land
+            # in mapped host memory: no separate query
+            e0 = envs[0]
+            self._q_step = self._shared.step_host(acts, obs=e0._use_observation, info_state=not e0._use_observation)
             if unknown and self._shared.error_count():
                 raise pyspiel.SpielError(f"illegal action among envs {unknown}")
-        self._q_step = self._query()
+        else:
+            self._q_step = self._query()
         return self._time_steps(self._q_step, resets)
 
     # ------------------------------------------------------------ public API

@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def _declared_functions():
     with open(os.path.join(ROOT, "include", "coup_mi355x.h")) as f:
         text = f.read()
-    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(coup_\w+)\s*\(", text, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|size_t|const char\*)\s+(coup_\w+)\s*\(", text, re.M)))
 
 
 def test_library_exports_every_declared_symbol():

@@ -191,3 +191,35 @@ def test_vector_env_falls_back_to_loop():
     ts = venv.reset()
     ts, _, _, _ = venv.step([_Out(t.observations["legal_actions"][t.current_player()][0]) for t in ts])
     assert all(t.mid() or t.last() for t in ts)
+
+
+@pytest.mark.parametrize("players,obs,info", [(2, True, False), (2, False, True), (6, True, False), (3, False, False)],
+                         ids=["2p-obs", "2p-info", "6p-obs", "3p"])
+@pytest.mark.parametrize("uniform", [True, False])
+def test_step_host_equals_step(players, obs, info, uniform):
+    """coup_step_host (outputs written into mapped host memory, one launch)
+    == coup_step on a twin env (device outputs, then queries), lane by lane,
+    with skipped lanes among caller actions."""
+    n, seed = 300, 41
+    kw = dict(seed=seed, env_id_base=9, auto_reset=False, num_players=players, history=info)
+    host = BatchedCoupEnv(n, obs=False, **kw)
+    dev = BatchedCoupEnv(n, obs=obs, info_state=info, **kw)
+    rng = np.random.default_rng(seed)
+    for t in range(60):
+        acts = None
+        if not uniform:
+            legal = dev.query(obs=False)["legal_mask"].cpu().numpy() & 0x3FFFF
+            acts = np.where(rng.random(n) < 0.25, -1, _random_legal(legal, rng)).astype(np.int8)
+        q = host.step_host(acts, obs=obs, info_state=info)
+        o = dev.step(None if acts is None else torch.from_numpy(acts))
+        assert np.array_equal(q["legal_mask"], o["legal_mask"].cpu().numpy()), t
+        assert np.array_equal(q["current_player"], o["current_player"].cpu().numpy()), t
+        assert np.array_equal(q["step_type"], o["step_type"].cpu().numpy()), t
+        assert np.array_equal(q["rewards"], o["rewards"].cpu().numpy()), t
+        assert np.array_equal(q["actions"], o["actions"].cpu().numpy()), t
+        if obs:
+            assert np.array_equal(q["obs"], o["obs"].cpu().numpy()), t
+        if info:
+            assert np.array_equal(q["info_state"], o["info_state"].cpu().numpy()), t
+    assert torch.equal(host.export_state(), dev.export_state())
+    assert host.error_count() == dev.error_count() == 0
