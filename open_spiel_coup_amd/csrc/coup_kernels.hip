@@ -1709,6 +1709,8 @@ struct coup_env {
   uint8_t* host_scratch;      // coup_step_host: input actions + outputs (mapped pinned, grown on demand)
   uint8_t* host_scratch_dev;
   size_t host_cap;
+  uint8_t* host_stage;        // coup_step_host with info_state: device staging of the outputs (grown on demand)
+  size_t host_stage_cap;
   bool batch_pending;         // an asynchronous coup_slot_ops may still read the requests
 };
 
@@ -1828,6 +1830,7 @@ void release(coup_env* env) {
   if (env->slot_scratch) (void)hipHostFree(env->slot_scratch);
   if (env->batch_scratch) (void)hipHostFree(env->batch_scratch);
   if (env->host_scratch) (void)hipHostFree(env->host_scratch);
+  if (env->host_stage) (void)hipFree(env->host_stage);
   delete env;
 }
 
@@ -1878,6 +1881,8 @@ int coup_create_ex(int64_t batch, uint64_t seed, uint32_t env_id_base, int flags
   env->host_scratch = nullptr;
   env->host_scratch_dev = nullptr;
   env->host_cap = 0;
+  env->host_stage = nullptr;
+  env->host_stage_cap = 0;
   const size_t lanes = (size_t)(batch > 0 ? batch : 1);
   hipError_t e = hipMalloc(&env->state, lanes * sizeof(uint4) * (generic ? 2 : 1));
   if (e == hipSuccess) e = hipMalloc(&env->err_count, sizeof(uint32_t));
@@ -2102,7 +2107,20 @@ int coup_step_host(coup_env* env, const int8_t* actions, int want, void* host_ou
     env->host_cap = in_bytes + total;
   }
   if (actions) std::memcpy(env->host_scratch, actions, (size_t)B);
-  uint8_t* dev = env->host_scratch_dev + in_bytes;
+  // small outputs (and obs) go straight into the mapped host buffer.  The
+  // 19,936-byte InformationStateTensor per lane is written after the step by
+  // k_info_elems (one thread per float4: the step kernel's wave-cooperative
+  // writer is one wave per 64 lanes, 218 us for one lane) into device memory,
+  // and everything comes over in one copy.
+  const bool stage = (want & COUP_HOST_INFO) != 0;
+  if (stage && total > env->host_stage_cap) {
+    if (env->host_stage) (void)hipFree(env->host_stage);
+    env->host_stage = nullptr;
+    env->host_stage_cap = 0;
+    COUP_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&env->host_stage), total));
+    env->host_stage_cap = total;
+  }
+  uint8_t* dev = stage ? env->host_stage : env->host_scratch_dev + in_bytes;
   coup_step_outputs o;
   std::memset(&o, 0, sizeof(o));
   o.legal_mask = reinterpret_cast<uint32_t*>(dev + off[0]);
@@ -2111,11 +2129,21 @@ int coup_step_host(coup_env* env, const int8_t* actions, int want, void* host_ou
   o.rewards = reinterpret_cast<int8_t*>(dev + off[3]);
   o.actions = reinterpret_cast<int8_t*>(dev + off[4]);
   if (want & COUP_HOST_OBS) o.obs = reinterpret_cast<float*>(dev + off[5]);
+  float* info_out = nullptr;
   if (want & COUP_HOST_INFO)
-    o.info_state = reinterpret_cast<float*>(dev + off[5] +
-                                            ((want & COUP_HOST_OBS) ? align16((size_t)B * env->players * 49u * env->players * 4u) : 0u));
+    info_out = reinterpret_cast<float*>(dev + off[5] +
+                                        ((want & COUP_HOST_OBS) ? align16((size_t)B * env->players * 49u * env->players * 4u) : 0u));
   const int r = coup_step(env, actions ? reinterpret_cast<const int8_t*>(env->host_scratch_dev) : nullptr, &o);
   if (r != COUP_OK) return r;
+  if (info_out) {
+    const int64_t nf4 = B * coup::kInfoF4;
+    coup::k_info_elems<<<(unsigned)((nf4 + coup::kThreads - 1) / coup::kThreads), coup::kThreads, 0, env->stream>>>(
+        env->state, env->hist, B, info_out);
+    COUP_HIP_TRY(hipGetLastError());
+  }
+  if (stage)
+    COUP_HIP_TRY(hipMemcpyAsync(env->host_scratch + in_bytes, env->host_stage, total, hipMemcpyDeviceToHost,
+                                env->stream));
   COUP_HIP_TRY(hipStreamSynchronize(env->stream));
   std::memcpy(host_out, env->host_scratch + in_bytes, total);
   return COUP_OK;
