@@ -867,10 +867,14 @@ hipError_t launch_reset(const Env& e, const uint8_t* mask, int mode, int deal) {
 // 25.7 / 22.7 us per step (3 and 4 players: 512 best for the step;
 // profiles/r02/ab/np_sort_block_size.log).  The step keeps its auto-resets
 // on one wave behind a barrier, which 1024-lane blocks make the longer
-// wait; the rollout sorts its resets like a decision.  COUP_NP_SORT_THREADS
-// = 256 / 512 / 1024 overrides both (A/B runs; 128 measured 47.4 us; every size gives the
-// same results, test_regrouped_*_block_size_invariant).
-constexpr int kStepSortLanes = 512;
+// wait; the rollout sorts its resets like a decision.  After the step's
+// phase 2 stopped testing terminal / chance at known decision nodes, the
+// 6-player step prefers 1024-lane blocks: 34.1 vs 34.7 / 35.2 us in two
+// interleaved processes (profiles/r02/ab/np_step_block_size_final.jsonl).
+// COUP_NP_SORT_THREADS = 256 / 512 / 1024 overrides both (A/B runs; 128
+// measured 47.4 us; every size gives the same results,
+// test_regrouped_*_block_size_invariant).
+constexpr int step_sort_lanes(int players) { return players >= 6 ? 1024 : 512; }
 constexpr int kRolloutSortLanes = 1024;
 
 hipError_t launch_step(const Env& e, const int8_t* actions, const coup_step_outputs* out) {
@@ -915,7 +919,7 @@ hipError_t launch_step(const Env& e, const int8_t* actions, const coup_step_outp
         else
           k_step_sorted<N, true, false, TB><<<g, TB, 0, e.stream>>>(a);
       };
-      switch (sort_lanes("COUP_NP_SORT_THREADS", kStepSortLanes)) {
+      switch (sort_lanes("COUP_NP_SORT_THREADS", step_sort_lanes(N))) {
         case 256: go(std::integral_constant<int, 256>()); break;
         case 1024: go(std::integral_constant<int, 1024>()); break;
         default: go(std::integral_constant<int, 512>()); break;
