@@ -90,6 +90,12 @@ class BatchedEnv {
   void Step(const int8_t* actions, const coup_step_outputs& out) {
     Check(coup_step(env_, actions, &out), "coup_step");
   }
+  // one step whose outputs land in host memory (coup_step_host): host
+  // actions (or null), COUP_HOST_* flags, host_out laid out as
+  // coup_step_host_layout describes
+  void StepHost(const int8_t* host_actions, int want, void* host_out) {
+    Check(coup_step_host(env_, host_actions, want, host_out), "coup_step_host");
+  }
   // `steps` uniform steps in one launch, step t's outputs in slice t of
   // out's [steps][B] buffers (coup_step_trajectory; no obs / info_state)
   void StepTrajectory(int64_t steps, const coup_step_outputs& out) {
