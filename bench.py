@@ -149,6 +149,9 @@ def parse():
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
                     help="collectives of a multi-process run: nccl (RCCL over xGMI, one GPU per rank) or gloo "
                          "(a rehearsal of the multi-GPU path with several ranks sharing a GPU)")
+    ap.add_argument("--force-collective", action="store_true",
+                    help="run the collectives (all-gather, barrier, max over ranks) even at one rank, over a "
+                         "one-rank communicator of --dist-backend (MASTER_ADDR / MASTER_PORT must be set)")
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
                     help="replay the K timed steps from one HIP graph (auto: on for c2, c3 and c4, "
                          "where it removes the per-step launch gaps)")
@@ -329,7 +332,9 @@ def main():
     from open_spiel_coup_amd import distributed as D
 
     rank, world, _ = D.world_info()
-    dev = D.init(args.dist_backend, gpu=True)  # RCCL over xGMI when world > 1
+    force = args.force_collective
+    dev = D.init(args.dist_backend, gpu=True, force=force)  # RCCL over xGMI when world > 1
+    grouped = world > 1 or force
 
     cfg = args.config
     B0, with_obs, with_info, fused, bytes_per_lane, workload, players = CONFIGS[cfg]
@@ -342,7 +347,7 @@ def main():
     stats = env.new_stats() if fused == "rollout" else None
 
     def barrier():
-        if world > 1:
+        if grouped:
             dist.barrier()
         torch.cuda.synchronize()
 
@@ -388,7 +393,7 @@ def main():
 
     # one collation outside the timed region: RCCL sets up its all-gather
     # channels lazily, and HIP loads torch's stack kernel on first use
-    D.collate(episode_payload())
+    D.collate(episode_payload(), force=force)
     if stats is not None:
         for t in stats.values():
             t.zero_()
@@ -419,7 +424,7 @@ def main():
         ev[0][1].record(stream)
     # collate every lane's finished-episode count and player-0 return sum over
     # xGMI (RCCL all-gather, [world * B, 2] int32; identity at one rank)
-    gathered = D.collate(episode_payload())
+    gathered = D.collate(episode_payload(), force=force)
     barrier()
     elapsed = time.perf_counter() - t0
     g_eps, g_ret = unpack_payload(gathered)
@@ -429,7 +434,16 @@ def main():
     # per env step: the span of the K steps (one replay, one fused launch or K
     # eager launches) / K, launch gaps included
     kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
-    elapsed = D.max_over_ranks(elapsed, dev)
+    elapsed = D.max_over_ranks(elapsed, dev, force=force)
+    # the collective tail of the timed region (payload + all-gather + barrier)
+    # and the max over ranks after it, timed again on their own with the GPU
+    # idle: the share of a K-step window that does not scale with the lanes
+    barrier()
+    tc = time.perf_counter()
+    D.collate(episode_payload(), force=force)
+    barrier()
+    D.max_over_ranks(0.0, dev, force=force)
+    collective_ms = (time.perf_counter() - tc) * 1e3
     errors = env.error_count()
     ceiling_ms = None
     if players == 2 and not fused and not with_info:
@@ -500,14 +514,17 @@ def main():
                                         "all_gather [world*B] int32 (return sum << 16 | episodes per lane)"
                                         if width == 4 else
                                         "all_gather [world*B, 2] int32 (episodes, return sum per lane)")
-                         if world > 1 else None},
+                         if grouped else None,
+                         "collective_ms": collective_ms,
+                         "collective_backend": (args.dist_backend + (" (one-rank communicator)" if world == 1 else ""))
+                         if grouped else None},
             "lane_errors": errors,
             "box": _box_identity(dev),
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, with_obs, with_info, players)
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if grouped:
         dist.destroy_process_group()
 
 

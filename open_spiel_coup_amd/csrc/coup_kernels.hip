@@ -2423,8 +2423,13 @@ int coup_slot_ops(coup_env* env, int64_t n, const coup_slot_req* reqs, const cou
                          : nullptr;
   b.obs = obs_out;
   if (poll) {
+    // flag_off moves with n and the tensor flags, so the words it lands on
+    // may hold an earlier call's requests or results -- even a value equal
+    // to this call's seq.  Clear them before the launch (0 is never a seq):
+    // a flag then equals seq only once its block has stored its result.
+    std::memset(env->batch_scratch + flag_off, 0, flag_bytes);
     b.done = reinterpret_cast<uint32_t*>(dev + flag_off);
-    b.seq = env->batch_seq + 1u == 0u ? 1u : env->batch_seq + 1u;  // 0: a fresh buffer's value
+    b.seq = env->batch_seq + 1u == 0u ? 1u : env->batch_seq + 1u;  // 0: a cleared flag
     env->batch_seq = b.seq;
   }
   hipStream_t s = env->stream;

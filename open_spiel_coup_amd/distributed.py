@@ -24,12 +24,16 @@ def env_id_base(rank, lanes_per_rank):
     return rank * lanes_per_rank
 
 
-def init(backend="nccl", gpu=None):
+def init(backend="nccl", gpu=None, force=False):
     """Initialise the process group for a torchrun launch (no-op for one
-    process).  Returns the torch device of this rank: cuda:LOCAL_RANK for
-    nccl (RCCL); for gloo the CPU, or with gpu=True a GPU shared round-robin
-    by the ranks (a rehearsal of the multi-GPU path on a box with fewer GPUs
-    than ranks; RCCL refuses two ranks on one GPU)."""
+    process unless `force`).  Returns the torch device of this rank:
+    cuda:LOCAL_RANK for nccl (RCCL); for gloo the CPU, or with gpu=True a GPU
+    shared round-robin by the ranks (a rehearsal of the multi-GPU path on a
+    box with fewer GPUs than ranks; RCCL refuses two ranks on one GPU).
+    force: create the group even for one process (a one-rank RCCL
+    communicator), so that collate / max_over_ranks(force=True) run the
+    collectives the multi-GPU job runs; the rendezvous still comes from
+    MASTER_ADDR / MASTER_PORT."""
     rank, world, local = world_info()
     if backend == "nccl":
         dev = torch.device("cuda", local)
@@ -39,17 +43,19 @@ def init(backend="nccl", gpu=None):
         torch.cuda.set_device(dev)
     else:
         dev = torch.device("cpu")
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force) and not dist.is_initialized():
         kw = {"device_id": dev} if backend == "nccl" else {}
         dist.init_process_group(backend, **kw)
     return dev
 
 
-def collate(t, dim=0):
+def collate(t, dim=0, force=False):
     """All-gather a per-lane tensor from every rank; lanes are along `dim`
     ([B, ...] by default, dim=1 for [T, B, ...] trajectories).  Returns the
-    concatenation along `dim` in rank (= global env id) order."""
-    if not dist.is_initialized() or dist.get_world_size() == 1:
+    concatenation along `dim` in rank (= global env id) order.  One rank
+    returns `t` itself unless `force` (and a group exists): then the
+    collective runs anyway, over a one-rank communicator."""
+    if not dist.is_initialized() or (dist.get_world_size() == 1 and not force):
         return t
     if dim == 0 and dist.get_backend() == "nccl":
         # RCCL writes the rank-ordered concatenation in place: no gather list, no cat
@@ -61,9 +67,9 @@ def collate(t, dim=0):
     return torch.cat(parts, dim)
 
 
-def max_over_ranks(x, device):
+def max_over_ranks(x, device, force=False):
     """Max of a host float over ranks (the bench's timing rule)."""
     t = torch.tensor([float(x)], dtype=torch.float64, device=device)
-    if dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_initialized() and (dist.get_world_size() > 1 or force):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())

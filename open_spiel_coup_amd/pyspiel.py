@@ -596,15 +596,21 @@ def apply_actions(states, actions):
     by_pool = {}
     for k, st in enumerate(states):
         by_pool.setdefault((id(st._pool), st._slot[0]), []).append(k)
+    failed = None
     for (_, seg), ks in by_pool.items():
         pool = states[ks[0]]._pool
         res = pool.ops(seg, [(states[k]._slot[1], -1, actions[k]) for k in ks])
+        # every state of the launch has advanced (or not) on the device:
+        # bring each host view up to date before reporting a failure
         for k, q in zip(ks, res):
             if not q["ok"]:
                 states[k]._q = pool.op(states[k]._slot)
-                raise SpielError(f"illegal action {actions[k]}")
+                failed = k if failed is None else failed
+                continue
             states[k]._q = q
             states[k]._history = states[k]._history + [(players[k], actions[k])]
+    if failed is not None:
+        raise SpielError(f"illegal action {actions[failed]}")
 
 
 def load_game(name, params=None):

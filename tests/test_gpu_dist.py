@@ -145,3 +145,33 @@ def test_bench_two_ranks_gloo_trajectory(config):
     assert rec["lane_errors"] == 0
     assert rec["episodes"]["finished"] > 0 and rec["episodes"]["collective"].startswith("all_gather")
     assert "trajectory" in rec["roofline"]["kernel"]
+
+
+def test_rccl_one_rank_collectives(tmp_path):
+    """The RCCL branch of collate / max_over_ranks (never reached by the
+    gloo rehearsals): one fresh process, init_process_group("nccl",
+    device_id=...), all_gather_into_tensor of bench.py's three payload widths
+    at the headline batch, unpacked == env.episode_stats()."""
+    out = tmp_path / "nccl.json"
+    _run_ranks(lambda r: [sys.executable, "-u", os.path.join(ROOT, "tests", "dist_nccl_worker.py"), str(out),
+                          str(1 << 20), "20"], 1, timeout=100)
+    res = json.loads(out.read_text())
+    assert res["backend"] == "nccl" and res["world"] == 1 and res["episodes"] > 0
+    assert res["width_at_k"] == 2 and set(res["widths"]) == {"2", "4", "8"}
+    assert res["widths"]["2"]["payload_bytes"] == 2 << 20
+    print("\nRCCL one-rank all-gather ms:", {w: round(v["all_gather_ms"], 3) for w, v in res["widths"].items()})
+
+
+def test_bench_one_rank_rccl_line():
+    """bench.py --force-collective --dist-backend nccl at one rank: the
+    multi-GPU line's code path over a one-rank RCCL communicator, with the
+    collective tail timed (episodes.collective_ms)."""
+    outs = _run_ranks(lambda r: [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--config", "c3", "--steps",
+                                 "20", "--warmup", "5", "--settle", "64", "--dist-backend", "nccl",
+                                 "--force-collective", "--no-cpu-baseline"], 1, timeout=110)
+    rec = json.loads([ln for ln in outs[0].splitlines() if ln.startswith("{")][-1])
+    ep = rec["episodes"]
+    assert ep["collective_backend"].startswith("nccl") and "int16" in ep["collective"]
+    assert ep["finished"] > 0 and rec["lane_errors"] == 0
+    assert ep["collective_ms"] > 0  # reported, not bounded: a one-rank communicator prices no xGMI hop
+    print("\nc3 one-rank RCCL line:", json.dumps({k: rec[k] for k in ("value", "ms_per_step")}), json.dumps(ep))

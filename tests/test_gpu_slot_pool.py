@@ -196,6 +196,49 @@ def test_apply_actions_advances_a_frontier():
         pyspiel.apply_actions([st, st], [0, 0])
 
 
+def test_slot_ops_alternating_batch_sizes_match_single_ops():
+    """coup_slot_ops' completion flags sit after its requests and results,
+    so their offset moves with the batch size and the tensor flags and lands
+    on words earlier calls wrote (request lanes, actions, result bytes).
+    Batches of 20, 1, 7, ... with obs on and off, each child against the
+    same child made by single coup_slot_op calls and against the oracle."""
+    rng = np.random.default_rng(8)
+    game = pyspiel.load_game("coup")
+    parents = []
+    for k in range(8):
+        st, ref = game.new_initial_state(), oracle.OracleState()
+        for _ in range(int(rng.integers(4, 26))):
+            if ref.is_terminal():
+                break
+            a = int(rng.choice(ref.legal_actions()))
+            st.apply_action(a)
+            ref.apply_action(a)
+        if ref.is_terminal():
+            continue
+        parents.append((st, ref))
+    plan = [(20, False), (1, False), (7, True), (20, True), (1, True), (7, False), (33, False), (2, True),
+            (1, False), (64, True), (3, False), (1, True)]
+    for i, (n, obs) in enumerate(plan):
+        st, ref = parents[i % len(parents)]
+        acts = [int(a) for a in rng.choice(ref.legal_actions(), size=n)]
+        kids = st.children(acts, obs=obs)
+        for a, ch in zip(acts, kids):
+            single = st.child(a)
+            assert ch.packed_record().tolist() == single.packed_record().tolist()
+            assert ch.history_bytes().tolist() == single.history_bytes().tolist()
+            for key in ("legal_mask", "current_player", "terminal", "ok"):
+                assert ch._q[key] == single._q[key], key
+            assert ch._q["rewards"].tolist() == single._q["rewards"].tolist()
+            assert ch._q["returns"].tolist() == single._q["returns"].tolist()
+            r2 = ref.clone()
+            r2.apply_action(a)
+            _same(ch, r2)
+            if obs:  # the batched call's own tensors, before any re-query
+                for p in (0, 1):
+                    assert ch._q["obs"][p].tolist() == list(r2.observation_tensor(p))
+        _same(st, ref)
+
+
 def test_slot_ops_rejects_dependent_requests():
     """coup_slot_ops requires independent requests: a repeated destination
     lane, or a destination that is another request's source, is refused
