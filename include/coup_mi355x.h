@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define COUP_ABI_VERSION 7
+#define COUP_ABI_VERSION 8
 
 #define COUP_NUM_PLAYERS 2          /* coup.h:42 */
 #define COUP_MAX_PLAYERS 6          /* N-player extension */
@@ -269,6 +269,35 @@ int coup_slot_op(coup_env* env, int64_t lane, const coup_env* src_env, int64_t s
  * synchronises the env's stream. */
 int coup_slot_ops(coup_env* env, int64_t n, const coup_slot_req* reqs, const coup_env* src_env, int flags,
                   void* host_out);
+
+/* --- device-resident op server ------------------------------------------ */
+
+/* A resident wave that runs coup_slot_op requests without kernel launches
+ * (DESIGN.md section 12).  It runs on its own non-blocking HIP stream of the
+ * current device and polls a ring of requests in mapped, coherent pinned host
+ * memory; an answered op is one host write the wave sees, the op, and one
+ * device->host write the host sees.  coup_slot_op on an env attached to a
+ * server (coup_attach_server), whose src_env is NULL or attached to the same
+ * server, goes through it; other entry points on such an env first wait for
+ * the server's pending requests, and the server waits for (synchronises) work
+ * enqueued on the env's stream before it reads the env's lanes, so the two
+ * paths stay ordered.  The wave leaves after idle_us microseconds without a
+ * request, on coup_server_destroy, or when the host finds it idle; the next
+ * request relaunches it.  Not thread-safe: calls on envs sharing a server
+ * must be serialised by the caller.  Replaces, for the per-state callers of
+ * rust_open_spiel.h:34-73 / pyspiel.cc:263-345, the launch-and-synchronise
+ * round trip of each State op. */
+typedef struct coup_server coup_server;
+int coup_server_create(int64_t idle_us, coup_server** out);
+/* Serves the pending requests, stops the wave and frees the server.  Detach
+ * (or destroy) its envs first. */
+int coup_server_destroy(coup_server* srv);
+/* Route env's coup_slot_op through srv (NULL detaches).  env: 2-player,
+ * COUP_FLAG_HISTORY. */
+int coup_attach_server(coup_env* env, coup_server* srv);
+/* out[0] requests served, out[1] wave launches, out[2] a wave may be running,
+ * out[3] idle_us. */
+int coup_server_stats(const coup_server* srv, uint64_t* out);
 
 /* Copy the packed lane records ([B][coup_state_bytes / 4] uint32, device)
  * out of / into the env. */

@@ -36,6 +36,7 @@
 #include <cstdint>
 #include <cstring>
 #include <memory>
+#include <cstdlib>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -221,8 +222,10 @@ inline std::string StateString(const Fields& f, const uint8_t* hist, int observe
 
 // Device-resident lane pool: every live CoupState owns one lane of a
 // 2-player history env (segments of kSeg lanes, grown on demand); each State
-// op is one coup_slot_op launch on that lane, and only ops that need an
-// answer copy the 128-byte coup_slot_result back.
+// op is one coup_slot_op on that lane -- run by the pool's device-resident
+// op server (coup_server_create: one resident wave, no launch per op;
+// COUP_SERVER=0 in the environment keeps one launch per op) -- and only ops
+// that need an answer copy the 128-byte coup_slot_result back.
 class Pool {
  public:
   static constexpr int64_t kSeg = 4096;
@@ -231,10 +234,26 @@ class Pool {
     int64_t lane = 0;
   };
 
+  Pool() {
+    const char* e = std::getenv("COUP_SERVER");
+    if (!(e && std::atoi(e) == 0)) {
+      const char* idle = std::getenv("COUP_SERVER_IDLE_US");
+      if (coup_server_create(idle ? std::atoll(idle) : 20000, &srv_) != COUP_OK) srv_ = nullptr;
+    }
+  }
+  ~Pool() {
+    // the wave leaves before the segments it serves are freed
+    for (auto& env : segs_) (void)coup_attach_server(env->get(), nullptr);
+    if (srv_) (void)coup_server_destroy(srv_);
+  }
+  Pool(const Pool&) = delete;
+  Pool& operator=(const Pool&) = delete;
+
   Slot Alloc() {
     std::lock_guard<std::mutex> g(mu_);
     if (free_.empty()) {
       segs_.emplace_back(new BatchedEnv(kSeg, 0, 0, COUP_FLAG_HISTORY));
+      if (srv_) Check(coup_attach_server(segs_.back()->get(), srv_), "coup_attach_server");
       const int k = (int)segs_.size() - 1;
       for (int64_t i = kSeg - 1; i >= 0; --i) free_.push_back({k, i});
     }
@@ -267,6 +286,7 @@ class Pool {
   std::vector<std::unique_ptr<BatchedEnv>> segs_;
   std::vector<Slot> free_;
   std::mutex mu_;
+  coup_server* srv_ = nullptr;
 };
 
 inline Pool& ThePool() {
@@ -350,10 +370,25 @@ class CoupState {
     q_ = r;
     history_.push_back({p, a});
   }
+  // Clone + ApplyAction as ONE op: the child's lane is a copy of this one
+  // with `a` applied
   std::unique_ptr<CoupState> Child(Action a) const {
-    auto c = Clone();
-    c->ApplyAction(a);
-    return c;
+    const Player p = CurrentPlayer();
+    if (a < 0 || a >= COUP_NUM_ACTIONS || !((Q().legal_mask >> a) & 1u) || p == kTerminalPlayerId)
+      throw SpielError("Child: illegal action " + std::to_string(a));
+    detail::Pool& pool = detail::ThePool();
+    const detail::Pool::Slot slot = pool.Alloc();
+    coup_slot_result r;
+    try {
+      pool.Op(slot, &slot_, (int)a, 0, &r);
+      if (!r.ok) throw SpielError("Child: illegal action " + std::to_string(a));
+    } catch (...) {
+      pool.Release(slot);
+      throw;
+    }
+    std::vector<PlayerAction> h = history_;
+    h.push_back({p, a});
+    return std::unique_ptr<CoupState>(new CoupState(game_, slot, std::move(h), r));
   }
   std::unique_ptr<CoupState> Clone() const { return std::unique_ptr<CoupState>(new CoupState(*this)); }
   // Child(a) for every a in `actions`, one coup_slot_ops launch per pool

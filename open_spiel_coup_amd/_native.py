@@ -11,7 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # COUP_LIB_PATH: load another build of the same library (A/B timing of two
 # builds, tools/ab_builds.sh); there is still no fallback
 LIB_PATH = os.environ.get("COUP_LIB_PATH") or os.path.join(HERE, "libcoup_mi355x.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 FLAG_AUTO_RESET, FLAG_HISTORY, FLAG_GENERIC = 1, 2, 4
 MAX_PLAYERS = 6
 HISTORY_BYTES = 96
@@ -26,6 +26,7 @@ SYMBOLS = (
     "coup_new_initial_state", "coup_apply_action", "coup_query",
     "coup_export_state", "coup_import_state", "coup_export_history",
     "coup_import_history", "coup_error_count", "coup_slot_op", "coup_slot_ops", "coup_measure_step_traffic",
+    "coup_server_create", "coup_server_destroy", "coup_attach_server", "coup_server_stats",
 )
 
 # coup_slot_op flags and result layout (coup_slot_result, 128 bytes)
@@ -105,6 +106,10 @@ def load():
         "coup_slot_op": ([vp, i64, vp, i64, i32, i32, vp], i32),
         "coup_slot_ops": ([vp, i64, ctypes.POINTER(SlotReq), vp, i32, vp], i32),
         "coup_measure_step_traffic": ([i64, vp, ctypes.POINTER(StepOutputs), vp], i32),
+        "coup_server_create": ([i64, ctypes.POINTER(vp)], i32),
+        "coup_server_destroy": ([vp], i32),
+        "coup_attach_server": ([vp, vp], i32),
+        "coup_server_stats": ([vp, ctypes.POINTER(ctypes.c_uint64)], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

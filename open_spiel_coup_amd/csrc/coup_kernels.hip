@@ -1457,52 +1457,52 @@ __global__ __launch_bounds__(kThreads) void k_query(QueryArgs a) {
 // 1246 float4 of a lane are spread over 1246 threads; each thread decodes its
 // lane's record and history bytes itself (L2-resident).
 // reqs (coup_slot_ops): output row l is the lane of request l.
+// One InformationStateTensor float4 (element c of [2][2492] / 4) of the lane
+// whose record is L and whose history bytes are h; k_info_elems' decode.
+__device__ __forceinline__ float4 info_f4(const uint32_t* pre, const uint8_t* h, uint32_t c) {
+  const uint32_t p = c >= (uint32_t)kInfoHalfF4 ? 1u : 0u;
+  const int f0 = 4 * (int)(c - p * (uint32_t)kInfoHalfF4);
+  const uint32_t meta = pre[4];
+  const uint32_t len = meta >> 16;
+  if (f0 >= 62 + 18 * (int)len) return make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  const uint64_t prefix = (uint64_t)pre[2 * p] | ((uint64_t)pre[2 * p + 1] << 32);
+  const int t0 = f0 - 62;
+  const uint32_t r0 = t0 < 0 ? 0u : (uint32_t)t0 / 18u;
+  const int col0 = t0 - 18 * (int)r0;
+  uint32_t va[2];
+#pragma unroll
+  for (uint32_t k = 0; k < 2; ++k) {
+    const uint32_t r = r0 + k;
+    const uint32_t e = h[r < (uint32_t)kHist ? r : 0u];
+    const bool seen = (e & 0x20u) == 0u || ((e >> 6) & 1u) == p;  // deals: observer's only
+    va[k] = (r < len && seen) ? (e & 0x1Fu) : 31u;
+  }
+  float v[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int f = f0 + e;
+    const int col = col0 + e;
+    const uint32_t row_act = col >= 18 ? va[1] : va[0];
+    const float hv = (row_act == (uint32_t)(col >= 18 ? col - 18 : col)) ? 1.0f : 0.0f;
+    const float pb = (float)((uint32_t)(prefix >> (f & 63)) & 1u);
+    const float coin = (float)(f == 60 ? (meta & 0xFFu) : ((meta >> 8) & 0xFFu));
+    v[e] = f < 60 ? pb : (f < 62 ? coin : hv);
+  }
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+
 __global__ __launch_bounds__(kThreads) void k_info_elems(const uint4* __restrict__ state,
                                                         const uint8_t* __restrict__ hist, int64_t n,
                                                         float* __restrict__ info,
                                                         const coup_slot_req* __restrict__ reqs = nullptr) {
-  typedef float v4f __attribute__((ext_vector_type(4)));
   const int64_t g = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (g >= n * kInfoF4) return;
   const int64_t row = g / kInfoF4;
   const uint32_t c = (uint32_t)(g - row * kInfoF4);
   const int64_t lane = reqs ? reqs[row].lane : row;
-  const uint32_t p = c >= (uint32_t)kInfoHalfF4 ? 1u : 0u;
-  const int f0 = 4 * (int)(c - p * (uint32_t)kInfoHalfF4);
-  const Lane L = unpack(state[lane]);
   uint32_t pre[kPreWords];
-  info_prefix_to_lds(L, pre);
-  const uint32_t meta = pre[4];
-  const uint32_t len = meta >> 16;
-  v4f w = {0.0f, 0.0f, 0.0f, 0.0f};
-  if (f0 < 62 + 18 * (int)len) {
-    const uint64_t prefix = (uint64_t)pre[2 * p] | ((uint64_t)pre[2 * p + 1] << 32);
-    const int t0 = f0 - 62;
-    const uint32_t r0 = t0 < 0 ? 0u : (uint32_t)t0 / 18u;
-    const int col0 = t0 - 18 * (int)r0;
-    const uint8_t* h = hist + lane * kHist;
-    uint32_t va[2];
-#pragma unroll
-    for (uint32_t k = 0; k < 2; ++k) {
-      const uint32_t r = r0 + k;
-      const uint32_t e = h[r < (uint32_t)kHist ? r : 0u];
-      const bool seen = (e & 0x20u) == 0u || ((e >> 6) & 1u) == p;  // deals: observer's only
-      va[k] = (r < len && seen) ? (e & 0x1Fu) : 31u;
-    }
-    float v[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int f = f0 + e;
-      const int col = col0 + e;
-      const uint32_t row_act = col >= 18 ? va[1] : va[0];
-      const float hv = (row_act == (uint32_t)(col >= 18 ? col - 18 : col)) ? 1.0f : 0.0f;
-      const float pb = (float)((uint32_t)(prefix >> (f & 63)) & 1u);
-      const float coin = (float)(f == 60 ? (meta & 0xFFu) : ((meta >> 8) & 0xFFu));
-      v[e] = f < 60 ? pb : (f < 62 ? coin : hv);
-    }
-    w = v4f{v[0], v[1], v[2], v[3]};
-  }
-  reinterpret_cast<v4f*>(info)[g] = w;
+  info_prefix_to_lds(unpack(state[lane]), pre);
+  reinterpret_cast<float4*>(info)[g] = info_f4(pre, hist + lane * kHist, c);
 }
 
 // Batches up to this size take k_info_elems for the InformationStateTensor
@@ -1678,6 +1678,113 @@ __global__ __launch_bounds__(64) void k_slot_batch(SlotBatchArgs b) {
     if (threadIdx.x == 0u) __hip_atomic_store(b.done + blockIdx.x, b.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
+
+// ------------------------------------------------- device-resident op server
+// coup_server: ONE resident wave serves the per-game
+// State ops of the envs attached to it, so an answered op costs a host write
+// the wave sees, the op itself and a device->host write -- no kernel launch,
+// no queue.  Requests sit in a ring of kSrvRing 128-byte slots in mapped,
+// coherent pinned host memory; the host fills a slot and then stores its
+// sequence number.  The wave polls the next slot's number (one relaxed
+// system-scope load per pass, s_sleep between passes), takes ONE acquire
+// when it matches (this CU's L1 dropped: the lanes may have been written by
+// kernels on other XCDs, whose completion released them), runs slot_op on
+// the request's lane, stores its result / tensors into host memory, drains
+// its stores, releases at system scope and publishes the number in
+// ctl.served.  Requests are served in order.  Exit: when the host stores the
+// wave's epoch in ctl.stop (after the pending requests), or after idle_ticks
+// (s_memrealtime, 100 MHz) with no request -- a host that stops calling, or
+// dies, never leaves a spinning wave; the next op relaunches it.
+constexpr uint32_t kSrvRing = 64;
+
+struct SrvReq {       // one ring slot (host memory), 128 bytes
+  uint64_t dst_state;  // uint4*  (device)
+  uint64_t dst_hist;   // uint8_t* (device)
+  uint64_t src_state;  // 0: no copy
+  uint64_t src_hist;
+  uint64_t out;        // coup_slot_result* (mapped host) or 0: no result
+  uint64_t obs;        // [2][98] floats (mapped host) or 0
+  uint64_t info;       // [2][2492] floats (mapped host) or 0
+  int32_t action;      // < 0: none
+  int32_t init;
+  uint32_t seq;        // stored last by the host
+  uint32_t pad[15];
+};
+static_assert(sizeof(SrvReq) == 128, "SrvReq layout");
+
+struct SrvCtl {        // host memory, one word per 128-byte line
+  uint32_t served;     // last sequence number served (the wave writes)
+  uint32_t pad0[31];
+  uint32_t stop;       // the host writes the epoch of the wave to stop
+  uint32_t pad1[31];
+};
+
+struct ServerArgs {
+  SrvReq* ring;        // device addresses of the mapped host memory
+  SrvCtl* ctl;
+  uint32_t first;      // sequence number of the first request to serve
+  uint32_t epoch;      // this launch's epoch (never 0)
+  uint64_t idle_ticks; // exit after this many 100 MHz ticks without a request
+};
+
+template <class T>
+__device__ __forceinline__ T srv_ld(const T* p) {  // host-written word: vector load, system scope
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(64) void k_server(ServerArgs s) {
+  __shared__ __attribute__((aligned(16))) uint8_t hist[kHist];
+  __shared__ __attribute__((aligned(16))) uint32_t bits[64 * 8];
+  __shared__ __attribute__((aligned(16))) uint32_t pre[kPreWords];
+  const uint32_t t = threadIdx.x;
+  uint32_t next = s.first;
+  uint64_t idle0 = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    SrvReq* q = s.ring + (next & (kSrvRing - 1u));
+    const uint32_t seq = (uint32_t)__builtin_amdgcn_readfirstlane((int)srv_ld(&q->seq));
+    if (seq != next) {
+      if ((uint32_t)__builtin_amdgcn_readfirstlane((int)srv_ld(&s.ctl->stop)) == s.epoch) break;
+      if (__builtin_amdgcn_s_memrealtime() - idle0 > s.idle_ticks) break;
+      __builtin_amdgcn_s_sleep(2);
+      continue;
+    }
+    // ONE acquire after the match: later loads of the request, the lanes and
+    // their histories are not served from this CU's stale L1 lines
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    SlotArgs a;
+    a.dst_state = reinterpret_cast<uint4*>(srv_ld(&q->dst_state));
+    a.dst_hist = reinterpret_cast<uint8_t*>(srv_ld(&q->dst_hist));
+    const uint64_t src = srv_ld(&q->src_state);
+    a.src_state = src ? reinterpret_cast<const uint4*>(src) : nullptr;
+    a.src_hist = src ? reinterpret_cast<const uint8_t*>(srv_ld(&q->src_hist)) : nullptr;
+    a.action = srv_ld(&q->action);
+    a.init = srv_ld(&q->init);
+    a.store = (src || a.init || a.action >= 0) ? 1 : 0;
+    a.out = reinterpret_cast<coup_slot_result*>(srv_ld(&q->out));
+    a.obs = reinterpret_cast<float*>(srv_ld(&q->obs));
+    float* info = reinterpret_cast<float*>(srv_ld(&q->info));
+    if (a.obs)
+      slot_op<true>(a, hist, bits);
+    else
+      slot_op<false>(a, hist, bits);
+    if (info) {
+      // the InformationStateTensor from the lane's new record (thread 0's
+      // store, re-read after the wave barrier) and its history bytes in LDS
+      wave_sync();
+      if (t == 0u) info_prefix_to_lds(unpack(*a.dst_state), pre);
+      wave_sync();
+      for (uint32_t c = t; c < (uint32_t)kInfoF4; c += 64u) reinterpret_cast<float4*>(info)[c] = info_f4(pre, hist, c);
+    }
+    // every thread's stores (lane, history, result, tensors) drained, then
+    // ONE system-scope release, then the number the host polls
+    __builtin_amdgcn_s_waitcnt(0);
+    wave_sync();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    if (t == 0u) __hip_atomic_store(&s.ctl->served, next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    next += 1u;
+    idle0 = __builtin_amdgcn_s_memrealtime();
+  }
+}
 }  // namespace coup
 
 // ====================================================================== C ABI
@@ -1712,6 +1819,26 @@ struct coup_env {
   uint8_t* host_stage;        // coup_step_host with info_state: device staging of the outputs (grown on demand)
   size_t host_stage_cap;
   bool batch_pending;         // an asynchronous coup_slot_ops may still read the requests
+  coup_server* server;        // coup_attach_server: coup_slot_op goes through this resident wave
+  bool dirty;                 // work enqueued on `stream` since its last synchronisation
+};
+
+// coup_server (coup_mi355x.h; kernel coup::k_server).  The ring, the control
+// words and the result area live in one mapped, coherent pinned host block.
+struct coup_server {
+  hipStream_t stream = nullptr;   // its own non-blocking stream: the wave never holds up other work
+  uint8_t* host = nullptr;        // ring [kSrvRing] | ctl | result (coup_slot_result + obs + info)
+  uint8_t* host_dev = nullptr;
+  coup::SrvReq* ring = nullptr;   // host views
+  coup::SrvCtl* ctl = nullptr;
+  uint8_t* result = nullptr;
+  uint8_t* result_dev = nullptr;
+  uint32_t posted = 0;            // last sequence number posted
+  uint32_t epoch = 0;             // epoch of the last launch
+  bool running = false;           // a wave was launched and may still be serving
+  uint64_t idle_us = 20000;
+  std::chrono::steady_clock::time_point last_post;
+  uint64_t requests = 0, launches = 0;
 };
 
 namespace {
@@ -1786,8 +1913,11 @@ int np_result(hipError_t e, const char* what) {
   return COUP_OK;
 }
 
+int launching(coup_env* env);
+
 int launch_reset(coup_env* env, const uint8_t* mask, int mode, int deal) {
   if (env->batch == 0) return COUP_OK;
+  COUP_TRY(launching(env));
   if (env->generic) return np_result(coup::np::launch_reset(np_env(env), mask, mode, deal), "reset");
   coup::k_reset<<<grid_for(env->batch), coup::kThreads, 0, env->stream>>>(
       env->state, env->batch, mask, mode, deal, (uint32_t)env->seed, (uint32_t)(env->seed >> 32), env->env_id_base,
@@ -1797,6 +1927,110 @@ int launch_reset(coup_env* env, const uint8_t* mask, int mode, int deal) {
 }
 
 size_t align16(size_t n) { return (n + 15u) & ~size_t(15); }
+
+// ---- coup_server host side
+constexpr size_t kSrvCtlOff = coup::kSrvRing * sizeof(coup::SrvReq);
+constexpr size_t kSrvResultOff = kSrvCtlOff + sizeof(coup::SrvCtl);
+constexpr size_t kSrvBytes = kSrvResultOff + sizeof(coup_slot_result) + 2u * COUP_OBS_SIZE * sizeof(float) +
+                             2u * COUP_INFO_STATE_SIZE * sizeof(float);
+
+uint32_t srv_served(const coup_server* s) { return __atomic_load_n(&s->ctl->served, __ATOMIC_ACQUIRE); }
+
+// (Re)launch the resident wave, serving from the first unserved request.
+int srv_launch(coup_server* s) {
+  coup::ServerArgs a;
+  a.ring = reinterpret_cast<coup::SrvReq*>(s->host_dev);
+  a.ctl = reinterpret_cast<coup::SrvCtl*>(s->host_dev + kSrvCtlOff);
+  a.first = srv_served(s) + 1u;
+  s->epoch = s->epoch + 1u == 0u ? 1u : s->epoch + 1u;
+  a.epoch = s->epoch;
+  a.idle_ticks = s->idle_us * 100u;  // s_memrealtime: 100 MHz
+  coup::k_server<<<1, 64, 0, s->stream>>>(a);
+  COUP_HIP_TRY(hipGetLastError());
+  s->running = true;
+  s->launches += 1u;
+  return COUP_OK;
+}
+
+// Stop the wave after the requests already posted (it serves them first)
+// and wait for it to leave.
+int srv_stop(coup_server* s) {
+  if (!s->running) return COUP_OK;
+  __atomic_store_n(&s->ctl->stop, s->epoch, __ATOMIC_RELEASE);
+  s->running = false;
+  COUP_HIP_TRY(hipStreamSynchronize(s->stream));
+  return COUP_OK;
+}
+
+// Wait until request `seq` has been served.  A wave that left (idle timeout
+// racing a post, or an error) is found by querying its stream every ~50 us of
+// waiting; the pending requests are still in the ring, so a relaunch from
+// the first unserved one completes them.
+int srv_wait(coup_server* s, uint32_t seq) {
+  auto t0 = std::chrono::steady_clock::now(), tq = t0;
+  for (uint32_t k = 1; (int32_t)(srv_served(s) - seq) < 0; ++k) {
+    __builtin_ia32_pause();
+    if ((k & 255u) != 0u) continue;
+    const auto now = std::chrono::steady_clock::now();
+    if (now - tq < std::chrono::microseconds(50)) continue;
+    tq = now;
+    const hipError_t q = hipStreamQuery(s->stream);
+    if (q == hipSuccess) {  // no wave: serve the rest with a new one
+      if ((int32_t)(srv_served(s) - seq) >= 0) break;
+      COUP_TRY(srv_launch(s));
+      t0 = now;
+    } else if (q != hipErrorNotReady) {
+      return fail(COUP_E_HIP, std::string("coup_server: ") + hipGetErrorString(q));
+    } else if (now - t0 > std::chrono::seconds(10)) {
+      return fail(COUP_E_HIP, "coup_server: a request was not served within 10 s");
+    }
+  }
+  return COUP_OK;
+}
+
+// Before work on `env` that does not go through its server: the server's
+// pending requests (they may write env's lanes) are served first.
+int srv_drain(const coup_env* env) {
+  if (!env || !env->server) return COUP_OK;
+  coup_server* s = env->server;
+  if (s->running && s->posted != srv_served(s)) COUP_TRY(srv_wait(s, s->posted));
+  return COUP_OK;
+}
+
+// Every entry point that enqueues work on an env's stream calls this first.
+int launching(coup_env* env) {
+  COUP_TRY(srv_drain(env));
+  env->dirty = true;
+  return COUP_OK;
+}
+
+// Post one request (a filled SrvReq without its number) and return its number.
+int srv_post(coup_server* s, const coup::SrvReq& r, uint32_t* seq_out) {
+  const auto now = std::chrono::steady_clock::now();
+  if (s->posted >= 0xFFFFFF00u) {
+    // the numbers would wrap: drain, stop, restart the count
+    COUP_TRY(srv_wait(s, s->posted));
+    COUP_TRY(srv_stop(s));
+    for (uint32_t k = 0; k < coup::kSrvRing; ++k) s->ring[k].seq = 0u;
+    __atomic_store_n(&s->ctl->served, 0u, __ATOMIC_RELEASE);
+    s->posted = 0u;
+  }
+  // The wave leaves after idle_us without a request.  A post within idle_us
+  // / 2 of the last one is seen long before that; otherwise the wave may be
+  // leaving: stop it for sure and start a new one (cheap next to the idle time).
+  if (s->running && now - s->last_post > std::chrono::microseconds(s->idle_us / 2u)) COUP_TRY(srv_stop(s));
+  if (!s->running) COUP_TRY(srv_launch(s));
+  const uint32_t seq = s->posted + 1u;
+  if (seq - srv_served(s) >= coup::kSrvRing) COUP_TRY(srv_wait(s, seq - coup::kSrvRing));  // ring full
+  coup::SrvReq* q = s->ring + (seq & (coup::kSrvRing - 1u));
+  std::memcpy(q, &r, offsetof(coup::SrvReq, seq));  // every field but the number, which goes last
+  __atomic_store_n(&q->seq, seq, __ATOMIC_RELEASE);  // after every field (x86: stores in order)
+  s->posted = seq;
+  s->last_post = now;
+  s->requests += 1u;
+  *seq_out = seq;
+  return COUP_OK;
+}
 
 }  // namespace
 
@@ -1883,6 +2117,8 @@ int coup_create_ex(int64_t batch, uint64_t seed, uint32_t env_id_base, int flags
   env->host_cap = 0;
   env->host_stage = nullptr;
   env->host_stage_cap = 0;
+  env->server = nullptr;
+  env->dirty = false;
   const size_t lanes = (size_t)(batch > 0 ? batch : 1);
   hipError_t e = hipMalloc(&env->state, lanes * sizeof(uint4) * (generic ? 2 : 1));
   if (e == hipSuccess) e = hipMalloc(&env->err_count, sizeof(uint32_t));
@@ -1910,6 +2146,7 @@ int coup_create_ex(int64_t batch, uint64_t seed, uint32_t env_id_base, int flags
 
 int coup_destroy(coup_env* env) {
   COUP_CHECK_ENV(env);
+  (void)srv_drain(env);
   hipError_t e1 = hipStreamSynchronize(env->stream);
   release(env);
   if (e1 != hipSuccess) return fail(COUP_E_HIP, "coup_destroy: HIP error while releasing the env");
@@ -1953,6 +2190,7 @@ uint64_t* coup_debug_get_trace() { return g_trace; }
 int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out) {
   COUP_CHECK_ENV(env);
   if (env->batch == 0) return COUP_OK;
+  COUP_TRY(launching(env));
   if (env->generic) {
     if (out && out->info_state) return fail(COUP_E_INVALID, "coup_step: info_state is 2-player only");
     return np_result(coup::np::launch_step(np_env(env), actions, out), "coup_step");
@@ -2058,6 +2296,7 @@ int coup_rollout(coup_env* env, int64_t steps, const coup_rollout_stats* stats) 
   if (steps < 0) return fail(COUP_E_INVALID, "coup_rollout: negative steps");
   if (env->hist) return fail(COUP_E_INVALID, "coup_rollout: not available on an env with COUP_FLAG_HISTORY");
   if (env->batch == 0 || steps == 0) return COUP_OK;
+  COUP_TRY(launching(env));
   if (env->generic) return np_result(coup::np::launch_rollout(np_env(env), steps, stats), "coup_rollout");
   coup::RolloutArgs a;
   std::memset(&a, 0, sizeof(a));
@@ -2145,6 +2384,7 @@ int coup_step_host(coup_env* env, const int8_t* actions, int want, void* host_ou
     COUP_HIP_TRY(hipMemcpyAsync(env->host_scratch + in_bytes, env->host_stage, total, hipMemcpyDeviceToHost,
                                 env->stream));
   COUP_HIP_TRY(hipStreamSynchronize(env->stream));
+  env->dirty = false;
   std::memcpy(host_out, env->host_scratch + in_bytes, total);
   return COUP_OK;
 }
@@ -2160,6 +2400,7 @@ int coup_step_trajectory(coup_env* env, int64_t steps, const coup_step_outputs* 
   if (out && (out->episodes == nullptr) != (out->return_sum == nullptr))
     return fail(COUP_E_INVALID, "coup_step_trajectory: episodes and return_sum go together");
   if (env->batch == 0 || steps == 0) return COUP_OK;
+  COUP_TRY(launching(env));
   if (env->generic) return np_result(coup::np::launch_trajectory(np_env(env), steps, out), "coup_step_trajectory");
   coup::StepArgs a;
   std::memset(&a, 0, sizeof(a));
@@ -2199,6 +2440,7 @@ int coup_apply_action(coup_env* env, const int8_t* actions) {
   COUP_CHECK_ENV(env);
   if (!actions) return fail(COUP_E_INVALID, "coup_apply_action: actions is null");
   if (env->batch == 0) return COUP_OK;
+  COUP_TRY(launching(env));
   if (env->generic) return np_result(coup::np::launch_apply(np_env(env), actions), "coup_apply_action");
   coup::k_apply<<<grid_for(env->batch), coup::kThreads, 0, env->stream>>>(env->state, env->batch, actions,
                                                                           env->hist, env->err_count);
@@ -2212,6 +2454,7 @@ int coup_query(coup_env* env, const coup_query_outputs* out) {
   if (out->info_state && !env->hist)
     return fail(COUP_E_INVALID, "coup_query: info_state needs an env created with COUP_FLAG_HISTORY");
   if (env->batch == 0) return COUP_OK;
+  COUP_TRY(launching(env));
   if (env->generic) return np_result(coup::np::launch_query(np_env(env), out), "coup_query");
   coup::QueryArgs a;
   a.state = env->state;
@@ -2292,6 +2535,42 @@ int coup_slot_op(coup_env* env, int64_t lane, const coup_env* src_env, int64_t s
   if (result && !host_out) return fail(COUP_E_INVALID, "coup_slot_op: host_out is null");
   const bool obs = result && (flags & COUP_SLOT_OBS), info = result && (flags & COUP_SLOT_INFO);
   const size_t obs_bytes = 2u * COUP_OBS_SIZE * sizeof(float), info_bytes = 2u * COUP_INFO_STATE_SIZE * sizeof(float);
+  if (env->server && (!src_env || src_env->server == env->server)) {
+    // the resident wave: no launch.  Stream work still in flight on either
+    // env may write the lanes it reads -- wait for it first.
+    coup_server* sv = env->server;
+    if (env->dirty) {
+      COUP_HIP_TRY(hipStreamSynchronize(env->stream));
+      env->dirty = false;
+    }
+    if (src_env && src_env != env && src_env->dirty) {
+      COUP_HIP_TRY(hipStreamSynchronize(src_env->stream));
+      const_cast<coup_env*>(src_env)->dirty = false;
+    }
+    coup::SrvReq r;
+    std::memset(&r, 0, sizeof(r));
+    r.dst_state = reinterpret_cast<uint64_t>(env->state + lane);
+    r.dst_hist = reinterpret_cast<uint64_t>(env->hist + lane * COUP_HISTORY_BYTES);
+    if (src_env) {
+      r.src_state = reinterpret_cast<uint64_t>(src_env->state + src_lane);
+      r.src_hist = reinterpret_cast<uint64_t>(src_env->hist + src_lane * COUP_HISTORY_BYTES);
+    }
+    r.action = action;
+    r.init = (flags & COUP_SLOT_INIT) ? 1 : 0;
+    if (result) {
+      r.out = reinterpret_cast<uint64_t>(sv->result_dev);
+      if (obs) r.obs = reinterpret_cast<uint64_t>(sv->result_dev + sizeof(coup_slot_result));
+      if (info) r.info = reinterpret_cast<uint64_t>(sv->result_dev + sizeof(coup_slot_result) + (obs ? obs_bytes : 0));
+    }
+    uint32_t seq = 0;
+    COUP_TRY(srv_post(sv, r, &seq));
+    if (!result) return COUP_OK;
+    COUP_TRY(srv_wait(sv, seq));
+    std::memcpy(host_out, sv->result, sizeof(coup_slot_result) + (obs ? obs_bytes : 0) + (info ? info_bytes : 0));
+    return COUP_OK;
+  }
+  COUP_TRY(launching(env));
+  COUP_TRY(srv_drain(src_env));
   if (result && !env->slot_scratch) {
     // the kernels store the result straight into pinned host memory over
     // PCIe: no copy kernel before the synchronisation
@@ -2343,6 +2622,7 @@ int coup_slot_op(coup_env* env, int64_t lane, const coup_env* src_env, int64_t s
   } else {
     COUP_HIP_TRY(hipStreamSynchronize(s));
   }
+  env->dirty = false;  // the op's stores are visible (flag after a system-scope fence, or the synchronisation)
   std::memcpy(host_out, env->slot_scratch, n);
   return COUP_OK;
 }
@@ -2397,6 +2677,8 @@ int coup_slot_ops(coup_env* env, int64_t n, const coup_slot_req* reqs, const cou
     COUP_HIP_TRY(hipStreamSynchronize(env->stream));
     env->batch_pending = false;
   }
+  COUP_TRY(launching(env));
+  COUP_TRY(srv_drain(src_env));
   if (flag_off + flag_bytes > env->batch_cap) {
     if (env->batch_scratch) (void)hipHostFree(env->batch_scratch);
     env->batch_scratch = nullptr;
@@ -2454,13 +2736,70 @@ int coup_slot_ops(coup_env* env, int64_t n, const coup_slot_req* reqs, const cou
   } else {
     COUP_HIP_TRY(hipStreamSynchronize(s));
   }
+  env->dirty = false;
   std::memcpy(host_out, env->batch_scratch + req_bytes, out_bytes);
+  return COUP_OK;
+}
+
+int coup_server_create(int64_t idle_us, coup_server** out) {
+  if (!out) return fail(COUP_E_INVALID, "coup_server_create: out is null");
+  *out = nullptr;
+  if (idle_us < 100 || idle_us > 10000000) return fail(COUP_E_INVALID, "coup_server_create: idle_us must be 100..1e7");
+  coup_server* s = new coup_server();
+  s->idle_us = (uint64_t)idle_us;
+  hipError_t e = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+  if (e == hipSuccess)
+    e = hipHostMalloc(reinterpret_cast<void**>(&s->host), kSrvBytes, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&s->host_dev), s->host, 0);
+  if (e != hipSuccess) {
+    if (s->host) (void)hipHostFree(s->host);
+    if (s->stream) (void)hipStreamDestroy(s->stream);
+    delete s;
+    return fail(COUP_E_HIP, std::string("coup_server_create: ") + hipGetErrorString(e));
+  }
+  std::memset(s->host, 0, kSrvBytes);  // every slot number 0 (never a request's), served 0, stop 0
+  s->ring = reinterpret_cast<coup::SrvReq*>(s->host);
+  s->ctl = reinterpret_cast<coup::SrvCtl*>(s->host + kSrvCtlOff);
+  s->result = s->host + kSrvResultOff;
+  s->result_dev = s->host_dev + kSrvResultOff;
+  s->last_post = std::chrono::steady_clock::now();
+  *out = s;
+  return COUP_OK;
+}
+
+int coup_server_destroy(coup_server* s) {
+  if (!s) return fail(COUP_E_INVALID, "null coup_server");
+  int rc = COUP_OK;
+  if (s->running && s->posted != srv_served(s)) rc = srv_wait(s, s->posted);
+  const int rc2 = srv_stop(s);
+  (void)hipStreamDestroy(s->stream);
+  (void)hipHostFree(s->host);
+  delete s;
+  return rc != COUP_OK ? rc : rc2;
+}
+
+int coup_server_stats(const coup_server* s, uint64_t* out) {
+  if (!s || !out) return fail(COUP_E_INVALID, "coup_server_stats: null argument");
+  out[0] = s->requests;
+  out[1] = s->launches;
+  out[2] = s->running ? 1u : 0u;
+  out[3] = s->idle_us;
+  return COUP_OK;
+}
+
+int coup_attach_server(coup_env* env, coup_server* srv) {
+  COUP_CHECK_ENV(env);
+  if (srv && (env->generic || !env->hist))
+    return fail(COUP_E_INVALID, "coup_attach_server: needs a 2-player env created with COUP_FLAG_HISTORY");
+  COUP_TRY(srv_drain(env));  // the old server's requests on env are done
+  env->server = srv;
   return COUP_OK;
 }
 
 int coup_export_state(coup_env* env, uint32_t* dst) {
   COUP_CHECK_ENV(env);
   if (!dst) return fail(COUP_E_INVALID, "coup_export_state: dst is null");
+  COUP_TRY(launching(env));
   if (env->generic) return np_result(coup::np::launch_export(np_env(env), dst), "coup_export_state");
   COUP_HIP_TRY(hipMemcpyAsync(dst, env->state, (size_t)env->batch * sizeof(uint4), hipMemcpyDeviceToDevice,
                               env->stream));
@@ -2470,6 +2809,7 @@ int coup_export_state(coup_env* env, uint32_t* dst) {
 int coup_import_state(coup_env* env, const uint32_t* src) {
   COUP_CHECK_ENV(env);
   if (!src) return fail(COUP_E_INVALID, "coup_import_state: src is null");
+  COUP_TRY(launching(env));
   if (env->generic) return np_result(coup::np::launch_import(np_env(env), src), "coup_import_state");
   COUP_HIP_TRY(hipMemcpyAsync(env->state, src, (size_t)env->batch * sizeof(uint4), hipMemcpyDeviceToDevice,
                               env->stream));
@@ -2480,6 +2820,7 @@ int coup_export_history(coup_env* env, uint8_t* dst) {
   COUP_CHECK_ENV(env);
   if (!dst) return fail(COUP_E_INVALID, "coup_export_history: dst is null");
   if (!env->hist) return fail(COUP_E_INVALID, "coup_export_history: env has no history (COUP_FLAG_HISTORY)");
+  COUP_TRY(launching(env));
   COUP_HIP_TRY(hipMemcpyAsync(dst, env->hist, (size_t)env->batch * COUP_HISTORY_BYTES, hipMemcpyDeviceToDevice,
                               env->stream));
   return COUP_OK;
@@ -2489,6 +2830,7 @@ int coup_import_history(coup_env* env, const uint8_t* src) {
   COUP_CHECK_ENV(env);
   if (!src) return fail(COUP_E_INVALID, "coup_import_history: src is null");
   if (!env->hist) return fail(COUP_E_INVALID, "coup_import_history: env has no history (COUP_FLAG_HISTORY)");
+  COUP_TRY(launching(env));
   COUP_HIP_TRY(hipMemcpyAsync(env->hist, src, (size_t)env->batch * COUP_HISTORY_BYTES, hipMemcpyDeviceToDevice,
                               env->stream));
   return COUP_OK;
@@ -2497,10 +2839,12 @@ int coup_import_history(coup_env* env, const uint8_t* src) {
 int coup_error_count(coup_env* env, int64_t* out) {
   COUP_CHECK_ENV(env);
   if (!out) return fail(COUP_E_INVALID, "coup_error_count: out is null");
+  COUP_TRY(launching(env));
   uint32_t h = 0;
   COUP_HIP_TRY(hipMemcpyAsync(&h, env->err_count, sizeof(uint32_t), hipMemcpyDeviceToHost, env->stream));
   COUP_HIP_TRY(hipMemsetAsync(env->err_count, 0, sizeof(uint32_t), env->stream));
   COUP_HIP_TRY(hipStreamSynchronize(env->stream));
+  env->dirty = false;
   *out = (int64_t)h;
   return COUP_OK;
 }

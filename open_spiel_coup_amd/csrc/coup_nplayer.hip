@@ -205,7 +205,33 @@ __device__ __forceinline__ uint32_t ahead_key(const NLane<N>& L, uint32_t x) {
 #endif
 }
 
-template <int N, bool UNIFORM, bool AHEAD, int T = kThreads>
+// kKeyEnding: a LoseCard that costs its player the last face-down card while
+// two seats are alive -- the decision that ends the game.  Drawn ahead
+// (step_key), such lanes sort into the same wave(s) of the block, and with
+// INLINE the wave that ends their games deals their next episodes at once
+// (below), which removes the block's reset phase and its barrier.  Any other
+// way a game ends (a lost assassination challenge's double flip, truncation)
+// resets inline too, in whatever wave holds the lane.  The decision is the
+// one LoseCard the hand allows (only slots 0 and 1 are offered, coup.cc:
+// 811-822, and exactly one face-down card is left).
+constexpr uint32_t kKeyEnding = 27u;
+
+template <int N>
+__device__ __forceinline__ uint32_t step_key(const NLane<N>& L, uint32_t x) {
+  if ((x == kLoseCard1 || x == kLoseCard2) && __popc(~hand(L, L.M) & 0x1111u) == 1u && __popc(alive_mask(L)) == 2)
+    return kKeyEnding;
+  return ahead_key(L, x);
+}
+
+template <int N>
+__device__ __forceinline__ uint32_t ending_action(const NLane<N>& L) {
+  return (nib(hand(L, L.M), 0) & 1u) ? (uint32_t)kLoseCard2 : (uint32_t)kLoseCard1;
+}
+
+// INLINE = false: the round-2 schedule, the block's auto-resets dealt after
+// phase 2 by its first threads behind one more barrier (A/B:
+// COUP_NP_RESET_INLINE=0).
+template <int N, bool UNIFORM, bool AHEAD, int T = kThreads, bool INLINE = true>
 #ifdef COUP_WAVE_TRACE
 // the stamps' registers must not cost the traced kernel its 8 blocks per CU
 #define NP_STEP_SORTED_BOUNDS __launch_bounds__(T, 8)
@@ -296,7 +322,7 @@ __global__ NP_STEP_SORTED_BOUNDS void k_step_sorted(StepArgs a) {
       bool pending = false, decision_node = false;
       NRng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, base + (m & (T - 1u))), 0u, make_uint4(0, 0, 0, 0)};
       if (k != kStepDone) {
-        const uint32_t x = key_action(k);
+        const uint32_t x = k == kKeyEnding ? ending_action(L) : key_action(k);
         const uint32_t err_before = L.err;
         apply_decision(L, x);
         L.move += 1u;
@@ -308,6 +334,13 @@ __global__ NP_STEP_SORTED_BOUNDS void k_step_sorted(StepArgs a) {
         if (a.ep_count && term) out |= (uint32_t)(returns(L, 0u) + 16) << 14;
         pending = term && a.auto_reset != 0;
         decision_node = !term;  // resolve_chance leaves a live lane at a decision node
+        if (INLINE && pending) {
+          // SyncVectorEnv's reset (vector_env.py:62-65) where the game ended;
+          // a new episode is at a decision node
+          L = new_episode<N>(L.episode + 1u, rng);
+          pending = false;
+          decision_node = true;
+        }
         if (pending) s_reset[atomicAdd(&s_nreset, 1u)] = t;
         uint4 wa, wb;
         pack(L, wa, wb);
@@ -322,8 +355,10 @@ __global__ NP_STEP_SORTED_BOUNDS void k_step_sorted(StepArgs a) {
         legal = decision_node ? decision_mask(L) : legal_mask(L);
         const int cp = decision_node ? (int)L.M : current_player(L);
         out |= ((uint32_t)cp & 0xFFu) << 24;
-        if (UNIFORM && AHEAD && k != kStepDone && cp >= 0)
-          s_b[t].w |= (ahead_key(L, sample_action(legal, rng.draw(L.episode, L.move))) + 1u) << kAheadShift;
+        if (UNIFORM && AHEAD && k != kStepDone && cp >= 0) {
+          const uint32_t x = sample_action(legal, rng.draw(L.episode, L.move));
+          s_b[t].w |= ((INLINE ? step_key(L, x) : ahead_key(L, x)) + 1u) << kAheadShift;
+        }
       }
       s_out[t] = out;
       s_legal[t] = legal;
@@ -334,7 +369,7 @@ __global__ NP_STEP_SORTED_BOUNDS void k_step_sorted(StepArgs a) {
   NP_TRACE(a, 5);
 
   // the auto-resets, packed onto the first threads
-  const uint32_t nreset = s_nreset;
+  const uint32_t nreset = INLINE ? 0u : s_nreset;
   for (uint32_t j = t; j < nreset; j += T) {
     const uint32_t slot = s_reset[j];
     NRng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, base + (s_meta[slot] & (T - 1u))), 0u,
@@ -350,7 +385,7 @@ __global__ NP_STEP_SORTED_BOUNDS void k_step_sorted(StepArgs a) {
     if (UNIFORM && AHEAD) s_b[slot].w |= (ahead_key(R, sample_action(legal, rng.draw(R.episode, R.move))) + 1u) << kAheadShift;
   }
   NP_TRACE(a, 6);
-  __syncthreads();
+  if (!INLINE) __syncthreads();
   NP_TRACE(a, 7);
 
   // phase 3: each thread stores its own lane
@@ -576,13 +611,37 @@ __global__ __launch_bounds__(T, 8) void k_rollout_sorted(RolloutArgs a) {
 // outputs, then decides (the resets of a block sort into one wave instead
 // of diverging every wave).  Results equal coup_step's, step for step.
 
-template <int N, int T = kThreads>
+// Step outputs staged in LDS by lane (s_out / s_olegal): the thread that
+// plays a lane in regrouped order records them, and the lane's home thread
+// stores them at the start of the next step -- behind that step's first
+// barrier, which every trajectory step has anyway -- so each output of a
+// step goes out as one coalesced store per wave instead of bytes scattered
+// over the block's range (PMC WRITE was 1.8x the 13 B per
+// lane-step).  s_out: act + 1 [4:0] | step type [6:5] | reward loser [9:7] |
+// reward count [12:10] | legal mask and player staged [13] | player [23:16].
+constexpr uint32_t kOutLegal = 1u << 13;
+
+__device__ __forceinline__ uint32_t stage_head(int act, uint32_t st, uint32_t rl, uint32_t rc) {
+  return (uint32_t)(act + 1) | (st << 5) | (rl << 7) | (rc << 10);
+}
+__device__ __forceinline__ uint32_t stage_player(int cp) { return kOutLegal | (((uint32_t)cp & 0xFFu) << 16); }
+
+template <int N>
+__device__ __forceinline__ void store_staged(const StepArgs& a, int64_t o, uint32_t w, uint32_t legal) {
+  store_step_head<N>(a, o, (int)(w & 31u) - 1, (w >> 5) & 3u, (w >> 7) & 7u, (w >> 10) & 7u);
+  if (w & kOutLegal) store_legal_player(a, o, legal, (int)(int8_t)(w >> 16));
+}
+
+// STAGE = false: the round-2 form, each output stored by the thread that
+// plays the lane (A/B: COUP_TRAJ_STAGE=0).
+template <int N, int T = kThreads, bool STAGE = true>
 __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t steps) {
   static_assert((T & (T - 1)) == 0 && T >= 64 && T <= 1024, "power-of-two block of whole waves");
   constexpr uint32_t kO = T <= 256 ? 8u : 10u;  // lane bits of s_meta
   __shared__ uint4 s_a[T], s_b[T];
   __shared__ uint32_t s_meta[T];            // slot -> lane | key << kO
   __shared__ int32_t s_eps[T], s_ret[T];    // by lane
+  __shared__ uint32_t s_out[T], s_olegal[T];  // last step's outputs, by lane
   __shared__ __attribute__((aligned(16))) uint32_t s_bin[2][32];
   const uint32_t t = threadIdx.x;
   const int64_t base = (int64_t)blockIdx.x * T;
@@ -603,9 +662,11 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
       key = m ? ahead_key(L, sample_action(m, rng.draw(L.episode, L.move))) : kKeyDead;
     }
   }
+  const bool home = base + t < a.n;  // thread t stores lane t's staged outputs
   for (int64_t s = 0; s < steps; ++s) {
     uint32_t* bin = s_bin[s & 1];
-    __syncthreads();  // this step's bins are zero; last step's slots are read
+    __syncthreads();  // this step's bins are zero; last step's slots and outputs are complete
+    if (STAGE && s > 0 && home) store_staged<N>(a, (s - 1) * a.n + base + t, s_out[t], s_olegal[t]);
     const uint32_t rank = atomicAdd(&bin[key], 1u);
     __syncthreads();
     const uint32_t pos = bins_below<7>(bin, key) + rank;  // keys up to kKeyFirst = 26
@@ -625,16 +686,28 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
     const int64_t o = s * a.n + li;
     rng.env_id = lane_stream_id(a.env_id_base, li);
     rng.blk_tag = 0u;
+    // every output of step s goes through out(): staged by lane (STAGE) or
+    // stored at once
+    auto out = [&](uint32_t w, uint32_t legal) {
+      if (STAGE) {
+        s_out[lane] = w;
+        s_olegal[lane] = legal;
+      } else {
+        store_staged<N>(a, o, w, legal);
+      }
+    };
     // a new episode and a non-terminal state after resolve_chance are
     // decision nodes: LegalActionsMask is decision_mask, the player L.M
     if (key == kKeyFirst) {  // step() after LAST (rl_environment.py:310-311)
       L = new_episode<N>(L.episode + 1u, rng);
       const uint32_t legal = decision_mask(L);
-      store_step_outputs<N>(a, o, -1, 0u, 0u, 0u, legal, (int)L.M);
+      out(stage_head(-1, 0u, 0u, 0u) | stage_player((int)L.M), legal);
       key = ahead_key(L, sample_action(legal, rng.draw(L.episode, L.move)));
       continue;
     }
     if (key == kKeyReset) {  // finished in step s - 1 with auto-reset (vector_env.py:62-65)
+      // step s - 1's legal mask and player, after the new deal: its staged
+      // head is already stored (above), so these two go out directly
       L = new_episode<N>(L.episode + 1u, rng);
       const uint32_t legal = decision_mask(L);
       store_legal_player(a, o - a.n, legal, (int)L.M);
@@ -642,7 +715,7 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
     }
     if (key == kKeyDead) {  // no legal decision: coup_step's rejected step
       errs += 1u;
-      store_step_outputs<N>(a, o, -1, 1u, 0u, 0u, legal_mask(L), current_player(L));
+      out(stage_head(-1, 1u, 0u, 0u) | stage_player(current_player(L)), legal_mask(L));
       continue;
     }
     const uint32_t x = key_action(key);
@@ -652,23 +725,26 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
     resolve_chance(L, rng);
     errs += (L.err && !err_before) ? 1u : 0u;
     const bool term = is_terminal(L);
-    store_step_head<N>(a, o, (int)x, term ? 2u : 1u, L.rloser, L.rcount);
+    const uint32_t head = stage_head((int)x, term ? 2u : 1u, L.rloser, L.rcount);
     if (term) {
       s_eps[lane] += 1;
       s_ret[lane] += returns(L, 0u);
       if (ar) {
-        key = kKeyReset;  // legal mask and player once the next episode is dealt
+        out(head, 0u);  // legal mask and player once the next episode is dealt
+        key = kKeyReset;
         continue;
       }
       key = kKeyFirst;
-      store_legal_player(a, o, 0u, -4);  // terminal: no legal actions, kTerminalPlayerId
+      out(head | stage_player(-4), 0u);  // terminal: no legal actions, kTerminalPlayerId
       continue;
     }
     const uint32_t legal = decision_mask(L);
-    store_legal_player(a, o, legal, (int)L.M);
+    out(head | stage_player((int)L.M), legal);
     if (s + 1 < steps) key = ahead_key(L, sample_action(legal, rng.draw(L.episode, L.move)));
   }
-  if (key == kKeyReset && base + lane < a.n) {  // finished on the last step
+  __syncthreads();  // the last step's staged outputs are complete
+  if (STAGE && steps > 0 && home) store_staged<N>(a, (steps - 1) * a.n + base + t, s_out[t], s_olegal[t]);
+  if (steps > 0 && key == kKeyReset && base + lane < a.n) {  // finished on the last step
     L = new_episode<N>(L.episode + 1u, rng);
     store_legal_player(a, (steps - 1) * a.n + base + lane, decision_mask(L), (int)L.M);
   }
@@ -912,10 +988,14 @@ hipError_t launch_step(const Env& e, const int8_t* actions, const coup_step_outp
       auto go = [&](auto lanes) {
         constexpr int TB = decltype(lanes)::value;
         const unsigned g = grid_for(e.n, TB);
+        const char* ri = std::getenv("COUP_NP_RESET_INLINE");  // 0: resets in a phase of their own (A/B)
+        const bool inl = ri ? std::atoi(ri) != 0 : true;
         if (actions)
           k_step_sorted<N, false, false, TB><<<g, TB, 0, e.stream>>>(a);
-        else if (ahead)
+        else if (ahead && inl)
           k_step_sorted<N, true, true, TB><<<g, TB, 0, e.stream>>>(a);
+        else if (ahead)
+          k_step_sorted<N, true, true, TB, false><<<g, TB, 0, e.stream>>>(a);
         else
           k_step_sorted<N, true, false, TB><<<g, TB, 0, e.stream>>>(a);
       };
@@ -958,7 +1038,16 @@ hipError_t launch_trajectory(const Env& e, int64_t steps, const coup_step_output
       switch (sort_lanes("COUP_NP_SORT_THREADS", kRolloutSortLanes)) {
         case 256: k_trajectory_sorted<N, 256><<<grid_for(e.n, 256), 256, 0, e.stream>>>(a, steps); break;
         case 512: k_trajectory_sorted<N, 512><<<grid_for(e.n, 512), 512, 0, e.stream>>>(a, steps); break;
-        default: k_trajectory_sorted<N, 1024><<<grid_for(e.n, 1024), 1024, 0, e.stream>>>(a, steps); break;
+        default: {
+          // COUP_TRAJ_STAGE=0: outputs stored where the lane is played, not
+          // staged by lane (A/B of the round-2 form, 1024-lane blocks)
+          const char* st = std::getenv("COUP_TRAJ_STAGE");
+          if (st && std::atoi(st) == 0)
+            k_trajectory_sorted<N, 1024, false><<<grid_for(e.n, 1024), 1024, 0, e.stream>>>(a, steps);
+          else
+            k_trajectory_sorted<N, 1024><<<grid_for(e.n, 1024), 1024, 0, e.stream>>>(a, steps);
+          break;
+        }
       }
     } else {
       k_step_trajectory<N><<<grid_for(e.n, kThreads), kThreads, 0, e.stream>>>(a, steps);

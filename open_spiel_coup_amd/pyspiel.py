@@ -17,9 +17,13 @@ legal mask, player, rewards, returns) is kept on the host and serves the
 accessors until the state changes; a clone is a device-side lane copy.  Strings are formatted on the host (strings.py).
 This is the compatibility path; batched learners use BatchedCoupEnv.
 """
+import atexit
 import ctypes
 import enum
+import os
+import struct
 import threading
+import weakref
 
 import numpy as np
 import torch
@@ -93,6 +97,15 @@ _SLOT_RESULT = np.dtype([("record", "<u4", (4,)), ("history", "u1", (96,)), ("le
                          ("cur_player", "i1"), ("terminal", "u1"), ("ok", "u1"), ("reserved", "u1"),
                          ("rewards", "i1", (2,)), ("returns", "i1", (2,)), ("pad", "u1", (4,))])
 assert _SLOT_RESULT.itemsize == 128
+_RESULT_TAIL = struct.Struct("<IbBBBbbbb")  # legal_mask .. returns, at byte 112
+
+
+def _parse_result(raw):
+    """One coup_slot_result (128 bytes) -> the facade's result dict."""
+    lm, cp, term, ok, _, r0, r1, t0, t1 = _RESULT_TAIL.unpack_from(raw, 112)
+    return {"record": np.frombuffer(raw, np.uint32, 4, 0), "history": np.frombuffer(raw, np.uint8, 96, 16),
+            "legal_mask": lm, "current_player": cp, "terminal": bool(term), "ok": bool(ok),
+            "rewards": np.frombuffer(raw, np.int8, 2, 120), "returns": np.frombuffer(raw, np.int8, 2, 122)}
 
 
 class _Pool:
@@ -119,8 +132,38 @@ class _Pool:
         nbytes = _native.SLOT_RESULT_BYTES + 2 * OBS_SIZE * 4 + 2 * INFO_STATE_SIZE * 4
         self.host = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
         self.buf = self.host.numpy()
-        self.res = self.buf[:_native.SLOT_RESULT_BYTES].view(_SLOT_RESULT)[0]
         self.host_ptr = ctypes.c_void_p(self.host.data_ptr())
+        # the device-resident op server (coup_server_*): single ops on the
+        # pool's lanes run on one resident wave instead of a launch each.
+        # COUP_SERVER=0 keeps the launch path (A/B); COUP_SERVER_IDLE_US sets
+        # how long the wave waits for the next op before it leaves.
+        self.srv = None
+        if os.environ.get("COUP_SERVER", "1") != "0":
+            h = ctypes.c_void_p()
+            with torch.cuda.device(self.device):
+                _native.check(self.lib.coup_server_create(int(os.environ.get("COUP_SERVER_IDLE_US", "20000")),
+                                                          ctypes.byref(h)))
+            self.srv = h
+        atexit.register(_close_pool, weakref.ref(self))
+
+    def close(self):
+        """Stop the op server (its wave leaves) and detach the segments."""
+        with self.lock:
+            if self.srv is None:
+                return
+            for env in self.segs:
+                if env._h:
+                    _native.check(self.lib.coup_attach_server(env._h, None))
+            _native.check(self.lib.coup_server_destroy(self.srv))
+            self.srv = None
+
+    def server_stats(self):
+        """(requests, wave launches, running, idle_us) of the op server, or None."""
+        if self.srv is None:
+            return None
+        out = (ctypes.c_uint64 * 4)()
+        _native.check(self.lib.coup_server_stats(self.srv, out))
+        return tuple(int(x) for x in out)
 
     def alloc(self):
         with self.lock:
@@ -129,6 +172,8 @@ class _Pool:
     def _alloc(self):
         if not self.free:
             env = BatchedCoupEnv(self.SEG, seed=0, auto_reset=False, obs=False, history=True, device=self.device)
+            if self.srv is not None:
+                _native.check(self.lib.coup_attach_server(env._h, self.srv))
             k = len(self.segs)
             self.segs.append(env)
             self.free.extend((k, i) for i in range(self.SEG - 1, -1, -1))
@@ -196,11 +241,8 @@ class _Pool:
                                             self.host_ptr if result else None))
         if not result:
             return None
-        r = self.res.copy()  # one copy of the 128-byte coup_slot_result
-        q = {"record": r["record"], "history": r["history"], "legal_mask": int(r["legal_mask"]),
-             "current_player": int(r["cur_player"]), "terminal": bool(r["terminal"]), "ok": bool(r["ok"]),
-             "rewards": r["rewards"], "returns": r["returns"]}
         b = self.buf
+        q = _parse_result(b[:_native.SLOT_RESULT_BYTES].tobytes())
         off = _native.SLOT_RESULT_BYTES
         if obs:
             q["obs"] = b[off:off + 2 * OBS_SIZE * 4].view(np.float32).reshape(2, OBS_SIZE).copy()
@@ -211,6 +253,15 @@ class _Pool:
 
 
 _pools = {}
+
+
+def _close_pool(ref):
+    pool = ref()
+    if pool is not None:
+        try:
+            pool.close()
+        except Exception:
+            pass
 
 
 def _pool(device=None):
@@ -457,9 +508,22 @@ class CoupState:
         self.apply_action(action)
 
     def child(self, action):
-        c = self.clone()
-        c.apply_action(action)
-        return c
+        """clone() + apply_action(action) as ONE op: the new state's lane is a
+        copy of this one with the action applied."""
+        player = self.current_player()
+        a = int(action)
+        if not 0 <= a < 18 or not (self._mask() >> a) & 1 or player == PlayerId.TERMINAL:
+            raise SpielError(f"illegal action {action}")
+        pool = self._pool
+        slot = pool.alloc()
+        try:
+            q = pool.op(slot, src=(pool.handle(self._slot), self._slot[1]), action=a)
+            if not q["ok"]:
+                raise SpielError(f"illegal action {action}")
+        except Exception:
+            pool.release(slot)
+            raise
+        return CoupState(self._game, _slot=slot, _q=q, _history=self._history + [(player, a)])
 
     def children(self, actions, obs=False, info_state=False):
         """[self.child(a) for a in actions] in one launch per pool segment

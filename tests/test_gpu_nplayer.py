@@ -292,3 +292,34 @@ def test_six_player_full_batch_sampled_lanes_match_spec(fused):
         np.testing.assert_array_equal(words[k:k + 256], ref["final_state"], err_msg=f"slice {k}")
     assert env.error_count() == 0
 
+
+
+@pytest.mark.parametrize("n_players", [3, 6])
+@pytest.mark.parametrize("lanes", ["256", "1024"])
+def test_regrouped_step_reset_schedule_invariant(monkeypatch, n_players, lanes):
+    """The regrouped uniform step deals an auto-reset where the game ends
+    (decisions that end a game drawn ahead as kKeyEnding and sorted into the
+    same waves; the default) == the round-2 schedule, the block's resets in
+    a phase of their own (COUP_NP_RESET_INLINE=0), lane by lane -- and so
+    does an env alternating the two kernels, where a kKeyEnding decision
+    parked by one is played by the other.  Outputs, records, accumulators."""
+    n, steps, seed = 3000, 200, 40 + n_players
+    monkeypatch.setenv("COUP_REGROUP", "1")
+    monkeypatch.setenv("COUP_NP_SORT_THREADS", lanes)
+    envs = {knob: BatchedCoupEnv(n, seed=seed, env_id_base=9 << 20, auto_reset=True, obs=False,
+                                 num_players=n_players, generic=True, episode_stats=True)
+            for knob in ("1", "0", "alt")}
+    for t in range(steps):
+        outs = {}
+        for knob, env in envs.items():
+            monkeypatch.setenv("COUP_NP_RESET_INLINE", knob if knob != "alt" else str(t % 2))
+            outs[knob] = {k: v.clone() for k, v in env.step().items()}
+        for knob in ("0", "alt"):
+            for k in ("actions", "rewards", "step_type", "legal_mask", "current_player"):
+                assert torch.equal(outs["1"][k], outs[knob][k]), (knob, t, k)
+            assert torch.equal(envs["1"].export_state(), envs[knob].export_state()), (knob, t)
+    for knob in ("0", "alt"):
+        for x, y in zip(envs["1"].episode_stats(), envs[knob].episode_stats()):
+            assert torch.equal(x, y), knob
+    assert int(envs["1"].episode_stats()[0].sum()) > 100
+    assert all(env.error_count() == 0 for env in envs.values())

@@ -1,11 +1,26 @@
-"""Per-op latency of the per-game State facade: the lane pool (coup_slot_op,
-one launch + one 128-byte read-back per answered op) against the previous
-design (one-lane scratch env: import record + history, apply, error count,
-export record + history), and the batched ops (coup_slot_ops: n children of
-one node, or one action on each of n states, per launch), timed in one
-process.  Measurement tool only."""
+"""Per-op latency of the per-game facades, as interleaved repeats in one
+process (measurement tool only).
+
+Rows:
+  - the State facade on the lane pool, with the device-resident op server
+    (default) and with one launch per op (a second pool built under
+    COUP_SERVER=0): child(a) + legal_actions(), clone(), the tensors;
+  - batched ops (coup_slot_ops): n children of one node, one action on each
+    of n states;
+  - rl_environment.Environment.step (INFORMATION_STATE, the reference's
+    default, and OBSERVATION) and 1-lane queries;
+  - SyncVectorEnv.step per env step, batched over one shared env against
+    the reference's loop over the envs.
+
+Every row is measured once per round, rounds interleaved (`--rounds`, default
+5), and reported as {median, min, max} microseconds per op: the spread
+between rounds shows run-to-run noise (host-core contention, clocks) next
+to the differences between rows.
+"""
+import argparse
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -14,23 +29,6 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from open_spiel_coup_amd import pyspiel  # noqa: E402
-from open_spiel_coup_amd.env import BatchedCoupEnv, HISTORY_BYTES  # noqa: E402
-
-
-def scratch_apply(env, rec, hist, action):
-    env.import_state(torch.from_numpy(rec.view(np.int32).reshape(1, 4)))
-    env.import_history(torch.from_numpy(hist.reshape(1, HISTORY_BYTES)))
-    env.apply_action(torch.tensor([int(action)], dtype=torch.int8))
-    assert env.error_count() == 0
-    return (env.export_state().cpu().numpy().view(np.uint32).reshape(4).copy(),
-            env.export_history().cpu().numpy().reshape(HISTORY_BYTES).copy())
-
-
-def scratch_query(env, rec, hist):
-    env.import_state(torch.from_numpy(rec.view(np.int32).reshape(1, 4)))
-    env.import_history(torch.from_numpy(hist.reshape(1, HISTORY_BYTES)))
-    q = env.query(obs=False, info_state=False)
-    return {k: v.cpu().numpy()[0] for k, v in q.items()}
 
 
 class _Out:
@@ -38,10 +36,100 @@ class _Out:
         self.action = a
 
 
+def _pool_game(server):
+    """A game bound to a pool of its own, with or without the op server."""
+    prev = os.environ.get("COUP_SERVER")
+    os.environ["COUP_SERVER"] = "1" if server else "0"
+    try:
+        pool = pyspiel._Pool(torch.device("cuda", torch.cuda.current_device()))
+    finally:
+        if prev is None:
+            os.environ.pop("COUP_SERVER", None)
+        else:
+            os.environ["COUP_SERVER"] = prev
+    game = pyspiel.load_game("coup")
+    game._pool = pool
+    return game, pool
+
+
+def _opening(game):
+    st = game.new_initial_state()
+    for a in (0, 1, 2, 3):
+        st.apply_action(a)
+    return st
+
+
+def _timed(fn, n):
+    t0 = time.perf_counter()
+    for _ in range(n):
+        fn()
+    return 1e6 * (time.perf_counter() - t0) / n
+
+
+def state_rows(tag, game, n):
+    st = _opening(game)
+    rows = {}
+    rows[f"{tag}_child_plus_legal_us"] = _timed(lambda: st.child(0).legal_actions(), n)
+    rows[f"{tag}_clone_us"] = _timed(st.clone, n)
+
+    def obs():
+        st.observation_tensor(0)
+        st._q.pop("obs", None)
+
+    def info():
+        st.information_state_tensor(0)
+        st._q.pop("info_state", None)
+    rows[f"{tag}_observation_tensor_us"] = _timed(obs, n)
+    rows[f"{tag}_information_state_tensor_us"] = _timed(info, max(n // 4, 50))
+    s2 = _opening(game)
+
+    def apply_one():
+        nonlocal s2
+        if s2.is_terminal():
+            s2 = _opening(game)
+        s2.apply_action(s2.legal_actions()[0])
+    rows[f"{tag}_apply_action_us"] = _timed(apply_one, n)
+    return rows
+
+
+def batched_rows(game, n):
+    st = _opening(game)
+    rows = {}
+    for k in (1, 7, 64, 1024):
+        acts = [0] * k
+        reps = max(10, n // k)
+        rows[f"children_n{k}_us_per_child"] = _timed(lambda: st.children(acts), reps) / k
+        rows[f"children_n{k}_with_info_state_us_per_child"] = _timed(
+            lambda: st.children(acts, info_state=True), max(5, reps // 4)) / k
+    frontier = [st.clone() for _ in range(1024)]
+    t0 = time.perf_counter()
+    pyspiel.apply_actions(frontier, [0] * 1024)
+    rows["apply_actions_n1024_us_per_state"] = 1e6 * (time.perf_counter() - t0) / 1024
+    return rows
+
+
+def rl_rows(n):
+    from open_spiel_coup_amd import rl_environment
+    rows = {}
+    rng = np.random.default_rng(0)
+    for otype, tag in ((rl_environment.ObservationType.INFORMATION_STATE, "info"),
+                       (rl_environment.ObservationType.OBSERVATION, "obs")):
+        env = rl_environment.Environment("coup", seed=3, observation_type=otype)
+        ts = [env.reset()]
+
+        def step():
+            t = ts[0]
+            p = t.observations["current_player"]
+            ts[0] = env.step([int(rng.choice(t.observations["legal_actions"][p]))]) if not t.last() else env.reset()
+        rows[f"rl_environment_step_{tag}_us"] = _timed(step, n)
+        e1 = env._env
+        rows[f"query_host_{tag}_us"] = _timed(lambda: e1.query_host(obs=tag == "obs", info_state=tag == "info"), n)
+    return rows
+
+
 def vector_env_rows(steps=40):
     """SyncVectorEnv.step(reset_if_done=True) per env step: one shared env
-    (batched) against the reference's loop over the envs, for both
-    observation types."""
+    (batched) against the reference's loop over the envs."""
     from open_spiel_coup_amd import rl_environment, vector_env
     rows = {}
     rng = np.random.default_rng(1)
@@ -65,89 +153,39 @@ def vector_env_rows(steps=40):
                 t0 = time.perf_counter()
                 run(steps, ts)
                 us = 1e6 * (time.perf_counter() - t0) / (steps * k)
-                rows[f"vector_env_{tag}_n{k}_{'batched' if batched else 'loop'}_us_per_env_step"] = round(us, 1)
+                rows[f"vector_env_{tag}_n{k}_{'batched' if batched else 'loop'}_us_per_env_step"] = us
     return rows
 
 
-def main(n=2000):
-    game = pyspiel.load_game("coup")
-    st = game.new_initial_state()
-    for a in (0, 1, 2, 3):
-        st.apply_action(a)
-    for _ in range(50):
-        st.child(0).legal_actions()
-    t0 = time.perf_counter()
-    for _ in range(n):
-        st.child(0).legal_actions()
-    pool_child = (time.perf_counter() - t0) / n
-    t0 = time.perf_counter()
-    for _ in range(n):
-        st.clone()
-    pool_clone = (time.perf_counter() - t0) / n
-    t0 = time.perf_counter()
-    for _ in range(n):
-        st.observation_tensor(0)
-        st._q.pop("obs", None)
-    pool_obs = (time.perf_counter() - t0) / n
-    env = BatchedCoupEnv(1, seed=0, auto_reset=False, obs=False, history=True)
-    rec, hist = st.packed_record(), st.history_bytes()
-    for _ in range(50):
-        scratch_apply(env, rec, hist, 0)
-    t0 = time.perf_counter()
-    for _ in range(n):
-        r2, h2 = scratch_apply(env, rec, hist, 0)
-        scratch_query(env, r2, h2)
-    scratch_child = (time.perf_counter() - t0) / n
-    # batched: all children of one node in one call, per child
-    batched = {}
-    for k in (1, 7, 64, 1024):
-        acts = [0] * k
-        for _ in range(5):
-            st.children(acts)
-        reps = max(20, n // k)
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            st.children(acts)
-        batched[f"children_n{k}_us_per_child"] = round(1e6 * (time.perf_counter() - t0) / (reps * k), 2)
-        t0 = time.perf_counter()
-        for _ in range(max(5, reps // 4)):
-            st.children(acts, info_state=True)
-        batched[f"children_n{k}_with_info_state_us_per_child"] = round(
-            1e6 * (time.perf_counter() - t0) / (max(5, reps // 4) * k), 2)
-    frontier = [st.clone() for _ in range(1024)]
-    for _ in range(3):
-        pyspiel.apply_actions(frontier, [0] * 1024)
-        frontier = [st.clone() for _ in range(1024)]
-    t0 = time.perf_counter()
-    pyspiel.apply_actions(frontier, [0] * 1024)
-    batched["apply_actions_n1024_us_per_state"] = round(1e6 * (time.perf_counter() - t0) / 1024, 2)
-    from open_spiel_coup_amd import rl_environment
-    renv = rl_environment.Environment("coup", seed=3)
-    ts = renv.reset()
-    rng = np.random.default_rng(0)
-    t0 = time.perf_counter()
-    for _ in range(n):
-        p = ts.observations["current_player"]
-        ts = renv.step([int(rng.choice(ts.observations["legal_actions"][p]))]) if p >= 0 else renv.reset()
-    rl_step = (time.perf_counter() - t0) / n
-    e1 = renv._env
-    t0 = time.perf_counter()
-    for _ in range(n):
-        {k: v.cpu().numpy()[0] for k, v in e1.query(obs=False, info_state=True).items()}
-    query_per_tensor = (time.perf_counter() - t0) / n
-    t0 = time.perf_counter()
-    for _ in range(n):
-        e1.query_host(obs=False, info_state=True)
-    query_one_copy = (time.perf_counter() - t0) / n
-    vector = vector_env_rows()
-    print(json.dumps({"tool": "facade_latency", "ops": n,
-                      "rl_environment_step_us": round(1e6 * rl_step, 1),
-                      "query_info_per_tensor_copies_us": round(1e6 * query_per_tensor, 1),
-                      "query_info_one_copy_us": round(1e6 * query_one_copy, 1),
-                      "pool_child_plus_legal_us": round(1e6 * pool_child, 1),
-                      "pool_clone_us": round(1e6 * pool_clone, 1),
-                      "pool_observation_tensor_us": round(1e6 * pool_obs, 1),
-                      "scratch_env_child_plus_legal_us": round(1e6 * scratch_child, 1), **batched, **vector}))
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ops", type=int, default=1000, help="ops per row per round")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--no-vector", action="store_true")
+    a = ap.parse_args()
+    g_srv, p_srv = _pool_game(True)
+    g_launch, p_launch = _pool_game(False)
+    # warm both paths (segments allocated, code paths and the wave started)
+    state_rows("warm_server", g_srv, 50)
+    state_rows("warm_launch", g_launch, 50)
+    samples = {}
+    for _ in range(a.rounds):
+        rows = {}
+        rows.update(state_rows("server", g_srv, a.ops))
+        rows.update(state_rows("launch", g_launch, a.ops))
+        rows.update(batched_rows(g_srv, a.ops))
+        rows.update(rl_rows(a.ops // 2))
+        if not a.no_vector:
+            rows.update(vector_env_rows())
+        for k, v in rows.items():
+            samples.setdefault(k, []).append(v)
+    out = {"tool": "facade_latency", "ops_per_round": a.ops, "rounds": a.rounds,
+           "server_stats": dict(zip(("requests", "launches", "running", "idle_us"), p_srv.server_stats())),
+           "rows_us": {k: {"median": round(statistics.median(v), 2), "min": round(min(v), 2), "max": round(max(v), 2)}
+                       for k, v in samples.items()}}
+    p_srv.close()
+    p_launch.close()
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

@@ -1,7 +1,8 @@
 """Same-process A/B of the fused trajectory launch (coup_step_trajectory)
-against itself with no output buffers bound and against the fused rollout
-(statistics only): the cost of storing every step's outputs.  Measurement
-tool only.
+against itself with no output buffers bound, against its round-2 store form
+(outputs stored where each lane is played instead of staged by lane in LDS,
+COUP_TRAJ_STAGE=0) and against the fused rollout (statistics only): the cost
+of storing every step's outputs.  Measurement tool only.
 
     python tools/traj_ab.py [--players 6] [--batch 2^20] [--steps 50] [--rounds 7]
 """
@@ -35,7 +36,14 @@ def main():
         _native.check(env.lib.coup_step_trajectory(env._h, a.steps, ctypes.byref(none_out)))
     stats = env.new_stats()
     roll = env.rollout_launcher(a.steps, stats)
-    variants = {"trajectory": full, "trajectory_no_outputs": bare, "rollout_stats": roll}
+    def unstaged():  # the round-2 store form of the regrouped kernel (COUP_TRAJ_STAGE=0)
+        os.environ["COUP_TRAJ_STAGE"] = "0"
+        try:
+            full()
+        finally:
+            os.environ.pop("COUP_TRAJ_STAGE", None)
+    variants = {"trajectory": full, "trajectory_unstaged": unstaged, "trajectory_no_outputs": bare,
+                "rollout_stats": roll}
     times = {k: [] for k in variants}
     s = torch.cuda.current_stream()
     for _ in range(a.rounds):
