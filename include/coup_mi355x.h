@@ -192,6 +192,10 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
 /* coup_step_host flags */
 #define COUP_HOST_OBS 1   /* also return ObservationTensor [B][P][49P] */
 #define COUP_HOST_INFO 2  /* also return InformationStateTensor [B][2][2492] (COUP_FLAG_HISTORY) */
+#define COUP_HOST_ACTIVE 4  /* tensors only for the lanes whose action is >= 0 (2 players, actions
+                               not NULL): m rows in lane order, obs [m][2][98] at off[5], then info
+                               [m][2][2492] at off[5] + align16(m * 784) -- one env of a shared
+                               SyncVectorEnv env stepping alone copies its own rows, not B */
 
 /* coup_step for small batches that want the answers on the host (the
  * per-game rl_environment.Environment and SyncVectorEnv, rl_environment.py:

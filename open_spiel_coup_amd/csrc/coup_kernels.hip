@@ -283,7 +283,9 @@ __device__ __forceinline__ void obs_bits_to_lds(const Lane& L, uint32_t* __restr
 // Store policy of the wave-bitmap writer: 0 plain, 1 non-temporal (global
 // stores), 2 sc1 write-through (buffer stores through a wave-uniform
 // resource whose range ends at the wave's last row, so rows past the batch
-// are dropped by the range check instead of a per-store predicate).
+// are dropped by the range check instead of a per-store predicate), 3 the
+// same with sc0 sc1 (system scope: the op server's stores into mapped host
+// memory, which need no L2 write-back afterwards).
 template <int POL, class V>
 __device__ __forceinline__ void store_f4(V* p, const V& v) {
   if (POL == 0)
@@ -304,7 +306,7 @@ __device__ __forceinline__ void write_obs_wave_bits(float* __restrict__ wave_obs
   const uint32_t lane = threadIdx.x & 63u;
   v4f* dst = reinterpret_cast<v4f*>(wave_obs) + lane;
   __amdgpu_buffer_rsrc_t rsrc;
-  if (POL == 2) rsrc = __builtin_amdgcn_make_buffer_rsrc(wave_obs, (short)0, (int)(n_valid * 2u * kObsSize * 4u), 0x00020000);
+  if (POL >= 2) rsrc = __builtin_amdgcn_make_buffer_rsrc(wave_obs, (short)0, (int)(n_valid * 2u * kObsSize * 4u), 0x00020000);
   uint32_t o = lane >= (uint32_t)kRowF4 ? 1u : 0u;
   uint32_t c = lane - o * (uint32_t)kRowF4;
 #pragma unroll 7
@@ -322,8 +324,9 @@ __device__ __forceinline__ void write_obs_wave_bits(float* __restrict__ wave_obs
     v.y = c == 15u ? c1 : v.y;
     v.z = c == 39u ? c0 : v.z;
     v.w = c == 39u ? c1 : v.w;
-    if (POL == 2)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), rsrc, (int)(16u * (64u * j + lane)), 0, 16);
+    if (POL >= 2)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), rsrc, (int)(16u * (64u * j + lane)), 0,
+                                             POL == 3 ? 17 : 16);
     else if (FULL || o < n_valid)
       store_f4<POL>(dst + 64u * j, v);
     c += 15u;
@@ -1505,6 +1508,16 @@ __global__ __launch_bounds__(kThreads) void k_info_elems(const uint4* __restrict
   reinterpret_cast<float4*>(info)[g] = info_f4(pre, hist + lane * kHist, c);
 }
 
+// ObservationTensor rows of the requests' lanes (coup_step_host with
+// COUP_HOST_ACTIVE): row l = lane reqs[l].lane, one thread per row.
+__global__ __launch_bounds__(kThreads) void k_obs_lanes(const uint4* __restrict__ state,
+                                                       const coup_slot_req* __restrict__ reqs, int64_t m,
+                                                       float* __restrict__ obs) {
+  const int64_t l = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (l >= m) return;
+  write_obs_pair(obs + l * (2 * kObsSize), unpack(state[reqs[l].lane]));
+}
+
 // Batches up to this size take k_info_elems for the InformationStateTensor
 // of coup_query (and coup_slot_op always does).
 constexpr int64_t kInfoElemsMaxBatch = 1024;
@@ -1683,34 +1696,37 @@ __global__ __launch_bounds__(64) void k_slot_batch(SlotBatchArgs b) {
 // coup_server: ONE resident wave serves the per-game
 // State ops of the envs attached to it, so an answered op costs a host write
 // the wave sees, the op itself and a device->host write -- no kernel launch,
-// no queue.  Requests sit in a ring of kSrvRing 128-byte slots in mapped,
-// coherent pinned host memory; the host fills a slot and then stores its
-// sequence number.  The wave polls the next slot's number (one relaxed
-// system-scope load per pass, s_sleep between passes), takes ONE acquire
-// when it matches (this CU's L1 dropped: the lanes may have been written by
-// kernels on other XCDs, whose completion released them), runs slot_op on
-// the request's lane, stores its result / tensors into host memory, drains
-// its stores, releases at system scope and publishes the number in
-// ctl.served.  Requests are served in order.  Exit: when the host stores the
-// wave's epoch in ctl.stop (after the pending requests), or after idle_ticks
-// (s_memrealtime, 100 MHz) with no request -- a host that stops calling, or
-// dies, never leaves a spinning wave; the next op relaunches it.
+// no queue.  Requests sit in a ring of kSrvRing slots in mapped, coherent
+// pinned host memory, one 64-byte host cache line each.  The wave polls the
+// next slot by reading the WHOLE line -- 16 lanes x 4 bytes, one request per
+// 32-byte half -- so the request arrives with the poll that finds it, one
+// host round trip instead of two.  Each half carries the slot's sequence
+// number, written after the fields of its half (x86 stores become visible in
+// program order, and a half is read as one snapshot), so a match of both
+// means every field is current.  The poll and the stop word are loaded
+// together (one round trip per pass), then s_sleep.  The op runs with no
+// fences (server_op: sc1 / sc0 sc1 accesses), its stores are drained, and
+// the number goes to ctl.served.  Requests are served in order.  Exit: when
+// the host stores the wave's epoch in ctl.stop (after the pending requests),
+// or after idle_ticks (s_memrealtime, 100 MHz) with no request -- a host that
+// stops calling, or dies, never leaves a spinning wave; the next op
+// relaunches it.
 constexpr uint32_t kSrvRing = 64;
 
-struct SrvReq {       // one ring slot (host memory), 128 bytes
+struct SrvReq {        // one ring slot (host memory), 64 bytes = one host cache line
+  // first half (32 bytes)
   uint64_t dst_state;  // uint4*  (device)
   uint64_t dst_hist;   // uint8_t* (device)
   uint64_t src_state;  // 0: no copy
+  uint32_t op;         // action (int8) [7:0] | init [8] | result [9] | obs [10] | info [11]
+  uint32_t seq_a;      // the sequence number, stored after the half's fields
+  // second half
   uint64_t src_hist;
-  uint64_t out;        // coup_slot_result* (mapped host) or 0: no result
-  uint64_t obs;        // [2][98] floats (mapped host) or 0
-  uint64_t info;       // [2][2492] floats (mapped host) or 0
-  int32_t action;      // < 0: none
-  int32_t init;
-  uint32_t seq;        // stored last by the host
-  uint32_t pad[15];
+  uint32_t pad[5];
+  uint32_t seq_b;      // stored last of all
 };
-static_assert(sizeof(SrvReq) == 128, "SrvReq layout");
+static_assert(sizeof(SrvReq) == 64, "SrvReq layout");
+constexpr uint32_t kSrvInit = 1u << 8, kSrvResult = 1u << 9, kSrvObs = 1u << 10, kSrvInfo = 1u << 11;
 
 struct SrvCtl {        // host memory, one word per 128-byte line
   uint32_t served;     // last sequence number served (the wave writes)
@@ -1722,6 +1738,7 @@ struct SrvCtl {        // host memory, one word per 128-byte line
 struct ServerArgs {
   SrvReq* ring;        // device addresses of the mapped host memory
   SrvCtl* ctl;
+  uint8_t* result;     // coup_slot_result, then obs [2][98], then info [2][2492] floats (mapped host)
   uint32_t first;      // sequence number of the first request to serve
   uint32_t epoch;      // this launch's epoch (never 0)
   uint64_t idle_ticks; // exit after this many 100 MHz ticks without a request
@@ -1732,54 +1749,120 @@ __device__ __forceinline__ T srv_ld(const T* p) {  // host-written word: vector 
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// 16-byte accesses through a buffer resource with explicit cache bits:
+// aux 16 = sc1 (device scope: past the CU's L1; stores write through),
+// 17 = sc0 sc1 (system scope).
+template <int AUX>
+__device__ __forceinline__ uint4 ld16(uint64_t base, uint32_t off) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(base), (short)0, (int)(off + 16u), 0x00020000);
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, AUX);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+template <int AUX>
+__device__ __forceinline__ void st16(uint64_t base, uint32_t off, uint4 x) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(base), (short)0, (int)(off + 16u), 0x00020000);
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  __builtin_amdgcn_raw_buffer_store_b128(v4u{x.x, x.y, x.z, x.w}, r, (int)off, 0, AUX);
+}
+constexpr int kAuxDevice = 16, kAuxSystem = 17;
+
+// One coup_slot_op on one lane by the server's wave: slot_op's steps with
+// the server's cache policy, which needs no fence: the lanes and histories
+// are read with sc1 loads (past this CU's L1: kernels on other XCDs may have
+// written them) and written with sc1 stores (write-through, so later kernels
+// on any XCD read them); the result and tensors go to host memory with
+// sc0 sc1 stores (system write-through -- plain stores would sit in this
+// XCD's L2 until a buffer_wbl2).  rs / hs: the lane (and history) to start
+// from; the transition and the accessors run out of line on thread 0
+// (slot_transition / slot_result, as in k_slot: DESIGN.md section 12).
+__device__ __forceinline__ void server_op(uint64_t rs, uint64_t hs, uint64_t dst_state, uint64_t dst_hist,
+                                          int32_t action, int32_t init, bool store, uint64_t out, uint64_t obs,
+                                          uint64_t info, uint8_t* hist, uint32_t* bits, uint32_t* pre,
+                                          coup_slot_result* res) {
+  const uint32_t t = threadIdx.x;
+  if (t < 6u)
+    reinterpret_cast<uint4*>(hist)[t] = init ? make_uint4(~0u, ~0u, ~0u, ~0u) : ld16<kAuxDevice>(hs, 16u * t);
+  wave_sync();
+  Lane L = initial_lane(0u);
+  if (t == 0u) {
+    uint4 rec = init ? pack(initial_lane(0u)) : ld16<kAuxDevice>(rs, 0u);
+    uint32_t ok = 1u;
+    if (action >= 0) {
+      const uint32_t r = slot_transition(rec, (uint32_t)action, &rec);
+      ok = r & 1u;
+      if (r & 2u) hist[(r >> 8) & 0xFFu] = (uint8_t)(r >> 16);
+    }
+    if (store) st16<kAuxDevice>(dst_state, 0u, rec);
+    if (out) slot_result(rec, ok, res);
+    L = unpack(rec);
+    if (info) info_prefix_to_lds(L, pre);
+  }
+  wave_sync();
+  if (t < 6u) {
+    const uint4 h = reinterpret_cast<const uint4*>(hist)[t];
+    if (store) st16<kAuxDevice>(dst_hist, 16u * t, h);
+    if (out) reinterpret_cast<uint4*>(res->history)[t] = h;
+  }
+  wave_sync();
+  if (out && t < 8u) st16<kAuxSystem>(out, 16u * t, reinterpret_cast<const uint4*>(res)[t]);
+  if (obs) {
+    if (t == 0u) obs_bits_to_lds(L, bits);
+    wave_sync();
+    write_obs_wave_bits<3, false>(reinterpret_cast<float*>(obs), bits, 1u);
+  }
+  if (info) {
+    // 19,936 bytes: plain stores, which the L2 gathers into whole lines, then
+    // one system-scope write-back, WAITED FOR by an asm wait after the fence
+    // (a builtin wait in front of it let the compiler drop the one after the
+    // buffer_wbl2: cdna_hip_programming.md G16 pitfall 12).  16-byte
+    // write-through stores straight to host memory took ~100 us here.
+    for (uint32_t c = t; c < (uint32_t)kInfoF4; c += 64u)
+      reinterpret_cast<float4*>(info)[c] = info_f4(pre, hist, c);
+    __threadfence_system();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
 __global__ __launch_bounds__(64) void k_server(ServerArgs s) {
   __shared__ __attribute__((aligned(16))) uint8_t hist[kHist];
   __shared__ __attribute__((aligned(16))) uint32_t bits[64 * 8];
   __shared__ __attribute__((aligned(16))) uint32_t pre[kPreWords];
+  __shared__ __attribute__((aligned(16))) coup_slot_result res;
   const uint32_t t = threadIdx.x;
   uint32_t next = s.first;
   uint64_t idle0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
-    SrvReq* q = s.ring + (next & (kSrvRing - 1u));
-    const uint32_t seq = (uint32_t)__builtin_amdgcn_readfirstlane((int)srv_ld(&q->seq));
-    if (seq != next) {
-      if ((uint32_t)__builtin_amdgcn_readfirstlane((int)srv_ld(&s.ctl->stop)) == s.epoch) break;
+    // the slot's 16 words (lanes 0..15) and the stop word in one round trip
+    const uint32_t* line = reinterpret_cast<const uint32_t*>(s.ring + (next & (kSrvRing - 1u)));
+    const uint32_t w = srv_ld(line + (t & 15u));
+    const uint32_t stop = srv_ld(&s.ctl->stop);
+    const uint32_t seq_a = (uint32_t)__builtin_amdgcn_readlane((int)w, 7);
+    const uint32_t seq_b = (uint32_t)__builtin_amdgcn_readlane((int)w, 15);
+    if (seq_a != next || seq_b != next) {
+      if ((uint32_t)__builtin_amdgcn_readfirstlane((int)stop) == s.epoch) break;
       if (__builtin_amdgcn_s_memrealtime() - idle0 > s.idle_ticks) break;
-      __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_s_sleep(1);
       continue;
     }
-    // ONE acquire after the match: later loads of the request, the lanes and
-    // their histories are not served from this CU's stale L1 lines
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    SlotArgs a;
-    a.dst_state = reinterpret_cast<uint4*>(srv_ld(&q->dst_state));
-    a.dst_hist = reinterpret_cast<uint8_t*>(srv_ld(&q->dst_hist));
-    const uint64_t src = srv_ld(&q->src_state);
-    a.src_state = src ? reinterpret_cast<const uint4*>(src) : nullptr;
-    a.src_hist = src ? reinterpret_cast<const uint8_t*>(srv_ld(&q->src_hist)) : nullptr;
-    a.action = srv_ld(&q->action);
-    a.init = srv_ld(&q->init);
-    a.store = (src || a.init || a.action >= 0) ? 1 : 0;
-    a.out = reinterpret_cast<coup_slot_result*>(srv_ld(&q->out));
-    a.obs = reinterpret_cast<float*>(srv_ld(&q->obs));
-    float* info = reinterpret_cast<float*>(srv_ld(&q->info));
-    if (a.obs)
-      slot_op<true>(a, hist, bits);
-    else
-      slot_op<false>(a, hist, bits);
-    if (info) {
-      // the InformationStateTensor from the lane's new record (thread 0's
-      // store, re-read after the wave barrier) and its history bytes in LDS
-      wave_sync();
-      if (t == 0u) info_prefix_to_lds(unpack(*a.dst_state), pre);
-      wave_sync();
-      for (uint32_t c = t; c < (uint32_t)kInfoF4; c += 64u) reinterpret_cast<float4*>(info)[c] = info_f4(pre, hist, c);
-    }
-    // every thread's stores (lane, history, result, tensors) drained, then
-    // ONE system-scope release, then the number the host polls
-    __builtin_amdgcn_s_waitcnt(0);
+    auto word = [&](int k) { return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)w, k); };
+    const uint64_t dst_state = word(0) | (word(1) << 32), dst_hist = word(2) | (word(3) << 32);
+    const uint64_t src_state = word(4) | (word(5) << 32), src_hist = word(8) | (word(9) << 32);
+    const uint32_t op = (uint32_t)word(6);
+    const int32_t action = (int32_t)(int8_t)(op & 0xFFu);
+    const int32_t init = (op & kSrvInit) ? 1 : 0;
+    const uint64_t res_base = reinterpret_cast<uint64_t>(s.result);
+    const uint64_t out = (op & kSrvResult) ? res_base : 0u;
+    const uint64_t obs = (op & kSrvObs) ? res_base + sizeof(coup_slot_result) : 0u;
+    const uint64_t info =
+        (op & kSrvInfo) ? res_base + sizeof(coup_slot_result) + ((op & kSrvObs) ? 2u * kObsSize * 4u : 0u) : 0u;
+    const bool store = src_state != 0u || init != 0 || action >= 0;
+    server_op(src_state ? src_state : dst_state, src_state ? src_hist : dst_hist, dst_state, dst_hist, action, init,
+              store, out, obs, info, hist, bits, pre, &res);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     wave_sync();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     if (t == 0u) __hip_atomic_store(&s.ctl->served, next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     next += 1u;
     idle0 = __builtin_amdgcn_s_memrealtime();
@@ -1929,7 +2012,7 @@ int launch_reset(coup_env* env, const uint8_t* mask, int mode, int deal) {
 size_t align16(size_t n) { return (n + 15u) & ~size_t(15); }
 
 // ---- coup_server host side
-constexpr size_t kSrvCtlOff = coup::kSrvRing * sizeof(coup::SrvReq);
+constexpr size_t kSrvCtlOff = coup::kSrvRing * sizeof(coup::SrvReq);  // 4 KiB: the ring starts the (page-aligned) block
 constexpr size_t kSrvResultOff = kSrvCtlOff + sizeof(coup::SrvCtl);
 constexpr size_t kSrvBytes = kSrvResultOff + sizeof(coup_slot_result) + 2u * COUP_OBS_SIZE * sizeof(float) +
                              2u * COUP_INFO_STATE_SIZE * sizeof(float);
@@ -1941,6 +2024,7 @@ int srv_launch(coup_server* s) {
   coup::ServerArgs a;
   a.ring = reinterpret_cast<coup::SrvReq*>(s->host_dev);
   a.ctl = reinterpret_cast<coup::SrvCtl*>(s->host_dev + kSrvCtlOff);
+  a.result = s->result_dev;
   a.first = srv_served(s) + 1u;
   s->epoch = s->epoch + 1u == 0u ? 1u : s->epoch + 1u;
   a.epoch = s->epoch;
@@ -2011,7 +2095,7 @@ int srv_post(coup_server* s, const coup::SrvReq& r, uint32_t* seq_out) {
     // the numbers would wrap: drain, stop, restart the count
     COUP_TRY(srv_wait(s, s->posted));
     COUP_TRY(srv_stop(s));
-    for (uint32_t k = 0; k < coup::kSrvRing; ++k) s->ring[k].seq = 0u;
+    for (uint32_t k = 0; k < coup::kSrvRing; ++k) s->ring[k].seq_a = s->ring[k].seq_b = 0u;
     __atomic_store_n(&s->ctl->served, 0u, __ATOMIC_RELEASE);
     s->posted = 0u;
   }
@@ -2023,8 +2107,12 @@ int srv_post(coup_server* s, const coup::SrvReq& r, uint32_t* seq_out) {
   const uint32_t seq = s->posted + 1u;
   if (seq - srv_served(s) >= coup::kSrvRing) COUP_TRY(srv_wait(s, seq - coup::kSrvRing));  // ring full
   coup::SrvReq* q = s->ring + (seq & (coup::kSrvRing - 1u));
-  std::memcpy(q, &r, offsetof(coup::SrvReq, seq));  // every field but the number, which goes last
-  __atomic_store_n(&q->seq, seq, __ATOMIC_RELEASE);  // after every field (x86: stores in order)
+  // each half's fields, then its number, the second half's last (x86 makes
+  // stores visible in program order; the compiler keeps them in order here)
+  std::memcpy(q, &r, offsetof(coup::SrvReq, seq_a));
+  std::memcpy(&q->src_hist, &r.src_hist, offsetof(coup::SrvReq, seq_b) - offsetof(coup::SrvReq, src_hist));
+  __atomic_store_n(&q->seq_a, seq, __ATOMIC_RELEASE);
+  __atomic_store_n(&q->seq_b, seq, __ATOMIC_RELEASE);
   s->posted = seq;
   s->last_post = now;
   s->requests += 1u;
@@ -2328,14 +2416,66 @@ int coup_rollout(coup_env* env, int64_t steps, const coup_rollout_stats* stats) 
 int coup_step_host(coup_env* env, const int8_t* actions, int want, void* host_out) {
   COUP_CHECK_ENV(env);
   if (!host_out) return fail(COUP_E_INVALID, "coup_step_host: host_out is null");
-  if (want & ~(COUP_HOST_OBS | COUP_HOST_INFO)) return fail(COUP_E_INVALID, "coup_step_host: unknown flags");
+  if (want & ~(COUP_HOST_OBS | COUP_HOST_INFO | COUP_HOST_ACTIVE))
+    return fail(COUP_E_INVALID, "coup_step_host: unknown flags");
   if ((want & COUP_HOST_INFO) && !env->hist)
     return fail(COUP_E_INVALID, "coup_step_host: info_state needs an env created with COUP_FLAG_HISTORY");
+  const bool active = (want & COUP_HOST_ACTIVE) && (want & (COUP_HOST_OBS | COUP_HOST_INFO));
+  if ((want & COUP_HOST_ACTIVE) && (!actions || env->generic))
+    return fail(COUP_E_INVALID, "coup_step_host: COUP_HOST_ACTIVE needs host actions and 2 players");
   const int64_t B = env->batch;
   if (B == 0) return COUP_OK;
   const size_t in_bytes = align16((size_t)B);
   size_t off[6];
   const size_t total = coup_step_host_layout(B, env->players, want, off);
+  if (active) {
+    // the active lanes' tensors, gathered after a step that writes none
+    int64_t m = 0;
+    for (int64_t i = 0; i < B; ++i) m += actions[i] >= 0 ? 1 : 0;
+    const size_t req_off = align16(in_bytes + total), req_bytes = (size_t)(m > 0 ? m : 1) * sizeof(coup_slot_req);
+    if (req_off + req_bytes > env->host_cap) {
+      if (env->host_scratch) (void)hipHostFree(env->host_scratch);
+      env->host_scratch = nullptr;
+      env->host_cap = 0;
+      COUP_HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&env->host_scratch), req_off + req_bytes,
+                                 hipHostMallocMapped | hipHostMallocCoherent));
+      COUP_HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&env->host_scratch_dev), env->host_scratch, 0));
+      env->host_cap = req_off + req_bytes;
+    }
+    coup_slot_req* reqs = reinterpret_cast<coup_slot_req*>(env->host_scratch + req_off);
+    for (int64_t i = 0, k = 0; i < B; ++i)
+      if (actions[i] >= 0) reqs[k++] = coup_slot_req{i, -1, 0, 0};
+    const int rc = coup_step_host(env, actions, 0, host_out);  // small outputs, no tensors (synchronises)
+    if (rc != COUP_OK || m == 0) return rc;
+    COUP_TRY(launching(env));
+    const coup_slot_req* reqs_dev = reinterpret_cast<const coup_slot_req*>(env->host_scratch_dev + req_off);
+    const size_t obs_bytes = (want & COUP_HOST_OBS) ? align16((size_t)m * 2u * COUP_OBS_SIZE * 4u) : 0u;
+    const size_t tensor_bytes = obs_bytes + ((want & COUP_HOST_INFO) ? (size_t)m * 2u * COUP_INFO_STATE_SIZE * 4u : 0u);
+    if (tensor_bytes > env->host_stage_cap) {
+      if (env->host_stage) (void)hipFree(env->host_stage);
+      env->host_stage = nullptr;
+      env->host_stage_cap = 0;
+      COUP_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&env->host_stage), tensor_bytes));
+      env->host_stage_cap = tensor_bytes;
+    }
+    hipStream_t s = env->stream;
+    if (want & COUP_HOST_OBS) {
+      coup::k_obs_lanes<<<(unsigned)((m + coup::kThreads - 1) / coup::kThreads), coup::kThreads, 0, s>>>(
+          env->state, reqs_dev, m, reinterpret_cast<float*>(env->host_stage));
+      COUP_HIP_TRY(hipGetLastError());
+    }
+    if (want & COUP_HOST_INFO) {
+      const int64_t nf4 = m * coup::kInfoF4;
+      coup::k_info_elems<<<(unsigned)((nf4 + coup::kThreads - 1) / coup::kThreads), coup::kThreads, 0, s>>>(
+          env->state, env->hist, m, reinterpret_cast<float*>(env->host_stage + obs_bytes), reqs_dev);
+      COUP_HIP_TRY(hipGetLastError());
+    }
+    COUP_HIP_TRY(hipMemcpyAsync(static_cast<uint8_t*>(host_out) + off[5], env->host_stage, tensor_bytes,
+                                hipMemcpyDeviceToHost, s));
+    COUP_HIP_TRY(hipStreamSynchronize(s));
+    env->dirty = false;
+    return COUP_OK;
+  }
   if (in_bytes + total > env->host_cap) {
     if (env->host_scratch) (void)hipHostFree(env->host_scratch);
     env->host_scratch = nullptr;
@@ -2555,13 +2695,9 @@ int coup_slot_op(coup_env* env, int64_t lane, const coup_env* src_env, int64_t s
       r.src_state = reinterpret_cast<uint64_t>(src_env->state + src_lane);
       r.src_hist = reinterpret_cast<uint64_t>(src_env->hist + src_lane * COUP_HISTORY_BYTES);
     }
-    r.action = action;
-    r.init = (flags & COUP_SLOT_INIT) ? 1 : 0;
-    if (result) {
-      r.out = reinterpret_cast<uint64_t>(sv->result_dev);
-      if (obs) r.obs = reinterpret_cast<uint64_t>(sv->result_dev + sizeof(coup_slot_result));
-      if (info) r.info = reinterpret_cast<uint64_t>(sv->result_dev + sizeof(coup_slot_result) + (obs ? obs_bytes : 0));
-    }
+    // the result and tensors land in the server's result area
+    r.op = ((uint32_t)action & 0xFFu) | ((flags & COUP_SLOT_INIT) ? coup::kSrvInit : 0u) |
+           (result ? coup::kSrvResult : 0u) | (obs ? coup::kSrvObs : 0u) | (info ? coup::kSrvInfo : 0u);
     uint32_t seq = 0;
     COUP_TRY(srv_post(sv, r, &seq));
     if (!result) return COUP_OK;

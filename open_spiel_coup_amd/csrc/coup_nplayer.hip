@@ -228,10 +228,10 @@ __device__ __forceinline__ uint32_t ending_action(const NLane<N>& L) {
   return (nib(hand(L, L.M), 0) & 1u) ? (uint32_t)kLoseCard2 : (uint32_t)kLoseCard1;
 }
 
-// INLINE = false: the round-2 schedule, the block's auto-resets dealt after
-// phase 2 by its first threads behind one more barrier (A/B:
-// COUP_NP_RESET_INLINE=0).
-template <int N, bool UNIFORM, bool AHEAD, int T = kThreads, bool INLINE = true>
+// INLINE = false (the default): the block's auto-resets dealt after phase 2
+// by its first threads behind one more barrier; INLINE = true: where the game
+// ends (COUP_NP_RESET_INLINE=1, measured slower).
+template <int N, bool UNIFORM, bool AHEAD, int T = kThreads, bool INLINE = false>
 #ifdef COUP_WAVE_TRACE
 // the stamps' registers must not cost the traced kernel its 8 blocks per CU
 #define NP_STEP_SORTED_BOUNDS __launch_bounds__(T, 8)
@@ -632,9 +632,12 @@ __device__ __forceinline__ void store_staged(const StepArgs& a, int64_t o, uint3
   if (w & kOutLegal) store_legal_player(a, o, legal, (int)(int8_t)(w >> 16));
 }
 
-// STAGE = false: the round-2 form, each output stored by the thread that
-// plays the lane (A/B: COUP_TRAJ_STAGE=0).
-template <int N, int T = kThreads, bool STAGE = true>
+// STAGE (A/B: COUP_TRAJ_STAGE=0): 1 (default) staged by lane, each lane's
+// outputs stored by its home thread (store_staged); 0 the round-2 form, each
+// output stored by the thread that plays the lane.  (A third form that also
+// packed the byte outputs of four lanes per dword store measured slower:
+// 27.5 vs 24.3 us per 2^20-lane step, profiles/r03/ab/traj_store_forms_6p.jsonl.)
+template <int N, int T = kThreads, int STAGE = 1>
 __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t steps) {
   static_assert((T & (T - 1)) == 0 && T >= 64 && T <= 1024, "power-of-two block of whole waves");
   constexpr uint32_t kO = T <= 256 ? 8u : 10u;  // lane bits of s_meta
@@ -662,11 +665,11 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
       key = m ? ahead_key(L, sample_action(m, rng.draw(L.episode, L.move))) : kKeyDead;
     }
   }
-  const bool home = base + t < a.n;  // thread t stores lane t's staged outputs
+  const uint32_t nvalid = base < a.n ? (uint32_t)(a.n - base < T ? a.n - base : T) : 0u;  // block-uniform
   for (int64_t s = 0; s < steps; ++s) {
     uint32_t* bin = s_bin[s & 1];
     __syncthreads();  // this step's bins are zero; last step's slots and outputs are complete
-    if (STAGE && s > 0 && home) store_staged<N>(a, (s - 1) * a.n + base + t, s_out[t], s_olegal[t]);
+    if (STAGE == 1 && s > 0 && t < nvalid) store_staged<N>(a, (s - 1) * a.n + base + t, s_out[t], s_olegal[t]);
     const uint32_t rank = atomicAdd(&bin[key], 1u);
     __syncthreads();
     const uint32_t pos = bins_below<7>(bin, key) + rank;  // keys up to kKeyFirst = 26
@@ -686,10 +689,10 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
     const int64_t o = s * a.n + li;
     rng.env_id = lane_stream_id(a.env_id_base, li);
     rng.blk_tag = 0u;
-    // every output of step s goes through out(): staged by lane (STAGE) or
-    // stored at once
+    // every output of step s goes through out(): staged by lane (STAGE > 0)
+    // or stored at once
     auto out = [&](uint32_t w, uint32_t legal) {
-      if (STAGE) {
+      if (STAGE != 0) {
         s_out[lane] = w;
         s_olegal[lane] = legal;
       } else {
@@ -743,7 +746,7 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
     if (s + 1 < steps) key = ahead_key(L, sample_action(legal, rng.draw(L.episode, L.move)));
   }
   __syncthreads();  // the last step's staged outputs are complete
-  if (STAGE && steps > 0 && home) store_staged<N>(a, (steps - 1) * a.n + base + t, s_out[t], s_olegal[t]);
+  if (STAGE == 1 && steps > 0 && t < nvalid) store_staged<N>(a, (steps - 1) * a.n + base + t, s_out[t], s_olegal[t]);
   if (steps > 0 && key == kKeyReset && base + lane < a.n) {  // finished on the last step
     L = new_episode<N>(L.episode + 1u, rng);
     store_legal_player(a, (steps - 1) * a.n + base + lane, decision_mask(L), (int)L.M);
@@ -988,14 +991,17 @@ hipError_t launch_step(const Env& e, const int8_t* actions, const coup_step_outp
       auto go = [&](auto lanes) {
         constexpr int TB = decltype(lanes)::value;
         const unsigned g = grid_for(e.n, TB);
-        const char* ri = std::getenv("COUP_NP_RESET_INLINE");  // 0: resets in a phase of their own (A/B)
-        const bool inl = ri ? std::atoi(ri) != 0 : true;
+        // COUP_NP_RESET_INLINE=1: resets dealt where the game ends (kKeyEnding),
+        // measured slower than the reset phase (34.07 vs 35.01 us per 2^20-lane
+        // step, same process: profiles/r03/ab/np_reset_inline.jsonl); A/B only
+        const char* ri = std::getenv("COUP_NP_RESET_INLINE");
+        const bool inl = ri ? std::atoi(ri) != 0 : false;
         if (actions)
           k_step_sorted<N, false, false, TB><<<g, TB, 0, e.stream>>>(a);
         else if (ahead && inl)
-          k_step_sorted<N, true, true, TB><<<g, TB, 0, e.stream>>>(a);
+          k_step_sorted<N, true, true, TB, true><<<g, TB, 0, e.stream>>>(a);
         else if (ahead)
-          k_step_sorted<N, true, true, TB, false><<<g, TB, 0, e.stream>>>(a);
+          k_step_sorted<N, true, true, TB><<<g, TB, 0, e.stream>>>(a);
         else
           k_step_sorted<N, true, false, TB><<<g, TB, 0, e.stream>>>(a);
       };
@@ -1039,11 +1045,10 @@ hipError_t launch_trajectory(const Env& e, int64_t steps, const coup_step_output
         case 256: k_trajectory_sorted<N, 256><<<grid_for(e.n, 256), 256, 0, e.stream>>>(a, steps); break;
         case 512: k_trajectory_sorted<N, 512><<<grid_for(e.n, 512), 512, 0, e.stream>>>(a, steps); break;
         default: {
-          // COUP_TRAJ_STAGE=0: outputs stored where the lane is played, not
-          // staged by lane (A/B of the round-2 form, 1024-lane blocks)
+          // COUP_TRAJ_STAGE=0: the round-2 stores (A/B, 1024-lane blocks)
           const char* st = std::getenv("COUP_TRAJ_STAGE");
           if (st && std::atoi(st) == 0)
-            k_trajectory_sorted<N, 1024, false><<<grid_for(e.n, 1024), 1024, 0, e.stream>>>(a, steps);
+            k_trajectory_sorted<N, 1024, 0><<<grid_for(e.n, 1024), 1024, 0, e.stream>>>(a, steps);
           else
             k_trajectory_sorted<N, 1024><<<grid_for(e.n, 1024), 1024, 0, e.stream>>>(a, steps);
           break;

@@ -68,6 +68,7 @@ class BatchedCoupEnv:
         self.device = torch.device(device if device is not None else "cuda")
         if self.device.type != "cuda":
             raise ValueError("BatchedCoupEnv runs on a HIP device only")
+        self._dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
         self.batch = int(batch)
         self.seed = int(seed)
         self.env_id_base = int(env_id_base)
@@ -100,7 +101,9 @@ class BatchedCoupEnv:
 
     # ------------------------------------------------------------ plumbing
     def _bind_stream(self):
-        s = torch.cuda.current_stream(self.device).cuda_stream
+        # the raw handle of torch's current stream (no Stream object: this runs
+        # before every launch of the per-game facades)
+        s = torch._C._cuda_getCurrentRawStream(self._dev_index)
         if s != getattr(self, "_bound_stream", None):
             _native.check(self.lib.coup_set_stream(self._h, ctypes.c_void_p(s)))
             self._bound_stream = s
@@ -157,16 +160,22 @@ class BatchedCoupEnv:
             out["info_state"] = self.info_state
         return out
 
-    def step_host(self, actions=None, obs=False, info_state=False):
+    def step_host(self, actions=None, obs=False, info_state=False, active_only=False):
         """`step` for small batches that want the answers on the host
         (coup_step_host: the kernel writes into mapped pinned memory, one
         launch and one synchronisation).  actions: host int8-convertible [B]
         (negative entries skip lanes) or None for the uniform policy.
         Returns numpy arrays: legal_mask, current_player, step_type, rewards,
-        actions, terminal (step type LAST), and obs / info_state if asked."""
+        actions, terminal (step type LAST), and obs / info_state if asked --
+        [B, ...], or with active_only (COUP_HOST_ACTIVE) only the rows of the
+        lanes whose action is >= 0, in lane order."""
         self._bind_stream()
         B, P = self.batch, self.num_players
         want = (_native.HOST_OBS if obs else 0) | (_native.HOST_INFO if info_state else 0)
+        if active_only:
+            if actions is None:
+                raise ValueError("active_only needs actions")
+            want |= _native.HOST_ACTIVE
         key = (want,)
         if getattr(self, "_sh_key", None) != key:
             off = (ctypes.c_size_t * 6)()
@@ -188,13 +197,14 @@ class BatchedCoupEnv:
                "actions": h[off[4]:off[4] + B].view(np.int8).copy()}
         out["terminal"] = (out["step_type"] == LAST).astype(np.uint8)
         o = off[5]
+        rows = int((self._sh_acts >= 0).sum()) if active_only else B
         if obs:
-            n = B * P * self.obs_size * 4
-            out["obs"] = h[o:o + n].view(np.float32).reshape(B, P, self.obs_size).copy()
+            n = rows * P * self.obs_size * 4
+            out["obs"] = h[o:o + n].view(np.float32).reshape(rows, P, self.obs_size).copy()
             o += (n + 15) // 16 * 16
         if info_state:
-            n = B * 2 * INFO_STATE_SIZE * 4
-            out["info_state"] = h[o:o + n].view(np.float32).reshape(B, 2, INFO_STATE_SIZE).copy()
+            n = rows * 2 * INFO_STATE_SIZE * 4
+            out["info_state"] = h[o:o + n].view(np.float32).reshape(rows, 2, INFO_STATE_SIZE).copy()
         return out
 
     def episode_stats(self):

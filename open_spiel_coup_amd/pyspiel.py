@@ -100,12 +100,44 @@ assert _SLOT_RESULT.itemsize == 128
 _RESULT_TAIL = struct.Struct("<IbBBBbbbb")  # legal_mask .. returns, at byte 112
 
 
+class _Result(dict):
+    """A coup_slot_result (128 bytes) as the facade's result dict.  The
+    scalars a walk reads at every node (legal mask, player, terminal, ok)
+    are unpacked at once; record, history, rewards and returns become numpy
+    views of the raw bytes on first use."""
+    __slots__ = ("_raw",)
+    _LAZY = {"record": (np.uint32, 4, 0), "history": (np.uint8, 96, 16), "rewards": (np.int8, 2, 120),
+             "returns": (np.int8, 2, 122)}
+
+    def __missing__(self, key):
+        dt, n, off = self._LAZY[key]
+        v = np.frombuffer(self._raw, dt, n, off)
+        self[key] = v
+        return v
+
+    def copy(self):
+        c = _Result(self)
+        c._raw = self._raw
+        return c
+
+
 def _parse_result(raw):
     """One coup_slot_result (128 bytes) -> the facade's result dict."""
-    lm, cp, term, ok, _, r0, r1, t0, t1 = _RESULT_TAIL.unpack_from(raw, 112)
-    return {"record": np.frombuffer(raw, np.uint32, 4, 0), "history": np.frombuffer(raw, np.uint8, 96, 16),
-            "legal_mask": lm, "current_player": cp, "terminal": bool(term), "ok": bool(ok),
-            "rewards": np.frombuffer(raw, np.int8, 2, 120), "returns": np.frombuffer(raw, np.int8, 2, 122)}
+    lm, cp, term, ok = _RESULT_TAIL.unpack_from(raw, 112)[:4]
+    q = _Result(legal_mask=lm, current_player=cp, terminal=bool(term), ok=bool(ok))
+    q._raw = raw
+    return q
+
+
+# mask (bits 0..17) -> ascending legal actions; masks repeat, so each is built once
+_LEGAL = {}
+
+
+def _legal_list(m):
+    t = _LEGAL.get(m)
+    if t is None:
+        t = _LEGAL[m] = tuple(a for a in range(18) if (m >> a) & 1)
+    return list(t)
 
 
 class _Pool:
@@ -383,7 +415,7 @@ class CoupState:
         else:  # Clone / snapshot: a device-side lane copy
             self._q = self._pool.op(self._slot, src=_src, result=_q is None)
             if _q is not None:
-                self._q = dict(_q)
+                self._q = _q.copy()
             self._history = _history
 
     def __del__(self):
@@ -439,10 +471,10 @@ class CoupState:
         return 18
 
     def current_player(self):
-        return int(self._query()["current_player"])
+        return self._q["current_player"]
 
     def is_terminal(self):
-        return bool(self._query()["terminal"])
+        return self._q["terminal"]
 
     def is_chance_node(self):
         return self.current_player() == PlayerId.CHANCE
@@ -457,17 +489,15 @@ class CoupState:
         return False
 
     def _mask(self):
-        return int(self._query()["legal_mask"]) & 0xFFFFFFFF
+        return self._q["legal_mask"] & 0xFFFFFFFF
 
     def legal_actions(self, player=None):
         """LegalActions() / LegalActions(player) (spiel.h:255-261)."""
-        cur = self.current_player()
-        if player is not None and player != cur:
+        q = self._q
+        cur = q["current_player"]
+        if (player is not None and player != cur) or cur == -4:  # PlayerId.TERMINAL
             return []
-        if cur == PlayerId.TERMINAL:
-            return []
-        m = self._mask() & 0x3FFFF
-        return [a for a in range(18) if (m >> a) & 1]
+        return _legal_list(q["legal_mask"] & 0x3FFFF)
 
     def legal_actions_mask(self, player=None):
         """LegalActionsMask (spiel.cc:371-377): length 5 at chance nodes."""
@@ -510,14 +540,15 @@ class CoupState:
     def child(self, action):
         """clone() + apply_action(action) as ONE op: the new state's lane is a
         copy of this one with the action applied."""
-        player = self.current_player()
+        q = self._q
+        player = q["current_player"]
         a = int(action)
-        if not 0 <= a < 18 or not (self._mask() >> a) & 1 or player == PlayerId.TERMINAL:
+        if not 0 <= a < 18 or not (q["legal_mask"] >> a) & 1 or player == -4:  # PlayerId.TERMINAL
             raise SpielError(f"illegal action {action}")
         pool = self._pool
         slot = pool.alloc()
         try:
-            q = pool.op(slot, src=(pool.handle(self._slot), self._slot[1]), action=a)
+            q = pool.op(slot, src=(pool.segs[self._slot[0]]._h, self._slot[1]), action=a)
             if not q["ok"]:
                 raise SpielError(f"illegal action {action}")
         except Exception:

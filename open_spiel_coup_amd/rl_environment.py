@@ -265,12 +265,15 @@ class Environment:
         if not 0 <= int(actions[0]) < 128:
             raise pyspiel.SpielError(f"illegal action {actions[0]}")  # not an int8 action id
         if self._sampler is None:
-            # one launch whose outputs land in mapped host memory (coup_step_host)
+            # one launch whose outputs land in mapped host memory (coup_step_host);
+            # on a SyncVectorEnv's shared env only this lane's tensor rows come
+            # back (COUP_HOST_ACTIVE), not every env's
+            shared = self._env.batch > 1
             q = self._env.step_host(self._lane_actions_host(actions[0]), obs=self._use_observation,
-                                    info_state=not self._use_observation)
+                                    info_state=not self._use_observation, active_only=shared)
             if not known_legal and self._env.error_count():
                 raise pyspiel.SpielError(f"illegal action {actions[0]}")
-            row = {k: v[self._lane] for k, v in q.items()}
+            row = {k: v[0 if shared and k in ("obs", "info_state") else self._lane] for k, v in q.items()}
             step_type = StepType.LAST if int(row["terminal"]) else StepType.MID
             self._should_reset = step_type == StepType.LAST
             return self._time_step(row, step_type, [float(x) for x in row["rewards"]])

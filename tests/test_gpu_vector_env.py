@@ -223,3 +223,28 @@ def test_step_host_equals_step(players, obs, info, uniform):
             assert np.array_equal(q["info_state"], o["info_state"].cpu().numpy()), t
     assert torch.equal(host.export_state(), dev.export_state())
     assert host.error_count() == dev.error_count() == 0
+
+
+@pytest.mark.parametrize("obs,info", [(True, False), (False, True), (True, True)], ids=["obs", "info", "both"])
+def test_step_host_active_rows(obs, info):
+    """coup_step_host with COUP_HOST_ACTIVE (an env of a shared SyncVectorEnv
+    env stepping alone): the small outputs of every lane as without it, and
+    the tensor rows of the stepped lanes only, in lane order -- equal to the
+    full step's rows of those lanes."""
+    n, seed = 64, 12
+    kw = dict(seed=seed, env_id_base=3, auto_reset=False, obs=False, history=True)
+    full, act = BatchedCoupEnv(n, **kw), BatchedCoupEnv(n, **kw)
+    rng = np.random.default_rng(seed)
+    for t in range(50):
+        legal = full.query(obs=False)["legal_mask"].cpu().numpy() & 0x3FFFF
+        keep = rng.random(n) < (0.05 if t % 2 else 0.5)
+        keep[t % n] = True
+        acts = np.where(keep, _random_legal(legal, rng), -1).astype(np.int8)
+        q = full.step_host(acts, obs=obs, info_state=info)
+        r = act.step_host(acts, obs=obs, info_state=info, active_only=True)
+        for k in ("legal_mask", "current_player", "step_type", "rewards", "actions"):
+            assert np.array_equal(q[k], r[k]), (t, k)
+        for k in (("obs",) if obs else ()) + (("info_state",) if info else ()):
+            assert np.array_equal(q[k][acts >= 0], r[k]), (t, k)
+    assert torch.equal(full.export_state(), act.export_state())
+    assert full.error_count() == act.error_count() == 0

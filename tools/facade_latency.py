@@ -92,6 +92,28 @@ def state_rows(tag, game, n):
     return rows
 
 
+def raw_rows(tag, game, n):
+    """coup_slot_op itself from a tight ctypes loop (no facade code): an
+    answered query (no action), an answered apply of the lane's first legal
+    action to a copy (child), an unanswered copy (clone)."""
+    import ctypes
+    from open_spiel_coup_amd import _native
+    st = _opening(game)
+    pool = st._pool
+    env = pool.segs[st._slot[0]]
+    env._bind_stream()
+    dst = pool.alloc()
+    h, lane, dh, dl, host = env._h, st._slot[1], pool.segs[dst[0]]._h, dst[1], pool.host_ptr
+    f = pool.lib.coup_slot_op
+    rows = {}
+    rows[f"raw_{tag}_query_us"] = _timed(lambda: f(h, lane, None, 0, -1, 0, host), n)
+    rows[f"raw_{tag}_child_us"] = _timed(lambda: f(dh, dl, h, lane, 0, 0, host), n)
+    rows[f"raw_{tag}_clone_us"] = _timed(lambda: f(dh, dl, h, lane, -1, _native.SLOT_NO_RESULT, None), n)
+    f(h, lane, None, 0, -1, 0, host)  # drain the clones
+    pool.release(dst)
+    return rows
+
+
 def batched_rows(game, n):
     st = _opening(game)
     rows = {}
@@ -173,6 +195,8 @@ def main():
         rows = {}
         rows.update(state_rows("server", g_srv, a.ops))
         rows.update(state_rows("launch", g_launch, a.ops))
+        rows.update(raw_rows("server", g_srv, a.ops))
+        rows.update(raw_rows("launch", g_launch, a.ops))
         rows.update(batched_rows(g_srv, a.ops))
         rows.update(rl_rows(a.ops // 2))
         if not a.no_vector:

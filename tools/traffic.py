@@ -65,15 +65,15 @@ def main():
         """Is `kn` the kernel bench.py times for this config?"""
         if fused == "traj":
             if players != 2:
-                return bool(re.search(r"np::k_(step_trajectory|trajectory_sorted)<%d(, \d+)?>|"
+                return bool(re.search(r"np::k_(step_trajectory|trajectory_sorted)<%d(, \w+)*>|"
                                       r"2np(17k_step_trajectory|19k_trajectory_sorted)ILi%dE" % (players, players), kn))
             return (("k_step_trajectory" in kn or "k_trajectory_sorted" in kn or "19k_trajectory_sorted" in kn)
                     and "np::" not in kn and "2np" not in kn)
         if players != 2:
             if fused:
-                return bool(re.search(r"np::k_rollout(_sorted)?<%d(, \d+)?>|2np(9k_rollout|16k_rollout_sorted)ILi%dE"
+                return bool(re.search(r"np::k_rollout(_sorted)?<%d(, \w+)*>|2np(9k_rollout|16k_rollout_sorted)ILi%dE"
                                       % (players, players), kn))
-            return bool(re.search(r"np::k_step(_sorted)?<%d, true(, (true|false))?(, \d+)?>|"
+            return bool(re.search(r"np::k_step(_sorted)?<%d, true(, \w+)*>|"
                                   r"2np(6k_step|13k_step_sorted)ILi%dELb1E" % (players, players), kn))
         if "np::" in kn or "2np" in kn:
             return False

@@ -36,13 +36,15 @@ def main():
         _native.check(env.lib.coup_step_trajectory(env._h, a.steps, ctypes.byref(none_out)))
     stats = env.new_stats()
     roll = env.rollout_launcher(a.steps, stats)
-    def unstaged():  # the round-2 store form of the regrouped kernel (COUP_TRAJ_STAGE=0)
-        os.environ["COUP_TRAJ_STAGE"] = "0"
-        try:
-            full()
-        finally:
-            os.environ.pop("COUP_TRAJ_STAGE", None)
-    variants = {"trajectory": full, "trajectory_unstaged": unstaged, "trajectory_no_outputs": bare,
+    def staged(form):  # other store forms of the regrouped kernel (COUP_TRAJ_STAGE)
+        def launch():
+            os.environ["COUP_TRAJ_STAGE"] = form
+            try:
+                full()
+            finally:
+                os.environ.pop("COUP_TRAJ_STAGE", None)
+        return launch
+    variants = {"trajectory": full, "trajectory_unstaged": staged("0"), "trajectory_no_outputs": bare,
                 "rollout_stats": roll}
     times = {k: [] for k in variants}
     s = torch.cuda.current_stream()
