@@ -123,6 +123,15 @@ def _regrouped(batch):
     return batch >= (1 << 18)
 
 
+def _np_step_lanes(players):
+    """Lanes per regrouping block of the N-player step kernel coup_step
+    launches (coup_nplayer.hip step_sort_lanes; COUP_NP_SORT_THREADS A/B)."""
+    e = os.environ.get("COUP_NP_SORT_THREADS")
+    if e in ("256", "512", "1024"):
+        return int(e)
+    return 1024 if players >= 6 else 512
+
+
 def _writer(mode_env):
     """(ObsMode template value, block size) of the step kernel that
     coup_step launches for COUP_OBS_MODE (default 9; csrc/coup_kernels.hip)."""
@@ -463,10 +472,12 @@ def main():
         sorted_ = "_sorted" if _regrouped(B) else ""
         if players != 2:
             ahead = os.environ.get("COUP_AHEAD", "1") != "0"
-            kernel = (("coup::np::k_trajectory_sorted<%d>" if sorted_ else "coup::np::k_step_trajectory<%d>") % players
+            kernel = (("coup::np::k_trajectory_sorted<%d, 1024>" if sorted_ else "coup::np::k_step_trajectory<%d>") % players
                       if fused == "traj" else
-                      "coup::np::k_rollout%s<%d>" % (sorted_, players) if fused else
-                      "coup::np::k_step_sorted<%d, true, %s>" % (players, "true" if ahead else "false") if sorted_ else
+                      ("coup::np::k_rollout_sorted<%d, 1024>" % players if sorted_ else
+                       "coup::np::k_rollout<%d>" % players) if fused else
+                      "coup::np::k_step_sorted<%d, true, %s, %d>" % (players, "true" if ahead else "false",
+                                                                    _np_step_lanes(players)) if sorted_ else
                       "coup::np::k_step<%d, true>" % players)
         elif fused == "traj":
             kernel = "coup::k_trajectory_sorted" if sorted_ else "coup::k_step_trajectory"

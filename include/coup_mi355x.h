@@ -122,6 +122,11 @@ typedef struct {
 #define COUP_SLOT_OBS 2        /* append ObservationTensor [2][98] float to the result */
 #define COUP_SLOT_INFO 4       /* append InformationStateTensor [2][2492] float (after obs if both) */
 #define COUP_SLOT_NO_RESULT 8  /* asynchronous: no result, host_out may be NULL */
+#define COUP_SLOT_RESET 16     /* first, start the lane's next episode (coup_reset on the lane: episode + 1,
+                                  NewInitialState); not with src_env or COUP_SLOT_INIT */
+#define COUP_SLOT_DEAL 32      /* last, resolve the pending chance deals under the sampling contract of the
+                                  lane's stream (seed, env_id_base + lane): rl_environment's chance sampling
+                                  until a decision node (rl_environment.py:369-382); entries to the history */
 
 /* One request of coup_slot_ops (24 bytes): the op coup_slot_op would run on
  * lane `lane` with src_lane (< 0: no copy), action (< 0: none) and flags

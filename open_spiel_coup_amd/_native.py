@@ -30,7 +30,7 @@ SYMBOLS = (
 )
 
 # coup_slot_op flags and result layout (coup_slot_result, 128 bytes)
-SLOT_INIT, SLOT_OBS, SLOT_INFO, SLOT_NO_RESULT = 1, 2, 4, 8
+SLOT_INIT, SLOT_OBS, SLOT_INFO, SLOT_NO_RESULT, SLOT_RESET, SLOT_DEAL = 1, 2, 4, 8, 16, 32
 HOST_OBS, HOST_INFO, HOST_ACTIVE = 1, 2, 4  # coup_step_host
 SLOT_RESULT_BYTES = 128
 

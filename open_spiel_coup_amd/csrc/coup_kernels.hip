@@ -1543,7 +1543,10 @@ struct SlotArgs {
   float* obs;              // [2][98] or null
   uint32_t* done = nullptr;  // k_slot: completion flag in mapped host memory (null: none)
   uint32_t seq = 0;          // the value k_slot stores there once its results are visible
+  uint32_t mode = 0;         // kSlotReset | kSlotDeal (COUP_SLOT_RESET / COUP_SLOT_DEAL)
+  uint32_t seed_lo = 0, seed_hi = 0, env_id = 0;  // the lane's sampling-contract stream (kSlotDeal)
 };
+constexpr uint32_t kSlotReset = 1u, kSlotDeal = 2u;
 
 // -DCOUP_SLOT_INLINE (investigation builds only): the
 // two pieces below inlined into the wave-uniform k_slot, the form the ROCm 7.2
@@ -1577,6 +1580,44 @@ __device__ COUP_SLOT_FN uint32_t slot_transition(uint4 w, uint32_t x, uint4* out
   const uint32_t ok = (L.err && !err_before) ? 0u : 1u;
   const uint32_t store = idx < (uint32_t)kHist ? 2u : 0u;
   return ok | store | (idx << 8) | (entry << 16);
+}
+
+// The rl_environment ops of a lane (COUP_SLOT_RESET / COUP_SLOT_DEAL):
+// kSlotReset starts the lane's next episode (coup_reset's k_reset, mode 1);
+// then decision x (< 18; 0xFF: none) is applied with its legality check;
+// then kSlotDeal resolves the pending chance deals under the sampling
+// contract, as rl_environment samples chance until a decision node
+// (rl_environment.py:369-382).  Every entry goes to the history bytes `hist`
+// (LDS).  Returns bit 0 = accepted without a new error; an illegal x leaves
+// the record untouched.  Out of line, like slot_transition.
+__device__ COUP_SLOT_FN uint32_t slot_step(uint4 w, uint32_t x, uint32_t mode, uint32_t seed_lo, uint32_t seed_hi,
+                                           uint32_t env_id, uint4* out, uint8_t* hist) {
+  Lane L = unpack(w);
+  if (mode & kSlotReset) {
+    L = initial_lane(L.episode + 1u);
+    L.err = L.episode == 0u ? 1u : 0u;  // counter wrap (coup_lane.h kEpisodeMask)
+  }
+  RegHistory rec;
+  uint32_t ok = 1u;
+  if (x < 18u) {
+    const uint32_t idx = L.move;
+    const uint32_t entry = is_chance(L) ? hist_deal(x, L.qids & 1u) : hist_decision(x, L.M);
+    const uint32_t err_before = L.err;
+    NoHistory none;
+    if (!apply_action(L, x, none)) {
+      *out = w;
+      return 0u;
+    }
+    rec.record(idx, entry);
+    ok = (L.err && !err_before) ? 0u : 1u;
+  }
+  if (mode & kSlotDeal) {
+    Rng rng{seed_lo, seed_hi, env_id, 0u, make_uint4(0, 0, 0, 0)};
+    resolve_chance(L, rng, rec);
+  }
+  rec.flush(hist);
+  *out = pack(L);
+  return ok;
 }
 
 __device__ COUP_SLOT_FN void slot_result(uint4 w, uint32_t ok, coup_slot_result* out) {
@@ -1617,7 +1658,10 @@ __device__ __forceinline__ void slot_op(const SlotArgs& a, uint8_t* __restrict__
   if (t == 0u) {
     uint4 rec = a.init ? pack(initial_lane(0u)) : *rs;
     uint32_t ok = 1u;
-    if (a.action >= 0) {
+    if (a.mode) {
+      ok = slot_step(rec, a.action >= 0 ? (uint32_t)a.action : 0xFFu, a.mode, a.seed_lo, a.seed_hi, a.env_id, &rec,
+                     hist);
+    } else if (a.action >= 0) {
       const uint32_t r = slot_transition(rec, (uint32_t)a.action, &rec);
       ok = r & 1u;
       if (r & 2u) hist[(r >> 8) & 0xFFu] = (uint8_t)(r >> 16);
@@ -1722,11 +1766,13 @@ struct SrvReq {        // one ring slot (host memory), 64 bytes = one host cache
   uint32_t seq_a;      // the sequence number, stored after the half's fields
   // second half
   uint64_t src_hist;
-  uint32_t pad[5];
+  uint32_t seed_lo, seed_hi, env_id;  // the lane's sampling-contract stream (deal / reset)
+  uint32_t pad[2];
   uint32_t seq_b;      // stored last of all
 };
 static_assert(sizeof(SrvReq) == 64, "SrvReq layout");
 constexpr uint32_t kSrvInit = 1u << 8, kSrvResult = 1u << 9, kSrvObs = 1u << 10, kSrvInfo = 1u << 11;
+constexpr uint32_t kSrvModeShift = 12;  // [13:12]: kSlotReset | kSlotDeal
 
 struct SrvCtl {        // host memory, one word per 128-byte line
   uint32_t served;     // last sequence number served (the wave writes)
@@ -1780,7 +1826,8 @@ constexpr int kAuxDevice = 16, kAuxSystem = 17;
 // (slot_transition / slot_result, as in k_slot: DESIGN.md section 12).
 __device__ __forceinline__ void server_op(uint64_t rs, uint64_t hs, uint64_t dst_state, uint64_t dst_hist,
                                           int32_t action, int32_t init, bool store, uint64_t out, uint64_t obs,
-                                          uint64_t info, uint8_t* hist, uint32_t* bits, uint32_t* pre,
+                                          uint64_t info, uint32_t mode, uint32_t seed_lo, uint32_t seed_hi,
+                                          uint32_t env_id, uint8_t* hist, uint32_t* bits, uint32_t* pre,
                                           coup_slot_result* res) {
   const uint32_t t = threadIdx.x;
   if (t < 6u)
@@ -1790,7 +1837,9 @@ __device__ __forceinline__ void server_op(uint64_t rs, uint64_t hs, uint64_t dst
   if (t == 0u) {
     uint4 rec = init ? pack(initial_lane(0u)) : ld16<kAuxDevice>(rs, 0u);
     uint32_t ok = 1u;
-    if (action >= 0) {
+    if (mode) {
+      ok = slot_step(rec, action >= 0 ? (uint32_t)action : 0xFFu, mode, seed_lo, seed_hi, env_id, &rec, hist);
+    } else if (action >= 0) {
       const uint32_t r = slot_transition(rec, (uint32_t)action, &rec);
       ok = r & 1u;
       if (r & 2u) hist[(r >> 8) & 0xFFu] = (uint8_t)(r >> 16);
@@ -1858,9 +1907,11 @@ __global__ __launch_bounds__(64) void k_server(ServerArgs s) {
     const uint64_t obs = (op & kSrvObs) ? res_base + sizeof(coup_slot_result) : 0u;
     const uint64_t info =
         (op & kSrvInfo) ? res_base + sizeof(coup_slot_result) + ((op & kSrvObs) ? 2u * kObsSize * 4u : 0u) : 0u;
-    const bool store = src_state != 0u || init != 0 || action >= 0;
+    const uint32_t mode = (op >> kSrvModeShift) & 3u;
+    const bool store = src_state != 0u || init != 0 || action >= 0 || mode != 0u;
     server_op(src_state ? src_state : dst_state, src_state ? src_hist : dst_hist, dst_state, dst_hist, action, init,
-              store, out, obs, info, hist, bits, pre, &res);
+              store, out, obs, info, mode, (uint32_t)word(10), (uint32_t)word(11), (uint32_t)word(12), hist, bits, pre,
+              &res);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     wave_sync();
     if (t == 0u) __hip_atomic_store(&s.ctl->served, next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -2662,8 +2713,12 @@ int coup_slot_op(coup_env* env, int64_t lane, const coup_env* src_env, int64_t s
   COUP_CHECK_ENV(env);
   if (env->generic || !env->hist)
     return fail(COUP_E_INVALID, "coup_slot_op: needs a 2-player env created with COUP_FLAG_HISTORY");
-  if (flags & ~(COUP_SLOT_INIT | COUP_SLOT_OBS | COUP_SLOT_INFO | COUP_SLOT_NO_RESULT))
+  if (flags & ~(COUP_SLOT_INIT | COUP_SLOT_OBS | COUP_SLOT_INFO | COUP_SLOT_NO_RESULT | COUP_SLOT_DEAL | COUP_SLOT_RESET))
     return fail(COUP_E_INVALID, "coup_slot_op: unknown flags");
+  if ((flags & COUP_SLOT_RESET) && (src_env || (flags & COUP_SLOT_INIT)))
+    return fail(COUP_E_INVALID, "coup_slot_op: COUP_SLOT_RESET takes no src_env and no COUP_SLOT_INIT");
+  const uint32_t mode = ((flags & COUP_SLOT_RESET) ? coup::kSlotReset : 0u) | ((flags & COUP_SLOT_DEAL) ? coup::kSlotDeal : 0u);
+  const uint32_t env_id = env->env_id_base + (uint32_t)lane;  // the lane's stream (sampling contract)
   if (lane < 0 || lane >= env->batch) return fail(COUP_E_INVALID, "coup_slot_op: lane out of range");
   if (src_env) {
     if (src_env->generic || !src_env->hist)
@@ -2697,7 +2752,11 @@ int coup_slot_op(coup_env* env, int64_t lane, const coup_env* src_env, int64_t s
     }
     // the result and tensors land in the server's result area
     r.op = ((uint32_t)action & 0xFFu) | ((flags & COUP_SLOT_INIT) ? coup::kSrvInit : 0u) |
-           (result ? coup::kSrvResult : 0u) | (obs ? coup::kSrvObs : 0u) | (info ? coup::kSrvInfo : 0u);
+           (result ? coup::kSrvResult : 0u) | (obs ? coup::kSrvObs : 0u) | (info ? coup::kSrvInfo : 0u) |
+           (mode << coup::kSrvModeShift);
+    r.seed_lo = (uint32_t)env->seed;
+    r.seed_hi = (uint32_t)(env->seed >> 32);
+    r.env_id = env_id;
     uint32_t seq = 0;
     COUP_TRY(srv_post(sv, r, &seq));
     if (!result) return COUP_OK;
@@ -2722,7 +2781,11 @@ int coup_slot_op(coup_env* env, int64_t lane, const coup_env* src_env, int64_t s
   a.src_hist = src_env ? src_env->hist + src_lane * COUP_HISTORY_BYTES : nullptr;
   a.action = action;
   a.init = (flags & COUP_SLOT_INIT) ? 1 : 0;
-  a.store = (src_env || a.init || action >= 0) ? 1 : 0;
+  a.store = (src_env || a.init || action >= 0 || mode) ? 1 : 0;
+  a.mode = mode;
+  a.seed_lo = (uint32_t)env->seed;
+  a.seed_hi = (uint32_t)(env->seed >> 32);
+  a.env_id = env_id;
   uint8_t* sc = env->slot_scratch_dev;
   a.out = result ? reinterpret_cast<coup_slot_result*>(sc) : nullptr;
   a.obs = obs ? reinterpret_cast<float*>(sc + sizeof(coup_slot_result)) : nullptr;

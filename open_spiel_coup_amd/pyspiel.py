@@ -170,6 +170,7 @@ class _Pool:
         # COUP_SERVER=0 keeps the launch path (A/B); COUP_SERVER_IDLE_US sets
         # how long the wave waits for the next op before it leaves.
         self.srv = None
+        self._attached = []  # weak references to other envs attached to the server (rl_environment)
         if os.environ.get("COUP_SERVER", "1") != "0":
             h = ctypes.c_void_p()
             with torch.cuda.device(self.device):
@@ -178,12 +179,21 @@ class _Pool:
             self.srv = h
         atexit.register(_close_pool, weakref.ref(self))
 
+    def attach(self, env):
+        """Route `env`'s single-lane ops (coup_slot_op) through this pool's op
+        server too (the per-game rl_environment envs); no-op without one."""
+        with self.lock:
+            if self.srv is not None:
+                _native.check(self.lib.coup_attach_server(env._h, self.srv))
+                self._attached.append(weakref.ref(env))
+
     def close(self):
-        """Stop the op server (its wave leaves) and detach the segments."""
+        """Stop the op server (its wave leaves) and detach the envs it serves."""
         with self.lock:
             if self.srv is None:
                 return
-            for env in self.segs:
+            others = [r() for r in self._attached]
+            for env in self.segs + [e for e in others if e is not None]:
                 if env._h:
                     _native.check(self.lib.coup_attach_server(env._h, None))
             _native.check(self.lib.coup_server_destroy(self.srv))
@@ -266,10 +276,21 @@ class _Pool:
     def _op(self, slot, src, action, init, obs, info, result):
         flags = ((_native.SLOT_INIT if init else 0) | (_native.SLOT_OBS if obs else 0)
                  | (_native.SLOT_INFO if info else 0) | (0 if result else _native.SLOT_NO_RESULT))
-        env = self.segs[slot[0]]
-        env._bind_stream()
         src_h, src_lane = src if src is not None else (None, 0)
-        _native.check(self.lib.coup_slot_op(env._h, slot[1], src_h, src_lane, int(action), flags,
+        return self._lane_op(self.segs[slot[0]], slot[1], src_h, src_lane, action, flags, obs, info, result)
+
+    def lane_op(self, env, lane, action=-1, flags=0, obs=False, info=False):
+        """One answered coup_slot_op on lane `lane` of `env` (any 2-player
+        history env, e.g. an rl_environment env attached with attach());
+        flags: extra COUP_SLOT_* (RESET / DEAL)."""
+        flags |= (_native.SLOT_OBS if obs else 0) | (_native.SLOT_INFO if info else 0)
+        with self.lock:
+            return self._lane_op(env, lane, None, 0, action, flags, obs, info, True)
+
+    def _lane_op(self, env, lane, src_h, src_lane, action, flags, obs, info, result):
+        if self.srv is None:
+            env._bind_stream()  # the server's ops launch nothing (pool lanes are private to the facade)
+        _native.check(self.lib.coup_slot_op(env._h, lane, src_h, src_lane, int(action), flags,
                                             self.host_ptr if result else None))
         if not result:
             return None

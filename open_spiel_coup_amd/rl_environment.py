@@ -33,7 +33,7 @@ import enum
 import numpy as np
 import torch
 
-from . import pyspiel
+from . import _native, pyspiel
 from .env import BatchedCoupEnv, HISTORY_BYTES
 
 
@@ -137,10 +137,14 @@ class Environment:
 
     # ------------------------------------------------------------ plumbing
     def _make_env(self):
-        # the step kernel writes no tensors here: each time step reads them
-        # (and everything else) with one query_host round trip
+        # one lane of a 2-player history env, attached to the device's op
+        # server (pyspiel's lane pool): reset and step are one coup_slot_op
+        # each (COUP_SLOT_RESET / COUP_SLOT_DEAL) whose 128-byte result and
+        # tensors come back in the same round trip
         self._env = BatchedCoupEnv(1, seed=self._seed, auto_reset=False, obs=False, info_state=False,
                                    history=True, device=self._device)
+        self._pool = pyspiel._pool(self._device)
+        self._pool.attach(self._env)
         self._lane = 0
         self._owner = None
         self._act = torch.empty(1, dtype=torch.int8, pin_memory=True)
@@ -150,6 +154,12 @@ class Environment:
         """Play on lane `lane` of `env` (a SyncVectorEnv's shared env, which
         already holds this game's record and history) from now on."""
         self._env, self._lane, self._owner = env, int(lane), owner
+
+    def _lane_op(self, action, flags):
+        """reset / step of this env's lane as one coup_slot_op, with the time
+        step's tensor."""
+        return self._pool.lane_op(self._env, self._lane, action, flags, obs=self._use_observation,
+                                  info=not self._use_observation)
 
     def _batchable(self):
         """Whether a SyncVectorEnv may adopt this env: in-kernel chance
@@ -265,18 +275,15 @@ class Environment:
         if not 0 <= int(actions[0]) < 128:
             raise pyspiel.SpielError(f"illegal action {actions[0]}")  # not an int8 action id
         if self._sampler is None:
-            # one launch whose outputs land in mapped host memory (coup_step_host);
-            # on a SyncVectorEnv's shared env only this lane's tensor rows come
-            # back (COUP_HOST_ACTIVE), not every env's
-            shared = self._env.batch > 1
-            q = self._env.step_host(self._lane_actions_host(actions[0]), obs=self._use_observation,
-                                    info_state=not self._use_observation, active_only=shared)
-            if not known_legal and self._env.error_count():
-                raise pyspiel.SpielError(f"illegal action {actions[0]}")
-            row = {k: v[0 if shared and k in ("obs", "info_state") else self._lane] for k, v in q.items()}
-            step_type = StepType.LAST if int(row["terminal"]) else StepType.MID
+            # the decision, then the chance deals that follow under the
+            # sampling contract, and the time step's answers: one op on the
+            # lane (the op server's wave when the pool has one)
+            q = self._lane_op(int(actions[0]), _native.SLOT_DEAL)
+            if not q["ok"]:
+                raise pyspiel.SpielError(f"illegal action {actions[0]}")  # the lane is unchanged
+            step_type = StepType.LAST if q["terminal"] else StepType.MID
             self._should_reset = step_type == StepType.LAST
-            return self._time_step(row, step_type, [float(x) for x in row["rewards"]])
+            return self._time_step(q, step_type, [float(x) for x in q["rewards"]])
         self._env.apply_action(self._lane_actions(actions[0]))
         self._sample_external_events()
         if not known_legal and self._env.error_count():
@@ -286,8 +293,7 @@ class Environment:
     def reset(self):
         self._should_reset = False
         if self._sampler is None:
-            self._env.reset(self._lane_mask())
-            q = self._query()
+            q = self._lane_op(-1, _native.SLOT_RESET | _native.SLOT_DEAL)
         else:
             self._env.new_initial_state()
             q = self._sample_external_events()

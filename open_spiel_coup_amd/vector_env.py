@@ -81,6 +81,7 @@ class SyncVectorEnv:
                                 device=envs[0]._device)
         shared.import_state(records)
         shared.import_history(hist)
+        envs[0]._pool.attach(shared)  # an env stepping alone goes through the op server too
         self._shared = shared
         for i, e in enumerate(envs):
             e._bind_lane(shared, i, self)

@@ -199,3 +199,46 @@ def test_no_wave_outlives_its_process():
         assert r.returncode == 0, r.stderr[-2000:]
         assert r.stdout.strip() == "[0, 1, 3, 5, 6]"
         assert time.perf_counter() - t0 < 60
+
+
+@pytest.mark.parametrize("otype", ["info", "obs"])
+def test_environment_lane_ops_equal_batched_steps(otype):
+    """rl_environment.Environment's reset and step are single lane ops
+    (COUP_SLOT_RESET | COUP_SLOT_DEAL, COUP_SLOT_DEAL; through the op
+    server): they deal exactly what coup_reset / coup_step deal on the same
+    stream.  A 1-lane BatchedCoupEnv with the same seed, driven by the same
+    actions, matches record and history for record, and every time step's
+    tensors equal its query."""
+    import torch
+    from open_spiel_coup_amd import BatchedCoupEnv
+    obs_type = (rl_environment.ObservationType.OBSERVATION if otype == "obs"
+                else rl_environment.ObservationType.INFORMATION_STATE)
+    env = rl_environment.Environment("coup", seed=123, observation_type=obs_type)
+    twin = BatchedCoupEnv(1, seed=123, auto_reset=False, obs=False, history=True)
+    assert env._pool.srv is not None
+    rng = np.random.default_rng(6)
+    ts = env.reset()
+    twin.reset()
+    episodes = 0
+    for k in range(300):
+        q = twin.query(obs=otype == "obs", info_state=otype == "info")
+        assert torch.equal(env._env.export_state(), twin.export_state()), k
+        mv = int(env.get_state.move_number())
+        assert torch.equal(env._env.export_history()[:, :mv], twin.export_history()[:, :mv]), k
+        t = q["obs" if otype == "obs" else "info_state"][0].cpu().numpy()
+        for p in (0, 1):
+            assert ts.observations["info_state"][p] == t[p].tolist(), k
+        cur = int(q["current_player"][0])
+        assert ts.observations["current_player"] == cur
+        if ts.last():
+            episodes += 1
+            ts = env.reset()
+            twin.reset()
+            continue
+        a = int(rng.choice(ts.observations["legal_actions"][cur]))
+        ts = env.step([a])
+        o = twin.step(torch.tensor([a], dtype=torch.int8))
+        assert ts.rewards == [float(x) for x in o["rewards"][0].cpu().tolist()]
+        assert ts.last() == (int(o["step_type"][0]) == 2)
+    assert episodes >= 3
+    assert twin.error_count() == 0

@@ -131,9 +131,19 @@ def main():
                                       key=lambda r: int(r[col(r, "start", "timestamp")]))
                         window = disp[-steps:]
                         if window:
-                            rp = sum(int(r[col(r, "end", "timestamp")]) - int(r[col(r, "start", "timestamp")])
-                                     for r in window) / len(window) * 1e-6
-                            summary["rocprof_compared_dispatch"] = f"mean of the last {len(window)} dispatches (the timed steps)"
+                            mean = sum(int(r[col(r, "end", "timestamp")]) - int(r[col(r, "start", "timestamp")])
+                                       for r in window) / len(window) * 1e-6
+                            # the bench times the span of the K launches / K (launch
+                            # gaps included: eager launches, or a graph replay); the
+                            # trace's first start to last end of the same K dispatches
+                            # is that span, its mean dispatch the kernel alone
+                            span = (int(window[-1][col(window[-1], "end", "timestamp")]) -
+                                    int(window[0][col(window[0], "start", "timestamp")])) / len(window) * 1e-6
+                            rp = span
+                            summary["rocprof_mean_dispatch_ms"] = mean
+                            summary["rocprof_launch_gap_ms"] = span - mean
+                            summary["rocprof_compared_dispatch"] = (f"span of the last {len(window)} dispatches (the "
+                                                                    "timed steps) / their count, as the bench times them")
                         else:
                             rp = summary["kernels"][tk]["avg_ns"] * 1e-6
                         summary["rocprof_all_dispatch_avg_ms"] = summary["kernels"][tk]["avg_ns"] * 1e-6
