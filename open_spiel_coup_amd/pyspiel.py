@@ -10,9 +10,10 @@ same surface with only an import swap:
     state = game.new_initial_state()
 
 A `CoupState` owns one lane of a device-resident lane pool; every rules
-operation (apply_action, legal actions, tensors, ...) is one coup_slot_op
-launch on that lane through the C ABI -- there is no CPU rules engine in
-the product.  The 128-byte result of the last op (record, history bytes,
+operation (apply_action, legal actions, tensors, ...) is one coup_slot_op on
+that lane through the C ABI, served by the pool's device-resident op server
+(one resident wave polling a request ring in host memory; COUP_SERVER=0 makes
+each op a kernel launch) -- there is no CPU rules engine in the product.  The 128-byte result of the last op (record, history bytes,
 legal mask, player, rewards, returns) is kept on the host and serves the
 accessors until the state changes; a clone is a device-side lane copy.  Strings are formatted on the host (strings.py).
 This is the compatibility path; batched learners use BatchedCoupEnv.
@@ -185,6 +186,7 @@ class _Pool:
         with self.lock:
             if self.srv is not None:
                 _native.check(self.lib.coup_attach_server(env._h, self.srv))
+                env._served = True
                 self._attached.append(weakref.ref(env))
 
     def close(self):
@@ -196,6 +198,7 @@ class _Pool:
             for env in self.segs + [e for e in others if e is not None]:
                 if env._h:
                     _native.check(self.lib.coup_attach_server(env._h, None))
+                env._served = False
             _native.check(self.lib.coup_server_destroy(self.srv))
             self.srv = None
 
@@ -216,6 +219,7 @@ class _Pool:
             env = BatchedCoupEnv(self.SEG, seed=0, auto_reset=False, obs=False, history=True, device=self.device)
             if self.srv is not None:
                 _native.check(self.lib.coup_attach_server(env._h, self.srv))
+                env._served = True
             k = len(self.segs)
             self.segs.append(env)
             self.free.extend((k, i) for i in range(self.SEG - 1, -1, -1))
@@ -288,8 +292,8 @@ class _Pool:
             return self._lane_op(env, lane, None, 0, action, flags, obs, info, True)
 
     def _lane_op(self, env, lane, src_h, src_lane, action, flags, obs, info, result):
-        if self.srv is None:
-            env._bind_stream()  # the server's ops launch nothing (pool lanes are private to the facade)
+        if not getattr(env, "_served", False):
+            env._bind_stream()  # a served env's ops launch nothing
         _native.check(self.lib.coup_slot_op(env._h, lane, src_h, src_lane, int(action), flags,
                                             self.host_ptr if result else None))
         if not result:

@@ -253,7 +253,9 @@ class Environment:
         self._should_reset = True
 
     def get_time_step(self):
-        q = self._query()
+        # an answered query op on the lane (no action): one round trip to the
+        # op server instead of a query launch
+        q = self._query() if self._sampler is not None else self._lane_op(-1, 0)
         step_type = StepType.LAST if int(q["terminal"]) else StepType.MID
         self._should_reset = step_type == StepType.LAST
         return self._time_step(q, step_type, [float(x) for x in q["rewards"]])
@@ -338,7 +340,8 @@ class Environment:
 
     @property
     def is_chance_node(self):
-        return int(self._query()["current_player"]) == pyspiel.PlayerId.CHANCE
+        q = self._query() if self._sampler is not None else self._lane_op(-1, 0)
+        return int(q["current_player"]) == pyspiel.PlayerId.CHANCE
 
     @property
     def game(self):

@@ -17,6 +17,11 @@ env's seed; the envs' own seeds no longer apply once
 adopted.  The reference's envs sample from independent RandomState(None)
 streams (rl_environment.py:119-131), which no caller can replay either.
 
+A vector env of at most LANE_OPS_UPTO envs steps them one lane op each
+(Environment.step on its lane, through the op server): below that size the
+lane ops' round trips cost less than a launch and a synchronisation.  Both
+forms give the same games (tests/test_gpu_vector_env.py).
+
 Envs with a caller-supplied chance sampler (the State API path), envs of
 different games / observation types / devices, or envs already adopted by
 another vector env are stepped in the reference's loop instead.
@@ -30,6 +35,9 @@ import torch
 
 from . import pyspiel
 from .env import BatchedCoupEnv
+
+
+LANE_OPS_UPTO = 2
 
 
 class SyncVectorEnv:
@@ -165,7 +173,7 @@ class SyncVectorEnv:
     # ------------------------------------------------------------ public API
     def step(self, step_outputs, reset_if_done=False):
         """vector_env.py:40-67: returns (time_steps, reward, done, unreset_time_steps)."""
-        if self._shared is None:
+        if self._shared is None or len(self.envs) <= LANE_OPS_UPTO:
             time_steps = [self.envs[i].step([step_outputs[i].action]) for i in range(len(self.envs))]
         else:
             time_steps = self._step_batched(step_outputs)
@@ -173,7 +181,7 @@ class SyncVectorEnv:
         done = [step.last() for step in time_steps]
         unreset_time_steps = time_steps
         if reset_if_done:
-            if self._shared is None:
+            if self._shared is None or len(self.envs) <= LANE_OPS_UPTO:
                 time_steps = self.reset(envs_to_reset=done)
             elif any(done):
                 # the envs that go on are unchanged since the step's query
@@ -187,7 +195,7 @@ class SyncVectorEnv:
         """vector_env.py:69-78"""
         if envs_to_reset is None:
             envs_to_reset = [True for _ in range(len(self.envs))]
-        if self._shared is None:
+        if self._shared is None or len(self.envs) <= LANE_OPS_UPTO:
             return [self.envs[i].reset() if envs_to_reset[i] else self.envs[i].get_time_step()
                     for i in range(len(self.envs))]
         resets = [bool(r) for r in envs_to_reset]

@@ -94,11 +94,14 @@ def _same_time_step(a, b):
 
 @pytest.mark.parametrize("obs_type", [rl_environment.ObservationType.INFORMATION_STATE,
                                       rl_environment.ObservationType.OBSERVATION], ids=["info", "obs"])
-def test_batched_sync_vector_env_equals_loop(obs_type):
-    """The batched vector env (one shared env, one launch per step) and the
+@pytest.mark.parametrize("n", [2, 24], ids=["lane-ops", "launch"])
+def test_batched_sync_vector_env_equals_loop(obs_type, n):
+    """The batched vector env (one shared env: one launch per step, or one
+    lane op per env at most vector_env.LANE_OPS_UPTO envs) and the
     reference's loop over the same games give identical time steps, with
     and without reset_if_done."""
-    n, seed = 24, 1234
+    assert (n <= vector_env.LANE_OPS_UPTO) == (n == 2)
+    seed = 1234
     batched = vector_env.SyncVectorEnv([rl_environment.Environment("coup", seed=seed, observation_type=obs_type)
                                         for _ in range(n)])
     loop = vector_env.SyncVectorEnv(_loop_envs(n, seed, obs_type), batched=False)
