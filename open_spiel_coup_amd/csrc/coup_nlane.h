@@ -626,14 +626,17 @@ __device__ __forceinline__ void resolve_chance(NLane<N>& L, NRng& rng) {
 // initial_lane + its 2N deals in straight-line form: deal k (slot k) goes to
 // seat k mod N, so seat s holds the face-down kinds of deals s and s + N in
 // ascending order.
-template <int N>
-__device__ __forceinline__ NLane<N> new_episode(uint32_t episode, NRng& rng) {
+// deal_episode: the same with deal k's draw from draw(k) (the episode's
+// draw index k), so a caller can compute the Philox blocks elsewhere
+// (k_step_sorted's grouped reset phase).
+template <int N, class Draw>
+__device__ __forceinline__ NLane<N> deal_episode(uint32_t episode, Draw&& draw) {
   NLane<N> L = initial_lane<N>(episode);
   L.err = L.episode == 0u ? 1u : 0u;  // the counter wrapped: this stream repeats episode 0's
   uint32_t t[2 * N];
 #pragma unroll
   for (int k = 0; k < 2 * N; ++k) {
-    t[k] = sample_card(L.deck, rng.draw(L.episode, (uint32_t)k));
+    t[k] = sample_card(L.deck, draw((uint32_t)k));
     L.deck -= 1u << (4u * t[k]);
   }
 #pragma unroll
@@ -644,6 +647,12 @@ __device__ __forceinline__ NLane<N> new_episode(uint32_t episode, NRng& rng) {
   L.init_left = 0u;
   L.move = 2u * N;
   return L;
+}
+
+template <int N>
+__device__ __forceinline__ NLane<N> new_episode(uint32_t episode, NRng& rng) {
+  const uint32_t ep = episode & kNpEpisodeMask;
+  return deal_episode<N>(episode, [&](uint32_t k) { return rng.draw(ep, k); });
 }
 
 // ObservationTensor (CoupObserver::WriteTensor, coup.cc:248-287, with

@@ -230,8 +230,13 @@ __device__ __forceinline__ uint32_t ending_action(const NLane<N>& L) {
 
 // INLINE = false (the default): the block's auto-resets dealt after phase 2
 // by its first threads behind one more barrier; INLINE = true: where the game
-// ends (COUP_NP_RESET_INLINE=1, measured slower).
-template <int N, bool UNIFORM, bool AHEAD, int T = kThreads, bool INLINE = false>
+// ends (COUP_NP_RESET_INLINE=1, measured slower).  RG: threads per reset in
+// that phase.  With RG = 4 thread q of a reset's group computes Philox block
+// q of the new episode's draws (its 2N deals and the decision drawn ahead,
+// draw 2N: at most 4 blocks), and the group shares them by cross-lane
+// shuffles, so a reset waits for one Philox instead of up to four in a row.
+// RG = 1 (COUP_NP_RESET_GROUP=1, A/B): one thread deals a reset alone.
+template <int N, bool UNIFORM, bool AHEAD, int T = kThreads, bool INLINE = false, int RG = 4>
 #ifdef COUP_WAVE_TRACE
 // the stamps' registers must not cost the traced kernel its 8 blocks per CU
 #define NP_STEP_SORTED_BOUNDS __launch_bounds__(T, 8)
@@ -370,7 +375,39 @@ __global__ NP_STEP_SORTED_BOUNDS void k_step_sorted(StepArgs a) {
 
   // the auto-resets, packed onto the first threads
   const uint32_t nreset = INLINE ? 0u : s_nreset;
-  for (uint32_t j = t; j < nreset; j += T) {
+  if (RG == 4) {
+    static_assert(RG == 1 || (2 * N) / 4 < 4, "a reset's draws fit four Philox blocks");
+    // whole groups: 4 * nreset and T are multiples of 4, so every shuffle's
+    // source lane runs the same iteration
+    for (uint32_t j = t; j < 4u * nreset; j += T) {
+      const uint32_t slot = s_reset[j >> 2], q = j & 3u;
+      const uint32_t env = lane_stream_id(a.env_id_base, base + (s_meta[slot] & (T - 1u)));
+      const uint32_t ep = (plane_episode(s_b[slot]) + 1u) & kNpEpisodeMask;
+      // NRng::draw's block q (draws 4q .. 4q + 3)
+      const uint4 blk = philox4x32_10(make_uint4(q, ep, a.seed_hi, 0x436F7570u), env, a.seed_lo);
+      const int g = (int)(t & 63u & ~3u);  // the group's first lane in the wave
+      uint32_t u[4 * ((2 * N) / 4 + 1)];
+#pragma unroll
+      for (int b = 0; b <= (2 * N) / 4; ++b) {
+        u[4 * b + 0] = __shfl(blk.x, g + b, 64);
+        u[4 * b + 1] = __shfl(blk.y, g + b, 64);
+        u[4 * b + 2] = __shfl(blk.z, g + b, 64);
+        u[4 * b + 3] = __shfl(blk.w, g + b, 64);
+      }
+      const NLane<N> R = deal_episode<N>(ep, [&](uint32_t k) { return u[k]; });
+      if (q == 0u) {
+        uint4 wa, wb;
+        pack(R, wa, wb);
+        const uint32_t legal = decision_mask(R);  // a new episode is at a decision node
+        if (UNIFORM && AHEAD) wb.w |= (ahead_key(R, sample_action(legal, u[2 * N])) + 1u) << kAheadShift;
+        s_a[slot] = wa;
+        s_b[slot] = wb;
+        s_legal[slot] = legal;
+        s_out[slot] = (s_out[slot] & 0x00FFFFFFu) | ((R.M & 0xFFu) << 24);
+      }
+    }
+  }
+  for (uint32_t j = t; RG == 1 && j < nreset; j += T) {
     const uint32_t slot = s_reset[j];
     NRng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, base + (s_meta[slot] & (T - 1u))), 0u,
              make_uint4(0, 0, 0, 0)};
@@ -996,10 +1033,14 @@ hipError_t launch_step(const Env& e, const int8_t* actions, const coup_step_outp
         // step, same process: profiles/r03/ab/np_reset_inline.jsonl); A/B only
         const char* ri = std::getenv("COUP_NP_RESET_INLINE");
         const bool inl = ri ? std::atoi(ri) != 0 : false;
+        const char* rg = std::getenv("COUP_NP_RESET_GROUP");  // 1: one thread per reset (A/B)
+        const bool single = rg ? std::atoi(rg) == 1 : false;
         if (actions)
           k_step_sorted<N, false, false, TB><<<g, TB, 0, e.stream>>>(a);
         else if (ahead && inl)
           k_step_sorted<N, true, true, TB, true><<<g, TB, 0, e.stream>>>(a);
+        else if (ahead && single)
+          k_step_sorted<N, true, true, TB, false, 1><<<g, TB, 0, e.stream>>>(a);
         else if (ahead)
           k_step_sorted<N, true, true, TB><<<g, TB, 0, e.stream>>>(a);
         else

@@ -595,6 +595,8 @@ class CoupState:
         if not actions:
             return []
         pool = self._pool
+        if len(actions) == 1 and pool.srv is not None and not (obs or info_state):
+            return [self.child(actions[0])]  # one op server request beats a launch
         slots = [pool.alloc() for _ in actions]
         out = [None] * len(actions)
         try:

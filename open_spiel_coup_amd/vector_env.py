@@ -181,8 +181,14 @@ class SyncVectorEnv:
         done = [step.last() for step in time_steps]
         unreset_time_steps = time_steps
         if reset_if_done:
-            if self._shared is None or len(self.envs) <= LANE_OPS_UPTO:
+            if self._shared is None:
                 time_steps = self.reset(envs_to_reset=done)
+            elif len(self.envs) <= LANE_OPS_UPTO:
+                # lane ops: an env that goes on keeps its time step, unless
+                # that was a FIRST, which get_time_step reports as MID (as the
+                # reference's reset(envs_to_reset) does)
+                time_steps = [e.reset() if d else (e.get_time_step() if t.first() else t)
+                              for e, d, t in zip(self.envs, done, time_steps)]
             elif any(done):
                 # the envs that go on are unchanged since the step's query
                 self._reset_lanes(done)

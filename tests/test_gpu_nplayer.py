@@ -297,29 +297,34 @@ def test_six_player_full_batch_sampled_lanes_match_spec(fused):
 @pytest.mark.parametrize("n_players", [3, 6])
 @pytest.mark.parametrize("lanes", ["256", "1024"])
 def test_regrouped_step_reset_schedule_invariant(monkeypatch, n_players, lanes):
-    """The regrouped uniform step deals an auto-reset where the game ends
-    (decisions that end a game drawn ahead as kKeyEnding and sorted into the
-    same waves; the default) == the round-2 schedule, the block's resets in
-    a phase of their own (COUP_NP_RESET_INLINE=0), lane by lane -- and so
-    does an env alternating the two kernels, where a kKeyEnding decision
-    parked by one is played by the other.  Outputs, records, accumulators."""
+    """The regrouped uniform step's auto-reset schedules agree lane by lane:
+    the block's resets in a phase of their own, each dealt by a group of 4
+    threads sharing the Philox blocks (the default), or by one thread
+    (COUP_NP_RESET_GROUP=1); and resets dealt where the game ends
+    (COUP_NP_RESET_INLINE=1, decisions that end a game drawn ahead as
+    kKeyEnding).  So does an env alternating the kernels, where a decision
+    parked by one is played by another.  Outputs, records, accumulators."""
     n, steps, seed = 3000, 200, 40 + n_players
     monkeypatch.setenv("COUP_REGROUP", "1")
     monkeypatch.setenv("COUP_NP_SORT_THREADS", lanes)
+    forms = {"phase": ("0", "4"), "single": ("0", "1"), "inline": ("1", "4")}
     envs = {knob: BatchedCoupEnv(n, seed=seed, env_id_base=9 << 20, auto_reset=True, obs=False,
                                  num_players=n_players, generic=True, episode_stats=True)
-            for knob in ("1", "0", "alt")}
+            for knob in ("phase", "single", "inline", "alt")}
+    cycle = ("phase", "inline", "single")
     for t in range(steps):
         outs = {}
         for knob, env in envs.items():
-            monkeypatch.setenv("COUP_NP_RESET_INLINE", knob if knob != "alt" else str(t % 2))
+            inline, group = forms[knob if knob != "alt" else cycle[t % 3]]
+            monkeypatch.setenv("COUP_NP_RESET_INLINE", inline)
+            monkeypatch.setenv("COUP_NP_RESET_GROUP", group)
             outs[knob] = {k: v.clone() for k, v in env.step().items()}
-        for knob in ("0", "alt"):
+        for knob in ("single", "inline", "alt"):
             for k in ("actions", "rewards", "step_type", "legal_mask", "current_player"):
-                assert torch.equal(outs["1"][k], outs[knob][k]), (knob, t, k)
-            assert torch.equal(envs["1"].export_state(), envs[knob].export_state()), (knob, t)
-    for knob in ("0", "alt"):
-        for x, y in zip(envs["1"].episode_stats(), envs[knob].episode_stats()):
+                assert torch.equal(outs["phase"][k], outs[knob][k]), (knob, t, k)
+            assert torch.equal(envs["phase"].export_state(), envs[knob].export_state()), (knob, t)
+    for knob in ("single", "inline", "alt"):
+        for x, y in zip(envs["phase"].episode_stats(), envs[knob].episode_stats()):
             assert torch.equal(x, y), knob
-    assert int(envs["1"].episode_stats()[0].sum()) > 100
+    assert int(envs["phase"].episode_stats()[0].sum()) > 100
     assert all(env.error_count() == 0 for env in envs.values())

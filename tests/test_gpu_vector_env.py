@@ -123,7 +123,7 @@ def test_batched_sync_vector_env_equals_loop(obs_type, n):
             _same_time_step(x, y)
         for x, y in zip(ua, ub):
             _same_time_step(x, y)
-    assert lasts > 10
+    assert lasts > 2 * n  # episodes end (~15 decisions each) and restart
 
 
 def test_adopted_envs_keep_their_games():
