@@ -293,7 +293,11 @@ __global__ NP_STEP_SORTED_BOUNDS void k_step_sorted(StepArgs a) {
   __syncthreads();
   const uint32_t rank = atomicAdd(&s_bin[key], 1u);
   __syncthreads();
-  if (t < 64u) {  // exclusive scan of the 20 bin counts in wave 0
+  // exclusive scan of the bin counts in wave 0.  (Every wave scanning the
+  // bins for itself, wave_bins_below, saves this barrier but measured slower:
+  // 34.12 vs 33.78 us per 2^20-lane step, profiles/r03/ab/
+  // np_step_wave_scan_rejected.jsonl.)
+  if (t < 64u) {
     const uint32_t v = t < 32u ? s_bin[t] : 0u;
     uint32_t inc = v;
 #pragma unroll
@@ -552,7 +556,29 @@ __device__ __forceinline__ uint32_t draw_key(const NLane<N>& L, NRng& rng, uint3
 // 8 waves per SIMD (64 VGPRs, a few spilled): 29.1 vs 30.3 us per step at
 // 6 waves.  Carrying each lane's cached Philox block through LDS with the
 // record measured no faster (30.2 us) and was dropped.
-template <int N, int T = kThreads>
+// bins_below (coup_regroup.h) computed by each wave for itself: lane j < 32 reads bin j,
+// a shuffle scan over the wave, and each lane picks its key's exclusive
+// prefix.  One LDS read and six cross-lane shuffles per wave instead of Q
+// 16-byte reads and 4Q selects per lane.  Used by the N-player sorted
+// rollout, where it measured faster; the 6-player step (wave-0 scan behind a
+// barrier) and the trajectory (bins_below) measured slower with it
+// (DESIGN.md section 5).  All 32 bins must be valid counts (zeroed when unused).
+__device__ __forceinline__ uint32_t wave_bins_below(const uint32_t* bin, uint32_t key) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t v = lane < 32u ? bin[lane] : 0u;
+  uint32_t inc = v;
+#pragma unroll
+  for (int d = 1; d < 32; d <<= 1) {
+    const uint32_t u = __shfl_up(inc, d, 64);
+    if (lane >= (uint32_t)d) inc += u;
+  }
+  return __shfl(inc - v, (int)key, 64);
+}
+
+// WS: the bin prefix per wave (wave_bins_below, default: 20.69 vs 21.46 us
+// per 6-player 2^20-lane step, profiles/r03/ab/np_scan_forms_traj_rollout.jsonl)
+// or per lane (bins_below, round 2; COUP_NP_SCAN=0 at 1024-lane blocks, A/B).
+template <int N, int T = kThreads, bool WS = true>
 __global__ __launch_bounds__(T, 8) void k_rollout_sorted(RolloutArgs a) {
   static_assert((T & (T - 1)) == 0 && T >= 64 && T <= 1024, "power-of-two block of whole waves");
   constexpr uint32_t kO = T <= 256 ? 8u : 10u;  // lane bits of s_meta
@@ -581,7 +607,7 @@ __global__ __launch_bounds__(T, 8) void k_rollout_sorted(RolloutArgs a) {
     __syncthreads();  // this step's bins are zero; last step's slots are read
     const uint32_t rank = atomicAdd(&bin[key], 1u);
     __syncthreads();
-    const uint32_t pos = bins_below<7>(bin, key) + rank;  // keys up to kKeyChallengeLost = 25
+    const uint32_t pos = (WS ? wave_bins_below(bin, key) : bins_below<7>(bin, key)) + rank;  // keys up to kKeyChallengeLost = 25
     if (t < 32u) s_bin[(s + 1) & 1][t] = 0u;  // read for the last time in step s - 1
     uint4 wa, wb;
     pack(L, wa, wb);
@@ -709,6 +735,8 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
     if (STAGE == 1 && s > 0 && t < nvalid) store_staged<N>(a, (s - 1) * a.n + base + t, s_out[t], s_olegal[t]);
     const uint32_t rank = atomicAdd(&bin[key], 1u);
     __syncthreads();
+    // (wave_bins_below here spills 38 VGPRs instead of 22 and measured 26.07
+    // vs 24.12 us per step: profiles/r03/ab/np_scan_forms_traj_rollout.jsonl)
     const uint32_t pos = bins_below<7>(bin, key) + rank;  // keys up to kKeyFirst = 26
     if (t < 32u) s_bin[(s + 1) & 1][t] = 0u;  // read for the last time in step s - 1
     uint4 wa, wb;
@@ -1124,7 +1152,12 @@ hipError_t launch_rollout(const Env& e, int64_t steps, const coup_rollout_stats*
       switch (sort_lanes("COUP_NP_SORT_THREADS", kRolloutSortLanes)) {
         case 512: k_rollout_sorted<N, 512><<<grid_for(e.n, 512), 512, 0, e.stream>>>(a); break;
         case 256: k_rollout_sorted<N, 256><<<grid, 256, 0, e.stream>>>(a); break;
-        default: k_rollout_sorted<N, 1024><<<grid_for(e.n, 1024), 1024, 0, e.stream>>>(a); break;
+        default:
+          if (!np_scan_mode())  // COUP_NP_SCAN=0: the per-lane bin prefix (A/B)
+            k_rollout_sorted<N, 1024, false><<<grid_for(e.n, 1024), 1024, 0, e.stream>>>(a);
+          else
+            k_rollout_sorted<N, 1024><<<grid_for(e.n, 1024), 1024, 0, e.stream>>>(a);
+          break;
       }
     } else {
       k_rollout<N><<<grid, kThreads, 0, e.stream>>>(a);

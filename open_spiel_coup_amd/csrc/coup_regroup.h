@@ -52,6 +52,13 @@ __device__ __forceinline__ uint32_t bins_below(const uint32_t* bin, uint32_t key
   return below;
 }
 
+// COUP_NP_SCAN: 1 (default) the N-player rollout's per-wave scan
+// (wave_bins_below), 0 its round-2 per-lane sums (A/B runs).
+inline uint32_t np_scan_mode() {
+  const char* e = std::getenv("COUP_NP_SCAN");
+  return e ? (uint32_t)(std::atoi(e) != 0) : 1u;
+}
+
 // Host side: regroup a launch of n lanes?  Measured on MI355X (tools/ab_step.py,
 // DESIGN.md section 5): the sort's barriers and LDS round trips cost more
 // than the divergence they remove below ~4 waves per SIMD (2^18 lanes on 256

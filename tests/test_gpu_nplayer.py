@@ -328,3 +328,29 @@ def test_regrouped_step_reset_schedule_invariant(monkeypatch, n_players, lanes):
             assert torch.equal(x, y), knob
     assert int(envs["phase"].episode_stats()[0].sum()) > 100
     assert all(env.error_count() == 0 for env in envs.values())
+
+
+@pytest.mark.parametrize("n_players", [3, 6])
+def test_regrouped_rollout_scan_forms_equal(monkeypatch, n_players):
+    """The sorted rollout's bin prefix computed by every wave for itself
+    (wave_bins_below, the default) == its round-2 per-lane sums
+    (COUP_NP_SCAN=0), 1024-lane blocks, ragged batch, starting mid-game:
+    records and statistics after launches of 1, 9 and 60 steps."""
+    n, seed = 2500, 71 + n_players
+    monkeypatch.setenv("COUP_REGROUP", "1")
+    monkeypatch.setenv("COUP_NP_SORT_THREADS", "1024")
+    envs = {knob: BatchedCoupEnv(n, seed=seed, env_id_base=3 << 20, auto_reset=True, obs=False,
+                                 num_players=n_players, generic=True) for knob in ("1", "0")}
+    for env in envs.values():
+        for _ in range(20):
+            env.step()
+    stats = {knob: env.new_stats() for knob, env in envs.items()}
+    for k in (1, 9, 60):
+        for knob, env in envs.items():
+            monkeypatch.setenv("COUP_NP_SCAN", knob)
+            env.rollout(k, stats[knob])
+        assert torch.equal(envs["1"].export_state(), envs["0"].export_state()), k
+        for key in ("episodes", "return_sum", "length_sum"):
+            assert torch.equal(stats["1"][key], stats["0"][key]), (k, key)
+    assert int(stats["1"]["episodes"].sum()) > 0
+    assert all(env.error_count() == 0 for env in envs.values())

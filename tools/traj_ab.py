@@ -1,8 +1,9 @@
 """Same-process A/B of the fused trajectory launch (coup_step_trajectory)
 against itself with no output buffers bound, against its round-2 store form
 (outputs stored where each lane is played instead of staged by lane in LDS,
-COUP_TRAJ_STAGE=0) and against the fused rollout (statistics only): the cost
-of storing every step's outputs.  Measurement tool only.
+COUP_TRAJ_STAGE=0) and against the fused rollout (statistics only; also with
+its round-2 bin prefix, COUP_NP_SCAN=0): the cost of storing every step's
+outputs.  Measurement tool only.
 
     python tools/traj_ab.py [--players 6] [--batch 2^20] [--steps 50] [--rounds 7]
 """
@@ -36,16 +37,17 @@ def main():
         _native.check(env.lib.coup_step_trajectory(env._h, a.steps, ctypes.byref(none_out)))
     stats = env.new_stats()
     roll = env.rollout_launcher(a.steps, stats)
-    def staged(form):  # other store forms of the regrouped kernel (COUP_TRAJ_STAGE)
+    def knob(var, val, fn):  # another form of the regrouped kernel, chosen at launch
         def launch():
-            os.environ["COUP_TRAJ_STAGE"] = form
+            os.environ[var] = val
             try:
-                full()
+                fn()
             finally:
-                os.environ.pop("COUP_TRAJ_STAGE", None)
+                os.environ.pop(var, None)
         return launch
-    variants = {"trajectory": full, "trajectory_unstaged": staged("0"), "trajectory_no_outputs": bare,
-                "rollout_stats": roll}
+    variants = {"trajectory": full, "trajectory_unstaged": knob("COUP_TRAJ_STAGE", "0", full),
+                "trajectory_no_outputs": bare,
+                "rollout_stats": roll, "rollout_lane_scan": knob("COUP_NP_SCAN", "0", roll)}
     times = {k: [] for k in variants}
     s = torch.cuda.current_stream()
     for _ in range(a.rounds):
