@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define COUP_ABI_VERSION 8
+#define COUP_ABI_VERSION 9
 
 #define COUP_NUM_PLAYERS 2          /* coup.h:42 */
 #define COUP_MAX_PLAYERS 6          /* N-player extension */
@@ -45,6 +45,9 @@ extern "C" {
 #define COUP_FLAG_AUTO_RESET 1      /* SyncVectorEnv(reset_if_done=True) semantics */
 #define COUP_FLAG_HISTORY 2         /* keep per-lane histories (InformationStateTensor, strings) */
 #define COUP_FLAG_GENERIC 4         /* use the N-player engine also at N = 2 (cross-checks) */
+#define COUP_FLAG_UNCHECKED 8       /* caller actions (coup_step, coup_step_host, coup_apply_action) outside
+                                       LegalActions() are applied as pyspiel's apply_action does (no legality
+                                       check, DoApplyAction's own checks decide; COUP_SLOT_UNCHECKED); 2 players */
 
 /* rl_environment.StepType (rl_environment.py:96-103) */
 #define COUP_STEP_FIRST 0
@@ -127,10 +130,14 @@ typedef struct {
 #define COUP_SLOT_DEAL 32      /* last, resolve the pending chance deals under the sampling contract of the
                                   lane's stream (seed, env_id_base + lane): rl_environment's chance sampling
                                   until a decision node (rl_environment.py:369-382); entries to the history */
+#define COUP_SLOT_UNCHECKED 64 /* apply `action` as pyspiel's apply_action (pyspiel.cc:266, spiel.cc:322-331): no
+                                  LegalActions() check, DoApplyAction's own checks decide (coup.cc:490-809);
+                                  result.ok = 0, the lane untouched, where the reference raises, on a terminal
+                                  state, or where the result leaves the record's fields */
 
 /* One request of coup_slot_ops (24 bytes): the op coup_slot_op would run on
  * lane `lane` with src_lane (< 0: no copy), action (< 0: none) and flags
- * (COUP_SLOT_INIT only; the output flags are per call). */
+ * (COUP_SLOT_INIT / COUP_SLOT_UNCHECKED; the output flags are per call). */
 typedef struct {
   int64_t lane;
   int64_t src_lane;

@@ -326,11 +326,13 @@ class CoupState {
   int NumPlayers() const { return COUP_NUM_PLAYERS; }
   int NumDistinctActions() const { return COUP_NUM_ACTIONS; }
 
-  // LegalActions (coup.cc:824-938): ascending
+  // LegalActions (coup.cc:824-938): ascending; throws at a decision node no
+  // legal play reaches (coup.cc:886, 892, 936), as the reference does
   std::vector<Action> LegalActions() const {
     std::vector<Action> out;
     if (IsTerminal()) return out;
     const uint32_t m = Q().legal_mask & 0x3FFFFu;
+    if (m == 0u && IsPlayerNode()) throw SpielError("Error in LegalActions(): Invalid action progression");
     for (int a = 0; a < COUP_NUM_ACTIONS; ++a)
       if ((m >> a) & 1u) out.push_back(a);
     return out;
@@ -356,32 +358,38 @@ class CoupState {
     return out;
   }
 
-  // State::ApplyAction (spiel.cc:322-331); throws for an illegal action
+  // State::ApplyAction (spiel.cc:322-331): no LegalActions() check, as the
+  // reference's; DoApplyAction's own checks decide (COUP_SLOT_UNCHECKED).
+  // Throws, the state unchanged, where the reference throws (coup.cc:
+  // 490-809), on a terminal state, or where the result leaves the packed
+  // record's fields.
   void ApplyAction(Action a) {
     const Player p = CurrentPlayer();
-    if (a < 0 || a >= COUP_NUM_ACTIONS || !((Q().legal_mask >> a) & 1u) || p == kTerminalPlayerId)
-      throw SpielError("ApplyAction: illegal action " + std::to_string(a));
+    CheckId(a, "ApplyAction");
     coup_slot_result r;
-    detail::ThePool().Op(slot_, nullptr, (int)a, 0, &r);
-    if (!r.ok) {
-      detail::ThePool().Op(slot_, nullptr, -1, 0, &q_);
-      throw SpielError("ApplyAction: illegal action " + std::to_string(a));
-    }
+    detail::ThePool().Op(slot_, nullptr, (int)a, COUP_SLOT_UNCHECKED, &r);
+    if (!r.ok) throw SpielError("ApplyAction(" + std::to_string(a) + "): DoApplyAction raises here");
     q_ = r;
     history_.push_back({p, a});
+  }
+  // State::ApplyActionWithLegalityCheck (spiel.cc:334-344)
+  void ApplyActionWithLegalityCheck(Action a) {
+    if (!Legal(a))
+      throw SpielError("Current player " + std::to_string(CurrentPlayer()) + " calling ApplyAction with illegal action (" +
+                       std::to_string(a) + ")");
+    ApplyAction(a);
   }
   // Clone + ApplyAction as ONE op: the child's lane is a copy of this one
   // with `a` applied
   std::unique_ptr<CoupState> Child(Action a) const {
     const Player p = CurrentPlayer();
-    if (a < 0 || a >= COUP_NUM_ACTIONS || !((Q().legal_mask >> a) & 1u) || p == kTerminalPlayerId)
-      throw SpielError("Child: illegal action " + std::to_string(a));
+    CheckId(a, "Child");
     detail::Pool& pool = detail::ThePool();
     const detail::Pool::Slot slot = pool.Alloc();
     coup_slot_result r;
     try {
-      pool.Op(slot, &slot_, (int)a, 0, &r);
-      if (!r.ok) throw SpielError("Child: illegal action " + std::to_string(a));
+      pool.Op(slot, &slot_, (int)a, COUP_SLOT_UNCHECKED, &r);
+      if (!r.ok) throw SpielError("Child(" + std::to_string(a) + "): DoApplyAction raises here");
     } catch (...) {
       pool.Release(slot);
       throw;
@@ -395,9 +403,8 @@ class CoupState {
   // segment: the expansion of a Deep CFR traverser node (deep_cfr.py:440-471)
   std::vector<std::unique_ptr<CoupState>> Children(const std::vector<Action>& actions) const {
     const Player p = CurrentPlayer();
-    for (Action a : actions)
-      if (a < 0 || a >= COUP_NUM_ACTIONS || !((Q().legal_mask >> a) & 1u) || p == kTerminalPlayerId)
-        throw SpielError("Children: illegal action " + std::to_string(a));
+    const int32_t rf = COUP_SLOT_UNCHECKED;
+    for (Action a : actions) CheckId(a, "Children");
     detail::Pool& pool = detail::ThePool();
     std::vector<detail::Pool::Slot> slots;
     for (size_t k = 0; k < actions.size(); ++k) slots.push_back(pool.Alloc());
@@ -410,14 +417,15 @@ class CoupState {
         std::vector<size_t> ks;
         for (size_t j = k; j < slots.size(); ++j)
           if (slots[j].seg == slots[k].seg) {
-            reqs.push_back({slots[j].lane, slot_.lane, (int32_t)actions[j], 0});
+            reqs.push_back({slots[j].lane, slot_.lane, (int32_t)actions[j], rf});
             ks.push_back(j);
             done.push_back(j);
           }
         std::vector<coup_slot_result> part(reqs.size());
         pool.Ops(slots[k].seg, reqs, slot_.seg, 0, part.data());
         for (size_t j = 0; j < ks.size(); ++j) {
-          if (!part[j].ok) throw SpielError("Children: illegal action " + std::to_string(actions[ks[j]]));
+          if (!part[j].ok)
+            throw SpielError("Children(" + std::to_string(actions[ks[j]]) + "): DoApplyAction raises here");
           res[ks[j]] = part[j];
         }
       }
@@ -481,6 +489,14 @@ class CoupState {
       : game_(game), slot_(slot), history_(std::move(history)), q_(q) {}
   // the result of the last op on this lane (every op refreshes it)
   const coup_slot_result& Q() const { return q_; }
+  // in LegalActions() (ApplyActionWithLegalityCheck)
+  bool Legal(Action a) const {
+    return a >= 0 && a < COUP_NUM_ACTIONS && ((Q().legal_mask >> a) & 1u) && CurrentPlayer() != kTerminalPlayerId;
+  }
+  // ids outside 0..17: DoApplyAction raises at any node (coup.cc:493, 806; spiel.cc:327)
+  static void CheckId(Action a, const char* what) {
+    if (a < 0 || a >= COUP_NUM_ACTIONS) throw SpielError(std::string(what) + ": invalid action " + std::to_string(a));
+  }
   std::array<uint32_t, 4> Rec() const { return {q_.record[0], q_.record[1], q_.record[2], q_.record[3]}; }
 
   const CoupGame* game_;

@@ -11,8 +11,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # COUP_LIB_PATH: load another build of the same library (A/B timing of two
 # builds, tools/ab_builds.sh); there is still no fallback
 LIB_PATH = os.environ.get("COUP_LIB_PATH") or os.path.join(HERE, "libcoup_mi355x.so")
-ABI_VERSION = 8
-FLAG_AUTO_RESET, FLAG_HISTORY, FLAG_GENERIC = 1, 2, 4
+ABI_VERSION = 9
+FLAG_AUTO_RESET, FLAG_HISTORY, FLAG_GENERIC, FLAG_UNCHECKED = 1, 2, 4, 8
 MAX_PLAYERS = 6
 HISTORY_BYTES = 96
 
@@ -30,7 +30,7 @@ SYMBOLS = (
 )
 
 # coup_slot_op flags and result layout (coup_slot_result, 128 bytes)
-SLOT_INIT, SLOT_OBS, SLOT_INFO, SLOT_NO_RESULT, SLOT_RESET, SLOT_DEAL = 1, 2, 4, 8, 16, 32
+SLOT_INIT, SLOT_OBS, SLOT_INFO, SLOT_NO_RESULT, SLOT_RESET, SLOT_DEAL, SLOT_UNCHECKED = 1, 2, 4, 8, 16, 32, 64
 HOST_OBS, HOST_INFO, HOST_ACTIVE = 1, 2, 4  # coup_step_host
 SLOT_RESULT_BYTES = 128
 

@@ -528,6 +528,8 @@ struct StepArgs {
   int ep_mode;         // episode accumulators: kEpEarly / kEpEarlyAll / kEpLate (COUP_EP_MODE, A/B)
   uint32_t* err_count;
   int xcd_remap;   // block -> lane group mapping (xcd_group)
+  int unchecked;   // caller actions outside LegalActions go through the reference's unchecked ApplyAction
+                   // (COUP_FLAG_UNCHECKED; in-place kernels with caller actions only)
 #ifdef COUP_WAVE_TRACE
   // measurement builds only (tools/wave_trace.py): per wave, 100 MHz
   // timestamps at entry, end of the step, end of store issue, stores
@@ -588,6 +590,22 @@ enum ObsMode : int {
 constexpr bool is_wave_bits(int m) { return m == kObsWaveBits || m == kObsWaveBitsPlain || m == kObsWaveBitsSc1; }
 constexpr int wave_bits_policy(int m) { return m == kObsWaveBitsPlain ? 0 : (m == kObsWaveBitsSc1 ? 2 : 1); }
 
+// A caller action under COUP_FLAG_UNCHECKED: the reference's unchecked
+// ApplyAction (apply_action_unchecked, coup_lane.h) on record w into *out;
+// returns whether it was applied (false: the reference raises, *out not
+// written).  Every caller action of such an env takes it, legal or not --
+// LegalActions can offer an action DoApplyAction then refuses once
+// unchecked play has left legal play's states (a Challenge of a Block of a
+// Tax: coup.cc:930-933 offers it, :691-692 raises).  Out of line, so the
+// caller-action kernels keep one transition's registers.
+__device__ __noinline__ uint32_t unchecked_decision(uint4 w, uint32_t x, uint4* out) {
+  Lane L = unpack(w);
+  NoHistory none;
+  if (!apply_action_unchecked(L, x, none)) return 0u;
+  *out = pack(L);
+  return 1u;
+}
+
 // The per-lane part of one env step: returns the decision applied (-1 if
 // none), the step type, player 0's reward and, at LAST, player 0's return of
 // the finished game; L is updated in place and every applied action is
@@ -628,17 +646,26 @@ __device__ __forceinline__ void step_lane(const StepArgs& a, int64_t i, Lane& L,
   }
   COUP_TRACE_ANY(a, 6);
   st = COUP_STEP_MID;
-  if (x > 17u || ((m >> x) & 1u) == 0u || is_terminal(L)) {
+  const uint32_t err_before = L.err;
+  if (!UNIFORM && a.unchecked) {
+    uint4 w;
+    if (!unchecked_decision(pack(L), x, &w)) {
+      count_error(a.err_count);
+      return;
+    }
+    hist.record(L.move, hist_decision(x, L.M));
+    L = unpack(w);
+  } else if (x > 17u || ((m >> x) & 1u) == 0u || is_terminal(L)) {
     count_error(a.err_count);
     return;
+  } else {
+    hist.record(L.move, hist_decision(x, L.M));
+    if (FLOW)
+      apply_decision_v1(L, x);
+    else
+      apply_decision(L, x);
+    L.move += 1u;
   }
-  const uint32_t err_before = L.err;
-  hist.record(L.move, hist_decision(x, L.M));
-  if (FLOW)
-    apply_decision_v1(L, x);
-  else
-    apply_decision(L, x);
-  L.move += 1u;
   COUP_TRACE_ANY(a, 7);
   resolve_chance(L, rng, hist);
   COUP_TRACE_ANY(a, 8);
@@ -1372,7 +1399,7 @@ __global__ __launch_bounds__(kThreads) void k_reset(uint4* state, int64_t n, con
 // State::ApplyAction per lane (decision or chance outcome); the entry goes
 // to the lane's history bytes when the env keeps a history.
 __global__ __launch_bounds__(kThreads) void k_apply(uint4* state, int64_t n, const int8_t* actions,
-                                                  uint8_t* hist, uint32_t* err_count) {
+                                                  uint8_t* hist, uint32_t* err_count, int unchecked) {
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= n) return;
   const int x = actions[i];
@@ -1384,7 +1411,14 @@ __global__ __launch_bounds__(kThreads) void k_apply(uint4* state, int64_t n, con
   const uint32_t idx = L.move;
   const uint32_t entry = is_chance(L) ? hist_deal((uint32_t)x, L.qids & 1u) : hist_decision((uint32_t)x, L.M);
   NoHistory none;
-  if (!apply_action(L, (uint32_t)x, none)) {
+  if (unchecked) {  // COUP_FLAG_UNCHECKED: the reference's unchecked ApplyAction
+    uint4 w;
+    if (!unchecked_decision(pack(L), (uint32_t)x, &w)) {
+      count_error(err_count);
+      return;
+    }
+    L = unpack(w);
+  } else if (!apply_action(L, (uint32_t)x, none)) {
     count_error(err_count);
     return;
   }
@@ -1543,10 +1577,10 @@ struct SlotArgs {
   float* obs;              // [2][98] or null
   uint32_t* done = nullptr;  // k_slot: completion flag in mapped host memory (null: none)
   uint32_t seq = 0;          // the value k_slot stores there once its results are visible
-  uint32_t mode = 0;         // kSlotReset | kSlotDeal (COUP_SLOT_RESET / COUP_SLOT_DEAL)
+  uint32_t mode = 0;         // kSlotReset | kSlotDeal | kSlotUnchecked (COUP_SLOT_RESET / _DEAL / _UNCHECKED)
   uint32_t seed_lo = 0, seed_hi = 0, env_id = 0;  // the lane's sampling-contract stream (kSlotDeal)
 };
-constexpr uint32_t kSlotReset = 1u, kSlotDeal = 2u;
+constexpr uint32_t kSlotReset = 1u, kSlotDeal = 2u, kSlotUnchecked = 4u;
 
 // -DCOUP_SLOT_INLINE (investigation builds only): the
 // two pieces below inlined into the wave-uniform k_slot, the form the ROCm 7.2
@@ -1563,29 +1597,31 @@ constexpr uint32_t kSlotReset = 1u, kSlotDeal = 2u;
 #endif
 
 // Out-of-line pieces of k_slot.  slot_transition applies action x to the
-// packed record `w` (State::ApplyAction with its legality check) into *out
-// and returns bit 0 = accepted without a new error, bit 1 = history entry to
+// packed record `w` (State::ApplyAction with its legality check, or without
+// it when `unchecked`: apply_action_unchecked, coup_lane.h) into *out and
+// returns bit 0 = accepted without a new error, bit 1 = history entry to
 // store, bits 8..15 its index, bits 16..23 the entry byte.
-__device__ COUP_SLOT_FN uint32_t slot_transition(uint4 w, uint32_t x, uint4* out) {
+__device__ COUP_SLOT_FN uint32_t slot_transition(uint4 w, uint32_t x, uint32_t unchecked, uint4* out) {
   Lane L = unpack(w);
   const uint32_t idx = L.move;
   const uint32_t entry = is_chance(L) ? hist_deal(x, L.qids & 1u) : hist_decision(x, L.M);
   const uint32_t err_before = L.err;
   NoHistory none;
-  if (!apply_action(L, x, none)) {  // an illegal action leaves the record untouched
+  if (!(unchecked ? apply_action_unchecked(L, x, none) : apply_action(L, x, none)) || (L.err && !err_before)) {
+    // a rejected action (or one the reference's DoApplyAction raises on)
+    // leaves the record untouched
     *out = w;
     return 0u;
   }
   *out = pack(L);
-  const uint32_t ok = (L.err && !err_before) ? 0u : 1u;
   const uint32_t store = idx < (uint32_t)kHist ? 2u : 0u;
-  return ok | store | (idx << 8) | (entry << 16);
+  return 1u | store | (idx << 8) | (entry << 16);
 }
 
 // The rl_environment ops of a lane (COUP_SLOT_RESET / COUP_SLOT_DEAL):
 // kSlotReset starts the lane's next episode (coup_reset's k_reset, mode 1);
-// then decision x (< 18; 0xFF: none) is applied with its legality check;
-// then kSlotDeal resolves the pending chance deals under the sampling
+// then decision x (< 18; 0xFF: none) is applied with its legality check
+// (without it under kSlotUnchecked); then kSlotDeal resolves the pending chance deals under the sampling
 // contract, as rl_environment samples chance until a decision node
 // (rl_environment.py:369-382).  Every entry goes to the history bytes `hist`
 // (LDS).  Returns bit 0 = accepted without a new error; an illegal x leaves
@@ -1604,12 +1640,12 @@ __device__ COUP_SLOT_FN uint32_t slot_step(uint4 w, uint32_t x, uint32_t mode, u
     const uint32_t entry = is_chance(L) ? hist_deal(x, L.qids & 1u) : hist_decision(x, L.M);
     const uint32_t err_before = L.err;
     NoHistory none;
-    if (!apply_action(L, x, none)) {
-      *out = w;
+    if (!((mode & kSlotUnchecked) ? apply_action_unchecked(L, x, none) : apply_action(L, x, none)) ||
+        (L.err && !err_before)) {
+      *out = w;  // untouched, the reset included
       return 0u;
     }
     rec.record(idx, entry);
-    ok = (L.err && !err_before) ? 0u : 1u;
   }
   if (mode & kSlotDeal) {
     Rng rng{seed_lo, seed_hi, env_id, 0u, make_uint4(0, 0, 0, 0)};
@@ -1658,11 +1694,11 @@ __device__ __forceinline__ void slot_op(const SlotArgs& a, uint8_t* __restrict__
   if (t == 0u) {
     uint4 rec = a.init ? pack(initial_lane(0u)) : *rs;
     uint32_t ok = 1u;
-    if (a.mode) {
+    if (a.mode & (kSlotReset | kSlotDeal)) {
       ok = slot_step(rec, a.action >= 0 ? (uint32_t)a.action : 0xFFu, a.mode, a.seed_lo, a.seed_hi, a.env_id, &rec,
                      hist);
     } else if (a.action >= 0) {
-      const uint32_t r = slot_transition(rec, (uint32_t)a.action, &rec);
+      const uint32_t r = slot_transition(rec, (uint32_t)a.action, a.mode & kSlotUnchecked, &rec);
       ok = r & 1u;
       if (r & 2u) hist[(r >> 8) & 0xFFu] = (uint8_t)(r >> 16);
     }
@@ -1725,6 +1761,7 @@ __global__ __launch_bounds__(64) void k_slot_batch(SlotBatchArgs b) {
   a.src_hist = r.src_lane >= 0 ? b.src_hist + r.src_lane * kHist : nullptr;
   a.action = r.action;
   a.init = (r.flags & COUP_SLOT_INIT) ? 1 : 0;
+  a.mode = (r.flags & COUP_SLOT_UNCHECKED) ? kSlotUnchecked : 0u;
   a.store = (r.src_lane >= 0 || a.init || r.action >= 0) ? 1 : 0;
   a.out = b.out ? b.out + blockIdx.x : nullptr;
   a.obs = OBS ? b.obs + (size_t)blockIdx.x * (2 * kObsSize) : nullptr;
@@ -1772,7 +1809,7 @@ struct SrvReq {        // one ring slot (host memory), 64 bytes = one host cache
 };
 static_assert(sizeof(SrvReq) == 64, "SrvReq layout");
 constexpr uint32_t kSrvInit = 1u << 8, kSrvResult = 1u << 9, kSrvObs = 1u << 10, kSrvInfo = 1u << 11;
-constexpr uint32_t kSrvModeShift = 12;  // [13:12]: kSlotReset | kSlotDeal
+constexpr uint32_t kSrvModeShift = 12;  // [14:12]: kSlotReset | kSlotDeal | kSlotUnchecked
 
 struct SrvCtl {        // host memory, one word per 128-byte line
   uint32_t served;     // last sequence number served (the wave writes)
@@ -1837,10 +1874,10 @@ __device__ __forceinline__ void server_op(uint64_t rs, uint64_t hs, uint64_t dst
   if (t == 0u) {
     uint4 rec = init ? pack(initial_lane(0u)) : ld16<kAuxDevice>(rs, 0u);
     uint32_t ok = 1u;
-    if (mode) {
+    if (mode & (kSlotReset | kSlotDeal)) {
       ok = slot_step(rec, action >= 0 ? (uint32_t)action : 0xFFu, mode, seed_lo, seed_hi, env_id, &rec, hist);
     } else if (action >= 0) {
-      const uint32_t r = slot_transition(rec, (uint32_t)action, &rec);
+      const uint32_t r = slot_transition(rec, (uint32_t)action, mode & kSlotUnchecked, &rec);
       ok = r & 1u;
       if (r & 2u) hist[(r >> 8) & 0xFFu] = (uint8_t)(r >> 16);
     }
@@ -1907,8 +1944,8 @@ __global__ __launch_bounds__(64) void k_server(ServerArgs s) {
     const uint64_t obs = (op & kSrvObs) ? res_base + sizeof(coup_slot_result) : 0u;
     const uint64_t info =
         (op & kSrvInfo) ? res_base + sizeof(coup_slot_result) + ((op & kSrvObs) ? 2u * kObsSize * 4u : 0u) : 0u;
-    const uint32_t mode = (op >> kSrvModeShift) & 3u;
-    const bool store = src_state != 0u || init != 0 || action >= 0 || mode != 0u;
+    const uint32_t mode = (op >> kSrvModeShift) & 7u;
+    const bool store = src_state != 0u || init != 0 || action >= 0 || (mode & (kSlotReset | kSlotDeal)) != 0u;
     server_op(src_state ? src_state : dst_state, src_state ? src_hist : dst_hist, dst_state, dst_hist, action, init,
               store, out, obs, info, mode, (uint32_t)word(10), (uint32_t)word(11), (uint32_t)word(12), hist, bits, pre,
               &res);
@@ -2225,11 +2262,13 @@ int coup_create_ex(int64_t batch, uint64_t seed, uint32_t env_id_base, int flags
   if (batch < 0 || batch > (int64_t(1) << 32)) return fail(COUP_E_INVALID, "coup_create: batch out of range");
   if ((int64_t)env_id_base + batch > (int64_t(1) << 32))
     return fail(COUP_E_INVALID, "coup_create: env_id_base + batch exceeds 2^32 (lanes would share random streams)");
-  if (flags & ~(COUP_FLAG_AUTO_RESET | COUP_FLAG_HISTORY | COUP_FLAG_GENERIC))
+  if (flags & ~(COUP_FLAG_AUTO_RESET | COUP_FLAG_HISTORY | COUP_FLAG_GENERIC | COUP_FLAG_UNCHECKED))
     return fail(COUP_E_INVALID, "coup_create: unknown flags");
   if (num_players < 2 || num_players > COUP_MAX_PLAYERS)
     return fail(COUP_E_INVALID, "coup_create: num_players must be 2..6");
   const bool generic = num_players != 2 || (flags & COUP_FLAG_GENERIC);
+  if (generic && (flags & COUP_FLAG_UNCHECKED))
+    return fail(COUP_E_INVALID, "coup_create: COUP_FLAG_UNCHECKED is the 2-player engine's (the reference's rules)");
   if (generic && (flags & COUP_FLAG_HISTORY))
     return fail(COUP_E_INVALID, "coup_create: COUP_FLAG_HISTORY is 2-player only (no N-player InformationStateTensor)");
   coup_env* env = new coup_env();
@@ -2372,12 +2411,13 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
   if (a.info && !a.hist)
     return fail(COUP_E_INVALID, "coup_step: info_state needs an env created with COUP_FLAG_HISTORY");
   const bool uniform = actions == nullptr;
+  a.unchecked = (!uniform && (env->flags & COUP_FLAG_UNCHECKED)) ? 1 : 0;
   const int info = a.info ? coup::kInfoWrite : (a.hist ? coup::kInfoHistory : coup::kInfoNone);
   int mode = a.obs == nullptr ? coup::kObsNone : obs_mode();
   if (info != coup::kInfoNone && mode != coup::kObsNone) mode = coup::kObsWaveBits;
   hipStream_t s = env->stream;
   const int64_t n = env->batch;
-  if (info == coup::kInfoNone && mode == coup::kObsNone && coup::regroup_lanes(n)) {
+  if (info == coup::kInfoNone && mode == coup::kObsNone && !a.unchecked && coup::regroup_lanes(n)) {
     // COUP_SORT_THREADS: lanes per regrouping block (A/B; coup_regroup.h)
     const int lanes = coup::sort_lanes("COUP_SORT_THREADS", coup::kStepSortLanes);
     auto go = [&](auto tb) {
@@ -2633,8 +2673,8 @@ int coup_apply_action(coup_env* env, const int8_t* actions) {
   if (env->batch == 0) return COUP_OK;
   COUP_TRY(launching(env));
   if (env->generic) return np_result(coup::np::launch_apply(np_env(env), actions), "coup_apply_action");
-  coup::k_apply<<<grid_for(env->batch), coup::kThreads, 0, env->stream>>>(env->state, env->batch, actions,
-                                                                          env->hist, env->err_count);
+  coup::k_apply<<<grid_for(env->batch), coup::kThreads, 0, env->stream>>>(
+      env->state, env->batch, actions, env->hist, env->err_count, (env->flags & COUP_FLAG_UNCHECKED) ? 1 : 0);
   COUP_HIP_TRY(hipGetLastError());
   return COUP_OK;
 }
@@ -2713,11 +2753,13 @@ int coup_slot_op(coup_env* env, int64_t lane, const coup_env* src_env, int64_t s
   COUP_CHECK_ENV(env);
   if (env->generic || !env->hist)
     return fail(COUP_E_INVALID, "coup_slot_op: needs a 2-player env created with COUP_FLAG_HISTORY");
-  if (flags & ~(COUP_SLOT_INIT | COUP_SLOT_OBS | COUP_SLOT_INFO | COUP_SLOT_NO_RESULT | COUP_SLOT_DEAL | COUP_SLOT_RESET))
+  if (flags & ~(COUP_SLOT_INIT | COUP_SLOT_OBS | COUP_SLOT_INFO | COUP_SLOT_NO_RESULT | COUP_SLOT_DEAL | COUP_SLOT_RESET |
+                COUP_SLOT_UNCHECKED))
     return fail(COUP_E_INVALID, "coup_slot_op: unknown flags");
   if ((flags & COUP_SLOT_RESET) && (src_env || (flags & COUP_SLOT_INIT)))
     return fail(COUP_E_INVALID, "coup_slot_op: COUP_SLOT_RESET takes no src_env and no COUP_SLOT_INIT");
-  const uint32_t mode = ((flags & COUP_SLOT_RESET) ? coup::kSlotReset : 0u) | ((flags & COUP_SLOT_DEAL) ? coup::kSlotDeal : 0u);
+  const uint32_t mode = ((flags & COUP_SLOT_RESET) ? coup::kSlotReset : 0u) | ((flags & COUP_SLOT_DEAL) ? coup::kSlotDeal : 0u) |
+                        ((flags & COUP_SLOT_UNCHECKED) ? coup::kSlotUnchecked : 0u);
   const uint32_t env_id = env->env_id_base + (uint32_t)lane;  // the lane's stream (sampling contract)
   if (lane < 0 || lane >= env->batch) return fail(COUP_E_INVALID, "coup_slot_op: lane out of range");
   if (src_env) {
@@ -2781,7 +2823,7 @@ int coup_slot_op(coup_env* env, int64_t lane, const coup_env* src_env, int64_t s
   a.src_hist = src_env ? src_env->hist + src_lane * COUP_HISTORY_BYTES : nullptr;
   a.action = action;
   a.init = (flags & COUP_SLOT_INIT) ? 1 : 0;
-  a.store = (src_env || a.init || action >= 0 || mode) ? 1 : 0;
+  a.store = (src_env || a.init || action >= 0 || (mode & (coup::kSlotReset | coup::kSlotDeal))) ? 1 : 0;
   a.mode = mode;
   a.seed_lo = (uint32_t)env->seed;
   a.seed_hi = (uint32_t)(env->seed >> 32);
@@ -2846,7 +2888,8 @@ int coup_slot_ops(coup_env* env, int64_t n, const coup_slot_req* reqs, const cou
   for (int64_t k = 0; k < n; ++k) {
     const coup_slot_req& r = reqs[k];
     if (r.lane < 0 || r.lane >= env->batch) return fail(COUP_E_INVALID, "coup_slot_ops: lane out of range");
-    if (r.flags & ~COUP_SLOT_INIT) return fail(COUP_E_INVALID, "coup_slot_ops: request flags other than INIT");
+    if (r.flags & ~(COUP_SLOT_INIT | COUP_SLOT_UNCHECKED))
+      return fail(COUP_E_INVALID, "coup_slot_ops: request flags other than INIT / UNCHECKED");
     if (r.action < -1 || r.action >= COUP_NUM_ACTIONS) return fail(COUP_E_INVALID, "coup_slot_ops: action out of range");
     if (r.src_lane >= 0) {
       if (!src_env) return fail(COUP_E_INVALID, "coup_slot_ops: a request copies but src_env is null");

@@ -778,6 +778,156 @@ __device__ __forceinline__ bool apply_action(Lane& L, uint32_t a, H& hist) {
   return true;
 }
 
+// ------------------------------------------------ unchecked ApplyAction
+//
+// pyspiel binds apply_action to State::ApplyAction (pyspiel.cc:266,
+// spiel.cc:322-331), which applies an action WITHOUT checking LegalActions:
+// DoApplyAction's own checks decide.  The reference's scripts rely on it
+// (policy_analysis.py:298 answers a Tax with Block, outside LegalActions,
+// coup.cc:867-871).  Per-game ops and caller-action steps apply actions
+// this way unless the caller asks for the legality check.  The transition
+// below is coup.cc:522-808 for ANY decision at a decision node, in the
+// reference's branch order, including the branches legal play never
+// reaches: a claim's second half when is_turn_begin_ is false (FA +2, Tax
+// +3, Exchange draws two, Steal takes), and the Pass recursion (coup.cc:628)
+// completing whatever the opponent did last.  Returns false where the
+// reference raises: SPIEL_CHECK_GE on coins (coup.cc:549, 568, 590),
+// LoseCard of a missing or face-up slot (:608), a Challenge of nothing
+// challengeable (:692, 770), an ExchangeReturn without 4 cards (:787-796,
+// or vector::erase past the end), any other id (:806), and the Pass that
+// answers a Pass (:628 recurses without end).
+__device__ __forceinline__ bool ref_decision_core(Lane& L, uint32_t a) {
+  const uint32_t M = L.M, O = M ^ 1u;
+  const uint32_t cc = COUP_PGET(L, c, M), oc = COUP_PGET(L, c, O);
+  L.r0 = 0;  // coup.cc:527
+  if (a == kChallenge) {
+    // coup.cc:635-771: a Block of the mover's FA / Assassinate / Steal, or
+    // the opponent's Tax / Exchange / Assassinate / Steal; else fatal
+    const uint32_t ol = COUP_PGET(L, l, O), cl = COUP_PGET(L, l, M);
+    const bool ok = ol == kBlock ? (cl == kForeignAid || cl == kAssassinate || cl == kSteal)
+                                 : (ol == kTax || ol == kExchange || ol == kAssassinate || ol == kSteal);
+    if (!ok) return false;
+    apply_challenge(L);
+    return L.err == 0u;
+  }
+  if (a >= kExchangeReturn12 && a <= kExchangeReturn34) {
+    if (hand_size(COUP_PGET(L, h, M)) != 4u) return false;
+    apply_decision_v1(L, a);  // coup.cc:773-804
+    return true;
+  }
+  const bool begin = L.begin != 0u;
+  switch (a) {
+    case kIncome:  // coup.cc:531-534
+      COUP_PSET(L, l, M, a);
+      COUP_PSET(L, c, M, cc + 1u);
+      next_turn(L);
+      return true;
+    case kForeignAid:  // coup.cc:536-546
+    case kTax:         // coup.cc:555-565
+      if (begin) {
+        COUP_PSET(L, l, M, a);
+        next_move(L);
+      } else {
+        COUP_PSET(L, c, M, cc + (a == kTax ? 3u : 2u));
+        next_turn(L);
+      }
+      return true;
+    case kCoup:         // coup.cc:548-553
+    case kAssassinate:  // coup.cc:567-573
+      if (cc < (a == kCoup ? 7u : 3u)) return false;
+      COUP_PSET(L, l, M, a);
+      COUP_PSET(L, c, M, cc - (a == kCoup ? 7u : 3u));
+      next_move(L);
+      return true;
+    case kExchange:  // coup.cc:575-587
+      if (begin) {
+        COUP_PSET(L, l, M, a);
+        next_move(L);
+      } else {
+        queue_push(L, M);
+        queue_push(L, M);
+      }
+      return true;
+    case kSteal:  // coup.cc:589-603
+      if (oc < 1u) return false;
+      if (begin) {
+        COUP_PSET(L, l, M, a);
+        next_move(L);
+      } else {
+        const uint32_t k = oc > 1u ? 2u : 1u;
+        COUP_PSET(L, c, M, cc + k);
+        COUP_PSET(L, c, O, oc - k);
+        next_turn(L);
+      }
+      return true;
+    case kLoseCard1:
+    case kLoseCard2: {  // coup.cc:605-616
+      const uint32_t slot = a - kLoseCard1, h = COUP_PGET(L, h, M);
+      if (slot >= hand_size(h) || (nib(h, slot) & 1u)) return false;
+      apply_decision_v1(L, a);
+      return true;
+    }
+    case kBlock:  // coup.cc:631-633
+      COUP_PSET(L, l, M, a);
+      next_move(L);
+      return true;
+    default:
+      return false;  // coup.cc:805-806 (Pass is ref_decision's)
+  }
+}
+
+__device__ __forceinline__ bool ref_decision(Lane& L, uint32_t a) {
+  if (a != kPass) return ref_decision_core(L, a);
+  // coup.cc:618-629
+  const uint32_t M = L.M, O = M ^ 1u;
+  const uint32_t pending = COUP_PGET(L, l, O);
+  L.r0 = 0;
+  COUP_PSET(L, l, M, kPass);
+  if (pending == kBlock) {
+    next_turn(L);
+    return true;
+  }
+  if (pending == kPass) return false;  // the recursion never ends
+  next_move(L);
+  return ref_decision_core(L, pending);  // DoApplyAction(op.last) for the opponent
+}
+
+// nibbles ascending (the empties, 0xF, on top): the order SortCards keeps
+__device__ __forceinline__ bool hand_sorted(uint32_t h) {
+  return nib(h, 0) <= nib(h, 1) && nib(h, 1) <= nib(h, 2) && nib(h, 2) <= nib(h, 3);
+}
+
+// The record's field widths: coins 0..15, at most 4
+// queued deals, at most 4 cards per hand counting the deals queued for it,
+// cur_rewards_[0] in -2..5, hands sorted.  Legal play stays inside them.  A
+// hand is left unsorted only by the double flip of a lost assassination
+// challenge (coup.cc:660-669, 733-742, no SortCards) on a hand of 3 or 4
+// cards, which unchecked play alone produces.
+__device__ __forceinline__ bool representable(const Lane& L) {
+  if (L.c0 > 15u || L.c1 > 15u || L.qlen > 4u || L.r0 < -2 || L.r0 > 5) return false;
+  if (!hand_sorted(L.h0) || !hand_sorted(L.h1)) return false;
+  const uint32_t to1 = (uint32_t)__popc(L.qids & ((1u << L.qlen) - 1u)), to0 = L.qlen - to1;
+  return hand_size(L.h0) + to0 <= 4u && hand_size(L.h1) + to1 <= 4u;
+}
+
+// pyspiel's apply_action on a lane: chance outcomes as apply_action (the
+// chance branch checks them, coup.cc:492-495); a decision through
+// ref_decision.  Returns false, the lane untouched, where the reference
+// raises, on a terminal state (the reference would go on applying decisions
+// to a finished game), and where the result leaves the record's fields
+// (valid in the reference, e.g. a 16th coin).
+template <class H>
+__device__ __forceinline__ bool apply_action_unchecked(Lane& L, uint32_t a, H& hist) {
+  if (a > 17u || is_terminal(L) || L.err) return false;
+  if (is_chance(L)) return apply_action(L, a, hist);
+  Lane R = L;
+  if (!ref_decision(R, a) || !representable(R)) return false;
+  hist.record(L.move, hist_decision(a, L.M));
+  R.move += 1u;
+  L = R;
+  return true;
+}
+
 // --------------------------------------------------- sampling contract
 
 // Philox4x32-10 (Salmon et al., SC'11), Random123 constants.

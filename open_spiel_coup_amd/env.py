@@ -58,10 +58,15 @@ class BatchedCoupEnv:
       episode_stats: keep per-lane int32 accumulators `episodes` and
         `return_sum` (player 0's Returns() of every game that ends, coup.cc:
         1016-1032), updated by every step at the lanes that reach LAST.
+      unchecked: caller actions outside LegalActions() (step, apply_action)
+        are applied as pyspiel's apply_action does -- no legality check,
+        DoApplyAction's own checks decide (COUP_FLAG_UNCHECKED, DESIGN.md
+        section 8); 2 players.  Otherwise such a lane is left unchanged and
+        counts in error_count().
     """
 
     def __init__(self, batch, seed=0, env_id_base=0, auto_reset=True, obs=True, info_state=False,
-                 history=False, device=None, num_players=2, generic=False, episode_stats=False):
+                 history=False, device=None, num_players=2, generic=False, episode_stats=False, unchecked=False):
         if not (0 <= int(env_id_base) and int(env_id_base) + int(batch) <= 1 << 32):
             raise ValueError("env ids are 32-bit: need 0 <= env_id_base and env_id_base + batch <= 2^32")
         self.lib = _native.load()
@@ -77,7 +82,7 @@ class BatchedCoupEnv:
         self.num_players = int(num_players)
         self.obs_size = obs_size(self.num_players)
         flags = ((_native.FLAG_AUTO_RESET if self.auto_reset else 0) | (_native.FLAG_HISTORY if self.history else 0)
-                 | (_native.FLAG_GENERIC if generic else 0))
+                 | (_native.FLAG_GENERIC if generic else 0) | (_native.FLAG_UNCHECKED if unchecked else 0))
         self._h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
             _native.check(self.lib.coup_create_ex(self.batch, self.seed, self.env_id_base, flags, self.num_players,

@@ -141,6 +141,31 @@ def _legal_list(m):
     return list(t)
 
 
+def _action_id(action):
+    """An action id for ApplyAction: outside 0..17 DoApplyAction raises at
+    any node (coup.cc:493 chance, :806 decision; spiel.cc:327 for -1)."""
+    a = int(action)
+    if not 0 <= a < 18:
+        raise SpielError(f"Invalid player action {a}")
+    return a
+
+
+def _action_string(player, action):
+    try:
+        return strings.action_to_string(player, action)
+    except Exception:
+        return str(action)
+
+
+def _apply_failed(player, action):
+    """The SpielError of an action the lane rejected: DoApplyAction raises
+    there in the reference (a SPIEL_CHECK or SpielFatalError of coup.cc:
+    490-809), the state is terminal, or the result leaves the packed record's
+    fields."""
+    return (f"ApplyAction({action}) by player {player} rejected: DoApplyAction raises here "
+            f"(or the state is terminal / the result leaves the record's fields)")
+
+
 class _Pool:
     """Device-resident lane pool: every live CoupState owns one lane of a
     2-player history env (segments of SEG lanes, grown on demand).  Each
@@ -232,18 +257,21 @@ class _Pool:
     def handle(self, slot):
         return self.segs[slot[0]]._h
 
-    def op(self, slot, src=None, action=-1, init=False, obs=False, info=False, result=True):
-        """coup_slot_op on `slot`; src = (coup_env handle, lane) or None."""
+    def op(self, slot, src=None, action=-1, init=False, obs=False, info=False, result=True, unchecked=False):
+        """coup_slot_op on `slot`; src = (coup_env handle, lane) or None;
+        unchecked: the action as pyspiel's apply_action applies it
+        (COUP_SLOT_UNCHECKED)."""
         with self.lock:
-            return self._op(slot, src, action, init, obs, info, result)
+            return self._op(slot, src, action, init, obs, info, result, unchecked)
 
-    def ops(self, seg, reqs, src_seg=None, obs=False, info=False):
+    def ops(self, seg, reqs, src_seg=None, obs=False, info=False, unchecked=False):
         """coup_slot_ops: the (lane, src_lane, action) requests on segment
         `seg` (copies from segment `src_seg`) in one launch; returns one
         result dict per request, like op()."""
         with self.lock:
             n = len(reqs)
-            arr = (_native.SlotReq * n)(*[_native.SlotReq(lane, src, action, 0) for lane, src, action in reqs])
+            rf = _native.SLOT_UNCHECKED if unchecked else 0
+            arr = (_native.SlotReq * n)(*[_native.SlotReq(lane, src, action, rf) for lane, src, action in reqs])
             per = _native.SLOT_RESULT_BYTES
             nbytes = n * (per + (2 * OBS_SIZE * 4 if obs else 0) + (2 * INFO_STATE_SIZE * 4 if info else 0))
             if getattr(self, "_batch_host", None) is None or self._batch_host.numel() < nbytes:
@@ -277,9 +305,10 @@ class _Pool:
                 out.append(q)
             return out
 
-    def _op(self, slot, src, action, init, obs, info, result):
+    def _op(self, slot, src, action, init, obs, info, result, unchecked=False):
         flags = ((_native.SLOT_INIT if init else 0) | (_native.SLOT_OBS if obs else 0)
-                 | (_native.SLOT_INFO if info else 0) | (0 if result else _native.SLOT_NO_RESULT))
+                 | (_native.SLOT_INFO if info else 0) | (0 if result else _native.SLOT_NO_RESULT)
+                 | (_native.SLOT_UNCHECKED if unchecked else 0))
         src_h, src_lane = src if src is not None else (None, 0)
         return self._lane_op(self.segs[slot[0]], slot[1], src_h, src_lane, action, flags, obs, info, result)
 
@@ -522,7 +551,12 @@ class CoupState:
         cur = q["current_player"]
         if (player is not None and player != cur) or cur == -4:  # PlayerId.TERMINAL
             return []
-        return _legal_list(q["legal_mask"] & 0x3FFFF)
+        mask = q["legal_mask"] & 0x3FFFF
+        if not mask and cur >= 0:
+            # a decision node no legal play reaches (unchecked actions):
+            # LegalActions() raises (coup.cc:886, 892, 936)
+            raise SpielError("Error in LegalActions(): Invalid action progression")
+        return _legal_list(mask)
 
     def legal_actions_mask(self, player=None):
         """LegalActionsMask (spiel.cc:371-377): length 5 at chance nodes."""
@@ -545,37 +579,45 @@ class CoupState:
     def legal_chance_outcomes(self):
         return [a for a, _ in self.chance_outcomes()]
 
+    def _legal(self, a):
+        return 0 <= a < 18 and (self._mask() >> a) & 1 and self.current_player() != PlayerId.TERMINAL
+
     def apply_action(self, action):
-        """State::ApplyAction (spiel.cc:322-331) on the GPU; raises SpielError
-        for an illegal action."""
+        """State::ApplyAction (spiel.cc:322-331) on the GPU, bound as pyspiel
+        binds it (pyspiel.cc:266): no legality check -- DoApplyAction's own
+        checks decide (COUP_SLOT_UNCHECKED), for legal
+        actions too (LegalActions can offer one DoApplyAction refuses once
+        unchecked play has left legal play's states).  Raises SpielError, the
+        state unchanged, where the reference raises."""
         player = self.current_player()
-        a = int(action)
-        if not 0 <= a < 18 or not (self._mask() >> a) & 1 or player == PlayerId.TERMINAL:
-            raise SpielError(f"illegal action {action}")
-        q = self._pool.op(self._slot, action=a)
+        a = _action_id(action)
+        q = self._pool.op(self._slot, action=a, unchecked=True)
         if not q["ok"]:
-            self._q = self._pool.op(self._slot)
-            raise SpielError(f"illegal action {action}")
+            raise SpielError(_apply_failed(player, a))
         self._q = q
         self._history = self._history + [(player, a)]
 
     def apply_action_with_legality_check(self, action):
-        self.apply_action(action)
+        """State::ApplyActionWithLegalityCheck (spiel.cc:334-344)."""
+        a = _action_id(action)
+        if not self._legal(a):
+            p = self.current_player()
+            raise SpielError(f"Current player {p} calling ApplyAction with illegal action ({a}): "
+                             f"{_action_string(p, a)}")
+        self.apply_action(a)
 
     def child(self, action):
-        """clone() + apply_action(action) as ONE op: the new state's lane is a
-        copy of this one with the action applied."""
+        """clone() + apply_action(action) (State::Child, spiel.h) as ONE op:
+        the new state's lane is a copy of this one with the action applied."""
         q = self._q
         player = q["current_player"]
-        a = int(action)
-        if not 0 <= a < 18 or not (q["legal_mask"] >> a) & 1 or player == -4:  # PlayerId.TERMINAL
-            raise SpielError(f"illegal action {action}")
+        a = _action_id(action)
         pool = self._pool
         slot = pool.alloc()
         try:
-            q = pool.op(slot, src=(pool.segs[self._slot[0]]._h, self._slot[1]), action=a)
+            q = pool.op(slot, src=(pool.segs[self._slot[0]]._h, self._slot[1]), action=a, unchecked=True)
             if not q["ok"]:
-                raise SpielError(f"illegal action {action}")
+                raise SpielError(_apply_failed(player, a))
         except Exception:
             pool.release(slot)
             raise
@@ -587,11 +629,8 @@ class CoupState:
         ApplyAction).  Deep CFR expands every legal action of a traverser
         node this way (deep_cfr.py:440-471).  With obs / info_state the
         children's tensors come back with the same round trip."""
-        actions = [int(a) for a in actions]
-        player, mask = self.current_player(), self._mask()
-        for a in actions:
-            if not 0 <= a < 18 or not (mask >> a) & 1 or player == PlayerId.TERMINAL:
-                raise SpielError(f"illegal action {a}")
+        actions = [_action_id(a) for a in actions]
+        player = self.current_player()
         if not actions:
             return []
         pool = self._pool
@@ -605,10 +644,10 @@ class CoupState:
                 by_seg.setdefault(s[0], []).append(k)
             for seg, ks in by_seg.items():
                 res = pool.ops(seg, [(slots[k][1], self._slot[1], actions[k]) for k in ks], src_seg=self._slot[0],
-                               obs=obs, info=info_state)
+                               obs=obs, info=info_state, unchecked=True)
                 for k, q in zip(ks, res):
                     if not q["ok"]:
-                        raise SpielError(f"illegal action {actions[k]}")
+                        raise SpielError(_apply_failed(player, actions[k]))
                     out[k] = CoupState(self._game, _slot=slots[k], _q=q,
                                        _history=self._history + [(player, actions[k])])
         except Exception:
@@ -702,26 +741,22 @@ def apply_actions(states, actions):
     """states[k].apply_action(actions[k]) for every k, one launch per pool
     segment (coup_slot_ops): a frontier of independent games advanced
     together (MCCFR walkers, many rl_environment-style games).  The states
-    must be distinct objects.  Raises SpielError before launching if any
-    action is illegal."""
-    states, actions = list(states), [int(a) for a in actions]
+    must be distinct objects.  Actions apply as apply_action applies them
+    (no legality check); where the reference would raise, that state stays
+    unchanged, every other one advances, and SpielError names the first."""
+    states, actions = list(states), [_action_id(a) for a in actions]
     if len(states) != len(actions):
         raise ValueError("one action per state")
     if len({id(s) for s in states}) != len(states):
         raise ValueError("apply_actions needs distinct states")
-    players = []
-    for st, a in zip(states, actions):
-        p = st.current_player()
-        if not 0 <= a < 18 or not (st._mask() >> a) & 1 or p == PlayerId.TERMINAL:
-            raise SpielError(f"illegal action {a}")
-        players.append(p)
+    players = [st.current_player() for st in states]
     by_pool = {}
     for k, st in enumerate(states):
         by_pool.setdefault((id(st._pool), st._slot[0]), []).append(k)
     failed = None
     for (_, seg), ks in by_pool.items():
         pool = states[ks[0]]._pool
-        res = pool.ops(seg, [(states[k]._slot[1], -1, actions[k]) for k in ks])
+        res = pool.ops(seg, [(states[k]._slot[1], -1, actions[k]) for k in ks], unchecked=True)
         # every state of the launch has advanced (or not) on the device:
         # bring each host view up to date before reporting a failure
         for k, q in zip(ks, res):
@@ -732,7 +767,7 @@ def apply_actions(states, actions):
             states[k]._q = q
             states[k]._history = states[k]._history + [(players[k], actions[k])]
     if failed is not None:
-        raise SpielError(f"illegal action {actions[failed]}")
+        raise SpielError(_apply_failed(players[failed], actions[failed]))
 
 
 def load_game(name, params=None):

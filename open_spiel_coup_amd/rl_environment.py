@@ -141,8 +141,12 @@ class Environment:
         # server (pyspiel's lane pool): reset and step are one coup_slot_op
         # each (COUP_SLOT_RESET / COUP_SLOT_DEAL) whose 128-byte result and
         # tensors come back in the same round trip
+        # unchecked: step() applies its action as the reference's does,
+        # through pyspiel's apply_action (rl_environment.py:296-298), which
+        # has no legality check (pyspiel.cc:266); enable_legality_check
+        # rejects an illegal one in Python first
         self._env = BatchedCoupEnv(1, seed=self._seed, auto_reset=False, obs=False, info_state=False,
-                                   history=True, device=self._device)
+                                   history=True, device=self._device, unchecked=True)
         self._pool = pyspiel._pool(self._device)
         self._pool.attach(self._env)
         self._lane = 0
@@ -206,6 +210,11 @@ class Environment:
     def _time_step(self, q, step_type, rewards):
         cur = int(q["current_player"])
         mask = int(q["legal_mask"]) & 0x3FFFF
+        if cur >= 0 and not mask:
+            # legal_actions(cur) raises at a decision node no legal play
+            # reaches (coup.cc:886, 892, 936), as in the reference's
+            # get_time_step (rl_environment.py:243-248)
+            raise pyspiel.SpielError("Error in LegalActions(): Invalid action progression")
         legal_cur = [a for a in range(18) if (mask >> a) & 1] if cur >= 0 else []
         key = "obs" if self._use_observation else "info_state"
         tensors = q[key]
@@ -280,16 +289,17 @@ class Environment:
             # the decision, then the chance deals that follow under the
             # sampling contract, and the time step's answers: one op on the
             # lane (the op server's wave when the pool has one)
-            q = self._lane_op(int(actions[0]), _native.SLOT_DEAL)
+            q = self._lane_op(int(actions[0]), _native.SLOT_DEAL | _native.SLOT_UNCHECKED)
             if not q["ok"]:
-                raise pyspiel.SpielError(f"illegal action {actions[0]}")  # the lane is unchanged
+                # DoApplyAction raised in the reference (coup.cc:490-809); the lane is unchanged
+                raise pyspiel.SpielError(f"apply_action({actions[0]}) failed")
             step_type = StepType.LAST if q["terminal"] else StepType.MID
             self._should_reset = step_type == StepType.LAST
             return self._time_step(q, step_type, [float(x) for x in q["rewards"]])
         self._env.apply_action(self._lane_actions(actions[0]))
         self._sample_external_events()
         if not known_legal and self._env.error_count():
-            raise pyspiel.SpielError(f"illegal action {actions[0]}")
+            raise pyspiel.SpielError(f"apply_action({actions[0]}) failed")
         return self.get_time_step()
 
     def reset(self):

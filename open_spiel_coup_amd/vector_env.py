@@ -27,8 +27,10 @@ different games / observation types / devices, or envs already adopted by
 another vector env are stepped in the reference's loop instead.
 
 Errors: an action outside 0..127 raises SpielError before anything is
-applied; an illegal action is rejected by its lane (the other envs' actions
-are applied) and raises SpielError after the launch, as Environment.step does.
+applied.  Actions outside LegalActions() are applied as Environment.step
+applies them (pyspiel's unchecked apply_action); one the reference's
+DoApplyAction would raise on is rejected by its lane (the other envs' actions
+are applied) and raises SpielError after the launch.
 """
 import numpy as np
 import torch
@@ -86,7 +88,7 @@ class SyncVectorEnv:
         records = torch.cat([e._env.export_state()[e._lane:e._lane + 1] for e in envs])
         hist = torch.cat([e._env.export_history()[e._lane:e._lane + 1] for e in envs])
         shared = BatchedCoupEnv(len(envs), seed=seed, auto_reset=False, obs=False, info_state=False, history=True,
-                                device=envs[0]._device)
+                                device=envs[0]._device, unchecked=True)  # as each env's own (rl_environment.py)
         shared.import_state(records)
         shared.import_history(hist)
         envs[0]._pool.attach(shared)  # an env stepping alone goes through the op server too
@@ -165,7 +167,8 @@ class SyncVectorEnv:
             e0 = envs[0]
             self._q_step = self._shared.step_host(acts, obs=e0._use_observation, info_state=not e0._use_observation)
             if unknown and self._shared.error_count():
-                raise pyspiel.SpielError(f"illegal action among envs {unknown}")
+                # DoApplyAction raised in the reference for one of them (coup.cc:490-809)
+                raise pyspiel.SpielError(f"apply_action failed among envs {unknown}")
         else:
             self._q_step = self._query()
         return self._time_steps(self._q_step, resets)

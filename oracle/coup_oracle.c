@@ -239,7 +239,9 @@ static void reward_to_mover(oc_state* s, int delta) {
   s->rewards[s->opp_player] -= delta;
 }
 
-static void do_apply(oc_state* s, int a);
+static void do_apply_d(oc_state* s, int a, int depth);
+
+static void do_apply(oc_state* s, int a) { do_apply_d(s, a, 0); }
 
 static void do_challenge(oc_state* s) {
   /* Challenge branch of DoApplyAction (coup.cc:635-771) */
@@ -349,8 +351,11 @@ static void do_challenge(oc_state* s) {
   }
 }
 
-static void do_apply(oc_state* s, int a) {
-  /* CoupState::DoApplyAction (coup.cc:490-809) */
+static void do_apply_d(oc_state* s, int a, int depth) {
+  /* CoupState::DoApplyAction (coup.cc:490-809).  `depth` counts the Pass
+   * recursion (coup.cc:628): legal play recurses once; an unchecked Pass
+   * answering a Pass recurses without end in the reference (a crash), which
+   * this restatement reports as an error instead. */
   if (oc_current_player(s) == -1) {
     /* chance branch (coup.cc:491-520) */
     if (a < 0 || a >= OC_NUM_TYPES || s->deck[a] <= 0 || s->qlen <= 0) {
@@ -451,9 +456,11 @@ static void do_apply(oc_state* s, int a) {
       int pending = op->last_action;
       if (pending == OC_BLOCK) {
         next_turn(s);
+      } else if (depth >= 4) {
+        s->error = OC_ERR_PROGRESSION; /* unbounded recursion in the reference */
       } else {
         next_move(s);
-        do_apply(s, pending); /* coup.cc:628: completes the original action */
+        do_apply_d(s, pending, depth + 1); /* coup.cc:628: completes the original action */
       }
       return;
     }
@@ -506,6 +513,47 @@ int oc_apply_action(oc_state* s, int a) {
   s->hist_len++;
   s->move_number++;
   return s->error;
+}
+
+/* Field widths of the product's 16-byte record:
+ * coins 0..15, at most 4 queued deals, at most 4 cards per hand counting
+ * the deals queued for it, cur_rewards_[0] in -2..5, hands in SortCards
+ * order.  Legal play stays far inside them; unchecked actions can leave
+ * them (a hand stays unsorted after the double flip of coup.cc:660-669 /
+ * 733-742 on 3 or 4 cards, which has no SortCards). */
+static int representable(const oc_state* s) {
+  if (s->qlen > 4) return 0;
+  for (int p = 0; p < OC_NUM_PLAYERS; ++p) {
+    int pending = 0;
+    for (int i = 0; i < s->qlen; ++i) pending += s->queue[i] == p;
+    if (s->pl[p].coins < 0 || s->pl[p].coins > 15) return 0;
+    if (s->pl[p].ncards + pending > OC_MAX_CARDS) return 0;
+    for (int i = 1; i < s->pl[p].ncards; ++i)
+      if (card_less(s->pl[p].cards[i], s->pl[p].cards[i - 1])) return 0;
+  }
+  return s->rewards[0] >= -2 && s->rewards[0] <= 5;
+}
+
+int oc_apply_action_unchecked(oc_state* s, int a) {
+  /* State::ApplyAction (spiel.cc:322-331) as pyspiel binds apply_action
+   * (pyspiel.cc:266): no LegalActions() check; DoApplyAction's own checks
+   * decide (coup.cc:492-495, 549, 568, 590, 608, 685-692, 770, 787, 796,
+   * 806).  On any error the state is left as it was. */
+  if (oc_is_terminal(s)) return OC_ERR_TERMINAL;
+  if (a < 0 || a >= OC_NUM_ACTIONS) return OC_ERR_ILLEGAL; /* coup.cc:493 / 806 */
+  if (s->error) return s->error;
+  oc_state t = *s;
+  int player = oc_current_player(&t);
+  t.hist_deal_to[t.hist_len] = -1;
+  do_apply(&t, a); /* ExchangeReturn needs 4 cards: coup.cc:793 erases past the end or :796 fails */
+  if (t.error) return t.error;
+  if (!representable(&t)) return OC_ERR_UNREPRESENTABLE;
+  t.hist_player[t.hist_len] = player;
+  t.hist_action[t.hist_len] = a;
+  t.hist_len++;
+  t.move_number++;
+  *s = t;
+  return OC_OK;
 }
 
 void oc_returns(const oc_state* s, int* out2) {

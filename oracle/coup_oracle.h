@@ -55,7 +55,8 @@ enum {
 };
 
 /* Error codes raised where the reference calls SpielFatalError / SPIEL_CHECK */
-enum { OC_OK = 0, OC_ERR_ILLEGAL = 1, OC_ERR_PROGRESSION = 2, OC_ERR_TERMINAL = 3 };
+enum { OC_OK = 0, OC_ERR_ILLEGAL = 1, OC_ERR_PROGRESSION = 2, OC_ERR_TERMINAL = 3,
+       OC_ERR_UNREPRESENTABLE = 4 /* valid in the reference, outside the packed record's fields */ };
 
 typedef struct {
   int value; /* card type */
@@ -97,6 +98,8 @@ int oc_current_player(const oc_state* s); /* -4 terminal, -1 chance */
 int oc_legal_actions(const oc_state* s, int* out); /* returns count */
 uint32_t oc_legal_mask(const oc_state* s);        /* bit a set if legal */
 int oc_apply_action(oc_state* s, int action);      /* returns error code */
+/* pyspiel's apply_action (no legality check); the state is unchanged on error */
+int oc_apply_action_unchecked(oc_state* s, int action);
 void oc_returns(const oc_state* s, int* out2);
 void oc_rewards(const oc_state* s, int* out2);
 int oc_chance_outcomes(const oc_state* s, int* actions, double* probs);

@@ -99,6 +99,7 @@ def lib():
         L.oc_legal_mask.argtypes = [P]
         L.oc_legal_mask.restype = ctypes.c_uint32
         L.oc_apply_action.argtypes = [P, ctypes.c_int]
+        L.oc_apply_action_unchecked.argtypes = [P, ctypes.c_int]
         L.oc_returns.argtypes = [P, ctypes.POINTER(ctypes.c_int)]
         L.oc_rewards.argtypes = [P, ctypes.POINTER(ctypes.c_int)]
         L.oc_chance_outcomes.argtypes = [P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_double)]
@@ -166,6 +167,15 @@ class OracleState:
         err = lib().oc_apply_action(ctypes.byref(self._s), int(a))
         if err:
             raise RuntimeError(f"oracle apply_action({a}) failed with code {err}")
+
+    def apply_action_unchecked(self, a):
+        """pyspiel's apply_action (pyspiel.cc:266, spiel.cc:322-331): no
+        legality check; raises RuntimeError, the state unchanged, where the
+        reference raises (or where the result leaves the packed record:
+        code 4)."""
+        err = lib().oc_apply_action_unchecked(ctypes.byref(self._s), int(a))
+        if err:
+            raise RuntimeError(f"oracle apply_action_unchecked({a}) failed with code {err}")
 
     def returns(self):
         buf = (ctypes.c_int * 2)()

@@ -197,6 +197,25 @@ int main(int argc, char** argv) {
     DeleteGame(game);
     return 0;
   }
+  if (argc >= 2 && strcmp(argv[1], "--unchecked") == 0) {
+    /* the actions, legal or not, then the current player, its legal
+     * actions and player 0's observation tensor */
+    void* st = GameNewInitialState(game);
+    for (int i = 2; i < argc; ++i) StateApplyAction(st, atol(argv[i]));
+    int n = 0;
+    long* legal = StateLegalActions(st, &n);
+    float obs[98];
+    StateObservationTensor(st, 0, obs, 98);
+    printf("{\"player\":%d,\"legal\":[", StateCurrentPlayer(st));
+    for (int i = 0; i < n; ++i) printf(i ? ",%ld" : "%ld", legal[i]);
+    printf("],\"obs0\":[");
+    for (int i = 0; i < 98; ++i) printf(i ? ",%g" : "%g", obs[i]);
+    printf("]}\n");
+    free(legal);
+    DeleteState(st);
+    DeleteGame(game);
+    return 0;
+  }
   if (argc >= 2 && strcmp(argv[1], "--illegal") == 0) {
     void* st = GameNewInitialState(game);
     const long deal[] = {4, 3, 2, 0};

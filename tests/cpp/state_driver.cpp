@@ -3,6 +3,7 @@
 // it with the reference's golden transcript.  Test tooling.
 //   state_driver <action> <action> ...      (the history to replay)
 //   state_driver --illegal                  (error behaviour check)
+//   state_driver --unchecked                (ApplyAction without a legality check)
 //   state_driver --children                 (batched Children == Child one by one)
 #include <cstdio>
 #include <cstdlib>
@@ -101,6 +102,24 @@ int main(int argc, char** argv) {
         }
       }
       std::printf("{\"children_checked\":%d}\n", checked);
+      return 0;
+    }
+    if (argc == 2 && std::string(argv[1]) == "--unchecked") {
+      // policy_analysis.py:283-299: a Tax answered by Block, outside
+      // LegalActions (coup.cc:867-871): the legality-checked form throws,
+      // ApplyAction applies it as the reference does
+      for (int a : {1, 1, 3, 3, 3}) state->ApplyAction(a);
+      bool checked_threw = false;
+      try {
+        state->ApplyActionWithLegalityCheck(10);
+      } catch (const SpielError&) {
+        checked_threw = true;
+      }
+      state->ApplyAction(10);
+      auto child = state->Child(9);  // the Pass that ends the blocked turn
+      std::printf("{\"checked_threw\":%s,\"history\":%s,\"child\":%s,\"child_player\":%d,\"child_legal\":%s}\n",
+                  checked_threw ? "true" : "false", List(state->History()).c_str(), List(child->History()).c_str(),
+                  child->CurrentPlayer(), List(child->LegalActions()).c_str());
       return 0;
     }
     if (argc == 2 && std::string(argv[1]) == "--illegal") {

@@ -82,6 +82,23 @@ def test_cpp_state_errors_clone_child(driver):
 
 
 @pytest.mark.gpu
+def test_cpp_unchecked_apply_action(driver):
+    """ApplyAction has the reference's semantics (no legality check,
+    spiel.cc:322-331): the Tax answered by Block of policy_analysis.py
+    applies, ApplyActionWithLegalityCheck refuses it; equal to the oracle."""
+    from oracle import oracle
+    out = subprocess.run([driver, "--unchecked"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    r = json.loads(out.stdout)
+    st = oracle.OracleState()
+    for a in [1, 1, 3, 3, 3, 10, 9]:
+        st.apply_action_unchecked(a)
+    assert r["checked_threw"] is True
+    assert r["history"] == [1, 1, 3, 3, 3, 10] and r["child"] == [1, 1, 3, 3, 3, 10, 9]
+    assert r["child_player"] == st.current_player() and r["child_legal"] == st.legal_actions()
+
+
+@pytest.mark.gpu
 def test_cpp_batched_children_equal_child(driver):
     """coup_amd::CoupState::Children (one coup_slot_ops launch for all legal
     actions) == Child(a) one by one, along six random games."""

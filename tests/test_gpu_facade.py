@@ -85,8 +85,17 @@ def test_pyspiel_clone_child_serialize_and_errors():
     assert s2.history() == ch.history() and str(s2) == str(ch)
     assert ch.legal_actions_mask() == [1 if a in (9, 11) else 0 for a in range(18)]
     with pytest.raises(pyspiel.SpielError):
-        ch.apply_action(0)  # Income is not a response to a block
+        ch.apply_action_with_legality_check(0)  # Income is not a response to a block
     assert ch.history() == [4, 3, 2, 0, 1, 10]
+    # pyspiel's apply_action has no legality check (pyspiel.cc:266): Income
+    # applies (coup.cc:531-534), as the oracle's unchecked apply does
+    from oracle import oracle
+    ref = oracle.OracleState()
+    for a in [4, 3, 2, 0, 1, 10, 0]:
+        ref.apply_action_unchecked(a)
+    ch.apply_action(0)
+    assert ch.history() == [4, 3, 2, 0, 1, 10, 0]
+    assert ch.packed_record().tolist() == [int(x) for x in ref.pack(0)]
 
 
 def test_rl_environment_matches_oracle():

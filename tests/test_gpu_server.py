@@ -88,10 +88,26 @@ def test_server_results_equal_launch_path_and_oracle(monkeypatch):
                         assert i == list(ref.information_state_tensor(p))
                         log.append((tuple(o), tuple(i)))
                 if k % 11 == 5 and not ref.is_terminal():
+                    # an action outside LegalActions: applied as the reference
+                    # applies it (no legality check), or refused where
+                    # DoApplyAction raises -- either way equal to the oracle
                     bad = next(x for x in range(18) if x not in ref.legal_actions())
-                    with pytest.raises(pyspiel.SpielError):
+                    r2 = ref.clone()
+                    try:
+                        r2.apply_action_unchecked(bad)
+                    except RuntimeError:
+                        with pytest.raises(pyspiel.SpielError):
+                            st.apply_action(bad)
+                        _same(st, ref)
+                    else:
+                        while r2.is_chance_node():
+                            r2.apply_action(r2.legal_actions()[0])
+                        if r2.current_player() >= 0 and not r2.legal_actions():
+                            continue  # a node no legal play reaches: not for this walk
                         st.apply_action(bad)
-                    _same(st, ref)
+                        ref.apply_action_unchecked(bad)
+                        log.append(("unchecked", bad))
+                        _same(st, ref)
             log.append(tuple(st.packed_record().tolist()))
         outs.append(log)
         pool.close()

@@ -190,7 +190,7 @@ def test_apply_actions_advances_a_frontier():
     before = st.packed_record().tolist()
     if not st.is_terminal():
         with pytest.raises(pyspiel.SpielError):
-            pyspiel.apply_actions([st], [17 if 17 not in st.legal_actions() else 18])
+            pyspiel.apply_actions([st], [18])  # not an action id (coup.cc:806)
     assert st.packed_record().tolist() == before
     with pytest.raises(ValueError):
         pyspiel.apply_actions([st, st], [0, 0])

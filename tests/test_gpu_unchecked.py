@@ -1,0 +1,260 @@
+"""ApplyAction without a legality check on the GPU (COUP_SLOT_UNCHECKED,
+COUP_FLAG_UNCHECKED): pyspiel's apply_action is State::ApplyAction, which
+applies any action DoApplyAction accepts (pyspiel.cc:266, spiel.cc:322-331,
+coup.cc:490-809).  Every path that applies caller actions -- the State
+facade's single ops (op server), its batched ops (coup_slot_ops), the
+batched env's apply / step kernels and the rl_environment / SyncVectorEnv
+steps -- is compared with the oracle's oc_apply_action_unchecked, whose
+branches tests/test_oracle_unchecked.py pins by hand against coup.cc."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+from open_spiel_coup_amd import pyspiel, rl_environment, vector_env  # noqa: E402
+from open_spiel_coup_amd.env import BatchedCoupEnv  # noqa: E402
+
+
+def _try(ref, a):
+    """The oracle's unchecked apply: True if applied, False if rejected."""
+    try:
+        ref.apply_action_unchecked(a)
+        return True
+    except RuntimeError:
+        return False
+
+
+def _same(st, ref, tensors=False):
+    assert st.packed_record().tolist() == [int(x) for x in ref.pack(0)]
+    assert st.history() == ref.history()
+    assert st.current_player() == ref.current_player()
+    if ref.current_player() >= 0 and not ref.legal_actions():
+        with pytest.raises(pyspiel.SpielError):  # LegalActions() raises (coup.cc:886, 892, 936)
+            st.legal_actions()
+    else:
+        assert st.legal_actions() == ref.legal_actions()
+    if tensors:
+        for p in (0, 1):
+            assert st.observation_tensor(p) == list(ref.observation_tensor(p))
+            assert st.information_state_tensor(p) == list(ref.information_state_tensor(p))
+
+
+def _outcome(ref, a):
+    """'reject' where the reference raises on `a`; 'stuck' where it applies
+    but the next decision node has no LegalActions (the reference raises
+    there, rl_environment's time step included); else 'ok'.  The deals in
+    between do not change which: the first card type stands in for them."""
+    r2 = ref.clone()
+    if not _try(r2, a):
+        return "reject"
+    while r2.is_chance_node():
+        r2.apply_action(r2.legal_actions()[0])
+    return "stuck" if r2.current_player() >= 0 and not r2.legal_actions() else "ok"
+
+
+def _replay(st):
+    ref = oracle.OracleState()
+    for (p, b) in st.full_history():
+        if p < 0:
+            ref.apply_action(b)
+        else:
+            ref.apply_action_unchecked(b)
+    return ref
+
+
+def _pick(rng, ref):
+    """Half legal actions, half any id 0..17 (at chance nodes a card type)."""
+    if ref.is_chance_node():
+        return int(rng.choice(ref.legal_actions()))
+    legal = ref.legal_actions()
+    if legal and rng.random() < 0.5:
+        return int(rng.choice(legal))
+    return int(rng.integers(0, 18))
+
+
+def test_facade_single_ops_match_oracle():
+    """apply_action / child on the op server: applied exactly where the oracle
+    applies, rejected (SpielError, state unchanged) exactly where it raises."""
+    rng = np.random.default_rng(101)
+    game = pyspiel.load_game("coup")
+    applied = rejected = 0
+    for g in range(40):
+        st, ref = game.new_initial_state(), oracle.OracleState()
+        for k in range(70):
+            if ref.is_terminal():
+                break
+            a = _pick(rng, ref)
+            r2 = ref.clone()
+            ok = _try(r2, a)
+            if k % 2:
+                if ok:
+                    st = st.child(a)
+                else:
+                    with pytest.raises(pyspiel.SpielError):
+                        st.child(a)
+            elif ok:
+                st.apply_action(a)
+            else:
+                with pytest.raises(pyspiel.SpielError):
+                    st.apply_action(a)
+            applied += ok
+            rejected += not ok
+            ref = r2
+            _same(st, ref, tensors=k % 9 == 4)
+            if not ok and not ref.is_terminal():  # go on along a legal action
+                legal = ref.legal_actions()
+                if not legal:
+                    break
+                b = int(rng.choice(legal))
+                st.apply_action(b)
+                ref.apply_action_unchecked(b)
+    assert applied > 500 and rejected > 100
+
+
+def test_facade_batched_ops_match_oracle():
+    """pyspiel.apply_actions (one coup_slot_ops launch, unchecked requests)
+    over 400 games: the accepted states advance, the rejected ones stay."""
+    rng = np.random.default_rng(202)
+    game = pyspiel.load_game("coup")
+    states = [game.new_initial_state() for _ in range(400)]
+    refs = [oracle.OracleState() for _ in states]
+    for rnd in range(60):
+        live = [k for k, r in enumerate(refs) if not r.is_terminal() and (r.legal_actions() or r.is_chance_node())]
+        if not live:
+            break
+        acts = [_pick(rng, refs[k]) for k in live]
+        oks = [_try(refs[k], a) for k, a in zip(live, acts)]
+        if all(oks):
+            pyspiel.apply_actions([states[k] for k in live], acts)
+        else:
+            with pytest.raises(pyspiel.SpielError):
+                pyspiel.apply_actions([states[k] for k in live], acts)
+        for k in live:
+            _same(states[k], refs[k], tensors=(rnd % 13 == 6 and k % 50 == 0))
+
+
+def test_batched_env_apply_matches_oracle():
+    """coup_apply_action on a COUP_FLAG_UNCHECKED env, 2048 lanes: every lane
+    equals its oracle state (rejected actions count in error_count)."""
+    n = 2048
+    rng = np.random.default_rng(303)
+    env = BatchedCoupEnv(n, seed=1, auto_reset=False, obs=False, history=True, unchecked=True)
+    env.new_initial_state()
+    refs = [oracle.OracleState() for _ in range(n)]
+    errors = 0
+    for rnd in range(80):
+        acts = np.full(n, -1, dtype=np.int8)
+        for i, ref in enumerate(refs):
+            if ref.is_terminal() or not (ref.is_chance_node() or ref.legal_actions()):
+                continue
+            a = _pick(rng, ref)
+            acts[i] = a
+            errors += not _try(ref, a)
+        env.apply_action(torch.from_numpy(acts).cuda())
+    rec = env.export_state().cpu().numpy().view(np.uint32).reshape(n, 4)
+    hist = env.export_history().cpu().numpy().reshape(n, 96)
+    for i, ref in enumerate(refs):
+        ep = int(rec[i][3]) >> 7  # new_initial_state starts the lanes' next episode
+        assert rec[i].tolist() == [int(x) for x in ref.pack(ep)], i
+        assert bytes(hist[i]) == ref.history_bytes(), i
+    assert env.error_count() == errors > 0
+    q = env.query(obs=True)
+    obs = q["obs"].cpu().numpy()
+    for i in range(0, n, 97):
+        for p in (0, 1):
+            np.testing.assert_array_equal(obs[i, p], np.asarray(refs[i].observation_tensor(p), dtype=np.float32))
+
+
+def test_batched_env_checked_by_default():
+    """Without COUP_FLAG_UNCHECKED an action outside LegalActions leaves the
+    lane unchanged (coup_step / coup_apply_action count it)."""
+    env = BatchedCoupEnv(2, seed=0, obs=False, auto_reset=False)
+    before = env.export_state().clone()
+    env.step(torch.tensor([10, 10], dtype=torch.int8).cuda())  # Block at turn begin
+    assert env.error_count() == 2 and torch.equal(env.export_state(), before)
+    env2 = BatchedCoupEnv(2, seed=0, obs=False, auto_reset=False, unchecked=True)
+    env2.step(torch.tensor([10, 10], dtype=torch.int8).cuda())
+    assert env2.error_count() == 0 and not torch.equal(env2.export_state(), before)
+
+
+class _Out:
+    def __init__(self, a):
+        self.action = a
+
+
+def _env_actions(rng, ts):
+    p = ts.observations["current_player"]
+    legal = ts.observations["legal_actions"][p] if p >= 0 else []
+    if legal and rng.random() < 0.6:
+        return int(rng.choice(legal))
+    return int(rng.integers(0, 18))
+
+
+def test_rl_environment_unchecked_step_matches_oracle():
+    """Environment.step applies its action like the reference's (pyspiel's
+    apply_action): the env's own history replayed on the oracle, decisions
+    unchecked, gives the env's record and tensors; a rejected action raises
+    SpielError and leaves the env as it was."""
+    rng = np.random.default_rng(404)
+    env = rl_environment.Environment("coup", seed=9, observation_type=rl_environment.ObservationType.OBSERVATION)
+    ts = env.reset()
+    rejected = 0
+    for k in range(300):
+        if ts.last():
+            ts = env.reset()
+        a = _env_actions(rng, ts)
+        before = env.get_state
+        how = _outcome(_replay(before), a)
+        if how == "stuck":
+            a = int(rng.choice(ts.observations["legal_actions"][ts.current_player()]))
+        if how == "reject":
+            rejected += 1
+            with pytest.raises(pyspiel.SpielError):
+                env.step([a])
+            assert env.get_state.history() == before.history()
+            ts = env.get_time_step()
+            continue
+        ts = env.step([a])
+        st = env.get_state
+        ref = _replay(st)
+        rec = st.packed_record().tolist()
+        assert rec == [int(x) for x in ref.pack(rec[3] >> 7)]  # the env's episode number
+        if not ts.last():
+            assert ts.observations["info_state"][0] == list(ref.observation_tensor(0))
+    assert rejected > 10
+
+
+def test_sync_vector_env_unchecked_equals_loop():
+    """SyncVectorEnv's batched step (one coup_step_host launch, caller
+    actions unchecked in the step kernel) == the same envs stepped one by one
+    (op-server lane ops), with actions that are often illegal."""
+    n, seed = 24, 1234
+    rng = np.random.default_rng(505)
+    vec_envs = [rl_environment.Environment("coup", seed=seed) for _ in range(n)]
+    # each loop env keyed like lane i of the vector env's shared env (global
+    # env id i under `seed`), as tests/test_gpu_vector_env.py's _loop_envs
+    loop_envs = [rl_environment.Environment("coup", seed=seed) for _ in range(n)]
+    for i, e in enumerate(loop_envs):
+        e._env = BatchedCoupEnv(1, seed=seed, env_id_base=i, auto_reset=False, obs=False, history=True,
+                                unchecked=True)
+    venv = vector_env.SyncVectorEnv(vec_envs)
+    ts_loop = [e.reset() for e in loop_envs]
+    ts_vec = venv.reset()
+    assert venv.batched
+    for t in range(60):
+        acts = [_env_actions(rng, ts) for ts in ts_loop]
+        # the envs where the reference raises: drop their action (act on the
+        # others) so both forms step the same envs
+        ok = [ts.last() or _outcome(_replay(e.get_state), a) == "ok"
+              for e, a, ts in zip(loop_envs, acts, ts_loop)]
+        acts = [a if o else int(rng.choice(ts.observations["legal_actions"][ts.current_player()]))
+                for a, o, ts in zip(acts, ok, ts_loop)]
+        ts_loop = [e.step([a]) for e, a in zip(loop_envs, acts)]
+        ts_vec, _, _, _ = venv.step([_Out(a) for a in acts])
+        for a_ts, b_ts in zip(ts_loop, ts_vec):
+            assert a_ts.step_type == b_ts.step_type and a_ts.rewards == b_ts.rewards
+            assert a_ts.observations["info_state"] == b_ts.observations["info_state"]
+            assert a_ts.observations["legal_actions"] == b_ts.observations["legal_actions"]

@@ -129,7 +129,8 @@ def test_batched_sync_vector_env_equals_loop(obs_type, n):
 def test_adopted_envs_keep_their_games():
     """After adoption each Environment still plays its own lane: get_state
     replays through the oracle to the last time step; a single env's step,
-    set_state and seed act on that lane only; an illegal action raises
+    set_state and seed act on that lane only; an action DoApplyAction
+    raises on (the reference's apply_action has no legality check) raises
     SpielError after the other envs' actions were applied."""
     n = 6
     envs = [rl_environment.Environment("coup", seed=100 + i) for i in range(n)]
@@ -167,12 +168,21 @@ def test_adopted_envs_keep_their_games():
     envs[0].set_state(envs[3].get_state)
     assert envs[0].get_state.history() == envs[3].get_state.history()
     ts[0] = envs[0].get_time_step()
-    # an illegal action: SpielError, the legal ones applied
+    # an action the reference rejects: SpielError, the others applied
     hist = [e.get_state.history() for e in envs]
     bad = [act(t) for t in ts]
     if not ts[4].last():
-        legal4 = ts[4].observations["legal_actions"][ts[4].current_player()]
-        bad[4] = next(a for a in range(18) if a not in legal4)
+        ref4 = oracle.OracleState()
+        for p, a in envs[4].get_state.full_history():
+            ref4.apply_action(a)
+
+        def rejected(a):
+            try:
+                ref4.clone().apply_action_unchecked(a)
+                return False
+            except RuntimeError:
+                return True
+        bad[4] = next((a for a in range(18) if rejected(a)), 18)
         with pytest.raises(pyspiel.SpielError):
             venv.step([_Out(a) for a in bad])
         assert envs[4].get_state.history() == hist[4]

@@ -4,7 +4,10 @@ hip_runtime.h) and walked against the oracle: random legal actions,
 decisions and chance outcomes, every record compared after every action
 (tools/lane_ubsan_walk.cpp).  Both forms of the decision transition: the
 effect form the rules-bound kernels use (apply_decision_v2, default) and the
-reference-shaped branches the store-bound kernels use (-DCOUP_RULES_V1)."""
+reference-shaped branches the store-bound kernels use (-DCOUP_RULES_V1).
+The unchecked walk applies any action id through apply_action_unchecked (the
+per-game ops' path: pyspiel's apply_action has no legality check) against
+oc_apply_action_unchecked: accepted / rejected and every record agree."""
 import os
 import shutil
 import subprocess
@@ -14,7 +17,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("form", ["effect", "branches"])
+@pytest.mark.parametrize("form", ["effect", "branches", "unchecked"])
 def test_lane_rules_walk_matches_oracle_under_ubsan(tmp_path, form):
     if shutil.which("g++") is None:
         pytest.skip("g++ not available")
@@ -26,6 +29,7 @@ def test_lane_rules_walk_matches_oracle_under_ubsan(tmp_path, form):
     if form == "branches":
         cmd.insert(1, "-DCOUP_RULES_V1")
     subprocess.check_call(cmd)
-    out = subprocess.run([exe, "4000"], capture_output=True, text=True, timeout=300)
+    out = subprocess.run([exe, "4000"] + (["unchecked"] if form == "unchecked" else []), capture_output=True,
+                         text=True, timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
     assert out.stdout.startswith("ok 4000 games")

@@ -130,8 +130,29 @@ def test_uniform_random_bots_finish_a_game(driver, seed):
 
 @pytest.mark.gpu
 def test_illegal_action_is_a_fatal_error(driver):
-    """SpielFatalError (spiel_utils.cc:119-136): message on stderr, exit 1."""
+    """SpielFatalError (spiel_utils.cc:119-136): message on stderr, exit 1.
+    A Pass at the first decision recurses into DoApplyAction(kNone), which
+    raises "Invalid player action" (coup.cc:628, 806)."""
     out = subprocess.run([driver, "--illegal"], capture_output=True, text=True, timeout=120)
     assert out.returncode == 1
     assert out.stdout.strip() == '{"before":"ok"}'
-    assert "Spiel Fatal Error:" in out.stderr and "illegal action 9" in out.stderr
+    assert "Spiel Fatal Error:" in out.stderr and "ApplyAction(9)" in out.stderr
+
+
+@pytest.mark.gpu
+def test_unchecked_apply_through_the_c_abi(driver):
+    """StateApplyAction applies an action outside LegalActions as the
+    reference's does (rust_open_spiel.cc -> State::ApplyAction, no legality
+    check): policy_analysis.py's Tax answered by Block, then the Pass that
+    ends the blocked turn, equal to the oracle's unchecked apply."""
+    from oracle import oracle
+    acts = [1, 1, 3, 3, 3, 10, 9]
+    out = subprocess.run([driver, "--unchecked"] + [str(a) for a in acts], capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode == 0, out.stderr
+    r = json.loads(out.stdout)
+    st = oracle.OracleState()
+    for a in acts:
+        st.apply_action_unchecked(a)
+    assert r["player"] == st.current_player() and r["legal"] == st.legal_actions()
+    assert r["obs0"] == [float(x) for x in st.observation_tensor(0)]
