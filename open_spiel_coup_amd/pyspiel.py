@@ -782,6 +782,18 @@ def registered_names():
     return ["coup"]
 
 
+def registered_games():
+    """RegisteredGames (pyspiel.cc): the GameType of every game this build
+    registers (rl_environment.registered_games, rl_environment.py:115-116)."""
+    return [GameType()]
+
+
+# the pybind class names callers annotate with or test against (pyspiel.Game,
+# pyspiel.State: rl_environment.py:156, 184; best_response.py:217)
+Game = CoupGame
+State = CoupState
+
+
 def serialize_game_and_state(game, state):
     """SerializeGameAndState (spiel.cc:428-448)."""
     return ("# Automatically generated by OpenSpiel SerializeGameAndState\n[Meta]\nVersion: 1\n\n"

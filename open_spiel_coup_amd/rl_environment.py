@@ -95,7 +95,7 @@ class ChanceEventSampler:
 
 
 def registered_games():
-    return pyspiel.registered_names()
+    return pyspiel.registered_games()
 
 
 def _resolve_seed(seed):

@@ -20,6 +20,10 @@ def test_game_metadata_matches_reference():
     assert g.max_game_length() == 90 and g.max_move_number() == 135
     assert str(g) == "coup()"
     assert pyspiel.registered_names() == ["coup"]
+    assert [t.short_name for t in pyspiel.registered_games()] == ["coup"]
+    from open_spiel_coup_amd import rl_environment
+    assert [t.short_name for t in rl_environment.registered_games()] == ["coup"]
+    assert pyspiel.Game is pyspiel.CoupGame and isinstance(g, pyspiel.Game)
     with pytest.raises(pyspiel.SpielError):
         pyspiel.load_game("kuhn_poker")
     with pytest.raises(pyspiel.SpielError):

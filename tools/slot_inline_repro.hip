@@ -141,7 +141,7 @@ __global__ __launch_bounds__(64) void k_slot_var(SlotArgs a) {
     uint32_t ok = 1u;
     if (V == 7 || a.action >= 0) {
       const uint32_t r = V == 6 ? transition_expr(rec, (uint32_t)a.action, &rec)
-                                : slot_transition(rec, (uint32_t)a.action, &rec);
+                                : slot_transition(rec, (uint32_t)a.action, 0u, &rec);
       ok = r & 1u;
       if (V != 1 && V != 2 && (r & 2u)) hist[(r >> 8) & 0xFFu] = (uint8_t)(r >> 16);
     }
