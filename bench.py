@@ -484,11 +484,11 @@ def main():
         elif fused:
             kernel = "coup::k_rollout" + sorted_
         elif with_info:
-            kernel = "coup::k_step<true, 0, 256, 2>"
+            kernel = "coup::k_step<true, 0, 256, 2, false>"
         elif with_obs:
-            kernel = "coup::k_step<true, %d, %d, 0>" % _writer(os.environ.get("COUP_OBS_MODE"))
+            kernel = "coup::k_step<true, %d, %d, 0, false>" % _writer(os.environ.get("COUP_OBS_MODE"))
         else:
-            kernel = "coup::k_step<true, 0, 256, 0>"
+            kernel = "coup::k_step<true, 0, 256, 0, false>"
         outputs = ("ObservationTensor fp32 [B][2][98] per step" if with_obs else
                    "InformationStateTensor fp32 [B][2][2492] per step" if with_info else
                    "per-episode statistics only" if fused == "rollout" else

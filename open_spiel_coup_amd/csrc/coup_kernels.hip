@@ -616,7 +616,14 @@ __device__ __noinline__ uint32_t unchecked_decision(uint4 w, uint32_t x, uint4* 
 // (same-process A/B, profiles/r02/ab/ab_rules_c3.txt: 160.6 vs 165.6 us per
 // 2^20-lane step); the rules-bound kernels take the effect form (c2 8.4 ->
 // 7.7 us, c2r 3.61 -> 3.20 us per step, profiles/r02/ab/ab_rules_c2*.txt).
-template <bool UNIFORM, bool FLOW, class H>
+//
+// UNCHECKED (COUP_FLAG_UNCHECKED, caller actions only): the decision goes
+// through unchecked_decision instead, legal or not.  A compile-time switch:
+// the checked kernels' code is exactly what it is without it -- with the
+// two paths as a run-time branch in one kernel, ROCm 7.2 produced the
+// DESIGN.md section 12 defect in the checked branch (record word 3 after a
+// Tax announcement, k_step<false, 0, 256, 1>; tests/test_gpu_server.py).
+template <bool UNIFORM, bool FLOW, bool UNCHECKED, class H>
 __device__ __forceinline__ void step_lane(const StepArgs& a, int64_t i, Lane& L, int& act, uint32_t& st,
                                           int32_t& rew, int32_t& ret, H& hist) {
   Rng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, i), 0u, make_uint4(0, 0, 0, 0)};
@@ -646,8 +653,9 @@ __device__ __forceinline__ void step_lane(const StepArgs& a, int64_t i, Lane& L,
   }
   COUP_TRACE_ANY(a, 6);
   st = COUP_STEP_MID;
-  const uint32_t err_before = L.err;
-  if (!UNIFORM && a.unchecked) {
+  uint32_t err_before;
+  if constexpr (UNCHECKED) {
+    err_before = L.err;
     uint4 w;
     if (!unchecked_decision(pack(L), x, &w)) {
       count_error(a.err_count);
@@ -655,10 +663,12 @@ __device__ __forceinline__ void step_lane(const StepArgs& a, int64_t i, Lane& L,
     }
     hist.record(L.move, hist_decision(x, L.M));
     L = unpack(w);
-  } else if (x > 17u || ((m >> x) & 1u) == 0u || is_terminal(L)) {
-    count_error(a.err_count);
-    return;
   } else {
+    if (x > 17u || ((m >> x) & 1u) == 0u || is_terminal(L)) {
+      count_error(a.err_count);
+      return;
+    }
+    err_before = L.err;
     hist.record(L.move, hist_decision(x, L.M));
     if (FLOW)
       apply_decision_v1(L, x);
@@ -741,7 +751,7 @@ struct StepLds {
   uint32_t pre[INFO == kInfoWrite ? T * kPreWords : 1];
 };
 
-template <bool UNIFORM, int OBS, int T, int INFO>
+template <bool UNIFORM, int OBS, int T, int INFO, bool UNCHECKED>
 __device__ __forceinline__ void step_group(const StepArgs& a, int64_t grp, StepLds<OBS, T, INFO>& lds, uint4 rec);
 
 // This thread's lane record of group grp (zeros past the batch).
@@ -756,7 +766,7 @@ __device__ __forceinline__ uint4 load_record(const StepArgs& a, int64_t grp) {
 // No early exit: the cooperative writers need every lane of the wave /
 // block.  INFO: maintain the per-lane history, and write the
 // InformationStateTensor of both players.
-template <bool UNIFORM, int OBS, int T, int INFO>
+template <bool UNIFORM, int OBS, int T, int INFO, bool UNCHECKED = false>
 __global__ __launch_bounds__(T, INFO == kInfoNone ? 8 : 4) void k_step(StepArgs a) {
   __shared__ StepLds<OBS, T, INFO> lds;
   if (StepLds<OBS, T, INFO>::kDesc) load_obs_desc(reinterpret_cast<uint32_t*>(lds.desc));
@@ -765,7 +775,7 @@ __global__ __launch_bounds__(T, INFO == kInfoNone ? 8 : 4) void k_step(StepArgs 
   // ahead -- measured no faster: DESIGN.md section 5.)
   COUP_TRACE(a, 0);
   const uint32_t grp = a.xcd_remap ? xcd_group(blockIdx.x, gridDim.x) : blockIdx.x;
-  step_group<UNIFORM, OBS, T, INFO>(a, grp, lds, load_record<T>(a, grp));
+  step_group<UNIFORM, OBS, T, INFO, UNCHECKED>(a, grp, lds, load_record<T>(a, grp));
 #ifdef COUP_WAVE_TRACE
   COUP_TRACE(a, 2);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -792,17 +802,17 @@ __device__ __forceinline__ void step_group_store(const StepArgs& a, int64_t grp,
 }
 
 // Step of group grp up to (for the wave-bitmap writers) the words in LDS.
-template <bool UNIFORM, int OBS, int T, int INFO>
+template <bool UNIFORM, int OBS, int T, int INFO, bool UNCHECKED>
 __device__ __forceinline__ void step_group_compute(const StepArgs& a, int64_t grp, StepLds<OBS, T, INFO>& lds,
                                                    uint4 rec);
 
-template <bool UNIFORM, int OBS, int T, int INFO>
+template <bool UNIFORM, int OBS, int T, int INFO, bool UNCHECKED>
 __device__ __forceinline__ void step_group(const StepArgs& a, int64_t grp, StepLds<OBS, T, INFO>& lds, uint4 rec) {
-  step_group_compute<UNIFORM, OBS, T, INFO>(a, grp, lds, rec);
+  step_group_compute<UNIFORM, OBS, T, INFO, UNCHECKED>(a, grp, lds, rec);
   if (is_wave_bits(OBS)) step_group_store<OBS, T, INFO>(a, grp, lds);
 }
 
-template <bool UNIFORM, int OBS, int T, int INFO>
+template <bool UNIFORM, int OBS, int T, int INFO, bool UNCHECKED>
 __device__ __forceinline__ void step_group_compute(const StepArgs& a, int64_t grp, StepLds<OBS, T, INFO>& lds,
                                                    uint4 rec) {
   constexpr bool kDesc = StepLds<OBS, T, INFO>::kDesc;
@@ -834,11 +844,11 @@ __device__ __forceinline__ void step_group_compute(const StepArgs& a, int64_t gr
     constexpr bool kFlow = OBS != kObsNone || INFO != kInfoNone;  // store-bound kernels (step_lane)
     if (INFO != kInfoNone) {
       RegHistory rec;
-      step_lane<UNIFORM, kFlow>(a, i, L, act, st, rew, ret, rec);
+      step_lane<UNIFORM, kFlow, UNCHECKED>(a, i, L, act, st, rew, ret, rec);
       rec.flush(lds.hist + threadIdx.x * kHist);
     } else {
       NoHistory none;
-      step_lane<UNIFORM, kFlow>(a, i, L, act, st, rew, ret, none);
+      step_lane<UNIFORM, kFlow, UNCHECKED>(a, i, L, act, st, rew, ret, none);
     }
     a.state[i] = pack(L);
     ep_update(a, i, eps, st, ret);
@@ -985,7 +995,7 @@ __global__ __launch_bounds__(kThreads) void k_step_trajectory(StepArgs a, int64_
     int act;
     uint32_t st;
     int32_t rew, ret = 0;
-    step_lane<true, false>(a, i, L, act, st, rew, ret, none);
+    step_lane<true, false, false>(a, i, L, act, st, rew, ret, none);
     const int64_t o = t * a.n + i;
     if (a.actions) a.actions[o] = (int8_t)act;
     if (a.rewards) {
@@ -1398,8 +1408,11 @@ __global__ __launch_bounds__(kThreads) void k_reset(uint4* state, int64_t n, con
 
 // State::ApplyAction per lane (decision or chance outcome); the entry goes
 // to the lane's history bytes when the env keeps a history.
+// UNCHECKED: COUP_FLAG_UNCHECKED (unchecked_decision); a compile-time
+// switch, as step_lane's.
+template <bool UNCHECKED>
 __global__ __launch_bounds__(kThreads) void k_apply(uint4* state, int64_t n, const int8_t* actions,
-                                                  uint8_t* hist, uint32_t* err_count, int unchecked) {
+                                                  uint8_t* hist, uint32_t* err_count) {
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= n) return;
   const int x = actions[i];
@@ -1410,17 +1423,19 @@ __global__ __launch_bounds__(kThreads) void k_apply(uint4* state, int64_t n, con
   // the byte store stays out of the inlined rules
   const uint32_t idx = L.move;
   const uint32_t entry = is_chance(L) ? hist_deal((uint32_t)x, L.qids & 1u) : hist_decision((uint32_t)x, L.M);
-  NoHistory none;
-  if (unchecked) {  // COUP_FLAG_UNCHECKED: the reference's unchecked ApplyAction
+  if constexpr (UNCHECKED) {  // the reference's unchecked ApplyAction
     uint4 w;
     if (!unchecked_decision(pack(L), (uint32_t)x, &w)) {
       count_error(err_count);
       return;
     }
     L = unpack(w);
-  } else if (!apply_action(L, (uint32_t)x, none)) {
-    count_error(err_count);
-    return;
+  } else {
+    NoHistory none;
+    if (!apply_action(L, (uint32_t)x, none)) {
+      count_error(err_count);
+      return;
+    }
   }
   if (L.err && !err_before) count_error(err_count);
   state[i] = pack(L);
@@ -1601,19 +1616,32 @@ constexpr uint32_t kSlotReset = 1u, kSlotDeal = 2u, kSlotUnchecked = 4u;
 // it when `unchecked`: apply_action_unchecked, coup_lane.h) into *out and
 // returns bit 0 = accepted without a new error, bit 1 = history entry to
 // store, bits 8..15 its index, bits 16..23 the entry byte.
-__device__ COUP_SLOT_FN uint32_t slot_transition(uint4 w, uint32_t x, uint32_t unchecked, uint4* out) {
+// The checked transition (State::ApplyAction with its legality check) on
+// record w into *out; false, *out not written, for an illegal action or one
+// that raises a new error.  Each transition form lives in a function of its
+// own (this one, unchecked_decision): one body combining both behind a
+// run-time flag is the shape the section-12 defect strikes (step_lane).
+__device__ COUP_SLOT_FN uint32_t checked_transition(uint4 w, uint32_t x, uint4* out) {
   Lane L = unpack(w);
-  const uint32_t idx = L.move;
-  const uint32_t entry = is_chance(L) ? hist_deal(x, L.qids & 1u) : hist_decision(x, L.M);
   const uint32_t err_before = L.err;
   NoHistory none;
-  if (!(unchecked ? apply_action_unchecked(L, x, none) : apply_action(L, x, none)) || (L.err && !err_before)) {
+  if (!apply_action(L, x, none) || (L.err && !err_before)) return 0u;
+  *out = pack(L);
+  return 1u;
+}
+
+__device__ COUP_SLOT_FN uint32_t slot_transition(uint4 w, uint32_t x, uint32_t unchecked, uint4* out) {
+  const Lane L = unpack(w);
+  const uint32_t idx = L.move;
+  const uint32_t entry = is_chance(L) ? hist_deal(x, L.qids & 1u) : hist_decision(x, L.M);
+  uint4 r;
+  if (!(unchecked ? unchecked_decision(w, x, &r) : checked_transition(w, x, &r))) {
     // a rejected action (or one the reference's DoApplyAction raises on)
     // leaves the record untouched
     *out = w;
     return 0u;
   }
-  *out = pack(L);
+  *out = r;
   const uint32_t store = idx < (uint32_t)kHist ? 2u : 0u;
   return 1u | store | (idx << 8) | (entry << 16);
 }
@@ -1634,17 +1662,15 @@ __device__ COUP_SLOT_FN uint32_t slot_step(uint4 w, uint32_t x, uint32_t mode, u
     L.err = L.episode == 0u ? 1u : 0u;  // counter wrap (coup_lane.h kEpisodeMask)
   }
   RegHistory rec;
-  uint32_t ok = 1u;
   if (x < 18u) {
     const uint32_t idx = L.move;
     const uint32_t entry = is_chance(L) ? hist_deal(x, L.qids & 1u) : hist_decision(x, L.M);
-    const uint32_t err_before = L.err;
-    NoHistory none;
-    if (!((mode & kSlotUnchecked) ? apply_action_unchecked(L, x, none) : apply_action(L, x, none)) ||
-        (L.err && !err_before)) {
+    uint4 r;
+    if (!((mode & kSlotUnchecked) ? unchecked_decision(pack(L), x, &r) : checked_transition(pack(L), x, &r))) {
       *out = w;  // untouched, the reset included
       return 0u;
     }
+    L = unpack(r);
     rec.record(idx, entry);
   }
   if (mode & kSlotDeal) {
@@ -1653,7 +1679,7 @@ __device__ COUP_SLOT_FN uint32_t slot_step(uint4 w, uint32_t x, uint32_t mode, u
   }
   rec.flush(hist);
   *out = pack(L);
-  return ok;
+  return 1u;
 }
 
 __device__ COUP_SLOT_FN void slot_result(uint4 w, uint32_t ok, coup_slot_result* out) {
@@ -1681,6 +1707,10 @@ __device__ __forceinline__ void slot_op(const SlotArgs& a, uint8_t* __restrict__
   const uint32_t t = threadIdx.x;
   const uint4* rs = a.src_state ? a.src_state : a.dst_state;
   const uint8_t* hs = a.src_state ? a.src_hist : a.dst_hist;
+  // the record's load goes out with the history's, one memory round trip
+  // for both (thread 0 used to issue it after the barrier)
+  uint4 rec = make_uint4(0u, 0u, 0u, 0u);
+  if (t == 0u) rec = a.init ? pack(initial_lane(0u)) : *rs;
   if (t < 6u)
     reinterpret_cast<uint4*>(hist)[t] =
         a.init ? make_uint4(~0u, ~0u, ~0u, ~0u) : reinterpret_cast<const uint4*>(hs)[t];
@@ -1692,7 +1722,6 @@ __device__ __forceinline__ void slot_op(const SlotArgs& a, uint8_t* __restrict__
   // moved them to scalar code and produced wrong records.
   Lane L = initial_lane(0u);
   if (t == 0u) {
-    uint4 rec = a.init ? pack(initial_lane(0u)) : *rs;
     uint32_t ok = 1u;
     if (a.mode & (kSlotReset | kSlotDeal)) {
       ok = slot_step(rec, a.action >= 0 ? (uint32_t)a.action : 0xFFu, a.mode, a.seed_lo, a.seed_hi, a.env_id, &rec,
@@ -1867,12 +1896,14 @@ __device__ __forceinline__ void server_op(uint64_t rs, uint64_t hs, uint64_t dst
                                           uint32_t env_id, uint8_t* hist, uint32_t* bits, uint32_t* pre,
                                           coup_slot_result* res) {
   const uint32_t t = threadIdx.x;
+  // the record's load goes out with the history's: one round trip for both
+  uint4 rec = make_uint4(0u, 0u, 0u, 0u);
+  if (t == 0u) rec = init ? pack(initial_lane(0u)) : ld16<kAuxDevice>(rs, 0u);
   if (t < 6u)
     reinterpret_cast<uint4*>(hist)[t] = init ? make_uint4(~0u, ~0u, ~0u, ~0u) : ld16<kAuxDevice>(hs, 16u * t);
   wave_sync();
   Lane L = initial_lane(0u);
   if (t == 0u) {
-    uint4 rec = init ? pack(initial_lane(0u)) : ld16<kAuxDevice>(rs, 0u);
     uint32_t ok = 1u;
     if (mode & (kSlotReset | kSlotDeal)) {
       ok = slot_step(rec, action >= 0 ? (uint32_t)action : 0xFFu, mode, seed_lo, seed_hi, env_id, &rec, hist);
@@ -2057,10 +2088,10 @@ int xcd_remap() {
 // Blocks of the step kernel: one per group of T lanes.
 unsigned step_grid(int64_t groups, int) { return (unsigned)(groups > 0 ? groups : 1); }
 
-template <bool U, int M, int T, int I>
+template <bool U, int M, int T, int I, bool UC = false>
 void launch_step(const coup_env*, const coup::StepArgs& a, int64_t n, unsigned dyn_lds, hipStream_t s) {
   const int64_t groups = (n + T - 1) / T;
-  coup::k_step<U, M, T, I><<<step_grid(groups, T), T, dyn_lds, s>>>(a);
+  coup::k_step<U, M, T, I, UC><<<step_grid(groups, T), T, dyn_lds, s>>>(a);
 }
 unsigned grid_for(int64_t n) { return (unsigned)((n + coup::kThreads - 1) / coup::kThreads); }
 
@@ -2461,6 +2492,25 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
   }
   if (uniform) {
     COUP_LAUNCH_MODES(true)
+  } else if (a.unchecked) {
+    // COUP_FLAG_UNCHECKED: the caller-action kernels with the reference's
+    // unchecked transition compiled in (the default writers only)
+    if (info == coup::kInfoNone) {
+      if (mode == 0)
+        launch_step<false, coup::kObsNone, 256, coup::kInfoNone, true>(env, a, n, dyn_lds, s);
+      else
+        launch_step<false, coup::kObsWaveBitsSc1, 256, coup::kInfoNone, true>(env, a, n, dyn_lds, s);
+    } else if (info == coup::kInfoHistory) {
+      if (mode == 0)
+        launch_step<false, coup::kObsNone, 256, coup::kInfoHistory, true>(env, a, n, dyn_lds, s);
+      else
+        launch_step<false, coup::kObsWaveBits, 256, coup::kInfoHistory, true>(env, a, n, dyn_lds, s);
+    } else {
+      if (mode == 0)
+        launch_step<false, coup::kObsNone, 256, coup::kInfoWrite, true>(env, a, n, dyn_lds, s);
+      else
+        launch_step<false, coup::kObsWaveBits, 256, coup::kInfoWrite, true>(env, a, n, dyn_lds, s);
+    }
   } else {
     COUP_LAUNCH_MODES(false)
   }
@@ -2673,8 +2723,12 @@ int coup_apply_action(coup_env* env, const int8_t* actions) {
   if (env->batch == 0) return COUP_OK;
   COUP_TRY(launching(env));
   if (env->generic) return np_result(coup::np::launch_apply(np_env(env), actions), "coup_apply_action");
-  coup::k_apply<<<grid_for(env->batch), coup::kThreads, 0, env->stream>>>(
-      env->state, env->batch, actions, env->hist, env->err_count, (env->flags & COUP_FLAG_UNCHECKED) ? 1 : 0);
+  if (env->flags & COUP_FLAG_UNCHECKED)
+    coup::k_apply<true><<<grid_for(env->batch), coup::kThreads, 0, env->stream>>>(env->state, env->batch, actions,
+                                                                                env->hist, env->err_count);
+  else
+    coup::k_apply<false><<<grid_for(env->batch), coup::kThreads, 0, env->stream>>>(env->state, env->batch, actions,
+                                                                                 env->hist, env->err_count);
   COUP_HIP_TRY(hipGetLastError());
   return COUP_OK;
 }

@@ -65,6 +65,8 @@ class BatchedCoupEnv:
         counts in error_count().
     """
 
+    _served = False  # attached to an op server (pyspiel's lane pool sets it)
+
     def __init__(self, batch, seed=0, env_id_base=0, auto_reset=True, obs=True, info_state=False,
                  history=False, device=None, num_players=2, generic=False, episode_stats=False, unchecked=False):
         if not (0 <= int(env_id_base) and int(env_id_base) + int(batch) <= 1 << 32):

@@ -185,6 +185,7 @@ class _Pool:
         self.device = torch.device(device)
         self.lock = threading.RLock()
         self.lib = _native.load()
+        self._slot_op = self.lib.coup_slot_op
         self.segs = []
         self.free = []
         nbytes = _native.SLOT_RESULT_BYTES + 2 * OBS_SIZE * 4 + 2 * INFO_STATE_SIZE * 4
@@ -256,6 +257,30 @@ class _Pool:
 
     def handle(self, slot):
         return self.segs[slot[0]]._h
+
+    def apply_op(self, slot, src_slot, action):
+        """The answered unchecked ApplyAction of apply_action (slot) and
+        child (slot None: a new one, a copy of src_slot first) as one C call
+        under one lock acquisition -- the per-node ops of a tree walk
+        (deep_cfr.py:440-447, outcome_sampling_mccfr.py:61-100) without the
+        general op's bookkeeping.  Returns (slot, result)."""
+        with self.lock:
+            new = slot is None
+            if new:
+                slot = self._alloc()
+            env = self.segs[slot[0]]
+            if not env._served:
+                env._bind_stream()
+            if src_slot is None:
+                rc = self._slot_op(env._h, slot[1], None, 0, action, _native.SLOT_UNCHECKED, self.host_ptr)
+            else:
+                rc = self._slot_op(env._h, slot[1], self.segs[src_slot[0]]._h, src_slot[1], action,
+                                   _native.SLOT_UNCHECKED, self.host_ptr)
+            if rc:
+                if new:
+                    self.free.append(slot)
+                _native.check(rc)
+            return slot, _parse_result(self.buf[:_native.SLOT_RESULT_BYTES].tobytes())
 
     def op(self, slot, src=None, action=-1, init=False, obs=False, info=False, result=True, unchecked=False):
         """coup_slot_op on `slot`; src = (coup_env handle, lane) or None;
@@ -589,9 +614,9 @@ class CoupState:
         actions too (LegalActions can offer one DoApplyAction refuses once
         unchecked play has left legal play's states).  Raises SpielError, the
         state unchanged, where the reference raises."""
-        player = self.current_player()
+        player = self._q["current_player"]
         a = _action_id(action)
-        q = self._pool.op(self._slot, action=a, unchecked=True)
+        _, q = self._pool.apply_op(self._slot, None, a)
         if not q["ok"]:
             raise SpielError(_apply_failed(player, a))
         self._q = q
@@ -609,18 +634,12 @@ class CoupState:
     def child(self, action):
         """clone() + apply_action(action) (State::Child, spiel.h) as ONE op:
         the new state's lane is a copy of this one with the action applied."""
-        q = self._q
-        player = q["current_player"]
+        player = self._q["current_player"]
         a = _action_id(action)
-        pool = self._pool
-        slot = pool.alloc()
-        try:
-            q = pool.op(slot, src=(pool.segs[self._slot[0]]._h, self._slot[1]), action=a, unchecked=True)
-            if not q["ok"]:
-                raise SpielError(_apply_failed(player, a))
-        except Exception:
-            pool.release(slot)
-            raise
+        slot, q = self._pool.apply_op(None, self._slot, a)
+        if not q["ok"]:
+            self._pool.release(slot)
+            raise SpielError(_apply_failed(player, a))
         return CoupState(self._game, _slot=slot, _q=q, _history=self._history + [(player, a)])
 
     def children(self, actions, obs=False, info_state=False):

@@ -207,9 +207,14 @@ def test_rl_environment_unchecked_step_matches_oracle():
             ts = env.reset()
         a = _env_actions(rng, ts)
         before = env.get_state
-        how = _outcome(_replay(before), a)
-        if how == "stuck":
-            a = int(rng.choice(ts.observations["legal_actions"][ts.current_player()]))
+        ref0 = _replay(before)
+        how = _outcome(ref0, a)
+        if how == "stuck":  # take one that applies and goes on, or start over
+            good = [b for b in range(18) if _outcome(ref0, b) == "ok"]
+            if not good:
+                ts = env.reset()
+                continue
+            a, how = int(rng.choice(good)), "ok"
         if how == "reject":
             rejected += 1
             with pytest.raises(pyspiel.SpielError):
@@ -246,15 +251,27 @@ def test_sync_vector_env_unchecked_equals_loop():
     assert venv.batched
     for t in range(60):
         acts = [_env_actions(rng, ts) for ts in ts_loop]
-        # the envs where the reference raises: drop their action (act on the
-        # others) so both forms step the same envs
-        ok = [ts.last() or _outcome(_replay(e.get_state), a) == "ok"
-              for e, a, ts in zip(loop_envs, acts, ts_loop)]
-        acts = [a if o else int(rng.choice(ts.observations["legal_actions"][ts.current_player()]))
-                for a, o, ts in zip(acts, ok, ts_loop)]
+        # where the reference raises (or the state would leave the record's
+        # fields) take an action that applies instead --
+        # legal ones can fail too once unchecked play has left legal play's
+        # states -- so both forms step the same envs
+        stuck = False
+        for i, (e, ts) in enumerate(zip(loop_envs, ts_loop)):
+            if ts.last():
+                continue
+            ref = _replay(e.get_state)
+            if _outcome(ref, acts[i]) != "ok":
+                good = [b for b in range(18) if _outcome(ref, b) == "ok"]
+                if not good:
+                    stuck = True
+                    break
+                acts[i] = int(rng.choice(good))
+        if stuck:
+            break
         ts_loop = [e.step([a]) for e, a in zip(loop_envs, acts)]
         ts_vec, _, _, _ = venv.step([_Out(a) for a in acts])
         for a_ts, b_ts in zip(ts_loop, ts_vec):
             assert a_ts.step_type == b_ts.step_type and a_ts.rewards == b_ts.rewards
             assert a_ts.observations["info_state"] == b_ts.observations["info_state"]
             assert a_ts.observations["legal_actions"] == b_ts.observations["legal_actions"]
+    assert t >= 30

@@ -79,7 +79,7 @@ def main():
             return False
         if fused:
             return "k_rollout" in kn
-        m = (re.search(r"k_step<true, (\d+), \d+, (\d+)>", kn) or
+        m = (re.search(r"k_step<true, (\d+), \d+, (\d+)(?:, false)?>", kn) or
              re.search(r"k_stepILb1ELi(\d+)ELi\d+ELi(\d+)E", kn))
         return bool(m) and (m.group(1) != "0") == want_obs and (m.group(2) == "2") == want_info
 
