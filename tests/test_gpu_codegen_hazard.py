@@ -6,12 +6,13 @@ per lane (every batched kernel's form; the expected result), on a
 wave-uniform record with the rules inlined, on a wave-uniform record with
 the rules behind __noinline__ functions (the shipped k_slot's form), and
 through copies of k_slot built with the rules inlined (COUP_SLOT_INLINE).
-The shipped form must agree with the per-lane form on every case; the
-inlined k_slot copies are reported (ROCm 7.2 at -O2/-O3 gets word 3 of the
-record wrong after Tax / Exchange / Steal / Block announcements).  The
-reproducer is built with the branch-form rules (-DCOUP_RULES_V1), the form
-that triggers it; it also reports round 1's k_apply with the history byte
-stored from inside the rules (apply_bytehist_*)."""
+The reproducer is built with the branch-form rules (-DCOUP_RULES_V1) and the
+product's flags, which turn LLVM's SLP vectorizer off: with it, ROCm 7.2 at
+-O2/-O3 gets word 3 of the record wrong after Tax / Exchange / Steal / Block
+announcements in every inlined copy (an opt-bisect pins the first failing
+pass to slp-vectorizer); without it every form must
+agree with the per-lane rules, inlined copies and round 1's k_apply with the
+history byte stored from inside the rules (apply_bytehist_*) included."""
 import json
 import os
 import subprocess
@@ -37,5 +38,7 @@ def test_shipped_slot_form_matches_per_lane_rules():
     assert summary["uniform_inline_mismatch"] == 0
     # every action id was exercised
     assert all(v[0] > 0 for v in summary["by_action"].values())
-    print("\ninlined k_slot copies, mismatching records of 20000:",
-          {k: v["mismatch"] for k, v in variants.items()})
+    counts = {k: v["mismatch"] for k, v in variants.items()}
+    print("\ninlined k_slot copies, mismatching records of 20000:", counts)
+    # built without the SLP vectorizer, the inlined shapes compile right too
+    assert all(c == 0 for c in counts.values()), counts

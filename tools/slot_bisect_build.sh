@@ -1,5 +1,6 @@
 #!/bin/bash
-# Build the k_slot reproducer (tools/slot_inline_repro.hip) with LLVM's
+# Build the k_slot reproducer (tools/slot_inline_repro.hip) WITH the SLP
+# vectorizer (the product builds without it: the defect's trigger) and LLVM's
 # -opt-bisect-limit=N for each N given: passes past N are skipped (in the
 # device and the host compilations alike; the host code only gets slower).
 # Running the binaries on a GPU finds the first device pass after which
