@@ -42,6 +42,12 @@ ARCH = os.environ.get("COUP_OFFLOAD_ARCH", "gfx950")
 # are 0.7-1% faster without it (profiles/r03/codegen/).
 NO_SLP = "-fno-slp-vectorize"
 
+# Optimisation level per source: the N-player kernels build at -O2, which
+# measured 1% faster for the 6-player step (33.7-34.0 against 33.9-34.5 us)
+# while -O2 cost the headline c3 step 0.5-1 us, so the 2-player file stays at
+# -O3 (alternating processes, profiles/r03/ab/compiler_flags.txt).
+OPT = {"coup_kernels.hip": "-O3", "coup_nplayer.hip": "-O2"}
+
 
 def command(resource_usage=False, out=OUT, defines=()):
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", NO_SLP, "-std=c++17", "-fPIC", "-shared",
@@ -113,7 +119,7 @@ def build(force=False, verbose=False, repro=False):
         for src in SOURCES:
             obj = os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
             objs.append(obj)
-            cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", NO_SLP, "-std=c++17", "-fPIC", "-Wall", "-I",
+            cmd = [HIPCC, f"--offload-arch={ARCH}", OPT[os.path.basename(src)], NO_SLP, "-std=c++17", "-fPIC", "-Wall", "-I",
                    os.path.join(ROOT, "include"), "-c", src, "-o", obj]
             if verbose:
                 cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
