@@ -42,11 +42,12 @@ ARCH = os.environ.get("COUP_OFFLOAD_ARCH", "gfx950")
 # are 0.7-1% faster without it (profiles/r03/codegen/).
 NO_SLP = "-fno-slp-vectorize"
 
-# Optimisation level per source: the N-player kernels build at -O2, which
-# measured 1% faster for the 6-player step (33.7-34.0 against 33.9-34.5 us)
-# while -O2 cost the headline c3 step 0.5-1 us, so the 2-player file stays at
-# -O3 (alternating processes, profiles/r03/ab/compiler_flags.txt).
-OPT = {"coup_kernels.hip": "-O3", "coup_nplayer.hip": "-O2"}
+# Optimisation level per source.  -O2 measured 1% faster than -O3 for the
+# 6-player step (33.7-34.0 against 33.9-34.5 us) but 6% slower for its
+# trajectory kernel (26.3-26.5 against 24.7-24.9 us per step) and 0.5-1 us
+# slower for the headline c3 step (alternating processes,
+# profiles/r03/ab/compiler_flags.txt, o2_vs_o3_np_trajectory.txt): -O3 for both.
+OPT = {"coup_kernels.hip": "-O3", "coup_nplayer.hip": "-O3"}
 
 
 def command(resource_usage=False, out=OUT, defines=()):
