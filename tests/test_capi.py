@@ -53,6 +53,11 @@ def test_create_ex_validates_players_and_flags():
     assert L.coup_create_ex(16, 0, 0, _native.FLAG_HISTORY | _native.FLAG_GENERIC, 2,
                             ctypes.byref(h)) == _native.COUP_E_INVALID
     assert L.coup_create_ex(16, 0, 0, 64, 2, ctypes.byref(h)) == _native.COUP_E_INVALID
+    # the reference's unchecked ApplyAction is the 2-player engine's
+    assert L.coup_create_ex(16, 0, 0, _native.FLAG_UNCHECKED, 3, ctypes.byref(h)) == _native.COUP_E_INVALID
+    assert b"UNCHECKED" in L.coup_last_error()
+    assert L.coup_create_ex(16, 0, 0, _native.FLAG_UNCHECKED | _native.FLAG_GENERIC, 2,
+                            ctypes.byref(h)) == _native.COUP_E_INVALID
     assert not h.value
     assert L.coup_num_players(None) == -1 and L.coup_state_bytes(None) == -1
 
@@ -127,3 +132,20 @@ def test_episode_counter_is_28_bits_in_the_record():
         r = packed.lane(np.array([st.pack(ep)], np.uint32))
         assert r["episode"] == ep
         assert {k: v for k, v in r.items() if k != "episode"} == {k: v for k, v in base.items() if k != "episode"}
+
+
+def test_device_builds_turn_the_slp_vectorizer_off(monkeypatch):
+    """Every device compile of the product (and the section-12 reproducer the
+    GPU suite runs) carries -fno-slp-vectorize: with LLVM's SLP vectorizer,
+    ROCm 7.2 miscompiles the packed-record rules in several code shapes
+    (DESIGN.md section 12).  The commands are inspected, nothing is built."""
+    from open_spiel_coup_amd import build as b
+    cmds = []
+    monkeypatch.setattr(b, "_run_all", lambda jobs, verbose=False: cmds.extend(jobs))
+    monkeypatch.setattr(b, "up_to_date", lambda *a, **k: False)
+    monkeypatch.setattr(b.subprocess, "check_call", lambda cmd, *a, **k: cmds.append(cmd))
+    b.build(force=True, repro=True)
+    device = [c for c in cmds if c[0] == b.HIPCC and any(str(x).endswith(".hip") for x in c)]
+    assert len(device) == 3  # the two product sources and the reproducer
+    assert all(b.NO_SLP in c for c in device)
+    assert b.NO_SLP in b.command() and b.NO_SLP in b.repro_command()
