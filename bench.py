@@ -2,6 +2,11 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c3i|c2|c2r|c2t|c4|c4r|c4t]
 
+--gpus N: N ranks, one process per GPU.  Under torchrun (WORLD_SIZE set) N
+must equal WORLD_SIZE; run directly with N > 1, this process starts the N
+rank processes itself (before it touches the GPU) with the torchrun
+environment, relays rank 0's line and fails if any rank fails.
+
 Workload (default c3 = configs[2] of BASELINE.json, the batch-2^20 config the
 metric is quoted on): 2-player Coup, B = 2^20 lanes per GPU, uniform-random
 policy drawn in-kernel, one env step per lane per launch, with the
@@ -46,7 +51,10 @@ host core, same per-lane workload.
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -88,10 +96,20 @@ def payload_width(players, steps, batch):
     return 4 if steps <= 1000 else 8
 
 
+def episode_stats_mode(width):
+    """BatchedCoupEnv(episode_stats=...) for a payload width: the packed word
+    the step kernels accumulate in place (2 / 4 bytes, csrc/coup_episodes.h),
+    so the payload needs no packing inside the timed window; the int32 pair
+    beyond 1000 steps."""
+    return width if width in (2, 4) else True
+
+
 def pack_episodes(eps, ret, width):
-    """[B] int32 episode counts and return sums -> the collective's payload:
-    int16 (return << 8 | episodes) with lane pairs viewed as int32 (RCCL has
-    no int16 type), int32 (return << 16 | episodes), or [B, 2] int32."""
+    """[B] int32 episode counts and return sums -> the payload format, as a
+    torch computation: what the kernels' packed word holds (int16 return << 8
+    | episodes with lane pairs viewed as int32, RCCL having no int16 type;
+    int32 return << 16 | episodes), or [B, 2] int32.  Tests compare the
+    kernels' words with it; the timed path does not run it."""
     import torch
     if width == 2:
         return ((ret.to(torch.int16) << 8) | eps.to(torch.int16)).view(torch.int32)
@@ -101,8 +119,8 @@ def pack_episodes(eps, ret, width):
 
 
 def unpack_episodes(g, width):
-    """Inverse of pack_episodes over the gathered payload: (episodes, return
-    sums) as int32 [world * B]."""
+    """The gathered payload (the packed words as int32, or [world * B, 2]
+    int32 pairs) -> (episodes, return sums) as int32 [world * B]."""
     import torch
     if width == 2:
         h = g.view(torch.int16)
@@ -142,7 +160,9 @@ def _writer(mode_env):
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one process per GPU); default WORLD_SIZE, or 1.  Without torchrun, N > 1 starts the "
+                         "N rank processes here")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--settle", type=int, default=256,
@@ -161,6 +181,8 @@ def parse():
     ap.add_argument("--force-collective", action="store_true",
                     help="run the collectives (all-gather, barrier, max over ranks) even at one rank, over a "
                          "one-rank communicator of --dist-backend (MASTER_ADDR / MASTER_PORT must be set)")
+    ap.add_argument("--dump-episodes", default=None,
+                    help="rank 0 saves the gathered per-lane episode counts and return sums (.npz; tests)")
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
                     help="replay the K timed steps from one HIP graph (auto: on for c2, c3 and c4, "
                          "where it removes the per-step launch gaps)")
@@ -332,8 +354,84 @@ def _calibrate_gate(env, stream):
     return max(1, math.ceil(3.0 * sorted(lat)[len(lat) // 2] / max(step_s, 1e-9)))
 
 
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n, argv, backend="nccl", script=None):
+    """--gpus N > 1 without torchrun: start N rank processes of `script`
+    (this file) with `argv` and the torchrun environment (RANK, LOCAL_RANK,
+    WORLD_SIZE, MASTER_ADDR / MASTER_PORT on 127.0.0.1), one GPU each.  This
+    process never initialises the GPU (torch.cuda.device_count() does not on
+    ROCm) and execs nothing: the ranks are child processes.  Relays rank 0's
+    JSON line; returns non-zero if any rank fails (the others are then
+    stopped) or rank 0 prints no line."""
+    script = script or os.path.abspath(__file__)
+    if backend == "nccl":
+        import torch
+        vis = torch.cuda.device_count()
+        if n > vis:
+            print(f"bench.py: --gpus {n} with nccl needs {n} visible GPUs, found {vis}", file=sys.stderr)
+            return 2
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, script] + list(argv), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr, text=True))
+    lines = []
+    reader = threading.Thread(target=lambda: lines.extend(procs[0].stdout), daemon=True)
+    reader.start()
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 1
+                print(f"bench.py: rank {procs.index(p)} exited with {c}; stopping the other ranks", file=sys.stderr)
+                for q in live:
+                    q.terminate()
+                deadline = time.time() + 30
+                for q in live:
+                    try:
+                        q.wait(max(0.1, deadline - time.time()))
+                    except subprocess.TimeoutExpired:
+                        q.kill()
+                        q.wait()
+                live = []
+        time.sleep(0.05)
+    reader.join(timeout=30)
+    for ln in lines:
+        if not ln.lstrip().startswith("{"):
+            sys.stderr.write(ln)
+    out = [ln for ln in lines if ln.lstrip().startswith("{")]
+    if rc == 0 and not out:
+        print("bench.py: rank 0 printed no line", file=sys.stderr)
+        rc = 1
+    if rc == 0:
+        print(out[-1].rstrip("\n"), flush=True)
+    return rc
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" in os.environ:
+        ws = int(os.environ["WORLD_SIZE"])
+        if args.gpus is not None and args.gpus != ws:
+            print(f"bench.py: --gpus {args.gpus} disagrees with WORLD_SIZE={ws}", file=sys.stderr)
+            sys.exit(2)
+    elif args.gpus is not None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], args.dist_backend))
+    elif args.gpus is not None and args.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr)
+        sys.exit(2)
     import torch
     import torch.distributed as dist
 
@@ -348,12 +446,17 @@ def main():
     cfg = args.config
     B0, with_obs, with_info, fused, bytes_per_lane, workload, players = CONFIGS[cfg]
     B = args.batch or B0
-    env = BatchedCoupEnv(B, seed=args.seed, env_id_base=D.env_id_base(rank, B), auto_reset=True, obs=with_obs,
-                         info_state=with_info, device=dev, num_players=players, episode_stats=fused != "rollout")
+    width = payload_width(players, args.steps, B)
     # per-lane finished-episode counts and player-0 return sums of the timed
-    # steps: the step kernels accumulate them (coup_step_outputs.episodes /
-    # return_sum), the fused rollout through coup_rollout_stats
-    stats = env.new_stats() if fused == "rollout" else None
+    # steps, accumulated by the kernels in the collective's own format: one
+    # packed word per lane (int16 return << 8 | episodes at the driver's K;
+    # coup_step_outputs.episode_word, coup_rollout_stats for the fused rollout)
+    env = BatchedCoupEnv(B, seed=args.seed, env_id_base=D.env_id_base(rank, B), auto_reset=True, obs=with_obs,
+                         info_state=with_info, device=dev, num_players=players,
+                         episode_stats=episode_stats_mode(width) if fused != "rollout" else False)
+    stats = None
+    if fused == "rollout":
+        stats = env.new_stats(width) if width in (2, 4) else env.new_stats()
 
     def barrier():
         if grouped:
@@ -387,15 +490,13 @@ def main():
             gate.steps = 0
         else:
             gate = env.rollout_launcher(_calibrate_gate(env, stream))
-    def episode_tensors():
-        if stats is not None:
-            return stats["episodes"], stats["return_sum"]
-        return env.episode_stats()
-
-    width = payload_width(players, args.steps, B)
-
     def episode_payload():
-        return pack_episodes(*episode_tensors(), width)
+        # the accumulators themselves (no kernel runs to build the payload)
+        if stats is None:
+            return env.episode_payload()
+        if "episode_word" in stats:
+            return stats["episode_word"].view(torch.int32) if width == 2 else stats["episode_word"]
+        return torch.stack((stats["episodes"], stats["return_sum"]), 1)
 
     def unpack_payload(g):
         return unpack_episodes(g, width)
@@ -439,6 +540,9 @@ def main():
     g_eps, g_ret = unpack_payload(gathered)
     ep_total = int(g_eps.sum())
     ret_total = int(g_ret.sum())
+    if args.dump_episodes and rank == 0:
+        import numpy as np
+        np.savez(args.dump_episodes, episodes=g_eps.cpu().numpy(), return_sum=g_ret.cpu().numpy())
 
     # per env step: the span of the K steps (one replay, one fused launch or K
     # eager launches) / K, launch gaps included
@@ -453,6 +557,9 @@ def main():
     barrier()
     D.max_over_ranks(0.0, dev, force=force)
     collective_ms = (time.perf_counter() - tc) * 1e3
+    # every rank's tail (rank 0 prints them; one value at one rank)
+    collective_ms_ranks = [float(x) for x in
+                           D.collate(torch.tensor([collective_ms], dtype=torch.float64, device=dev), force=force)]
     errors = env.error_count()
     ceiling_ms = None
     if players == 2 and not fused and not with_info:
@@ -527,6 +634,7 @@ def main():
                                         "all_gather [world*B, 2] int32 (episodes, return sum per lane)")
                          if grouped else None,
                          "collective_ms": collective_ms,
+                         "collective_ms_ranks": collective_ms_ranks,
                          "collective_backend": (args.dist_backend + (" (one-rank communicator)" if world == 1 else ""))
                          if grouped else None},
             "lane_errors": errors,

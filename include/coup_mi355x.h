@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define COUP_ABI_VERSION 9
+#define COUP_ABI_VERSION 10
 
 #define COUP_NUM_PLAYERS 2          /* coup.h:42 */
 #define COUP_MAX_PLAYERS 6          /* N-player extension */
@@ -93,6 +93,16 @@ typedef struct {
    * (SURVEY.md 8(e)).  Both or neither. */
   int32_t* episodes;    /* [B] */
   int32_t* return_sum;  /* [B] */
+  /* The same accumulators packed into ONE word per lane (instead of
+   * episodes / return_sum, not with them): return_sum << 8 | episodes as
+   * int16 (episode_word_bytes = 2) or return_sum << 16 | episodes as int32
+   * (4), two's complement, updated by adding (return << S) + 1 at each
+   * finished episode.  The word is the all-gather payload as it stands
+   * (2 bytes per lane each way at 2 bytes).  Fields do not saturate: the
+   * caller bounds the steps between clears (int16: <= 255 episodes and
+   * |return_sum| <= 127, i.e. 2 (N - 1) K <= 127). */
+  void* episode_word;          /* [B] int16 or int32 */
+  int32_t episode_word_bytes;  /* 2 or 4 when episode_word != NULL */
 } coup_step_outputs;
 
 /* Per-lane query of the current state (State accessors); all optional. */
@@ -150,6 +160,10 @@ typedef struct {
   int32_t* episodes;    /* [B] episodes finished */
   int32_t* return_sum;  /* [B] sum over finished episodes of player 0's return */
   int32_t* length_sum;  /* [B] sum over finished episodes of decisions taken */
+  /* episodes / return_sum packed as coup_step_outputs.episode_word (instead
+   * of the pair, not with it) */
+  void* episode_word;
+  int32_t episode_word_bytes;
 } coup_rollout_stats;
 
 /* ABI version of the loaded library (== COUP_ABI_VERSION). */

@@ -11,7 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # COUP_LIB_PATH: load another build of the same library (A/B timing of two
 # builds, tools/ab_builds.sh); there is still no fallback
 LIB_PATH = os.environ.get("COUP_LIB_PATH") or os.path.join(HERE, "libcoup_mi355x.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
 FLAG_AUTO_RESET, FLAG_HISTORY, FLAG_GENERIC, FLAG_UNCHECKED = 1, 2, 4, 8
 MAX_PLAYERS = 6
 HISTORY_BYTES = 96
@@ -40,7 +40,8 @@ class StepOutputs(ctypes.Structure):
                 ("step_type", ctypes.c_void_p), ("legal_mask", ctypes.c_void_p),
                 ("cur_player", ctypes.c_void_p), ("obs", ctypes.c_void_p),
                 ("info_state", ctypes.c_void_p), ("episodes", ctypes.c_void_p),
-                ("return_sum", ctypes.c_void_p)]
+                ("return_sum", ctypes.c_void_p), ("episode_word", ctypes.c_void_p),
+                ("episode_word_bytes", ctypes.c_int32)]
 
 
 class QueryOutputs(ctypes.Structure):
@@ -52,7 +53,8 @@ class QueryOutputs(ctypes.Structure):
 
 class RolloutStats(ctypes.Structure):
     _fields_ = [("episodes", ctypes.c_void_p), ("return_sum", ctypes.c_void_p),
-                ("length_sum", ctypes.c_void_p)]
+                ("length_sum", ctypes.c_void_p), ("episode_word", ctypes.c_void_p),
+                ("episode_word_bytes", ctypes.c_int32)]
 
 
 class SlotReq(ctypes.Structure):

@@ -20,7 +20,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 SOURCES = [os.path.join(CSRC, "coup_kernels.hip"), os.path.join(CSRC, "coup_nplayer.hip")]
-DEPS = SOURCES + [os.path.join(CSRC, h) for h in ("coup_lane.h", "coup_nlane.h", "coup_np.h", "coup_regroup.h")] + [
+DEPS = SOURCES + [os.path.join(CSRC, h) for h in ("coup_lane.h", "coup_nlane.h", "coup_np.h", "coup_regroup.h", "coup_episodes.h")] + [
     os.path.join(ROOT, "include", "coup_mi355x.h")]
 OUT = os.path.join(HERE, "libcoup_mi355x.so")
 OBJ_DIR = os.path.join(ROOT, "build", "obj")  # git-ignored (build/)

@@ -523,9 +523,7 @@ struct StepArgs {
   float* obs;
   uint8_t* hist;   // [B][96] history bytes (INFO != kInfoNone)
   float* info;     // [B][2][2492] (INFO == kInfoWrite)
-  int32_t* ep_count;   // [B] per-episode accumulators (coup_step_outputs.episodes)
-  int32_t* ep_return;  // [B] (coup_step_outputs.return_sum)
-  int ep_mode;         // episode accumulators: kEpEarly / kEpEarlyAll / kEpLate (COUP_EP_MODE, A/B)
+  EpAcc ep;        // per-episode accumulators (coup_step_outputs.episodes / return_sum or episode_word)
   uint32_t* err_count;
   int xcd_remap;   // block -> lane group mapping (xcd_group)
   int unchecked;   // caller actions outside LegalActions go through the reference's unchecked ApplyAction
@@ -693,43 +691,22 @@ __device__ __forceinline__ void step_lane(const StepArgs& a, int64_t i, Lane& L,
   COUP_TRACE_ANY(a, 9);
 }
 
-// How a step updates the per-episode accumulators (coup_step_outputs.
-// episodes / return_sum).  kEpEarlyAll (default): the lane's two words are
+// The per-episode accumulators (coup_episodes.h): the lane's word(s) are
 // loaded with its record, before the rules, and every lane stores them back
-// (coalesced, unchanged where no episode ended); kEpEarly: the same load,
-// stores only where an episode ended; kEpLate: load-add-store after the
-// rules at the finished lanes only.  Same-process A/B on the c3 step
-// (2^20 lanes, obs x2; profiles/r02/ab/ab_epstats.jsonl): no accumulators
-// 148.8 us, kEpEarlyAll 153.0, kEpEarly 163.3, kEpLate 163.9 -- the ~7% of
-// lanes that finish scatter 4-byte stores over most lines, and those
-// partial-line writes cost more than 16 MB of full-line ones.
-enum EpMode : int { kEpEarlyAll = 0, kEpEarly = 1, kEpLate = 2 };
-
-struct EpStats {
-  int32_t count = 0, ret = 0;
-};
-
-__device__ __forceinline__ EpStats ep_prefetch(const StepArgs& a, int64_t i, bool active) {
-  EpStats e;
-  if (a.ep_count && a.ep_mode != kEpLate && active) {
-    e.count = a.ep_count[i];
-    e.ret = a.ep_return[i];
-  }
-  return e;
+// (coalesced; unchanged where no episode ended).  Same-process A/B on the c3
+// step with the int32 pair (2^20 lanes, obs x2; profiles/r02/ab/
+// ab_epstats.jsonl): no accumulators 148.8 us, this form 153.0, stores only
+// where an episode ended 163.3, load-add-store after the rules at those lanes
+// 163.9 -- the ~7% of lanes that finish scatter their stores over most lines,
+// and those partial-line writes cost more than full-line ones.  The packed
+// int16 word (round 4) moves 2 bytes per lane each way instead of 8.
+__device__ __forceinline__ int2 ep_prefetch(const StepArgs& a, int64_t i, bool active) {
+  return active ? a.ep.load(i) : make_int2(0, 0);
 }
 
-__device__ __forceinline__ void ep_update(const StepArgs& a, int64_t i, const EpStats& e, uint32_t st, int32_t ret) {
-  if (!a.ep_count) return;
+__device__ __forceinline__ void ep_update(const StepArgs& a, int64_t i, int2 e, uint32_t st, int32_t ret) {
   const bool last = st == COUP_STEP_LAST;
-  if (a.ep_mode == kEpLate) {
-    if (last) {
-      a.ep_count[i] += 1;
-      a.ep_return[i] += ret;
-    }
-  } else if (last || a.ep_mode == kEpEarlyAll) {
-    a.ep_count[i] = e.count + (last ? 1 : 0);
-    a.ep_return[i] = e.ret + (last ? ret : 0);
-  }
+  a.ep.store(i, e, last ? 1 : 0, last ? ret : 0);
 }
 
 // Wave-scope hand-off of LDS data between lanes of one wave.
@@ -826,7 +803,7 @@ __device__ __forceinline__ void step_group_compute(const StepArgs& a, int64_t gr
   const int64_t wleft = a.n - wave0;
   const uint32_t wave_valid = wleft >= 64 ? 64u : (wleft > 0 ? (uint32_t)wleft : 0u);  // wave-uniform
   uint8_t* hist_wave = lds.hist + wl * kHist;
-  const EpStats eps = ep_prefetch(a, i, active);
+  const int2 eps = ep_prefetch(a, i, active);
   if (INFO != kInfoNone) {
     if (wave_valid) wave_hist_copy<true>(a.hist + wave0 * kHist, hist_wave, wave_valid);
     wave_sync();
@@ -934,8 +911,7 @@ struct RolloutArgs {
   int64_t n;
   uint32_t seed_lo, seed_hi, env_id_base;
   int64_t steps;
-  int32_t* episodes;
-  int32_t* return_sum;
+  EpAcc ep;  // coup_rollout_stats: episodes / return_sum or episode_word
   int32_t* length_sum;
   uint32_t* err_count;
 };
@@ -973,8 +949,7 @@ __global__ __launch_bounds__(kThreads) void k_rollout(RolloutArgs a) {
     }
   }
   a.state[i] = pack(L);
-  if (a.episodes) a.episodes[i] += eps;
-  if (a.return_sum) a.return_sum[i] += ret;
+  a.ep.add(i, eps, ret);
   if (a.length_sum) a.length_sum[i] += len;
   if (errs) atomicAdd(a.err_count, errs);
 }
@@ -1011,10 +986,7 @@ __global__ __launch_bounds__(kThreads) void k_step_trajectory(StepArgs a, int64_
     }
   }
   a.state[i] = pack(L);
-  if (a.ep_count) {
-    a.ep_count[i] += eps;
-    a.ep_return[i] += ret_sum;
-  }
+  a.ep.add(i, eps, ret_sum);
 }
 
 // The regrouping key of decision x at L: x itself, or refine_key
@@ -1062,7 +1034,7 @@ __global__ __launch_bounds__(T, 8) void k_step_sorted(StepArgs a) {
   // phase 1: up to the decision (step_lane)
   Lane L = initial_lane(0u);
   uint32_t key = kKeyDead, st = COUP_STEP_MID;
-  const EpStats eps = ep_prefetch(a, i, live);
+  const int2 eps = ep_prefetch(a, i, live);
   if (live) {
     L = unpack(a.state[i]);
     Rng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, i), 0u, make_uint4(0, 0, 0, 0)};
@@ -1111,7 +1083,7 @@ __global__ __launch_bounds__(T, 8) void k_step_sorted(StepArgs a) {
         if (L.err && !err_before) count_error(a.err_count);
         const bool term = is_terminal(L);
         out = (x + 1u) | ((term ? COUP_STEP_LAST : COUP_STEP_MID) << 5) | ((uint32_t)(L.r0 + 2) << 7);
-        if (a.ep_count && term) out |= (uint32_t)(return0(L) + 2) << 10;
+        if (a.ep.on() && term) out |= (uint32_t)(return0(L) + 2) << 10;
         pending = term && a.auto_reset != 0;
         if (pending) s_reset[atomicAdd(&s_nreset, 1u)] = t;
         s_rec[t] = pack(L);
@@ -1244,8 +1216,7 @@ __global__ __launch_bounds__(T, 8) void k_rollout_sorted(RolloutArgs a) {
   if (live) {
     const int64_t i = base + t;
     a.state[i] = s_rec[t];
-    if (a.episodes) a.episodes[i] += s_eps[t];
-    if (a.return_sum) a.return_sum[i] += s_ret[t];
+    a.ep.add(i, s_eps[t], s_ret[t]);
     if (a.length_sum) a.length_sum[i] += s_len[t];
   }
   if (errs) atomicAdd(a.err_count, errs);
@@ -1374,10 +1345,7 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
   if (base + t < a.n) {
     const int64_t i = base + t;
     a.state[i] = s_rec[t];
-    if (a.ep_count) {
-      a.ep_count[i] += s_eps[t];
-      a.ep_return[i] += s_ret[t];
-    }
+    a.ep.add(i, s_eps[t], s_ret[t]);
   }
   if (errs) atomicAdd(a.err_count, errs);
 }
@@ -2430,15 +2398,8 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
     a.cur_player = out->cur_player;
     a.obs = out->obs;
     a.info = out->info_state;
-    a.ep_count = out->episodes;
-    a.ep_return = out->return_sum;
   }
-  {
-    const char* em = std::getenv("COUP_EP_MODE");  // A/B of the accumulator update (coup::EpMode)
-    a.ep_mode = em ? std::atoi(em) : coup::kEpEarlyAll;
-  }
-  if ((a.ep_count == nullptr) != (a.ep_return == nullptr))
-    return fail(COUP_E_INVALID, "coup_step: episodes and return_sum go together");
+  if (const char* why = coup::ep_acc_of(out, a.ep)) return fail(COUP_E_INVALID, std::string("coup_step: ") + why);
   if (a.info && !a.hist)
     return fail(COUP_E_INVALID, "coup_step: info_state needs an env created with COUP_FLAG_HISTORY");
   const bool uniform = actions == nullptr;
@@ -2537,8 +2498,7 @@ int coup_rollout(coup_env* env, int64_t steps, const coup_rollout_stats* stats) 
   a.steps = steps;
   a.err_count = env->err_count;
   if (stats) {
-    a.episodes = stats->episodes;
-    a.return_sum = stats->return_sum;
+    if (const char* why = coup::ep_acc_of(stats, a.ep)) return fail(COUP_E_INVALID, std::string("coup_rollout: ") + why);
     a.length_sum = stats->length_sum;
   }
   if (coup::regroup_lanes(env->batch)) {
@@ -2678,8 +2638,11 @@ int coup_step_trajectory(coup_env* env, int64_t steps, const coup_step_outputs* 
   // launches: 196 vs 162 us per 2^20-lane step)
   if (out && (out->obs || out->info_state))
     return fail(COUP_E_INVALID, "coup_step_trajectory: obs / info_state are written by coup_step only");
-  if (out && (out->episodes == nullptr) != (out->return_sum == nullptr))
-    return fail(COUP_E_INVALID, "coup_step_trajectory: episodes and return_sum go together");
+  {
+    coup::EpAcc ep;
+    if (const char* why = coup::ep_acc_of(out, ep))
+      return fail(COUP_E_INVALID, std::string("coup_step_trajectory: ") + why);
+  }
   if (env->batch == 0 || steps == 0) return COUP_OK;
   COUP_TRY(launching(env));
   if (env->generic) return np_result(coup::np::launch_trajectory(np_env(env), steps, out), "coup_step_trajectory");
@@ -2698,9 +2661,8 @@ int coup_step_trajectory(coup_env* env, int64_t steps, const coup_step_outputs* 
     a.step_type = out->step_type;
     a.legal = out->legal_mask;
     a.cur_player = out->cur_player;
-    a.ep_count = out->episodes;
-    a.ep_return = out->return_sum;
   }
+  (void)coup::ep_acc_of(out, a.ep);
   const int64_t n = env->batch;
   if (coup::regroup_lanes(n)) {
     switch (coup::sort_lanes("COUP_SORT_THREADS", coup::kRolloutSortLanes)) {

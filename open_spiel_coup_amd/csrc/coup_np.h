@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "coup_episodes.h"
 #include "coup_mi355x.h"
 
 namespace coup {

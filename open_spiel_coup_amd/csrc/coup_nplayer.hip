@@ -60,8 +60,7 @@ struct StepArgs {
   uint8_t* step_type;
   uint32_t* legal;
   int8_t* cur_player;
-  int32_t* ep_count;   // [B] per-episode accumulators (coup_step_outputs.episodes)
-  int32_t* ep_return;  // [B] (coup_step_outputs.return_sum)
+  EpAcc ep;            // per-episode accumulators (coup_step_outputs.episodes / return_sum or episode_word)
   uint32_t* err_count;
 #ifdef COUP_WAVE_TRACE
   // measurement builds only (tools/np_wave_trace.py): per wave of
@@ -91,21 +90,16 @@ struct StepArgs {
   } while (0)
 #endif
 
-// Episode accumulators (coup_step_outputs.episodes / return_sum): the
-// lane's two words are loaded with its record, before the rules, and every
-// lane stores them back (coalesced; unchanged unless the episode ended), so
-// no wave waits on a late load and no line is written partially (the
-// 2-player kernels' kEpEarlyAll, coup_kernels.hip).
-__device__ __forceinline__ int2 load_episode(const StepArgs& a, int64_t i) {
-  return a.ep_count ? make_int2(a.ep_count[i], a.ep_return[i]) : make_int2(0, 0);
-}
+// Episode accumulators (coup_episodes.h): the lane's word(s) are loaded
+// with its record, before the rules, and every lane stores them back
+// (coalesced; unchanged unless the episode ended), so no wave waits on a late
+// load and no line is written partially (as the 2-player kernels,
+// coup_kernels.hip ep_update).
+__device__ __forceinline__ int2 load_episode(const StepArgs& a, int64_t i) { return a.ep.load(i); }
 
 __device__ __forceinline__ void store_episode(const StepArgs& a, int64_t i, int2 e, uint32_t st, int32_t ret0) {
-  if (a.ep_count) {
-    const bool last = st == 2u;
-    a.ep_count[i] = e.x + (last ? 1 : 0);
-    a.ep_return[i] = e.y + (last ? ret0 : 0);
-  }
+  const bool last = st == 2u;
+  a.ep.store(i, e, last ? 1 : 0, last ? ret0 : 0);
 }
 
 // The per-lane outputs of a step: applied action, Rewards() as (loser,
@@ -340,7 +334,7 @@ __global__ NP_STEP_SORTED_BOUNDS void k_step_sorted(StepArgs a) {
         if (err) count_error(a.err_count);
         const bool term = is_terminal(L);
         out = (x + 1u) | ((term ? 2u : 1u) << 5) | (L.rloser << 7) | (L.rcount << 10) | ((uint32_t)err << 13);
-        if (a.ep_count && term) out |= (uint32_t)(returns(L, 0u) + 16) << 14;
+        if (a.ep.on() && term) out |= (uint32_t)(returns(L, 0u) + 16) << 14;
         pending = term && a.auto_reset != 0;
         decision_node = !term;  // resolve_chance leaves a live lane at a decision node
         if (INLINE && pending) {
@@ -471,10 +465,7 @@ __global__ __launch_bounds__(kThreads) void k_step_trajectory(StepArgs a, int64_
   pack(L, wa, wb);
   a.sa[i] = wa;
   a.sb[i] = wb;
-  if (a.ep_count) {
-    a.ep_count[i] += eps;
-    a.ep_return[i] += ret_sum;
-  }
+  a.ep.add(i, eps, ret_sum);
   if (errs) atomicAdd(a.err_count, errs);
 }
 
@@ -484,8 +475,7 @@ struct RolloutArgs {
   int64_t n;
   uint32_t seed_lo, seed_hi, env_id_base;
   int64_t steps;
-  int32_t* episodes;
-  int32_t* return_sum;
+  EpAcc ep;  // coup_rollout_stats: episodes / return_sum or episode_word
   int32_t* length_sum;
   uint32_t* err_count;
 };
@@ -525,8 +515,7 @@ __global__ __launch_bounds__(kThreads) void k_rollout(RolloutArgs a) {
   pack(L, wa, wb);
   a.sa[i] = wa;
   a.sb[i] = wb;
-  if (a.episodes) a.episodes[i] += eps;
-  if (a.return_sum) a.return_sum[i] += ret;
+  a.ep.add(i, eps, ret);
   if (a.length_sum) a.length_sum[i] += len;
   if (errs) atomicAdd(a.err_count, errs);
 }
@@ -655,8 +644,7 @@ __global__ __launch_bounds__(T, 8) void k_rollout_sorted(RolloutArgs a) {
     const int64_t i = base + t;
     a.sa[i] = s_a[t];
     a.sb[i] = s_b[t];
-    if (a.episodes) a.episodes[i] += s_eps[t];
-    if (a.return_sum) a.return_sum[i] += s_ret[t];
+    a.ep.add(i, s_eps[t], s_ret[t]);
     if (a.length_sum) a.length_sum[i] += s_len[t];
   }
   if (errs) atomicAdd(a.err_count, errs);
@@ -826,10 +814,7 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
     const int64_t i = base + t;
     a.sa[i] = s_a[t];
     a.sb[i] = s_b[t];
-    if (a.ep_count) {
-      a.ep_count[i] += s_eps[t];
-      a.ep_return[i] += s_ret[t];
-    }
+    a.ep.add(i, s_eps[t], s_ret[t]);
   }
   if (errs) atomicAdd(a.err_count, errs);
 }
@@ -1043,8 +1028,7 @@ hipError_t launch_step(const Env& e, const int8_t* actions, const coup_step_outp
     a.step_type = out->step_type;
     a.legal = out->legal_mask;
     a.cur_player = out->cur_player;
-    a.ep_count = out->episodes;
-    a.ep_return = out->return_sum;
+    (void)ep_acc_of(out, a.ep);  // checked by the C ABI
     obs = out->obs;
   }
   return dispatch(e.players, [&](auto np) {
@@ -1104,8 +1088,7 @@ hipError_t launch_trajectory(const Env& e, int64_t steps, const coup_step_output
     a.step_type = out->step_type;
     a.legal = out->legal_mask;
     a.cur_player = out->cur_player;
-    a.ep_count = out->episodes;
-    a.ep_return = out->return_sum;
+    (void)ep_acc_of(out, a.ep);  // checked by the C ABI
   }
   return dispatch(e.players, [&](auto np) {
     constexpr int N = decltype(np)::value;
@@ -1141,8 +1124,7 @@ hipError_t launch_rollout(const Env& e, int64_t steps, const coup_rollout_stats*
   a.steps = steps;
   a.err_count = e.err_count;
   if (stats) {
-    a.episodes = stats->episodes;
-    a.return_sum = stats->return_sum;
+    (void)ep_acc_of(stats, a.ep);  // checked by the C ABI
     a.length_sum = stats->length_sum;
   }
   return dispatch(e.players, [&](auto np) {

@@ -55,9 +55,16 @@ class BatchedCoupEnv:
       num_players: 2 (the reference game) .. 6.  N > 2 has no history /
         info_state; rewards / returns are [B, N], obs [B, N, 49 N].
       generic: run the N-player engine also at N = 2 (cross-checks).
-      episode_stats: keep per-lane int32 accumulators `episodes` and
-        `return_sum` (player 0's Returns() of every game that ends, coup.cc:
-        1016-1032), updated by every step at the lanes that reach LAST.
+      episode_stats: keep per-lane accumulators of the episodes that end and
+        player 0's Returns() of each (coup.cc:1016-1032), updated by every
+        step at the lanes that reach LAST.  True: int32 tensors `episodes`
+        and `return_sum`; 2 or 4: ONE packed word per lane of that many bytes,
+        `return_sum << (4 * bytes) | episodes` (`episode_word`,
+        csrc/coup_episodes.h), the multi-GPU collective's payload as it
+        stands (episode_payload()).  A packed word holds
+        episode_capacity() steps; eager steps past that fold it into int32
+        totals first (graph replays are not seen: clear or fold between
+        them).  episode_stats() returns the unpacked int32 pair either way.
       unchecked: caller actions outside LegalActions() (step, apply_action)
         are applied as pyspiel's apply_action does -- no legality check,
         DoApplyAction's own checks decide (COUP_FLAG_UNCHECKED, DESIGN.md
@@ -99,14 +106,39 @@ class BatchedCoupEnv:
         self.obs = torch.zeros(B, P, self.obs_size, dtype=torch.float32, device=dev) if obs else None
         self.info_state = (torch.zeros(B, 2, INFO_STATE_SIZE, dtype=torch.float32, device=dev)
                            if info_state else None)
-        self.episodes = torch.zeros(B, dtype=torch.int32, device=dev) if episode_stats else None
-        self.return_sum = torch.zeros(B, dtype=torch.int32, device=dev) if episode_stats else None
+        packed = episode_stats is not True and episode_stats in (2, 4)
+        if episode_stats and not packed and episode_stats is not True and episode_stats != 1:
+            raise ValueError("episode_stats: False, True (int32 pair) or 2 / 4 (packed word bytes)")
+        self.episode_word_bytes = int(episode_stats) if packed else 0
+        self.episode_word = (torch.zeros(B, dtype=torch.int16 if episode_stats == 2 else torch.int32, device=dev)
+                             if packed else None)
+        self._ep_fold = None  # int32 (episodes, return sums) folded out of the packed word
+        self._ep_steps = 0    # steps accumulated in the packed word since its last fold / clear
+        self.episodes = torch.zeros(B, dtype=torch.int32, device=dev) if episode_stats and not packed else None
+        self.return_sum = torch.zeros(B, dtype=torch.int32, device=dev) if episode_stats and not packed else None
         self._out = _native.StepOutputs(
             _addr(self.actions), _addr(self.rewards), _addr(self.step_type), _addr(self.legal_mask),
-            _addr(self.cur_player), _addr(self.obs), _addr(self.info_state), _addr(self.episodes),
-            _addr(self.return_sum))
+            _addr(self.cur_player), _addr(self.obs), _addr(self.info_state), *self._ep_fields())
 
     # ------------------------------------------------------------ plumbing
+    def _ep_fields(self):
+        """The accumulator fields of a coup_step_outputs (episodes,
+        return_sum, episode_word, episode_word_bytes)."""
+        return (_addr(self.episodes), _addr(self.return_sum), _addr(self.episode_word), self.episode_word_bytes)
+
+    def _ep_reserve(self, steps):
+        """Account for `steps` eager steps about to accumulate into the
+        packed word: fold it first if they would overflow its fields."""
+        if self.episode_word is None:
+            return
+        cap = self.episode_capacity()
+        if steps > cap:
+            raise ValueError(f"{steps} steps in one launch overflow the {self.episode_word_bytes}-byte episode word "
+                             f"(capacity {cap}); use episode_stats=4 or True")
+        if self._ep_steps + steps > cap:
+            self.fold_episode_stats()
+        self._ep_steps += steps
+
     def _bind_stream(self):
         # the raw handle of torch's current stream (no Stream object: this runs
         # before every launch of the per-game facades)
@@ -158,6 +190,7 @@ class BatchedCoupEnv:
                 raise ValueError("actions must have one entry per lane")
             self._keep_actions = actions
             a = _ptr(actions)
+        self._ep_reserve(1)
         _native.check(self.lib.coup_step(self._h, a, ctypes.byref(self._out)))
         out = {"actions": self.actions, "rewards": self.rewards, "step_type": self.step_type,
                "legal_mask": self.legal_mask, "current_player": self.cur_player}
@@ -214,17 +247,73 @@ class BatchedCoupEnv:
             out["info_state"] = h[o:o + n].view(np.float32).reshape(rows, 2, INFO_STATE_SIZE).copy()
         return out
 
+    def episode_capacity(self):
+        """Steps the packed episode word holds between folds: every field
+        must stay in range with one episode per step and |Returns()[0]| <=
+        2 (N - 1) (None for the int32 pair)."""
+        if self.episode_word is None:
+            return None
+        lim = 127 if self.episode_word_bytes == 2 else 32767
+        return min(2 * lim + 1, lim // (2 * (self.num_players - 1)))
+
+    def _unpack_word(self):
+        w = self.episode_word
+        if self.episode_word_bytes == 2:
+            return (w & 0xFF).to(torch.int32), (w >> 8).to(torch.int32)  # arithmetic shift: signed sums
+        return w & 0xFFFF, w >> 16
+
+    def fold_episode_stats(self):
+        """Move the packed word's counts into int32 totals and zero it."""
+        if self.episode_word is None:
+            return
+        eps, ret = self._unpack_word()
+        if self._ep_fold is None:
+            self._ep_fold = (eps.clone(), ret.clone())
+        else:
+            self._ep_fold[0].add_(eps)
+            self._ep_fold[1].add_(ret)
+        self.episode_word.zero_()
+        self._ep_steps = 0
+
     def episode_stats(self):
         """(episodes, return_sum) per lane since the last clear_episode_stats
-        (int32 [B] device tensors; needs episode_stats=True)."""
-        if self.episodes is None:
-            raise ValueError("env created without episode_stats=True")
-        return self.episodes, self.return_sum
+        (int32 [B] device tensors; needs episode_stats).  The pair form
+        returns the env's own tensors, the packed form an unpacked copy."""
+        if self.episodes is not None:
+            return self.episodes, self.return_sum
+        if self.episode_word is None:
+            raise ValueError("env created without episode_stats")
+        eps, ret = self._unpack_word()
+        if self._ep_fold is not None:
+            eps, ret = eps + self._ep_fold[0], ret + self._ep_fold[1]
+        return eps, ret
+
+    def episode_payload(self):
+        """The per-lane accumulators as the collective's payload: the packed
+        word itself, viewed as int32 (an int16 word's lane pairs; RCCL has no
+        int16 type; needs an even batch), or [B, 2] int32 (episodes,
+        return_sum) for the pair form.  The packed payload is exact only
+        while nothing was folded out of it (clear_episode_stats before the
+        window it covers)."""
+        if self.episode_word is not None:
+            if self._ep_fold is not None:
+                raise ValueError("the packed word was folded: clear_episode_stats before collecting a payload")
+            if self.episode_word_bytes == 2:
+                if self.batch % 2:
+                    raise ValueError("an int16 payload needs an even batch")
+                return self.episode_word.view(torch.int32)
+            return self.episode_word
+        eps, ret = self.episode_stats()
+        return torch.stack((eps, ret), 1)
 
     def clear_episode_stats(self):
         if self.episodes is not None:
             self.episodes.zero_()
             self.return_sum.zero_()
+        if self.episode_word is not None:
+            self.episode_word.zero_()
+            self._ep_fold = None
+            self._ep_steps = 0
 
     def capture_steps(self, steps, actions=None):
         """Record `steps` batched env steps (uniform policy, or the fixed
@@ -237,6 +326,7 @@ class BatchedCoupEnv:
             actions = actions.to(device=self.device, dtype=torch.int8).contiguous()
             self._graph_actions = actions
             a = _ptr(actions)
+        self._ep_reserve(int(steps))  # the first replay's steps (later replays: the caller clears or folds)
         g = torch.cuda.CUDAGraph()
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
@@ -267,7 +357,7 @@ class BatchedCoupEnv:
     def _slice_outputs(self, buf, t):
         return _native.StepOutputs(*[_addr(buf[k][t]) if k in buf else None for k in
                                      ("actions", "rewards", "step_type", "legal_mask", "current_player", "obs",
-                                      "info_state")], _addr(self.episodes), _addr(self.return_sum))
+                                      "info_state")], *self._ep_fields())
 
     def _fused_trajectory(self, buf):
         """Whether coup_step_trajectory can write `buf` in one launch: no
@@ -279,7 +369,7 @@ class BatchedCoupEnv:
     def _trajectory_outputs(self, buf):
         return _native.StepOutputs(*[_addr(buf[k]) if k in buf else None for k in
                                      ("actions", "rewards", "step_type", "legal_mask", "current_player", "obs",
-                                      "info_state")], _addr(self.episodes), _addr(self.return_sum))
+                                      "info_state")], *self._ep_fields())
 
     def collect_trajectory(self, steps, buf=None):
         """`steps` uniform-policy env steps whose outputs land in slice t of
@@ -289,6 +379,7 @@ class BatchedCoupEnv:
         per slice.  Same results either way."""
         buf = buf if buf is not None else self.trajectory_buffers(steps)
         self._bind_stream()
+        self._ep_reserve(int(steps))
         if self._fused_trajectory(buf):
             out = self._trajectory_outputs(buf)
             _native.check(self.lib.coup_step_trajectory(self._h, int(steps), ctypes.byref(out)))
@@ -306,8 +397,10 @@ class BatchedCoupEnv:
         self._bind_stream()
         out = self._trajectory_outputs(buf)
         fn, h, k, ref = self.lib.coup_step_trajectory, self._h, int(steps), ctypes.byref(out)
+        reserve = self._ep_reserve
 
         def launch():
+            reserve(k)
             _native.check(fn(h, k, ref))
         launch.out = out  # keeps the struct alive with the callable
         launch.buf = buf
@@ -318,6 +411,7 @@ class BatchedCoupEnv:
         steps the env `steps` times and refills the same [T, B, ...] buffers.
         Returns (graph, buffers).  The env must outlive the graph."""
         buf = buf if buf is not None else self.trajectory_buffers(steps)
+        self._ep_reserve(int(steps))  # the first replay's steps (later replays: the caller clears or folds)
         fused = self._fused_trajectory(buf)
         self._traj_outs = ([self._trajectory_outputs(buf)] if fused else
                            [self._slice_outputs(buf, t) for t in range(int(steps))])
@@ -337,7 +431,8 @@ class BatchedCoupEnv:
     def rollout(self, steps, stats=None):
         """`steps` uniform-random steps per lane in one launch.  stats: optional
         dict with int32 [B] tensors 'episodes', 'return_sum', 'length_sum'
-        (accumulated)."""
+        (accumulated), or {'episode_word': int16 / int32 [B]} for the packed
+        form (new_stats(packed_bytes))."""
         self.rollout_launcher(steps, stats)()
 
     def rollout_launcher(self, steps, stats=None):
@@ -347,8 +442,10 @@ class BatchedCoupEnv:
         self._bind_stream()
         s = None
         if stats is not None:
-            s = _native.RolloutStats(_addr(stats["episodes"]), _addr(stats["return_sum"]),
-                                     _addr(stats["length_sum"]))
+            w = stats.get("episode_word")
+            s = _native.RolloutStats(_addr(stats.get("episodes")), _addr(stats.get("return_sum")),
+                                     _addr(stats.get("length_sum")), _addr(w),
+                                     0 if w is None else w.element_size())
         fn, h, k, ref = self.lib.coup_rollout, self._h, int(steps), ctypes.byref(s) if s else None
 
         def launch():
@@ -357,7 +454,15 @@ class BatchedCoupEnv:
         launch.steps = k
         return launch
 
-    def new_stats(self):
+    def new_stats(self, packed_bytes=None):
+        """Zeroed rollout statistics: int32 'episodes', 'return_sum' and
+        'length_sum', or with packed_bytes = 2 / 4 one packed 'episode_word'
+        (csrc/coup_episodes.h; no lengths)."""
+        if packed_bytes is not None:
+            if packed_bytes not in (2, 4):
+                raise ValueError("packed_bytes: 2 or 4")
+            dt = torch.int16 if packed_bytes == 2 else torch.int32
+            return {"episode_word": torch.zeros(self.batch, dtype=dt, device=self.device)}
         z = lambda: torch.zeros(self.batch, dtype=torch.int32, device=self.device)  # noqa: E731
         return {"episodes": z(), "return_sum": z(), "length_sum": z()}
 

@@ -583,6 +583,7 @@ int np_rollout(const np_rollout_args* a) {
         for (int p = 0; p < P; ++p) a->rewards[o * P + p] = (int8_t)rw[p];
       if (a->step_type) a->step_type[o] = st;
       if (a->legal) a->legal[o] = np_legal_mask(&s);
+      if (a->cur_player) a->cur_player[o] = (int8_t)np_current_player(&s);
       if (a->obs)
         for (int p = 0; p < P; ++p) np_observation_tensor(&s, p, a->obs + (o * P + p) * 49 * P);
     }

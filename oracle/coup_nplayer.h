@@ -85,6 +85,7 @@ typedef struct {
   int64_t* return_sum_p0;
   int32_t* lane_episodes;   /* [n] per lane (optional) */
   int32_t* lane_return_sum; /* [n] per lane (optional) */
+  int8_t* cur_player;       /* [steps][n] CurrentPlayer() after the step (optional) */
 } np_rollout_args;
 int np_rollout(const np_rollout_args* a);
 

@@ -73,7 +73,8 @@ class _NpRolloutArgs(ctypes.Structure):
                 ("actions", ctypes.c_void_p), ("rewards", ctypes.c_void_p), ("step_type", ctypes.c_void_p),
                 ("legal", ctypes.c_void_p), ("obs", ctypes.c_void_p), ("final_state", ctypes.c_void_p),
                 ("episodes_done", ctypes.c_void_p), ("return_sum_p0", ctypes.c_void_p),
-                ("lane_episodes", ctypes.c_void_p), ("lane_return_sum", ctypes.c_void_p)]
+                ("lane_episodes", ctypes.c_void_p), ("lane_return_sum", ctypes.c_void_p),
+                ("cur_player", ctypes.c_void_p)]
 
 
 _lib = None
@@ -375,5 +376,6 @@ def np_rollout(n_players, seed, n, steps, env_id_base=0, auto_reset=True, want_o
     a.return_sum_p0 = buf("return_sum_p0", (1,), np.int64)
     a.lane_episodes = buf("lane_episodes", (n,), np.int32)
     a.lane_return_sum = buf("lane_return_sum", (n,), np.int32)
+    a.cur_player = buf("cur_player", (steps, n), np.int8)
     lib().np_rollout(ctypes.byref(a))
     return out

@@ -6,9 +6,11 @@ bench.py does for a multi-GPU job -- init_process_group("nccl",
 device_id=...) -- but forces the collectives that a single process would
 skip: the all_gather_into_tensor of bench.py's per-lane episode payloads
 (int16 pairs viewed as int32, int32, and [B, 2] int32), their unpacking,
-a records gather and the max-over-ranks all_reduce.  Every gathered tensor
-must equal its source (a one-rank gather is a copy), and the unpacked
-episodes / return sums must equal env.episode_stats().
+a records gather and the max-over-ranks all_reduce.  The payloads are the
+envs' own accumulators (packed words for widths 2 and 4, as bench.py's),
+which must equal bench.pack_episodes of the int32 pair; every gathered
+tensor must equal its source (a one-rank gather is a copy), and the
+unpacked episodes / return sums must equal env.episode_stats().
 
     python tests/dist_nccl_worker.py OUT_JSON BATCH STEPS
 """
@@ -34,16 +36,22 @@ def main():
     assert world == 1 and rank == 0
     dev = D.init("nccl", gpu=True, force=True)
     assert dist.is_initialized() and dist.get_backend() == "nccl" and dist.get_world_size() == 1
-    env = BatchedCoupEnv(B, seed=5, env_id_base=D.env_id_base(rank, B), obs=False, episode_stats=True, device=dev)
-    env.rollout(64)
-    env.clear_episode_stats()
-    for _ in range(K):
-        env.step()
+    # the int32 pair, and the packed words the kernels accumulate for the
+    # bench's payload widths 2 and 4 (twin envs, same games)
+    envs = {w: BatchedCoupEnv(B, seed=5, env_id_base=D.env_id_base(rank, B), obs=False,
+                              episode_stats=bench.episode_stats_mode(w), device=dev) for w in (2, 4, 8)}
+    for e in envs.values():
+        e.rollout(64)
+        e.clear_episode_stats()
+        for _ in range(K):
+            e.step()
+    env = envs[8]
     eps, ret = env.episode_stats()
     res = {"backend": dist.get_backend(), "world": dist.get_world_size(), "episodes": int(eps.sum()),
            "widths": {}}
     for width in (2, 4, 8):
-        payload = bench.pack_episodes(eps, ret, width)
+        payload = envs[width].episode_payload()
+        assert torch.equal(payload, bench.pack_episodes(eps, ret, width)), width
         g = D.collate(payload, force=True)
         assert g.data_ptr() != payload.data_ptr(), "the collective must not be short-circuited"
         assert torch.equal(g, payload), width
@@ -55,7 +63,7 @@ def main():
         t0 = time.perf_counter()
         reps = 20
         for _ in range(reps):
-            D.collate(bench.pack_episodes(eps, ret, width), force=True)
+            D.collate(envs[width].episode_payload(), force=True)
         dist.barrier()
         torch.cuda.synchronize()
         res["widths"][str(width)] = {"payload_bytes": payload.numel() * payload.element_size(),

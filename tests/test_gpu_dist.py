@@ -175,3 +175,68 @@ def test_bench_one_rank_rccl_line():
     assert ep["finished"] > 0 and rec["lane_errors"] == 0
     assert ep["collective_ms"] > 0  # reported, not bounded: a one-rank communicator prices no xGMI hop
     print("\nc3 one-rank RCCL line:", json.dumps({k: rec[k] for k in ("value", "ms_per_step")}), json.dumps(ep))
+
+
+def _bench(args, timeout):
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                       timeout=timeout, cwd=ROOT,
+                       env={k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")})
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_gpus_flag_starts_the_ranks(tmp_path):
+    """`bench.py --gpus 2` with no torchrun starts its 2
+    rank processes itself (gloo here: both share the box's GPU) and prints
+    rank 0's line with n_gpus 2; the gathered per-lane episode counts and
+    return sums equal one process over the same 2B env ids."""
+    batch = 1 << 14
+    common = ["--config", "c2", "--steps", "8", "--warmup", "2", "--settle", "16"]
+    two = _bench(["--gpus", "2", "--batch", str(batch), "--dist-backend", "gloo",
+                  "--dump-episodes", str(tmp_path / "two.npz")] + common, timeout=140)
+    assert two["n_gpus"] == 2 and two["config"]["global_batch"] == 2 * batch and two["lane_errors"] == 0
+    assert len(two["episodes"]["collective_ms_ranks"]) == 2
+    one = _bench(["--gpus", "1", "--batch", str(2 * batch), "--no-cpu-baseline",
+                  "--dump-episodes", str(tmp_path / "one.npz")] + common, timeout=140)
+    a, b = np.load(tmp_path / "two.npz"), np.load(tmp_path / "one.npz")
+    for k in ("episodes", "return_sum"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    assert int(a["episodes"].sum()) == two["episodes"]["finished"] == one["episodes"]["finished"] > 0
+
+
+def test_config5_rehearsal_eight_ranks_of_2_20(tmp_path):
+    """BASELINE config 5's workload at its size -- 8 ranks
+    x 2^20 lanes (2^23 games), env ids sharded by rank, the timed region
+    ending in the all-gather of every lane's episode count and player-0
+    return sum (Returns(), coup.cc:1016-1032) -- as a one-box rehearsal: 8
+    gloo ranks share the GPU (RCCL takes one rank per GPU), launched by
+    `bench.py --gpus 8`.  Rank 0's gathered arrays must equal one process over
+    the 2^23 lanes, and the oracle at every rank boundary (256 lanes from
+    r * 2^20 - 128).  collective_ms per rank is reported, not bounded: ranks
+    sharing one GPU and gloo say nothing about xGMI."""
+    B, K, W, settle, seed = 1 << 20, 20, 5, 256, 1
+    common = ["--config", "c2", "--steps", str(K), "--warmup", str(W), "--settle", str(settle), "--seed", str(seed)]
+    eight = _bench(["--gpus", "8", "--batch", str(B), "--dist-backend", "gloo",
+                    "--dump-episodes", str(tmp_path / "eight.npz")] + common, timeout=170)
+    assert eight["n_gpus"] == 8 and eight["config"]["global_batch"] == 8 * B and eight["lane_errors"] == 0
+    assert "int16" in eight["episodes"]["collective"]
+    one = _bench(["--gpus", "1", "--batch", str(8 * B), "--no-cpu-baseline",
+                  "--dump-episodes", str(tmp_path / "one.npz")] + common, timeout=140)
+    g, s = np.load(tmp_path / "eight.npz"), np.load(tmp_path / "one.npz")
+    assert g["episodes"].shape == (8 * B,)
+    for k in ("episodes", "return_sum"):
+        np.testing.assert_array_equal(g[k], s[k], err_msg=k)
+    for r in range(9):
+        base = min(max(r * B - 128, 0), 8 * B - 256)
+        ref = oracle.rollout(seed=seed, n=256, steps=settle + W + K, env_id_base=base, want_trajectory=False)
+        pre = oracle.rollout(seed=seed, n=256, steps=settle + W, env_id_base=base, want_trajectory=False)
+        np.testing.assert_array_equal(g["episodes"][base:base + 256], ref["lane_episodes"] - pre["lane_episodes"],
+                                      err_msg=f"episodes at {base}")
+        np.testing.assert_array_equal(g["return_sum"][base:base + 256],
+                                      ref["lane_return_sum"] - pre["lane_return_sum"], err_msg=f"returns at {base}")
+    print("\nconfig 5 rehearsal (8 gloo ranks x 2^20 on one GPU):",
+          json.dumps({"finished": eight["episodes"]["finished"], "mean_return_p0": eight["episodes"]["mean_return_p0"],
+                      "collective_ms_ranks": eight["episodes"]["collective_ms_ranks"],
+                      "ms_per_step": eight["ms_per_step"]}))

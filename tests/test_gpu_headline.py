@@ -20,6 +20,7 @@ import numpy as np
 import pytest
 import torch
 
+import bench
 from oracle import oracle
 
 pytestmark = pytest.mark.gpu
@@ -88,7 +89,10 @@ def test_c3_headline_kernel_full_batch_slices_match_oracle():
     1-step graph (each step checked), and one replay of a K = 20-step graph
     (bench.py's timed region; its last step and the records checked)."""
     B, seed, settle, warm, K = 1 << 20, 1, 256, 5, 20
-    env = BatchedCoupEnv(B, seed=seed, env_id_base=0, auto_reset=True, obs=True, episode_stats=True)
+    # the bench's accumulators: the packed int16 word at K = 20 (bench.payload_width)
+    env = BatchedCoupEnv(B, seed=seed, env_id_base=0, auto_reset=True, obs=True,
+                         episode_stats=bench.episode_stats_mode(bench.payload_width(2, K, B)))
+    assert env.episode_word_bytes == 2
     total = settle + warm + 3 * K
     refs = {k: oracle.rollout(seed=seed, n=256, steps=total, env_id_base=k, auto_reset=True, want_obs=True)
             for k in _slices(B)}
@@ -130,7 +134,7 @@ def test_c3i_info_state_kernel_full_batch_slices_match_oracle():
     records, history bytes and accumulators."""
     B, seed, warm, K = 1 << 18, 1, 5, 20
     env = BatchedCoupEnv(B, seed=seed, env_id_base=0, auto_reset=True, obs=False, info_state=True,
-                         episode_stats=True)
+                         episode_stats=bench.episode_stats_mode(bench.payload_width(2, K, B)))
     total = warm + K
     for _ in range(warm):
         env.step()
@@ -143,4 +147,45 @@ def test_c3i_info_state_kernel_full_batch_slices_match_oracle():
         for k, ref in refs.items():
             _check_step(o, ref, t, k, "info")
     _check_records(env, B, seed, total, stats_from=warm)
+    assert env.error_count() == 0
+
+
+def test_c4_bench_kernel_full_batch_slices_match_oracle():
+    """bench.py --config c4 at its size: 6 players,
+    2^20 lanes, settle 256 through the regrouped fused rollout, 5 warm-up and
+    20 eager coup_step launches of np::k_step_sorted<6, true, true, 1024> (the
+    decision drawn ahead, resets dealt by 4-thread groups), the bench's
+    packed accumulators.  At every timed step the actions, rewards, step
+    types, legal masks and current players of three 256-lane slices against
+    the written N-player spec (oracle/coup_nplayer.c, parity unpinned w.r.t.
+    the 2-player reference: coup.h:42); then the full records and the
+    per-episode accumulators."""
+    B, seed, settle, warm, K, P = 1 << 20, 1, 256, 5, 20, 6
+    env = BatchedCoupEnv(B, seed=seed, env_id_base=0, auto_reset=True, obs=False, num_players=P,
+                         episode_stats=bench.episode_stats_mode(bench.payload_width(P, K, B)))
+    total = settle + warm + K
+    refs = {k: oracle.np_rollout(P, seed=seed, n=256, steps=total, env_id_base=k) for k in _slices(B)}
+    env.rollout(settle)
+    for _ in range(warm):
+        env.step()
+    env.clear_episode_stats()
+    for t in range(settle + warm, total):
+        o = env.step()
+        for k, ref in refs.items():
+            sl, msg = slice(k, k + 256), f"slice {k} step {t}"
+            np.testing.assert_array_equal(_np(o["actions"][sl]), ref["actions"][t], err_msg=msg)
+            np.testing.assert_array_equal(_np(o["rewards"][sl]), ref["rewards"][t], err_msg=msg)
+            np.testing.assert_array_equal(_np(o["step_type"][sl]), ref["step_type"][t], err_msg=msg)
+            np.testing.assert_array_equal(_np(o["legal_mask"][sl]).astype(np.uint32), ref["legal"][t], err_msg=msg)
+            np.testing.assert_array_equal(_np(o["current_player"][sl]), ref["cur_player"][t], err_msg=msg)
+    words = _np(env.export_state()).astype(np.uint32)
+    eps, ret = env.episode_stats()
+    for k, ref in refs.items():
+        np.testing.assert_array_equal(words[k:k + 256], ref["final_state"], err_msg=f"records, slice {k}")
+        pre = oracle.np_rollout(P, seed=seed, n=256, steps=settle + warm, env_id_base=k)
+        np.testing.assert_array_equal(_np(eps[k:k + 256]), ref["lane_episodes"] - pre["lane_episodes"],
+                                      err_msg=f"episodes, slice {k}")
+        np.testing.assert_array_equal(_np(ret[k:k + 256]), ref["lane_return_sum"] - pre["lane_return_sum"],
+                                      err_msg=f"return sums, slice {k}")
+    assert int(eps.sum()) > 0
     assert env.error_count() == 0
