@@ -312,9 +312,17 @@ int coup_slot_ops(coup_env* env, int64_t n, const coup_slot_req* reqs, const cou
  * the server's pending requests, and the server waits for (synchronises) work
  * enqueued on the env's stream before it reads the env's lanes, so the two
  * paths stay ordered.  The wave leaves after idle_us microseconds without a
- * request, on coup_server_destroy, or when the host finds it idle; the next
- * request relaunches it.  Not thread-safe: calls on envs sharing a server
- * must be serialised by the caller.  Replaces, for the per-state callers of
+ * request, on coup_server_destroy, on coup_destroy of any env (freeing
+ * memory synchronises the device, which would otherwise wait out the idle
+ * time), or when the host finds it idle; the next request relaunches it.
+ * While a wave idles, a device-wide synchronisation (hipDeviceSynchronize,
+ * torch.cuda.synchronize) waits for it to leave: at most idle_us (the Python
+ * pool's default is 2000, COUP_SERVER_IDLE_US).  The server's host side is
+ * serialised by a lock of its own (a post, its wait and the copy of its
+ * result are one section), so ops on envs sharing a server may come from
+ * several threads; calls on one env are still not reentrant.  Each request
+ * carries a checksum the wave verifies, so a torn read of its ring slot is
+ * polled again instead of served.  Replaces, for the per-state callers of
  * rust_open_spiel.h:34-73 / pyspiel.cc:263-345, the launch-and-synchronise
  * round trip of each State op. */
 typedef struct coup_server coup_server;

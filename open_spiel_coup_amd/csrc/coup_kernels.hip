@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -621,10 +622,10 @@ __device__ __noinline__ uint32_t unchecked_decision(uint4 w, uint32_t x, uint4* 
 // two paths as a run-time branch in one kernel, ROCm 7.2 produced the
 // DESIGN.md section 12 defect in the checked branch (record word 3 after a
 // Tax announcement, k_step<false, 0, 256, 1>; tests/test_gpu_server.py).
-template <bool UNIFORM, bool FLOW, bool UNCHECKED, class H>
-__device__ __forceinline__ void step_lane(const StepArgs& a, int64_t i, Lane& L, int& act, uint32_t& st,
-                                          int32_t& rew, int32_t& ret, H& hist) {
-  Rng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, i), 0u, make_uint4(0, 0, 0, 0)};
+template <bool UNIFORM, bool FLOW, bool UNCHECKED, class H, class R>
+__device__ __forceinline__ void step_lane_rng(const StepArgs& a, int64_t i, Lane& L, int& act, uint32_t& st,
+                                              int32_t& rew, int32_t& ret, H& hist, R& rng,
+                                              bool count = true) {
   act = -1;
   rew = 0;
   if (!UNIFORM && (int8_t)a.actions_in[i] < 0) {
@@ -656,14 +657,14 @@ __device__ __forceinline__ void step_lane(const StepArgs& a, int64_t i, Lane& L,
     err_before = L.err;
     uint4 w;
     if (!unchecked_decision(pack(L), x, &w)) {
-      count_error(a.err_count);
+      if (count) count_error(a.err_count);
       return;
     }
     hist.record(L.move, hist_decision(x, L.M));
     L = unpack(w);
   } else {
     if (x > 17u || ((m >> x) & 1u) == 0u || is_terminal(L)) {
-      count_error(a.err_count);
+      if (count) count_error(a.err_count);
       return;
     }
     err_before = L.err;
@@ -677,7 +678,7 @@ __device__ __forceinline__ void step_lane(const StepArgs& a, int64_t i, Lane& L,
   COUP_TRACE_ANY(a, 7);
   resolve_chance(L, rng, hist);
   COUP_TRACE_ANY(a, 8);
-  if (L.err && !err_before) count_error(a.err_count);
+  if (count && L.err && !err_before) count_error(a.err_count);
   act = (int)x;
   rew = L.r0;
   if (is_terminal(L)) {
@@ -689,6 +690,13 @@ __device__ __forceinline__ void step_lane(const StepArgs& a, int64_t i, Lane& L,
     }
   }
   COUP_TRACE_ANY(a, 9);
+}
+
+template <bool UNIFORM, bool FLOW, bool UNCHECKED, class H>
+__device__ __forceinline__ void step_lane(const StepArgs& a, int64_t i, Lane& L, int& act, uint32_t& st,
+                                          int32_t& rew, int32_t& ret, H& hist) {
+  Rng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, i), 0u, make_uint4(0, 0, 0, 0)};
+  step_lane_rng<UNIFORM, FLOW, UNCHECKED>(a, i, L, act, st, rew, ret, hist, rng);
 }
 
 // The per-episode accumulators (coup_episodes.h): the lane's word(s) are
@@ -866,6 +874,85 @@ __device__ __forceinline__ void step_group_compute(const StepArgs& a, int64_t gr
   } else if (kDesc && wave_valid > 0) {
     write_obs_wave<OBS == kObsWaveNT>(a.obs + wave0 * (2 * kObsSize), obs_key(L), wave_valid, lds.desc);
   }
+}
+
+// Lane k (0..3) of this thread's quad, by DPP quad_perm (a VALU operand
+// modifier: no LDS round trip, unlike __shfl's ds_bpermute).
+template <int K>
+__device__ __forceinline__ uint32_t quad_bcast(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, K * 0x55, 0xF, 0xF, true);
+}
+template <int K>
+__device__ __forceinline__ uint4 quad_bcast4(uint4 v) {
+  return make_uint4(quad_bcast<K>(v.x), quad_bcast<K>(v.y), quad_bcast<K>(v.z), quad_bcast<K>(v.w));
+}
+
+// The rules-bound step (no observation, no history; c2's kernel at 65,536
+// lanes, where 256-lane blocks give ONE wave per SIMD and a lane's dependent
+// chain -- record load, Philox, rules, deals, reset -- is exposed).  TPL
+// threads play each lane: the Philox blocks the step can need (PrefRng) are
+// computed ahead by the group's threads in parallel (TPL = 4: thread q
+// computes block q of {current, next, next episode's first}; TPL = 2: two
+// each; TPL = 1: all three, interleaved) and traded by DPP within the quad;
+// then every thread of the group runs the same rules (branch-free for the
+// group, so a wave diverges over 64 / TPL lanes instead of 64), and thread 0
+// stores.  TPL > 1 puts TPL waves on each SIMD to hide each other's latency.
+// Same draws as k_step (PrefRng::draw == Rng::draw), so the same games.
+template <int TPL, bool UNIFORM>
+__global__ __launch_bounds__(256) void k_step_group(StepArgs a) {
+  static_assert(TPL == 1 || TPL == 2 || TPL == 4, "threads per lane");
+  constexpr int kLanes = 256 / TPL;
+  const uint32_t q = threadIdx.x % TPL;
+  const int64_t i = (int64_t)blockIdx.x * kLanes + threadIdx.x / TPL;
+  const bool active = i < a.n;
+  const uint4 rec = active ? a.state[i] : pack(initial_lane(0u));
+  const int2 eps = ep_prefetch(a, i, active && q == 0u);
+  Lane L = unpack(rec);
+  const uint32_t id = lane_stream_id(a.env_id_base, i);
+  const uint32_t b = L.move >> 2, ep = L.episode, ep1 = (L.episode + 1u) & kEpisodeMask;
+  uint4 c0, c1, r0;
+  if (TPL == 4) {
+    const uint32_t e = q < 2u ? ep : ep1, bb = q == 0u ? b : (q == 1u ? b + 1u : 0u);
+    const uint4 mine = PrefRng::block(a.seed_lo, a.seed_hi, id, e, bb);
+    c0 = quad_bcast4<0>(mine);
+    c1 = quad_bcast4<1>(mine);
+    r0 = quad_bcast4<2>(mine);
+  } else if (TPL == 2) {
+    // thread 0 of the pair: current + next block; thread 1: next episode's
+    // first + next block (the same number of evaluations on both)
+    const uint4 m0 = PrefRng::block(a.seed_lo, a.seed_hi, id, q == 0u ? ep : ep1, q == 0u ? b : 0u);
+    const uint4 m1 = PrefRng::block(a.seed_lo, a.seed_hi, id, ep, b + 1u);
+    c1 = m1;
+    const uint4 o = make_uint4(
+        (uint32_t)__builtin_amdgcn_mov_dpp((int)m0.x, 0xB1, 0xF, 0xF, true),  // quad_perm [1,0,3,2]: the pair's other
+        (uint32_t)__builtin_amdgcn_mov_dpp((int)m0.y, 0xB1, 0xF, 0xF, true),
+        (uint32_t)__builtin_amdgcn_mov_dpp((int)m0.z, 0xB1, 0xF, 0xF, true),
+        (uint32_t)__builtin_amdgcn_mov_dpp((int)m0.w, 0xB1, 0xF, 0xF, true));
+    c0 = q == 0u ? m0 : o;
+    r0 = q == 0u ? o : m0;
+  } else {
+    c0 = PrefRng::block(a.seed_lo, a.seed_hi, id, ep, b);
+    c1 = PrefRng::block(a.seed_lo, a.seed_hi, id, ep, b + 1u);
+    r0 = PrefRng::block(a.seed_lo, a.seed_hi, id, ep1, 0u);
+  }
+  if (!active) return;  // after the trades: every quad lane took part
+  PrefRng rng{a.seed_lo, a.seed_hi, id, ep, b, c0, c1, r0};
+  int act;
+  uint32_t st;
+  int32_t rew, ret = 0;
+  NoHistory none;
+  step_lane_rng<UNIFORM, false, false>(a, i, L, act, st, rew, ret, none, rng, q == 0u);  // one count per lane
+  if (q != 0u) return;
+  a.state[i] = pack(L);
+  ep_update(a, i, eps, st, ret);
+  if (a.actions) a.actions[i] = (int8_t)act;
+  if (a.rewards) {
+    a.rewards[2 * i] = (int8_t)rew;
+    a.rewards[2 * i + 1] = (int8_t)(-rew);
+  }
+  if (a.step_type) a.step_type[i] = (uint8_t)st;
+  if (a.legal) a.legal[i] = legal_mask(L);
+  if (a.cur_player) a.cur_player[i] = (int8_t)current_player(L);
 }
 
 // coup_measure_step_traffic: the bytes of k_step<*, kObsWaveBitsSc1, 256,
@@ -1801,10 +1888,28 @@ struct SrvReq {        // one ring slot (host memory), 64 bytes = one host cache
   // second half
   uint64_t src_hist;
   uint32_t seed_lo, seed_hi, env_id;  // the lane's sampling-contract stream (deal / reset)
-  uint32_t pad[2];
+  uint32_t check;      // srv_check of the fields and the number (a torn read of the line is polled again)
+  uint32_t pad;
   uint32_t seq_b;      // stored last of all
 };
 static_assert(sizeof(SrvReq) == 64, "SrvReq layout");
+
+// Checksum of a request's words 0-6 and 8-12 and its number.  The wave reads
+// the line as 16 separate 4-byte system-scope loads; neither the HIP memory
+// model nor PCIe ordering promises that they see one snapshot of it, so
+// matching numbers alone could pair a new number with an older request's
+// fields.  A mismatch is treated as "not posted yet".  Host and device use
+// this one function (scalar arithmetic on the device: the words are
+// readlane'd into SGPRs anyway).
+__host__ __device__ __forceinline__ uint32_t srv_check(const uint32_t* w, uint32_t seq) {
+  uint32_t h = seq * 0x9E3779B1u + 0x7F4A7C15u;
+  for (int k = 0; k < 13; ++k) {
+    if (k == 7) continue;
+    h = (h ^ w[k]) * 0x85EBCA6Bu;
+    h ^= h >> 13;
+  }
+  return h;
+}
 constexpr uint32_t kSrvInit = 1u << 8, kSrvResult = 1u << 9, kSrvObs = 1u << 10, kSrvInfo = 1u << 11;
 constexpr uint32_t kSrvModeShift = 12;  // [14:12]: kSlotReset | kSlotDeal | kSlotUnchecked
 
@@ -1819,7 +1924,6 @@ struct ServerArgs {
   SrvReq* ring;        // device addresses of the mapped host memory
   SrvCtl* ctl;
   uint8_t* result;     // coup_slot_result, then obs [2][98], then info [2][2492] floats (mapped host)
-  uint32_t first;      // sequence number of the first request to serve
   uint32_t epoch;      // this launch's epoch (never 0)
   uint64_t idle_ticks; // exit after this many 100 MHz ticks without a request
 };
@@ -1917,7 +2021,10 @@ __global__ __launch_bounds__(64) void k_server(ServerArgs s) {
   __shared__ __attribute__((aligned(16))) uint32_t pre[kPreWords];
   __shared__ __attribute__((aligned(16))) coup_slot_result res;
   const uint32_t t = threadIdx.x;
-  uint32_t next = s.first;
+  // the first unserved request, read here rather than passed at launch: a
+  // wave queued behind another on the server stream (two relaunches) starts
+  // after the earlier one has left, so it never serves a request again
+  uint32_t next = (uint32_t)__builtin_amdgcn_readfirstlane((int)srv_ld(&s.ctl->served)) + 1u;
   uint64_t idle0 = __builtin_amdgcn_s_memrealtime();
   for (;;) {
     // the slot's 16 words (lanes 0..15) and the stop word in one round trip
@@ -1933,6 +2040,15 @@ __global__ __launch_bounds__(64) void k_server(ServerArgs s) {
       continue;
     }
     auto word = [&](int k) { return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)w, k); };
+    {
+      uint32_t fw[13];
+#pragma unroll
+      for (int k = 0; k < 13; ++k) fw[k] = (uint32_t)word(k);
+      if (srv_check(fw, next) != (uint32_t)word(13)) {  // a torn snapshot of the line: poll again
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+    }
     const uint64_t dst_state = word(0) | (word(1) << 32), dst_hist = word(2) | (word(3) << 32);
     const uint64_t src_state = word(4) | (word(5) << 32), src_hist = word(8) | (word(9) << 32);
     const uint32_t op = (uint32_t)word(6);
@@ -1991,6 +2107,7 @@ struct coup_env {
   bool batch_pending;         // an asynchronous coup_slot_ops may still read the requests
   coup_server* server;        // coup_attach_server: coup_slot_op goes through this resident wave
   bool dirty;                 // work enqueued on `stream` since its last synchronisation
+  hipEvent_t stream_event;    // coup_set_stream: orders a new stream after the old one's pending work
 };
 
 // coup_server (coup_mi355x.h; kernel coup::k_server).  The ring, the control
@@ -2006,10 +2123,25 @@ struct coup_server {
   uint32_t posted = 0;            // last sequence number posted
   uint32_t epoch = 0;             // epoch of the last launch
   bool running = false;           // a wave was launched and may still be serving
-  uint64_t idle_us = 20000;
+  uint64_t idle_us = 2000;
   std::chrono::steady_clock::time_point last_post;
   uint64_t requests = 0, launches = 0;
+  // Every host path that reads or writes the fields above, the ring or the
+  // result area holds this: a post, its wait and the copy of its result are
+  // one critical section (the result area is shared by all requests), and
+  // drains / stops from other threads (coup_destroy of another env, a stream
+  // op on a served env) cannot interleave with them.  Recursive: srv_post
+  // waits and stops inside its own section.
+  std::recursive_mutex mu;
 };
+
+namespace {
+// Live op servers: coup_destroy stops their waves before it frees memory
+// (hipFree / hipHostFree synchronise the device, which would otherwise wait
+// out a resident wave's idle time).
+std::mutex g_servers_mu;
+std::vector<coup_server*> g_servers;
+}  // namespace
 
 namespace {
 
@@ -2051,6 +2183,14 @@ int obs_mode() {
 int xcd_remap() {
   const char* e = std::getenv("COUP_XCD_REMAP");
   return e ? (std::atoi(e) != 0) : 1;
+}
+
+// COUP_STEP_TPL: threads per lane of the rules-bound step (coup::k_step_group;
+// 0 = k_step).  Read at every launch (A/B in one process).
+int step_tpl() {
+  const char* e = std::getenv("COUP_STEP_TPL");
+  const int v = e ? std::atoi(e) : 0;
+  return (v == 1 || v == 2 || v == 4) ? v : 0;
 }
 
 // Blocks of the step kernel: one per group of T lanes.
@@ -2112,7 +2252,6 @@ int srv_launch(coup_server* s) {
   a.ring = reinterpret_cast<coup::SrvReq*>(s->host_dev);
   a.ctl = reinterpret_cast<coup::SrvCtl*>(s->host_dev + kSrvCtlOff);
   a.result = s->result_dev;
-  a.first = srv_served(s) + 1u;
   s->epoch = s->epoch + 1u == 0u ? 1u : s->epoch + 1u;
   a.epoch = s->epoch;
   a.idle_ticks = s->idle_us * 100u;  // s_memrealtime: 100 MHz
@@ -2126,6 +2265,7 @@ int srv_launch(coup_server* s) {
 // Stop the wave after the requests already posted (it serves them first)
 // and wait for it to leave.
 int srv_stop(coup_server* s) {
+  std::lock_guard<std::recursive_mutex> lk(s->mu);
   if (!s->running) return COUP_OK;
   __atomic_store_n(&s->ctl->stop, s->epoch, __ATOMIC_RELEASE);
   s->running = false;
@@ -2138,6 +2278,7 @@ int srv_stop(coup_server* s) {
 // waiting; the pending requests are still in the ring, so a relaunch from
 // the first unserved one completes them.
 int srv_wait(coup_server* s, uint32_t seq) {
+  std::lock_guard<std::recursive_mutex> lk(s->mu);
   auto t0 = std::chrono::steady_clock::now(), tq = t0;
   for (uint32_t k = 1; (int32_t)(srv_served(s) - seq) < 0; ++k) {
     __builtin_ia32_pause();
@@ -2164,6 +2305,7 @@ int srv_wait(coup_server* s, uint32_t seq) {
 int srv_drain(const coup_env* env) {
   if (!env || !env->server) return COUP_OK;
   coup_server* s = env->server;
+  std::lock_guard<std::recursive_mutex> lk(s->mu);
   if (s->running && s->posted != srv_served(s)) COUP_TRY(srv_wait(s, s->posted));
   return COUP_OK;
 }
@@ -2176,7 +2318,8 @@ int launching(coup_env* env) {
 }
 
 // Post one request (a filled SrvReq without its number) and return its number.
-int srv_post(coup_server* s, const coup::SrvReq& r, uint32_t* seq_out) {
+int srv_post(coup_server* s, const coup::SrvReq& req, uint32_t* seq_out) {
+  std::lock_guard<std::recursive_mutex> lk(s->mu);
   const auto now = std::chrono::steady_clock::now();
   if (s->posted >= 0xFFFFFF00u) {
     // the numbers would wrap: drain, stop, restart the count
@@ -2194,6 +2337,8 @@ int srv_post(coup_server* s, const coup::SrvReq& r, uint32_t* seq_out) {
   const uint32_t seq = s->posted + 1u;
   if (seq - srv_served(s) >= coup::kSrvRing) COUP_TRY(srv_wait(s, seq - coup::kSrvRing));  // ring full
   coup::SrvReq* q = s->ring + (seq & (coup::kSrvRing - 1u));
+  coup::SrvReq r = req;
+  r.check = coup::srv_check(reinterpret_cast<const uint32_t*>(&r), seq);
   // each half's fields, then its number, the second half's last (x86 makes
   // stores visible in program order; the compiler keeps them in order here)
   std::memcpy(q, &r, offsetof(coup::SrvReq, seq_a));
@@ -2325,6 +2470,15 @@ int coup_destroy(coup_env* env) {
   COUP_CHECK_ENV(env);
   (void)srv_drain(env);
   hipError_t e1 = hipStreamSynchronize(env->stream);
+  // release() frees device and pinned memory, which synchronises the whole
+  // device: a resident op-server wave (this env's or any other's) would hold
+  // that up for its idle time.  Stop every wave first; the next op on a
+  // server starts a new one.
+  {
+    std::lock_guard<std::mutex> g(g_servers_mu);
+    for (coup_server* s : g_servers) (void)srv_stop(s);
+  }
+  if (env->stream_event) (void)hipEventDestroy(env->stream_event);
   release(env);
   if (e1 != hipSuccess) return fail(COUP_E_HIP, "coup_destroy: HIP error while releasing the env");
   return COUP_OK;
@@ -2332,7 +2486,16 @@ int coup_destroy(coup_env* env) {
 
 int coup_set_stream(coup_env* env, void* hip_stream) {
   COUP_CHECK_ENV(env);
-  env->stream = (hipStream_t)hip_stream;
+  const hipStream_t next = (hipStream_t)hip_stream;
+  if (env->dirty && next != env->stream) {
+    // work still queued on the old stream: the new one waits for it, so
+    // everything later on env (and the op server's dirty check, which
+    // synchronises env->stream) is ordered after it
+    if (!env->stream_event) COUP_HIP_TRY(hipEventCreateWithFlags(&env->stream_event, hipEventDisableTiming));
+    COUP_HIP_TRY(hipEventRecord(env->stream_event, env->stream));
+    COUP_HIP_TRY(hipStreamWaitEvent(next, env->stream_event, 0));
+  }
+  env->stream = next;
   return COUP_OK;
 }
 
@@ -2428,6 +2591,28 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
       go(std::integral_constant<int, 256>());
     COUP_HIP_TRY(hipGetLastError());
     return COUP_OK;
+  }
+  if (info == coup::kInfoNone && mode == coup::kObsNone && !a.unchecked) {
+    // COUP_STEP_TPL=1/2/4: the group-Philox step (coup::k_step_group; A/B)
+    const int tpl = step_tpl();
+    if (tpl) {
+      auto go = [&](auto tp) {
+        constexpr int TP = decltype(tp)::value;
+        const unsigned g = (unsigned)((n + 256 / TP - 1) / (256 / TP));
+        if (uniform)
+          coup::k_step_group<TP, true><<<g, 256, 0, s>>>(a);
+        else
+          coup::k_step_group<TP, false><<<g, 256, 0, s>>>(a);
+      };
+      if (tpl == 4)
+        go(std::integral_constant<int, 4>());
+      else if (tpl == 2)
+        go(std::integral_constant<int, 2>());
+      else
+        go(std::integral_constant<int, 1>());
+      COUP_HIP_TRY(hipGetLastError());
+      return COUP_OK;
+    }
   }
 #define COUP_LAUNCH_STEP(U, M, T, I) launch_step<U, M, T, I>(env, a, n, dyn_lds, s)
 #define COUP_LAUNCH_MODES(U)                                                                         \
@@ -2792,6 +2977,7 @@ int coup_slot_op(coup_env* env, int64_t lane, const coup_env* src_env, int64_t s
     // the resident wave: no launch.  Stream work still in flight on either
     // env may write the lanes it reads -- wait for it first.
     coup_server* sv = env->server;
+    std::lock_guard<std::recursive_mutex> lk(sv->mu);  // post, wait and the result copy as one section
     if (env->dirty) {
       COUP_HIP_TRY(hipStreamSynchronize(env->stream));
       env->dirty = false;
@@ -3021,15 +3207,26 @@ int coup_server_create(int64_t idle_us, coup_server** out) {
   s->result = s->host + kSrvResultOff;
   s->result_dev = s->host_dev + kSrvResultOff;
   s->last_post = std::chrono::steady_clock::now();
+  {
+    std::lock_guard<std::mutex> g(g_servers_mu);
+    g_servers.push_back(s);
+  }
   *out = s;
   return COUP_OK;
 }
 
 int coup_server_destroy(coup_server* s) {
   if (!s) return fail(COUP_E_INVALID, "null coup_server");
-  int rc = COUP_OK;
-  if (s->running && s->posted != srv_served(s)) rc = srv_wait(s, s->posted);
-  const int rc2 = srv_stop(s);
+  {
+    std::lock_guard<std::mutex> g(g_servers_mu);
+    g_servers.erase(std::remove(g_servers.begin(), g_servers.end(), s), g_servers.end());
+  }
+  int rc = COUP_OK, rc2 = COUP_OK;
+  {
+    std::lock_guard<std::recursive_mutex> lk(s->mu);
+    if (s->running && s->posted != srv_served(s)) rc = srv_wait(s, s->posted);
+    rc2 = srv_stop(s);
+  }
   (void)hipStreamDestroy(s->stream);
   (void)hipHostFree(s->host);
   delete s;
@@ -3038,6 +3235,7 @@ int coup_server_destroy(coup_server* s) {
 
 int coup_server_stats(const coup_server* s, uint64_t* out) {
   if (!s || !out) return fail(COUP_E_INVALID, "coup_server_stats: null argument");
+  std::lock_guard<std::recursive_mutex> lk(const_cast<coup_server*>(s)->mu);
   out[0] = s->requests;
   out[1] = s->launches;
   out[2] = s->running ? 1u : 0u;

@@ -975,6 +975,34 @@ struct Rng {
   }
 };
 
+// The same draws with the Philox blocks one env step can need computed
+// ahead, outside the rules' branches (step kernels of the rules-bound
+// configurations): the lane's current block and the next one (the decision
+// at slot move_number_ and up to three deals after it, so slots m..m+3, span
+// at most these two) and block 0 of the next episode (an auto-reset's four
+// deals).  Any other draw -- a state off that pattern -- computes its block
+// as Rng does, so every draw equals Rng::draw.
+struct PrefRng {
+  uint32_t seed_lo, seed_hi, env_id;
+  uint32_t ep, b;  // c0 = block (ep, b), c1 = (ep, b + 1), r0 = ((ep + 1) & kEpisodeMask, 0)
+  uint4 c0, c1, r0;
+
+  __device__ __forceinline__ static uint4 block(uint32_t seed_lo, uint32_t seed_hi, uint32_t env_id, uint32_t ep,
+                                                uint32_t b) {
+    return philox4x32_10(make_uint4(b, ep, seed_hi, 0x436F7570u), env_id, seed_lo);
+  }
+
+  __device__ __forceinline__ uint32_t draw(uint32_t e, uint32_t idx) {
+    const uint32_t bb = idx >> 2;
+    const bool h0 = e == ep && bb == b, h1 = e == ep && bb == b + 1u;
+    const bool h2 = e == ((ep + 1u) & kEpisodeMask) && bb == 0u;
+    uint4 blk = h0 ? c0 : (h1 ? c1 : r0);
+    if (!(h0 || h1 || h2)) blk = block(seed_lo, seed_hi, env_id, e, bb);
+    const uint32_t j = idx & 3u;
+    return j == 0 ? blk.x : (j == 1 ? blk.y : (j == 2 ? blk.z : blk.w));
+  }
+};
+
 // Chance draw: r = floor(u * sum(deck) / 2^32), first type whose cumulative
 // count exceeds r.
 __device__ __forceinline__ uint32_t sample_card(uint32_t deck, uint32_t u) {
@@ -1024,8 +1052,8 @@ __device__ __forceinline__ uint32_t sample_action_select(uint32_t mask, uint32_t
 // A deal adds a face-down card, so a player alive before it is alive after
 // it: once the state is not terminal, only truncation (move_number_ > 90,
 // coup.cc:989-992) can end the deals early.
-template <class H>
-__device__ __forceinline__ void resolve_chance(Lane& L, Rng& rng, H& hist) {
+template <class R, class H>
+__device__ __forceinline__ void resolve_chance(Lane& L, R& rng, H& hist) {
   if (L.qlen == 0u || is_terminal(L)) return;
   do {
     const uint32_t u = rng.draw(L.episode, L.move);
@@ -1047,8 +1075,8 @@ __device__ __forceinline__ void resolve_chance(Lane& L, Rng& rng) {
 // of the episode from the full deck minus the earlier deals, and each hand
 // ends as its two face-down kinds in ascending order.  Every wave with a
 // finishing lane runs this on an auto-reset step.
-template <class H>
-__device__ __forceinline__ Lane new_episode(uint32_t episode, Rng& rng, H& hist) {
+template <class R, class H>
+__device__ __forceinline__ Lane new_episode(uint32_t episode, R& rng, H& hist) {
   Lane L = initial_lane(episode);
   L.err = L.episode == 0u ? 1u : 0u;  // the counter wrapped: this stream repeats episode 0's
   uint32_t t[4];

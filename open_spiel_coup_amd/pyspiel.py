@@ -201,7 +201,7 @@ class _Pool:
         if os.environ.get("COUP_SERVER", "1") != "0":
             h = ctypes.c_void_p()
             with torch.cuda.device(self.device):
-                _native.check(self.lib.coup_server_create(int(os.environ.get("COUP_SERVER_IDLE_US", "20000")),
+                _native.check(self.lib.coup_server_create(int(os.environ.get("COUP_SERVER_IDLE_US", "2000")),
                                                           ctypes.byref(h)))
             self.srv = h
         atexit.register(_close_pool, weakref.ref(self))

@@ -200,6 +200,83 @@ def test_server_idle_exit_and_relaunch(monkeypatch):
     assert pool.server_stats() is None
 
 
+def test_destroy_does_not_wait_out_an_idle_wave(monkeypatch):
+    """coup_destroy frees memory, which synchronises the device: it stops the
+    resident waves first instead of waiting out their idle time (here 2 s),
+    and the next op starts a new wave."""
+    import torch
+    from open_spiel_coup_amd import BatchedCoupEnv
+    game, pool = _fresh_pool(monkeypatch, COUP_SERVER_IDLE_US="2000000")
+    st = game.new_initial_state()
+    for a in (0, 1, 2, 3):
+        st = st.child(a)  # the wave is up and idling
+    other = BatchedCoupEnv(64, seed=3, device="cuda")
+    torch.cuda.synchronize()
+    launches = pool.server_stats()[1]
+    st = st.child(st.legal_actions()[0])
+    t0 = time.perf_counter()
+    other.close()
+    dt = time.perf_counter() - t0
+    assert dt < 0.5, f"coup_destroy took {dt:.3f} s: it waited for the idle wave"
+    ref = oracle.OracleState()
+    for a in st.history():
+        ref.apply_action(a)
+    st = st.child(ref.legal_actions()[0])
+    ref.apply_action(ref.legal_actions()[0])
+    _same(st, ref)
+    assert pool.server_stats()[1] == launches + 1  # stopped by the destroy, relaunched by the op
+    pool.close()
+
+
+def test_server_ops_alongside_env_create_destroy_in_threads():
+    """Pool ops in one thread while another creates, steps and destroys
+    rl_environment envs attached to the same server (coup_destroy, stream ops
+    and drains from a second thread): every state of the first
+    thread equals the oracle's, and every env's games are legal play."""
+    import gc
+    import threading
+    game = pyspiel.load_game("coup")
+    errors = []
+
+    def playouts():
+        try:
+            rng = np.random.default_rng(5)
+            for g in range(20):
+                st, ref = game.new_initial_state(), oracle.OracleState()
+                while not ref.is_terminal():
+                    a = int(rng.choice(ref.legal_actions()))
+                    st = st.child(a) if rng.integers(2) else st
+                    if st.history() != ref.history() + [a]:
+                        st.apply_action(a)
+                    ref.apply_action(a)
+                    _same(st, ref)
+        except Exception as e:  # noqa: BLE001 - reported by the main thread
+            errors.append(e)
+
+    def envs():
+        try:
+            for k in range(25):
+                env = rl_environment.Environment("coup", seed=k)
+                ts = env.reset()
+                for _ in range(6):
+                    if ts.last():
+                        ts = env.reset()
+                    p = ts.observations["current_player"]
+                    ts = env.step([ts.observations["legal_actions"][p][0]])
+                del env
+                gc.collect()
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    ts = [threading.Thread(target=playouts), threading.Thread(target=envs)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=100)
+    assert not any(t.is_alive() for t in ts), "a thread hung"
+    assert not errors, errors
+
+
 def test_no_wave_outlives_its_process():
     """A process that uses the server and exits without closing the pool
     leaves nothing running: it exits promptly and a second process finds
