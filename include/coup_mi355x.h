@@ -124,7 +124,9 @@ typedef struct {
   int8_t cur_player;     /* CurrentPlayer() (coup.cc:458-466) */
   uint8_t terminal;      /* IsTerminal() (coup.cc:989-1010) */
   uint8_t ok;            /* 0: the action was rejected (lane left unchanged) */
-  uint8_t reserved;
+  uint8_t unrepresentable; /* with ok = 0 under COUP_SLOT_UNCHECKED: the reference's DoApplyAction ACCEPTS the
+                              action, but its result leaves the packed record's fields (a 16th coin, an unsorted
+                              3-4 card hand) -- a known parity gap, not a reference raise */
   int8_t rewards[2];     /* Rewards() (coup.cc:1012-1014) */
   int8_t returns[2];     /* Returns() (coup.cc:1016-1032) */
   uint8_t pad[4];
@@ -143,7 +145,8 @@ typedef struct {
 #define COUP_SLOT_UNCHECKED 64 /* apply `action` as pyspiel's apply_action (pyspiel.cc:266, spiel.cc:322-331): no
                                   LegalActions() check, DoApplyAction's own checks decide (coup.cc:490-809);
                                   result.ok = 0, the lane untouched, where the reference raises, on a terminal
-                                  state, or where the result leaves the record's fields */
+                                  state, or where the result leaves the record's fields (then
+                                  result.unrepresentable = 1) */
 
 /* One request of coup_slot_ops (24 bytes): the op coup_slot_op would run on
  * lane `lane` with src_lane (< 0: no copy), action (< 0: none) and flags

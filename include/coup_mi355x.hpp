@@ -57,6 +57,24 @@ class SpielError : public std::runtime_error {
   using std::runtime_error::runtime_error;
 };
 
+// An action the reference's DoApplyAction ACCEPTS whose result leaves the
+// packed record's fields (coup_slot_result.unrepresentable; a 16th coin, an
+// unsorted 3-4 card hand): a known parity gap, not a
+// reference raise.  The state is left unchanged.
+class UnrepresentableActionError : public SpielError {
+ public:
+  using SpielError::SpielError;
+};
+
+namespace detail {
+[[noreturn]] inline void ThrowRejected(const std::string& op, int64_t a, const coup_slot_result& r) {
+  if (r.unrepresentable)
+    throw UnrepresentableActionError(op + "(" + std::to_string(a) +
+                                     "): the reference accepts it, but the result leaves the packed record's fields");
+  throw SpielError(op + "(" + std::to_string(a) + "): DoApplyAction raises here");
+}
+}  // namespace detail
+
 inline void Check(int rc, const char* what) {
   if (rc != COUP_OK) throw SpielError(std::string(what) + ": " + coup_last_error());
 }
@@ -368,7 +386,7 @@ class CoupState {
     CheckId(a, "ApplyAction");
     coup_slot_result r;
     detail::ThePool().Op(slot_, nullptr, (int)a, COUP_SLOT_UNCHECKED, &r);
-    if (!r.ok) throw SpielError("ApplyAction(" + std::to_string(a) + "): DoApplyAction raises here");
+    if (!r.ok) detail::ThrowRejected("ApplyAction", a, r);
     q_ = r;
     history_.push_back({p, a});
   }
@@ -389,7 +407,7 @@ class CoupState {
     coup_slot_result r;
     try {
       pool.Op(slot, &slot_, (int)a, COUP_SLOT_UNCHECKED, &r);
-      if (!r.ok) throw SpielError("Child(" + std::to_string(a) + "): DoApplyAction raises here");
+      if (!r.ok) detail::ThrowRejected("Child", a, r);
     } catch (...) {
       pool.Release(slot);
       throw;
@@ -424,8 +442,7 @@ class CoupState {
         std::vector<coup_slot_result> part(reqs.size());
         pool.Ops(slots[k].seg, reqs, slot_.seg, 0, part.data());
         for (size_t j = 0; j < ks.size(); ++j) {
-          if (!part[j].ok)
-            throw SpielError("Children(" + std::to_string(actions[ks[j]]) + "): DoApplyAction raises here");
+          if (!part[j].ok) detail::ThrowRejected("Children", actions[ks[j]], part[j]);
           res[ks[j]] = part[j];
         }
       }

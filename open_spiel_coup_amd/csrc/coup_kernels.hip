@@ -1685,6 +1685,18 @@ __device__ COUP_SLOT_FN uint32_t checked_transition(uint4 w, uint32_t x, uint4* 
   return 1u;
 }
 
+// Whether the reference's DoApplyAction accepts decision x on record w while
+// its result leaves the packed record's fields (apply_action_unchecked's
+// `representable` test, coup_lane.h): for a rejected unchecked action, tells
+// a known parity gap from a reference raise (coup_slot_result.
+// unrepresentable).  Out of line, on the rejection path only.
+__device__ COUP_SLOT_FN uint32_t unrepresentable_decision(uint4 w, uint32_t x) {
+  Lane R = unpack(w);
+  if (x > 17u || is_terminal(R) || R.err || is_chance(R)) return 0u;
+  return (ref_decision(R, x) && !representable(R)) ? 1u : 0u;
+}
+
+// Returns bit 2 = rejected but unrepresentable (unrepresentable_decision).
 __device__ COUP_SLOT_FN uint32_t slot_transition(uint4 w, uint32_t x, uint32_t unchecked, uint4* out) {
   const Lane L = unpack(w);
   const uint32_t idx = L.move;
@@ -1694,7 +1706,7 @@ __device__ COUP_SLOT_FN uint32_t slot_transition(uint4 w, uint32_t x, uint32_t u
     // a rejected action (or one the reference's DoApplyAction raises on)
     // leaves the record untouched
     *out = w;
-    return 0u;
+    return (unchecked && unrepresentable_decision(w, x)) ? 4u : 0u;
   }
   *out = r;
   const uint32_t store = idx < (uint32_t)kHist ? 2u : 0u;
@@ -1707,8 +1719,9 @@ __device__ COUP_SLOT_FN uint32_t slot_transition(uint4 w, uint32_t x, uint32_t u
 // (without it under kSlotUnchecked); then kSlotDeal resolves the pending chance deals under the sampling
 // contract, as rl_environment samples chance until a decision node
 // (rl_environment.py:369-382).  Every entry goes to the history bytes `hist`
-// (LDS).  Returns bit 0 = accepted without a new error; an illegal x leaves
-// the record untouched.  Out of line, like slot_transition.
+// (LDS).  Returns bit 0 = accepted without a new error, bit 2 = rejected but
+// unrepresentable (as slot_transition); an illegal x leaves the record
+// untouched.  Out of line, like slot_transition.
 __device__ COUP_SLOT_FN uint32_t slot_step(uint4 w, uint32_t x, uint32_t mode, uint32_t seed_lo, uint32_t seed_hi,
                                            uint32_t env_id, uint4* out, uint8_t* hist) {
   Lane L = unpack(w);
@@ -1723,7 +1736,7 @@ __device__ COUP_SLOT_FN uint32_t slot_step(uint4 w, uint32_t x, uint32_t mode, u
     uint4 r;
     if (!((mode & kSlotUnchecked) ? unchecked_decision(pack(L), x, &r) : checked_transition(pack(L), x, &r))) {
       *out = w;  // untouched, the reset included
-      return 0u;
+      return ((mode & kSlotUnchecked) && unrepresentable_decision(pack(L), x)) ? 4u : 0u;
     }
     L = unpack(r);
     rec.record(idx, entry);
@@ -1737,6 +1750,7 @@ __device__ COUP_SLOT_FN uint32_t slot_step(uint4 w, uint32_t x, uint32_t mode, u
   return 1u;
 }
 
+// ok: bit 0 accepted, bit 2 rejected but unrepresentable (slot_transition).
 __device__ COUP_SLOT_FN void slot_result(uint4 w, uint32_t ok, coup_slot_result* out) {
   const Lane L = unpack(w);
   out->record[0] = w.x;
@@ -1746,8 +1760,8 @@ __device__ COUP_SLOT_FN void slot_result(uint4 w, uint32_t ok, coup_slot_result*
   out->legal_mask = legal_mask(L);
   out->cur_player = (int8_t)current_player(L);
   out->terminal = is_terminal(L) ? 1 : 0;
-  out->ok = (uint8_t)ok;
-  out->reserved = 0;
+  out->ok = (uint8_t)(ok & 1u);
+  out->unrepresentable = (uint8_t)((ok >> 2) & 1u);
   out->rewards[0] = (int8_t)L.r0;
   out->rewards[1] = (int8_t)(-L.r0);
   const int32_t r0 = return0(L);
@@ -1783,7 +1797,7 @@ __device__ __forceinline__ void slot_op(const SlotArgs& a, uint8_t* __restrict__
                      hist);
     } else if (a.action >= 0) {
       const uint32_t r = slot_transition(rec, (uint32_t)a.action, a.mode & kSlotUnchecked, &rec);
-      ok = r & 1u;
+      ok = r & 5u;
       if (r & 2u) hist[(r >> 8) & 0xFFu] = (uint8_t)(r >> 16);
     }
     if (a.store) *a.dst_state = rec;
@@ -1981,7 +1995,7 @@ __device__ __forceinline__ void server_op(uint64_t rs, uint64_t hs, uint64_t dst
       ok = slot_step(rec, action >= 0 ? (uint32_t)action : 0xFFu, mode, seed_lo, seed_hi, env_id, &rec, hist);
     } else if (action >= 0) {
       const uint32_t r = slot_transition(rec, (uint32_t)action, mode & kSlotUnchecked, &rec);
-      ok = r & 1u;
+      ok = r & 5u;
       if (r & 2u) hist[(r >> 8) & 0xFFu] = (uint8_t)(r >> 16);
     }
     if (store) st16<kAuxDevice>(dst_state, 0u, rec);

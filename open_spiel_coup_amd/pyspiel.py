@@ -36,6 +36,14 @@ from .env import BatchedCoupEnv, INFO_STATE_SIZE, OBS_SIZE
 SpielError = CoupError
 
 
+class UnrepresentableActionError(SpielError):
+    """A SpielError for an action the reference's DoApplyAction ACCEPTS but
+    whose result leaves the packed record's fields (a 16th coin, an unsorted
+    3-4 card hand; only unchecked play reaches such states): a known parity
+    gap of the packed representation, not an action the
+    reference rejects.  The state is left unchanged."""
+
+
 class PlayerId(enum.IntEnum):
     """open_spiel/spiel_globals.h:28-36"""
     DEFAULT = -1
@@ -95,7 +103,7 @@ class GameType:
 
 # coup_slot_result (include/coup_mi355x.h), 128 bytes
 _SLOT_RESULT = np.dtype([("record", "<u4", (4,)), ("history", "u1", (96,)), ("legal_mask", "<u4"),
-                         ("cur_player", "i1"), ("terminal", "u1"), ("ok", "u1"), ("reserved", "u1"),
+                         ("cur_player", "i1"), ("terminal", "u1"), ("ok", "u1"), ("unrepresentable", "u1"),
                          ("rewards", "i1", (2,)), ("returns", "i1", (2,)), ("pad", "u1", (4,))])
 assert _SLOT_RESULT.itemsize == 128
 _RESULT_TAIL = struct.Struct("<IbBBBbbbb")  # legal_mask .. returns, at byte 112
@@ -124,8 +132,8 @@ class _Result(dict):
 
 def _parse_result(raw):
     """One coup_slot_result (128 bytes) -> the facade's result dict."""
-    lm, cp, term, ok = _RESULT_TAIL.unpack_from(raw, 112)[:4]
-    q = _Result(legal_mask=lm, current_player=cp, terminal=bool(term), ok=bool(ok))
+    lm, cp, term, ok, unrep = _RESULT_TAIL.unpack_from(raw, 112)[:5]
+    q = _Result(legal_mask=lm, current_player=cp, terminal=bool(term), ok=bool(ok), unrepresentable=bool(unrep))
     q._raw = raw
     return q
 
@@ -157,13 +165,18 @@ def _action_string(player, action):
         return str(action)
 
 
-def _apply_failed(player, action):
+def _apply_failed(player, action, q=None):
     """The SpielError of an action the lane rejected: DoApplyAction raises
     there in the reference (a SPIEL_CHECK or SpielFatalError of coup.cc:
-    490-809), the state is terminal, or the result leaves the packed record's
-    fields."""
-    return (f"ApplyAction({action}) by player {player} rejected: DoApplyAction raises here "
-            f"(or the state is terminal / the result leaves the record's fields)")
+    490-809) or the state is terminal -- or, UnrepresentableActionError, the
+    reference accepts it but the result leaves the packed record's fields
+    (coup_slot_result.unrepresentable)."""
+    if q is not None and q.get("unrepresentable"):
+        return UnrepresentableActionError(
+            f"ApplyAction({action}) by player {player}: the reference accepts this action, but its result "
+            f"leaves the packed record's fields (known parity gap, DESIGN.md section 8); state unchanged")
+    return SpielError(f"ApplyAction({action}) by player {player} rejected: DoApplyAction raises here "
+                      f"(or the state is terminal)")
 
 
 class _Pool:
@@ -322,6 +335,7 @@ class _Pool:
                 r = res[k]
                 q = {"record": r["record"], "history": r["history"], "legal_mask": int(r["legal_mask"]),
                      "current_player": int(r["cur_player"]), "terminal": bool(r["terminal"]), "ok": bool(r["ok"]),
+                     "unrepresentable": bool(r["unrepresentable"]),
                      "rewards": r["rewards"], "returns": r["returns"]}
                 if obs:
                     q["obs"] = obs_t[k]
@@ -618,7 +632,7 @@ class CoupState:
         a = _action_id(action)
         _, q = self._pool.apply_op(self._slot, None, a)
         if not q["ok"]:
-            raise SpielError(_apply_failed(player, a))
+            raise _apply_failed(player, a, q)
         self._q = q
         self._history = self._history + [(player, a)]
 
@@ -639,7 +653,7 @@ class CoupState:
         slot, q = self._pool.apply_op(None, self._slot, a)
         if not q["ok"]:
             self._pool.release(slot)
-            raise SpielError(_apply_failed(player, a))
+            raise _apply_failed(player, a, q)
         return CoupState(self._game, _slot=slot, _q=q, _history=self._history + [(player, a)])
 
     def children(self, actions, obs=False, info_state=False):
@@ -666,7 +680,7 @@ class CoupState:
                                obs=obs, info=info_state, unchecked=True)
                 for k, q in zip(ks, res):
                     if not q["ok"]:
-                        raise SpielError(_apply_failed(player, actions[k]))
+                        raise _apply_failed(player, actions[k], q)
                     out[k] = CoupState(self._game, _slot=slots[k], _q=q,
                                        _history=self._history + [(player, actions[k])])
         except Exception:
@@ -781,12 +795,13 @@ def apply_actions(states, actions):
         for k, q in zip(ks, res):
             if not q["ok"]:
                 states[k]._q = pool.op(states[k]._slot)
-                failed = k if failed is None else failed
+                if failed is None:
+                    failed, failed_q = k, q
                 continue
             states[k]._q = q
             states[k]._history = states[k]._history + [(players[k], actions[k])]
     if failed is not None:
-        raise SpielError(_apply_failed(players[failed], actions[failed]))
+        raise _apply_failed(players[failed], actions[failed], failed_q)
 
 
 def load_game(name, params=None):

@@ -336,8 +336,9 @@ class Environment:
             # lane (the op server's wave when the pool has one)
             q = self._lane_op(int(actions[0]), _native.SLOT_DEAL | _native.SLOT_UNCHECKED)
             if not q["ok"]:
-                # DoApplyAction raised in the reference (coup.cc:490-809); the lane is unchanged
-                raise pyspiel.SpielError(f"apply_action({actions[0]}) failed")
+                # DoApplyAction raised in the reference (coup.cc:490-809), or the
+                # result leaves the packed record (a known gap); the lane is unchanged
+                raise pyspiel._apply_failed(self._last["current_player"] if self._last else -1, int(actions[0]), q)
             step_type = StepType.LAST if q["terminal"] else StepType.MID
             self._should_reset = step_type == StepType.LAST
             return self._time_step(q, step_type, [float(x) for x in q["rewards"]])

@@ -106,7 +106,7 @@ def test_slot_result_layout_matches_header(tmp_path):
         pytest.skip("gcc not available")
     from open_spiel_coup_amd import pyspiel
     src = tmp_path / "layout.c"
-    fields = ["record", "history", "legal_mask", "cur_player", "terminal", "ok", "reserved", "rewards", "returns",
+    fields = ["record", "history", "legal_mask", "cur_player", "terminal", "ok", "unrepresentable", "rewards", "returns",
               "pad"]
     src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "coup_mi355x.h"\nint main(void) {\n'
                    + "".join(f'  printf("{f} %zu\\n", offsetof(coup_slot_result, {f}));\n' for f in fields)

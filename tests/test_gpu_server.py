@@ -218,13 +218,14 @@ def test_destroy_does_not_wait_out_an_idle_wave(monkeypatch):
     other.close()
     dt = time.perf_counter() - t0
     assert dt < 0.5, f"coup_destroy took {dt:.3f} s: it waited for the idle wave"
+    assert pool.server_stats()[2] == 0  # the destroy stopped the wave
     ref = oracle.OracleState()
     for a in st.history():
         ref.apply_action(a)
     st = st.child(ref.legal_actions()[0])
     ref.apply_action(ref.legal_actions()[0])
     _same(st, ref)
-    assert pool.server_stats()[1] == launches + 1  # stopped by the destroy, relaunched by the op
+    assert pool.server_stats()[1] > launches  # the ops after it started a new wave
     pool.close()
 
 

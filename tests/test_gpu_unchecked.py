@@ -275,3 +275,49 @@ def test_sync_vector_env_unchecked_equals_loop():
             assert a_ts.observations["info_state"] == b_ts.observations["info_state"]
             assert a_ts.observations["legal_actions"] == b_ts.observations["legal_actions"]
     assert t >= 30
+
+
+def test_unrepresentable_action_is_told_apart_from_a_reference_raise():
+    """an action the reference ACCEPTS whose result leaves the
+    packed record (a 16th coin, coup.cc:531-534 has no cap) raises
+    UnrepresentableActionError -- a known parity gap, coup_slot_result.
+    unrepresentable = 1 -- while an action the reference rejects raises a
+    plain SpielError; both leave the state unchanged (oracle:
+    OC_ERR_UNREPRESENTABLE = 4 against the reference-raise codes)."""
+    game = pyspiel.load_game("coup")
+    st = game.new_initial_state()
+    ref = oracle.OracleState()
+    for a in (1, 1, 3, 3):
+        st.apply_action(a)
+        ref.apply_action_unchecked(a)
+    while ref.coins(1) < 15:
+        for _ in range(2):
+            st.apply_action(0)  # Income, legal or not
+            ref.apply_action_unchecked(0)
+    st.apply_action(0)
+    ref.apply_action_unchecked(0)
+    assert st.packed_record().tolist() == [int(x) for x in ref.pack(0)]
+    before = st.packed_record().tolist()
+    with pytest.raises(pyspiel.UnrepresentableActionError):
+        st.apply_action(0)  # P2's 16th coin
+    with pytest.raises(pyspiel.UnrepresentableActionError):
+        st.child(0)
+    assert st.packed_record().tolist() == before
+    # an action the reference itself rejects here: a plain SpielError
+    raised = []
+    for a in range(18):
+        r2 = ref.clone()
+        try:
+            r2.apply_action_unchecked(a)
+        except RuntimeError as err:
+            if "code 4" not in str(err):
+                raised.append(a)
+    assert raised
+    for a in raised:
+        with pytest.raises(pyspiel.SpielError) as e:
+            st.apply_action(a)
+        assert not isinstance(e.value, pyspiel.UnrepresentableActionError), a
+    kids = None
+    with pytest.raises(pyspiel.UnrepresentableActionError):
+        kids = st.children([0])
+    assert kids is None and st.packed_record().tolist() == before

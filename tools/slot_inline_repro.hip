@@ -210,6 +210,7 @@ static bool same(const Result& a, const Result& b) {
          a.legal == b.legal && a.cur == b.cur && a.term == b.term && a.r0 == b.r0 && a.ret0 == b.ret0;
 }
 
+#ifndef REPRO_NO_MAIN  // tools/w3_module_check.hip reuses the kernels above
 int main(int argc, char** argv) {
   const int n = argc > 1 ? std::atoi(argv[1]) : 200000;
   uint4* recs;
@@ -345,3 +346,4 @@ int main(int argc, char** argv) {
   std::printf("}}\n");
   return 0;
 }
+#endif  // REPRO_NO_MAIN
