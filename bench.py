@@ -595,7 +595,9 @@ def main():
         elif with_obs:
             kernel = "coup::k_step<true, %d, %d, 0, false>" % _writer(os.environ.get("COUP_OBS_MODE"))
         else:
-            kernel = "coup::k_step<true, 0, 256, 0, false>"
+            tpl = os.environ.get("COUP_STEP_TPL", "1")
+            kernel = ("coup::k_step_group<%s, true>" % tpl if tpl in ("1", "2", "4") else
+                      "coup::k_step<true, 0, 256, 0, false>")
         outputs = ("ObservationTensor fp32 [B][2][98] per step" if with_obs else
                    "InformationStateTensor fp32 [B][2][2492] per step" if with_info else
                    "per-episode statistics only" if fused == "rollout" else

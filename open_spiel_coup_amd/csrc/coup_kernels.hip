@@ -2199,11 +2199,14 @@ int xcd_remap() {
   return e ? (std::atoi(e) != 0) : 1;
 }
 
-// COUP_STEP_TPL: threads per lane of the rules-bound step (coup::k_step_group;
-// 0 = k_step).  Read at every launch (A/B in one process).
+// COUP_STEP_TPL: threads per lane of the rules-bound in-place step
+// (coup::k_step_group; 0 = k_step).  Default 1: the Philox blocks computed
+// ahead with ILP, 7.08 -> 6.95 us per c2 step; 2 and 4 lanes' threads per
+// lane measured 7.59 and 9.74 us (profiles/r04/ab/c2_tpl.jsonl).  Read at
+// every launch (A/B in one process).
 int step_tpl() {
   const char* e = std::getenv("COUP_STEP_TPL");
-  const int v = e ? std::atoi(e) : 0;
+  const int v = e ? std::atoi(e) : 1;
   return (v == 1 || v == 2 || v == 4) ? v : 0;
 }
 

@@ -992,14 +992,22 @@ struct PrefRng {
     return philox4x32_10(make_uint4(b, ep, seed_hi, 0x436F7570u), env_id, seed_lo);
   }
 
+  __device__ __forceinline__ static uint32_t word(uint4 v, uint32_t j) {
+    return j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w));
+  }
+
+  // Word by word, never a select between the blocks themselves: a select of
+  // whole uint4 members became a select of their addresses, which put the
+  // struct in memory (promoted to 20 KB of LDS per block) and made the c2
+  // step 3x slower.
   __device__ __forceinline__ uint32_t draw(uint32_t e, uint32_t idx) {
-    const uint32_t bb = idx >> 2;
+    const uint32_t bb = idx >> 2, j = idx & 3u;
     const bool h0 = e == ep && bb == b, h1 = e == ep && bb == b + 1u;
     const bool h2 = e == ((ep + 1u) & kEpisodeMask) && bb == 0u;
-    uint4 blk = h0 ? c0 : (h1 ? c1 : r0);
-    if (!(h0 || h1 || h2)) blk = block(seed_lo, seed_hi, env_id, e, bb);
-    const uint32_t j = idx & 3u;
-    return j == 0 ? blk.x : (j == 1 ? blk.y : (j == 2 ? blk.z : blk.w));
+    const uint32_t w0 = word(c0, j), w1 = word(c1, j), w2 = word(r0, j);
+    uint32_t u = h0 ? w0 : (h1 ? w1 : w2);
+    if (!(h0 || h1 || h2)) u = word(block(seed_lo, seed_hi, env_id, e, bb), j);
+    return u;
   }
 };
 

@@ -1,7 +1,8 @@
 """coup::k_step_group (COUP_STEP_TPL = 1 / 2 / 4): the rules-bound step with
 the Philox blocks one step can need computed ahead by the lane's thread
-group (PrefRng) and traded by DPP, against the plain k_step (COUP_STEP_TPL
-unset) and the oracle.  Same sampling contract, so the same games: every
+group (PrefRng) and traded by DPP (TPL 1, the default, computes them in
+one thread with ILP), against the plain k_step (COUP_STEP_TPL=0) and the
+oracle.  Same sampling contract, so the same games: every
 output of every step, the records and the episode accumulators are equal,
 at c2's batch (65,536 lanes: one wave per SIMD) and ragged batches whose
 last group is partial.  Caller actions (legal, illegal: counted once per
@@ -22,10 +23,7 @@ KEYS = ("actions", "rewards", "step_type", "legal_mask", "current_player")
 
 
 def _run(monkeypatch, tpl, B, steps, seed=3, auto_reset=True, actions_fn=None, env_id_base=0):
-    if tpl:
-        monkeypatch.setenv("COUP_STEP_TPL", str(tpl))
-    else:
-        monkeypatch.delenv("COUP_STEP_TPL", raising=False)
+    monkeypatch.setenv("COUP_STEP_TPL", str(tpl))  # 0: k_step
     env = BatchedCoupEnv(B, seed=seed, auto_reset=auto_reset, obs=False, device="cuda", episode_stats=True,
                          env_id_base=env_id_base)
     outs = []
@@ -58,11 +56,12 @@ def test_group_step_equals_k_step_uniform(monkeypatch, B):
         _same(_run(monkeypatch, tpl, B, 80), ref, f"TPL {tpl} B {B}")
 
 
-def test_group_step_equals_oracle_slices(monkeypatch):
-    """k_step_group<4> at c2's batch against the oracle directly, on three
-    256-lane slices at every step."""
+@pytest.mark.parametrize("tpl", [1, 4])
+def test_group_step_equals_oracle_slices(monkeypatch, tpl):
+    """k_step_group at c2's batch (TPL 1: the default c2 kernel) against the
+    oracle directly, on three 256-lane slices at every step."""
     B, K = 65536, 60
-    outs, rec, _, _, err = _run(monkeypatch, 4, B, K, seed=11)
+    outs, rec, _, _, err = _run(monkeypatch, tpl, B, K, seed=11)
     assert err == 0
     for k in (0, B // 2 + 77, B - 256):
         ref = oracle.rollout(seed=11, n=256, steps=K, env_id_base=k)
@@ -103,8 +102,8 @@ def test_group_step_caller_actions_and_errors(monkeypatch):
 
 
 def test_group_step_env_id_base_and_default_kernel(monkeypatch):
-    """Lanes keyed by env_id_base + i (a rank's shard), and the variable
-    unset or out of range selects k_step."""
+    """Lanes keyed by env_id_base + i (a rank's shard), and an out-of-range
+    value selects k_step."""
     ref = _run(monkeypatch, 0, 2048, 30, env_id_base=123457)
     _same(_run(monkeypatch, 4, 2048, 30, env_id_base=123457), ref, "env_id_base")
     monkeypatch.setenv("COUP_STEP_TPL", "3")

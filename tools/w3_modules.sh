@@ -31,6 +31,11 @@ for v in slp noslp slpscal; do
     $B/llc -O$o -mtriple=amdgcn-amd-amdhsa -mcpu=gfx950 "$O/kmin_$v.ll" -o "$O/kmin_${v}_O$o.s"
   done
 done
+# the SLP IR once more through GlobalISel instead of SelectionDAG
+for v in slp noslp; do
+  $B/llc -O3 -global-isel -mtriple=amdgcn-amd-amdhsa -mcpu=gfx950 -filetype=obj "$O/kmin_$v.ll" -o "$O/kmin_${v}_O3gisel.o"
+  $B/ld.lld -shared "$O/kmin_${v}_O3gisel.o" -o "$O/kmin_${v}_O3gisel.co"
+done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fno-slp-vectorize -std=c++17 -I "$R/include" \
   -I "$R/open_spiel_coup_amd/csrc" -I "$R/tools" "$R/tools/w3_module_check.hip" \
   "$R/open_spiel_coup_amd/csrc/coup_nplayer.hip" -o "$O/w3_module_check"

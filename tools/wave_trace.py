@@ -1,4 +1,5 @@
-"""Per-wave timeline of one c3 step (measurement builds only).
+"""Per-wave timeline of one c3 step, or with --obs 0 one c2 step (measurement
+builds only).
 
     python -m open_spiel_coup_amd.build --out ab/trace.so --define COUP_WAVE_TRACE
     COUP_LIB_PATH=ab/trace.so python tools/wave_trace.py [--batch B] [--steps K]
@@ -29,6 +30,7 @@ def main():
     ap.add_argument("--bin-us", type=float, default=4.0)
     ap.add_argument("--mode", default=None, help="COUP_OBS_MODE for the traced steps")
     ap.add_argument("--quiet", action="store_true", help="summary only")
+    ap.add_argument("--obs", type=int, default=1, help="0: the c2 step (no observation writer)")
     a = ap.parse_args()
     if a.mode:
         os.environ["COUP_OBS_MODE"] = a.mode
@@ -40,7 +42,7 @@ def main():
     if not hasattr(lib, "coup_debug_set_trace"):
         raise SystemExit("not a COUP_WAVE_TRACE build (set COUP_LIB_PATH)")
     lib.coup_debug_set_trace.argtypes = [ctypes.c_void_p]
-    env = BatchedCoupEnv(a.batch, seed=1, auto_reset=True, obs=True, device="cuda:0")
+    env = BatchedCoupEnv(a.batch, seed=1, auto_reset=True, obs=bool(a.obs), device="cuda:0")
     env.rollout(256)
     for _ in range(5):
         env.step()
@@ -75,7 +77,7 @@ def main():
         if ok.any():
             seg[name] = [round(float(v), 2) for v in np.percentile((a1[ok] - a0[ok]) / 100.0, [5, 50, 95])]
     q = lambda x: [round(float(v), 2) for v in np.percentile(x, [5, 50, 95])]
-    summary = {"mode": a.mode, "event_us": round(e0.elapsed_time(e1) * 1e3, 2), "span_us": round(float(span), 2), "waves": int(waves),
+    summary = {"mode": a.mode, "obs": a.obs, "batch": a.batch, "event_us": round(e0.elapsed_time(e1) * 1e3, 2), "span_us": round(float(span), 2), "waves": int(waves),
                "compute_us_p5_50_95": q(comp), "issue_us_p5_50_95": q(issue), "drain_us_p5_50_95": q(drain),
                "load_us_p5_50_95": q(load), "late_waves_load_us_p5_50_95": q(load[late]),
                "late_waves_compute_us_p5_50_95": q(comp[late]),
@@ -97,7 +99,7 @@ def main():
         rows.append({"t_us": lo, "computing": c, "issuing": i, "draining": d, "issue_GBps": round(gbs)})
         if not a.quiet:
             print(f"{lo:7.1f}  comp {c:6d}  issue {i:6d}  drain {d:6d}  issue-rate {gbs:8.0f} GB/s")
-    with open(os.path.join(ROOT, "gpurun_out", f"wave_trace_m{a.mode or 'default'}.json"), "w") as f:
+    with open(os.path.join(ROOT, "gpurun_out", f"wave_trace_m{a.mode or 'default'}_obs{a.obs}_b{a.batch}.json"), "w") as f:
         json.dump({"summary": summary, "timeline": rows}, f)
 
 
