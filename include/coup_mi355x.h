@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define COUP_ABI_VERSION 10
+#define COUP_ABI_VERSION 11
 
 #define COUP_NUM_PLAYERS 2          /* coup.h:42 */
 #define COUP_MAX_PLAYERS 6          /* N-player extension */
@@ -302,6 +302,35 @@ int coup_slot_op(coup_env* env, int64_t lane, const coup_env* src_env, int64_t s
  * synchronises the env's stream. */
 int coup_slot_ops(coup_env* env, int64_t n, const coup_slot_req* reqs, const coup_env* src_env, int flags,
                   void* host_out);
+
+/* --- host-resident per-game states --------------------------------------- */
+
+/* A single State op is ~0.1 us of integer code; a device round trip is a
+ * PCIe crossing each way (the op server above: ~7 us).  For the per-state
+ * callers of rust_open_spiel.h:34-73 / pyspiel.cc:263-345 (one op per node:
+ * outcome_sampling_mccfr.py:81-87, deep_cfr.py:440-444) the library also
+ * runs the SAME rules (coup_lane.h) and tensor decoders (coup_tensor.h) on
+ * the host, over a coup_slot_result as the state (record, history bytes and
+ * the answers), so a host state and a device lane convert with one copy
+ * (coup_slot_op's result one way, coup_write_lane the other).  Batched work
+ * stays on the device.  These run on the calling thread; no HIP call. */
+int coup_host_state_init(coup_slot_result* out);                    /* NewInitialState (coup.cc:393-428) */
+/* State::ApplyAction on `in` into `out` (may alias): flags COUP_SLOT_UNCHECKED
+ * as pyspiel's apply_action (spiel.cc:322-331, no legality check), else with
+ * it; ok / unrepresentable exactly as coup_slot_op reports them. */
+int coup_host_state_apply(const coup_slot_result* in, int action, int flags, coup_slot_result* out);
+/* ObservationTensor [2][98] and / or InformationStateTensor [2][2492] of
+ * both players (either pointer may be NULL; coup.cc:1044-1056). */
+int coup_host_state_tensors(const coup_slot_result* st, float* obs, float* info);
+/* ObservationString(player) (kind 0), InformationStateString(player) (1) --
+ * CoupObserver::StringFrom, coup.cc:290-373 -- or ToString() (2, coup.cc:
+ * 945-987) of st into buf (cap bytes, NUL-terminated when it fits).  Returns
+ * the length (>= cap: truncated), -1 for a bad argument. */
+int64_t coup_host_state_string(const coup_slot_result* st, int kind, int player, char* buf, int64_t cap);
+/* Write host state `src` (its record and history bytes) into lane `lane` of
+ * a 2-player COUP_FLAG_HISTORY env (State::SetState-style migration to the
+ * device), ordered after the env's pending stream and server work. */
+int coup_write_lane(coup_env* env, int64_t lane, const coup_slot_result* src);
 
 /* --- device-resident op server ------------------------------------------ */
 

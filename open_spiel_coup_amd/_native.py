@@ -11,7 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # COUP_LIB_PATH: load another build of the same library (A/B timing of two
 # builds, tools/ab_builds.sh); there is still no fallback
 LIB_PATH = os.environ.get("COUP_LIB_PATH") or os.path.join(HERE, "libcoup_mi355x.so")
-ABI_VERSION = 10
+ABI_VERSION = 11
 FLAG_AUTO_RESET, FLAG_HISTORY, FLAG_GENERIC, FLAG_UNCHECKED = 1, 2, 4, 8
 MAX_PLAYERS = 6
 HISTORY_BYTES = 96
@@ -27,6 +27,8 @@ SYMBOLS = (
     "coup_export_state", "coup_import_state", "coup_export_history",
     "coup_import_history", "coup_error_count", "coup_slot_op", "coup_slot_ops", "coup_measure_step_traffic",
     "coup_server_create", "coup_server_destroy", "coup_attach_server", "coup_server_stats",
+    "coup_host_state_init", "coup_host_state_apply", "coup_host_state_tensors", "coup_host_state_string",
+    "coup_write_lane",
 )
 
 # coup_slot_op flags and result layout (coup_slot_result, 128 bytes)
@@ -112,6 +114,11 @@ def load():
         "coup_server_destroy": ([vp], i32),
         "coup_attach_server": ([vp, vp], i32),
         "coup_server_stats": ([vp, ctypes.POINTER(ctypes.c_uint64)], i32),
+        "coup_host_state_init": ([vp], i32),
+        "coup_host_state_apply": ([ctypes.c_char_p, i32, i32, vp], i32),
+        "coup_host_state_tensors": ([ctypes.c_char_p, vp, vp], i32),
+        "coup_host_state_string": ([ctypes.c_char_p, i32, i32, vp, i64], i64),
+        "coup_write_lane": ([vp, i64, ctypes.c_char_p], i32),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

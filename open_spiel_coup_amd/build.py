@@ -20,8 +20,13 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 SOURCES = [os.path.join(CSRC, "coup_kernels.hip"), os.path.join(CSRC, "coup_nplayer.hip")]
-DEPS = SOURCES + [os.path.join(CSRC, h) for h in ("coup_lane.h", "coup_nlane.h", "coup_np.h", "coup_regroup.h", "coup_episodes.h")] + [
-    os.path.join(ROOT, "include", "coup_mi355x.h")]
+# the per-game State ops on the host (same rules header, g++), linked into the
+# same library (csrc/coup_host.cpp)
+HOST_SRC = os.path.join(CSRC, "coup_host.cpp")
+HOST_INC = os.path.join(CSRC, "host")
+DEPS = SOURCES + [os.path.join(CSRC, h) for h in ("coup_lane.h", "coup_nlane.h", "coup_np.h", "coup_regroup.h", "coup_episodes.h",
+                                                 "coup_tensor.h")] + [
+    os.path.join(ROOT, "include", "coup_mi355x.h"), HOST_SRC, os.path.join(HOST_INC, "hip", "hip_runtime.h")]
 OUT = os.path.join(HERE, "libcoup_mi355x.so")
 OBJ_DIR = os.path.join(ROOT, "build", "obj")  # git-ignored (build/)
 RUST_SRC = os.path.join(CSRC, "rust_spiel.cpp")
@@ -50,9 +55,21 @@ NO_SLP = "-fno-slp-vectorize"
 OPT = {"coup_kernels.hip": "-O3", "coup_nplayer.hip": "-O3"}
 
 
+def host_command(obj):
+    """coup_host.cpp -> obj: host C++ (g++), the lane rules through the
+    csrc/host stand-in of the few HIP names they use."""
+    return [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-fPIC", "-Wall", "-I", HOST_INC, "-I", CSRC, "-I",
+            os.path.join(ROOT, "include"), "-c", HOST_SRC, "-o", obj]
+
+
+HOST_OBJ = os.path.join(OBJ_DIR, "coup_host.o")
+
+
 def command(resource_usage=False, out=OUT, defines=()):
+    """Measurement builds: one hipcc command over the HIP sources and the
+    host object (build it first with host_command(HOST_OBJ))."""
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", NO_SLP, "-std=c++17", "-fPIC", "-shared",
-           "-Wall", "-I", os.path.join(ROOT, "include"), "-o", out] + [f"-D{d}" for d in defines] + SOURCES
+           "-Wall", "-I", os.path.join(ROOT, "include"), "-o", out] + [f"-D{d}" for d in defines] + SOURCES + [HOST_OBJ]
     if resource_usage:
         cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
     return cmd
@@ -125,6 +142,8 @@ def build(force=False, verbose=False, repro=False):
             if verbose:
                 cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
             jobs.append(cmd)
+        objs.append(HOST_OBJ)
+        jobs.append(host_command(HOST_OBJ))
     if repro and (force or not up_to_date(REPRO_OUT, [REPRO_SRC] + DEPS)):
         os.makedirs(os.path.dirname(REPRO_OUT), exist_ok=True)
         jobs.append(repro_command())
@@ -148,6 +167,8 @@ def main():
     a = ap.parse_args()
     if a.out or a.define:
         out = os.path.abspath(a.out or OUT)
+        os.makedirs(OBJ_DIR, exist_ok=True)
+        subprocess.check_call(host_command(HOST_OBJ))
         subprocess.check_call(command(a.verbose, out, a.define))
         print(out)
         return

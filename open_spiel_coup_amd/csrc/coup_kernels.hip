@@ -34,6 +34,7 @@ __device__ __forceinline__ void count_philox_eval() {
 #include "coup_mi355x.h"
 #include "coup_np.h"
 #include "coup_regroup.h"
+#include "coup_tensor.h"
 
 namespace coup {
 
@@ -42,7 +43,6 @@ constexpr int kThreads = 256;
 // (profiles/r02/ab/sort_block_size_2p.log)
 constexpr int kStepSortLanes = 512;
 constexpr int kRolloutSortLanes = 1024;
-constexpr int kObsSize = COUP_OBS_SIZE;
 
 // The RNG key of lane i (global env id).  A measurement
 // build with -DCOUP_ABLATE_SAME_STREAM gives every lane the same stream, so
@@ -59,38 +59,6 @@ __device__ __forceinline__ uint32_t lane_stream_id(uint32_t env_id_base, int64_t
 
 // ------------------------------------------------------- observation tensor
 
-// CoupObserver::WriteTensor with kDefaultObsType (coup.cc:248-287,
-// observer.h:287-290) through ContiguousAllocator (zero-filled, blocks laid
-// out back to back, observer.h:173-176):
-//   [0:2] observer one-hot          [2:22] P1 cards [4][5]   [22:42] P2 cards
-//   [42:44] cur_move_player one-hot (zeros when terminal)
-//   [44:60] cards_state [2][4][2]   [60:62] coins           [62:98] last_action [2][18]
-// A card's type is visible for the owner's face-down cards and for every
-// face-up card.  `f` is a compile-time constant after unrolling, so every
-// element folds to one or two compares on a nibble.
-template <int P>
-__device__ __forceinline__ float obs_at(const Lane& L, bool term, const int f) {
-  if (f < 2) return f == P ? 1.0f : 0.0f;
-  if (f < 42) {
-    const int q = (f - 2) / 20, i = ((f - 2) % 20) / 5, t = (f - 2) % 5;
-    const uint32_t n = nib(q ? L.h1 : L.h0, (uint32_t)i);
-    const bool v = (n == (uint32_t)(2 * t + 1)) || (q == P && n == (uint32_t)(2 * t));
-    return v ? 1.0f : 0.0f;
-  }
-  if (f < 44) return (!term && L.M == (uint32_t)(f - 42)) ? 1.0f : 0.0f;
-  if (f < 60) {
-    const int q = (f - 44) / 8, i = ((f - 44) % 8) / 2, s = (f - 44) % 2;
-    const uint32_t n = nib(q ? L.h1 : L.h0, (uint32_t)i);
-    return (n != 0xFu && (n & 1u) == (uint32_t)s) ? 1.0f : 0.0f;
-  }
-  if (f < 62) return (float)(f == 60 ? L.c0 : L.c1);
-  const int q = (f - 62) / 18, a = (f - 62) % 18;
-  return ((q ? L.l1 : L.l0) == (uint32_t)a) ? 1.0f : 0.0f;
-}
-
-__device__ __forceinline__ float obs_pair_at(const Lane& L, bool term, const int g) {
-  return g < kObsSize ? obs_at<0>(L, term, g) : obs_at<1>(L, term, g - kObsSize);
-}
 
 // Both players' 98-float rows of one lane: 784 contiguous bytes = 49 float4.
 __device__ __forceinline__ void write_obs_pair(float* __restrict__ dst, const Lane& L) {
@@ -234,30 +202,6 @@ __device__ __forceinline__ void write_obs_wave(float* __restrict__ wave_obs, con
 // float4 at offset 4c.  Coins sit at row offsets 60-61: float4 15 (.x, .y)
 // of the P1 row and float4 39 (.z, .w) of the P2 row.
 
-// One observer's 98-bit row (bit f = element f of ObservationTensor(P)).
-template <int P>
-__device__ __forceinline__ void obs_row_bits(const Lane& L, bool term, uint64_t& lo, uint64_t& hi) {
-  lo = 1ull << P;  // observer one-hot
-#pragma unroll
-  for (uint32_t k = 0; k < 8; ++k) {
-    const uint32_t q = k >> 2, i = k & 3u;
-    const uint32_t n = nib(q ? L.h1 : L.h0, i);
-    const bool exists = n != 0xFu;
-    const bool visible = exists && (q == (uint32_t)P || (n & 1u));
-    lo |= (uint64_t)visible << (2u + 20u * q + 5u * i + (n >> 1));
-    lo |= (uint64_t)exists << (44u + 8u * q + 2u * i + (n & 1u));
-  }
-  lo |= (uint64_t)(!term) << (42u + L.M);
-  hi = 0;
-#pragma unroll
-  for (uint32_t q = 0; q < 2; ++q) {
-    const uint32_t a = q ? L.l1 : L.l0;
-    const uint32_t p = 62u + 18u * q + a;
-    const bool has = a != kNoAction;
-    lo |= (uint64_t)(has && p < 64u) << (p & 63u);
-    hi |= (uint64_t)(has && p >= 64u) << ((p - 64u) & 63u);
-  }
-}
 
 // 8 LDS words of a lane: the 196-bit string (row P1 at bits 0..97, row P2
 // at 98..195) in words 0..6, coins (P1 | P2 << 8) in word 7.
@@ -390,27 +334,11 @@ __device__ __forceinline__ void write_obs_block_bits(float* __restrict__ block_o
 // the global history buffer) and 6 words of prefix (pre_lds): [0..1] the
 // P1-view prefix bits (element f of 0..61 at bit f), [2..3] the P2 view,
 // [4] coins (P1 | P2 << 8) | move_number << 16.
-constexpr int kInfoSize = COUP_INFO_STATE_SIZE;  // 2492
-constexpr int kInfoHalfF4 = kInfoSize / 4;       // 623 float4 per player
-constexpr int kInfoF4 = 2 * kInfoHalfF4;         // 1246 float4 per lane
-constexpr int kPreWords = 6;
-constexpr int kHist = (int)kHistoryBytes;
 #ifndef COUP_INFO_STORE_POLICY
 #define COUP_INFO_STORE_POLICY 2  // 2 sc1 buffer stores (4% faster than 1, non-temporal: DESIGN.md section 5)
 #endif
 constexpr int kInfoStorePolicy = COUP_INFO_STORE_POLICY;
 
-__device__ __forceinline__ void info_prefix_to_lds(const Lane& L, uint32_t* __restrict__ pre) {
-  const bool term = is_terminal(L);
-  uint64_t a_lo, a_hi, b_lo, b_hi;
-  obs_row_bits<0>(L, term, a_lo, a_hi);
-  obs_row_bits<1>(L, term, b_lo, b_hi);
-  const uint64_t m62 = (1ull << 62) - 1ull;  // drop the observation's last_action bits
-  reinterpret_cast<uint2*>(pre)[0] = make_uint2((uint32_t)a_lo, (uint32_t)((a_lo & m62) >> 32));
-  reinterpret_cast<uint2*>(pre)[1] = make_uint2((uint32_t)b_lo, (uint32_t)((b_lo & m62) >> 32));
-  pre[4] = L.c0 | (L.c1 << 8) | (L.move << 16);
-  pre[5] = 0;
-}
 
 // All 64 lanes of the wave must call this.  (x, o, c) = (64 j + lane,
 // x / 1246, x % 1246) advance incrementally.  A float4 whose first element
@@ -499,11 +427,6 @@ __device__ __forceinline__ void wave_hist_copy(uint8_t* __restrict__ global_wave
 __device__ __forceinline__ void load_obs_desc(uint32_t* desc_lds) {
   for (int g = threadIdx.x; g < 2 * kObsSize; g += blockDim.x) desc_lds[g] = obs_desc(g);
   __syncthreads();
-}
-
-__device__ __forceinline__ int32_t return0(const Lane& L) {
-  // Returns (coup.cc:1016-1032): face-up(P2) - face-up(P1)
-  return (int32_t)face_up_count(L.h1) - (int32_t)face_up_count(L.h0);
 }
 
 __device__ __forceinline__ void count_error(uint32_t* err_count) { atomicAdd(err_count, 1u); }
@@ -1564,39 +1487,6 @@ __global__ __launch_bounds__(kThreads) void k_query(QueryArgs a) {
 // 1246 float4 of a lane are spread over 1246 threads; each thread decodes its
 // lane's record and history bytes itself (L2-resident).
 // reqs (coup_slot_ops): output row l is the lane of request l.
-// One InformationStateTensor float4 (element c of [2][2492] / 4) of the lane
-// whose record is L and whose history bytes are h; k_info_elems' decode.
-__device__ __forceinline__ float4 info_f4(const uint32_t* pre, const uint8_t* h, uint32_t c) {
-  const uint32_t p = c >= (uint32_t)kInfoHalfF4 ? 1u : 0u;
-  const int f0 = 4 * (int)(c - p * (uint32_t)kInfoHalfF4);
-  const uint32_t meta = pre[4];
-  const uint32_t len = meta >> 16;
-  if (f0 >= 62 + 18 * (int)len) return make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  const uint64_t prefix = (uint64_t)pre[2 * p] | ((uint64_t)pre[2 * p + 1] << 32);
-  const int t0 = f0 - 62;
-  const uint32_t r0 = t0 < 0 ? 0u : (uint32_t)t0 / 18u;
-  const int col0 = t0 - 18 * (int)r0;
-  uint32_t va[2];
-#pragma unroll
-  for (uint32_t k = 0; k < 2; ++k) {
-    const uint32_t r = r0 + k;
-    const uint32_t e = h[r < (uint32_t)kHist ? r : 0u];
-    const bool seen = (e & 0x20u) == 0u || ((e >> 6) & 1u) == p;  // deals: observer's only
-    va[k] = (r < len && seen) ? (e & 0x1Fu) : 31u;
-  }
-  float v[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int f = f0 + e;
-    const int col = col0 + e;
-    const uint32_t row_act = col >= 18 ? va[1] : va[0];
-    const float hv = (row_act == (uint32_t)(col >= 18 ? col - 18 : col)) ? 1.0f : 0.0f;
-    const float pb = (float)((uint32_t)(prefix >> (f & 63)) & 1u);
-    const float coin = (float)(f == 60 ? (meta & 0xFFu) : ((meta >> 8) & 0xFFu));
-    v[e] = f < 60 ? pb : (f < 62 ? coin : hv);
-  }
-  return make_float4(v[0], v[1], v[2], v[3]);
-}
 
 __global__ __launch_bounds__(kThreads) void k_info_elems(const uint4* __restrict__ state,
                                                         const uint8_t* __restrict__ hist, int64_t n,
@@ -3306,6 +3196,22 @@ int coup_import_history(coup_env* env, const uint8_t* src) {
   COUP_TRY(launching(env));
   COUP_HIP_TRY(hipMemcpyAsync(env->hist, src, (size_t)env->batch * COUP_HISTORY_BYTES, hipMemcpyDeviceToDevice,
                               env->stream));
+  return COUP_OK;
+}
+
+int coup_write_lane(coup_env* env, int64_t lane, const coup_slot_result* src) {
+  COUP_CHECK_ENV(env);
+  if (!src) return fail(COUP_E_INVALID, "coup_write_lane: src is null");
+  if (env->generic || !env->hist)
+    return fail(COUP_E_INVALID, "coup_write_lane: needs a 2-player env created with COUP_FLAG_HISTORY");
+  if (lane < 0 || lane >= env->batch) return fail(COUP_E_INVALID, "coup_write_lane: lane out of range");
+  COUP_TRY(launching(env));  // after the server's pending requests and the stream's work
+  COUP_HIP_TRY(hipMemcpyAsync(env->state + lane, src->record, sizeof(uint4), hipMemcpyHostToDevice, env->stream));
+  COUP_HIP_TRY(hipMemcpyAsync(env->hist + lane * COUP_HISTORY_BYTES, src->history, COUP_HISTORY_BYTES,
+                              hipMemcpyHostToDevice, env->stream));
+  // src is the caller's memory (pageable): the copies are done on return
+  COUP_HIP_TRY(hipStreamSynchronize(env->stream));
+  env->dirty = false;
   return COUP_OK;
 }
 

@@ -184,6 +184,12 @@ __device__ __forceinline__ bool is_terminal(const Lane& L) {
 
 __device__ __forceinline__ bool is_chance(const Lane& L) { return L.qlen != 0; }
 
+// Returns()[0] (coup.cc:1016-1032): face-up(P2) - face-up(P1); Returns()[1]
+// is its negation.
+__device__ __forceinline__ int32_t return0(const Lane& L) {
+  return (int32_t)face_up_count(L.h1) - (int32_t)face_up_count(L.h0);
+}
+
 // CurrentPlayer (coup.cc:458-466)
 __device__ __forceinline__ int current_player(const Lane& L) {
   return is_terminal(L) ? -4 : (is_chance(L) ? -1 : (int)L.M);

@@ -9,13 +9,18 @@ same surface with only an import swap:
     game = pyspiel.load_game("coup")
     state = game.new_initial_state()
 
-A `CoupState` owns one lane of a device-resident lane pool; every rules
-operation (apply_action, legal actions, tensors, ...) is one coup_slot_op on
-that lane through the C ABI, served by the pool's device-resident op server
-(one resident wave polling a request ring in host memory; COUP_SERVER=0 makes
-each op a kernel launch) -- there is no CPU rules engine in the product.  The 128-byte result of the last op (record, history bytes,
-legal mask, player, rewards, returns) is kept on the host and serves the
-accessors until the state changes; a clone is a device-side lane copy.  Strings are formatted on the host (strings.py).
+A `CoupState` is, by default, host-resident: its 128-byte coup_slot_result
+(record, history bytes, legal mask, player, rewards, returns) is the state,
+and every op -- apply_action, child, tensors, strings -- runs the library's
+host build of the same lane rules and decoders the kernels run
+(coup_host_state_*, csrc/coup_host.cpp; ~1 us from Python, where any device
+round trip is 7-10 us).  The library, and a HIP device, are still required:
+there is no separate CPU rules engine and no build without the GPU library.
+With COUP_STATE_DEVICE=1 (or game._device_states) a State instead owns one
+lane of a device-resident lane pool and each op is a coup_slot_op on that
+lane, served by the pool's resident op-server wave (COUP_SERVER=0: a launch
+per op).  Strings are formatted by the library's host formatter
+(coup_host_state_string; strings.py is the same in Python).
 This is the compatibility path; batched learners use BatchedCoupEnv.
 """
 import atexit
@@ -321,7 +326,7 @@ class _Pool:
             _native.check(self.lib.coup_slot_ops(env._h, n, arr, src_h, flags,
                                                  ctypes.c_void_p(self._batch_host.data_ptr())))
             buf = self._batch_host.numpy()[:nbytes]
-            res = buf[:n * per].view(_SLOT_RESULT).copy()
+            raw = buf[:n * per].tobytes()
             off = n * per
             obs_t = info_t = None
             if obs:
@@ -332,11 +337,7 @@ class _Pool:
                     n, 2, INFO_STATE_SIZE).copy()
             out = []
             for k in range(n):
-                r = res[k]
-                q = {"record": r["record"], "history": r["history"], "legal_mask": int(r["legal_mask"]),
-                     "current_player": int(r["cur_player"]), "terminal": bool(r["terminal"]), "ok": bool(r["ok"]),
-                     "unrepresentable": bool(r["unrepresentable"]),
-                     "rewards": r["rewards"], "returns": r["returns"]}
+                q = _parse_result(raw[k * per:(k + 1) * per])
                 if obs:
                     q["obs"] = obs_t[k]
                 if info:
@@ -379,6 +380,70 @@ class _Pool:
 
 _pools = {}
 
+# Per-game States are host-resident by default: the library's host build of
+# the lane rules (coup_host_state_*, csrc/coup_host.cpp) applies each op on
+# the calling thread, ~1 us from Python, against ~7-10 us for any device
+# round trip.  COUP_STATE_DEVICE=1 keeps them on the
+# device lane pool (every op a coup_slot_op on the op server), as before
+# round 4; a game can also choose per instance (CoupGame._device_states).
+DEVICE_STATES = os.environ.get("COUP_STATE_DEVICE", "0") == "1"
+
+
+class _Host:
+    """The host-resident State ops of libcoup_mi355x.so.  A host state is
+    its 128-byte coup_slot_result (record, history bytes, answers), kept as
+    an immutable bytes object inside its _Result: clones share it."""
+
+    def __init__(self):
+        lib = _native.load()
+        self._init = lib.coup_host_state_init
+        self._apply = lib.coup_host_state_apply
+        self._tensors = lib.coup_host_state_tensors
+        self._string = lib.coup_host_state_string
+        self._lock = threading.Lock()
+        self._out = ctypes.create_string_buffer(_native.SLOT_RESULT_BYTES)
+
+    def init(self):
+        with self._lock:
+            _native.check(self._init(self._out))
+            return _parse_result(self._out.raw)
+
+    def apply(self, raw, action, flags):
+        with self._lock:
+            rc = self._apply(raw, action, flags, self._out)
+            if rc:
+                _native.check(rc)
+            return _parse_result(self._out.raw)
+
+    def string(self, raw, kind, player):
+        """coup_host_state_string: 0 ObservationString, 1
+        InformationStateString, 2 ToString."""
+        buf = ctypes.create_string_buffer(1024)
+        n = self._string(raw, kind, player, buf, 1024)
+        if n < 0:
+            raise SpielError(f"invalid player {player}")
+        if n >= 1024:
+            buf = ctypes.create_string_buffer(n + 1)
+            self._string(raw, kind, player, buf, n + 1)
+        return buf.value.decode()
+
+    def tensors(self, raw, obs, info):
+        """[2][98] and / or [2][2492] float32 arrays (None where not asked)."""
+        o = np.empty((2, OBS_SIZE), np.float32) if obs else None
+        i = np.empty((2, INFO_STATE_SIZE), np.float32) if info else None
+        _native.check(self._tensors(raw, o.ctypes.data if obs else None, i.ctypes.data if info else None))
+        return o, i
+
+
+_host_ops = None
+
+
+def _host():
+    global _host_ops
+    if _host_ops is None:
+        _host_ops = _Host()
+    return _host_ops
+
 
 def _close_pool(ref):
     pool = ref()
@@ -408,6 +473,7 @@ class CoupGame:
         self._type = GameType()
         self._device = device
         self._pool = None  # the lane pool of `device`, bound on first use
+        self._device_states = DEVICE_STATES  # States on device lanes instead of the host (module doc)
 
     def _bind_pool(self):
         self._pool = _pool(self._device)
@@ -493,13 +559,35 @@ class CoupGame:
 
 
 class CoupState:
-    """open_spiel::coup::CoupState (coup.h:111-197) over the GPU engine."""
+    """open_spiel::coup::CoupState (coup.h:111-197) over the MI355X engine.
 
-    def __init__(self, game, _src=None, _history=None, _q=None, _slot=None):
+    Host-resident (the default, _slot None): the state is the 128-byte
+    coup_slot_result in self._q and every op runs the library's host build
+    of the lane rules.  Device-resident (game._device_states): the state
+    owns a lane of the device pool and every op is a coup_slot_op.  Both
+    give the same results (tests/test_gpu_facade.py runs both)."""
+
+    def __init__(self, game, _src=None, _history=None, _q=None, _slot=None, _host_q=None):
         self._game = game
+        # the device pool is bound for host states too: the facade needs the
+        # HIP device (snapshots, batched ops with tensors), and says so at once
         self._pool = game._pool if game._pool is not None else game._bind_pool()
+        if _host_q is not None:  # a host state
+            self._slot, self._q, self._history = None, _host_q, _history
+            return
         if _slot is not None:  # filled by a batched op (children / apply_actions)
             self._slot, self._q, self._history = _slot, _q, _history
+            return
+        if not game._device_states:
+            self._slot = None
+            if _src is None:
+                self._q, self._history = _host().init(), []
+            else:  # snapshot of a device lane (rl_environment.get_state): one answered read
+                h, lane = _src
+                with self._pool.lock:
+                    _native.check(self._pool.lib.coup_slot_op(h, lane, None, 0, -1, 0, self._pool.host_ptr))
+                    self._q = _parse_result(self._pool.buf[:_native.SLOT_RESULT_BYTES].tobytes())
+                self._history = _history
             return
         self._slot = self._pool.alloc()
         if _src is None:
@@ -513,7 +601,8 @@ class CoupState:
 
     def __del__(self):
         try:
-            self._pool.release(self._slot)
+            if self._slot is not None:
+                self._pool.release(self._slot)
         except Exception:
             pass
 
@@ -524,6 +613,10 @@ class CoupState:
 
     def _copy_to_env(self, env_handle, lane):
         """Write this state into lane `lane` of a 2-player history env."""
+        if self._slot is None:
+            with self._pool.lock:
+                _native.check(self._pool.lib.coup_write_lane(env_handle, lane, self._q._raw))
+            return
         env = self._pool.segs[self._slot[0]]
         with self._pool.lock:
             env._bind_stream()
@@ -534,6 +627,13 @@ class CoupState:
     def _query(self, obs=False, info=False):
         need_obs = obs and "obs" not in self._q
         need_info = info and "info_state" not in self._q
+        if (need_obs or need_info) and self._slot is None:
+            o, i = _host().tensors(self._q._raw, need_obs, need_info)
+            if need_obs:
+                self._q["obs"] = o
+            if need_info:
+                self._q["info_state"] = i
+            return self._q
         if need_obs or need_info:
             q = self._pool.op(self._slot, obs=obs, info=info)
             for k in ("obs", "info_state"):
@@ -611,7 +711,8 @@ class CoupState:
         """ChanceOutcomes (coup.cc:1062-1077): exact count/total doubles."""
         if not self.is_chance_node():
             raise SpielError("chance_outcomes() at a non-chance node")
-        deck = packed.lane(self._words())["deck"]
+        w1 = struct.unpack_from("<I", self._q._raw, 4)[0]
+        deck = [(w1 >> (4 * t)) & 0xF for t in range(5)]  # w1 [19:0], type t at 4t
         total = float(sum(deck))
         return [(t, deck[t] / total) for t in range(5) if deck[t] > 0]
 
@@ -630,7 +731,10 @@ class CoupState:
         state unchanged, where the reference raises."""
         player = self._q["current_player"]
         a = _action_id(action)
-        _, q = self._pool.apply_op(self._slot, None, a)
+        if self._slot is None:
+            q = _host().apply(self._q._raw, a, _native.SLOT_UNCHECKED)
+        else:
+            _, q = self._pool.apply_op(self._slot, None, a)
         if not q["ok"]:
             raise _apply_failed(player, a, q)
         self._q = q
@@ -650,6 +754,11 @@ class CoupState:
         the new state's lane is a copy of this one with the action applied."""
         player = self._q["current_player"]
         a = _action_id(action)
+        if self._slot is None:
+            q = _host().apply(self._q._raw, a, _native.SLOT_UNCHECKED)
+            if not q["ok"]:
+                raise _apply_failed(player, a, q)
+            return CoupState(self._game, _history=self._history + [(player, a)], _host_q=q)
         slot, q = self._pool.apply_op(None, self._slot, a)
         if not q["ok"]:
             self._pool.release(slot)
@@ -666,6 +775,14 @@ class CoupState:
         player = self.current_player()
         if not actions:
             return []
+        if self._slot is None:
+            out = []
+            for a in actions:
+                c = self.child(a)
+                if obs or info_state:
+                    c._query(obs=obs, info=info_state)
+                out.append(c)
+            return out
         pool = self._pool
         if len(actions) == 1 and pool.srv is not None and not (obs or info_state):
             return [self.child(actions[0])]  # one op server request beats a launch
@@ -698,6 +815,8 @@ class CoupState:
         return list(zip(acts, self.children(acts, obs=obs, info_state=info_state)))
 
     def clone(self):
+        if self._slot is None:  # the result bytes are immutable: shared
+            return CoupState(self._game, _history=list(self._history), _host_q=self._q)
         return CoupState(self._game, _src=(self._pool.handle(self._slot), self._slot[1]),
                          _history=list(self._history), _q=self._q)
 
@@ -729,11 +848,13 @@ class CoupState:
 
     def observation_string(self, player=None):
         p = self.current_player() if player is None else player
-        return strings.observation_string(self._words(), self._hist, p)
+        return _host().string(self._q._raw, 0, p)
 
     def information_state_string(self, player=None):
+        """InformationStateString (coup.cc:290-373), the MCCFR info-set key
+        (outcome_sampling_mccfr.py:81-87): the library's host formatter."""
         p = self.current_player() if player is None else player
-        return strings.information_state_string(self._words(), self._hist, p)
+        return _host().string(self._q._raw, 1, p)
 
     def action_to_string(self, player, action=None):
         if action is None:  # action_to_string(action) for the current player
@@ -750,14 +871,14 @@ class CoupState:
         return ", ".join(str(a) for a in self.history())
 
     def move_number(self):
-        return packed.lane(self._words())["move_number"]
+        return (struct.unpack_from("<I", self._q._raw, 8)[0] >> 22) & 0x7F  # w2 [28:22]
 
     def serialize(self):
         """State::Serialize (spiel.cc:297-311)."""
         return "".join(f"{a}\n" for a in self.history())
 
     def __str__(self):
-        return strings.to_string(self._words(), self._hist)
+        return _host().string(self._q._raw, 2, 0)
 
     def to_string(self):
         return str(self)
@@ -784,9 +905,18 @@ def apply_actions(states, actions):
         raise ValueError("apply_actions needs distinct states")
     players = [st.current_player() for st in states]
     by_pool = {}
-    for k, st in enumerate(states):
-        by_pool.setdefault((id(st._pool), st._slot[0]), []).append(k)
     failed = None
+    for k, st in enumerate(states):
+        if st._slot is None:  # host states: the host op each
+            q = _host().apply(st._q._raw, actions[k], _native.SLOT_UNCHECKED)
+            if not q["ok"]:
+                if failed is None or k < failed:
+                    failed, failed_q = k, q
+                continue
+            st._q = q
+            st._history = st._history + [(players[k], actions[k])]
+            continue
+        by_pool.setdefault((id(st._pool), st._slot[0]), []).append(k)
     for (_, seg), ks in by_pool.items():
         pool = states[ks[0]]._pool
         res = pool.ops(seg, [(states[k]._slot[1], -1, actions[k]) for k in ks], unchecked=True)
@@ -795,7 +925,7 @@ def apply_actions(states, actions):
         for k, q in zip(ks, res):
             if not q["ok"]:
                 states[k]._q = pool.op(states[k]._slot)
-                if failed is None:
+                if failed is None or k < failed:
                     failed, failed_q = k, q
                 continue
             states[k]._q = q

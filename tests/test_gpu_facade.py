@@ -6,7 +6,7 @@ import pytest
 from oracle import oracle
 from tests import golden_util as G
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("state_mode")]
 
 from open_spiel_coup_amd import pyspiel, rl_environment, vector_env  # noqa: E402
 

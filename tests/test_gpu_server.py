@@ -40,11 +40,13 @@ def _fresh_pool(monkeypatch, **env):
     pool = pyspiel._Pool(torch.device("cuda", torch.cuda.current_device()))
     game = pyspiel.load_game("coup")
     game._pool = pool
+    game._device_states = True  # these tests are about the device path
     return game, pool
 
 
 def test_server_is_on_by_default_and_serves_the_facade():
     game = pyspiel.load_game("coup")
+    game._device_states = True
     st = game.new_initial_state()
     pool = st._pool
     assert pool.srv is not None, "the pool should start an op server (COUP_SERVER unset)"

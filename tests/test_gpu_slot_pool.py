@@ -1,6 +1,8 @@
-"""The device-resident lane pool behind the per-game State facade
-(coup_slot_op): clones, children and many live states, checked node by node
-against the oracle (oracle.OracleState mirrors every facade state)."""
+"""The per-game State facade -- host-resident states (the library's host
+build of the lane rules) and the device-resident lane pool (coup_slot_op),
+each test run with both (conftest state_mode): clones, children and many
+live states, checked node by node against the oracle (oracle.OracleState
+mirrors every facade state)."""
 import time
 
 import numpy as np
@@ -8,7 +10,7 @@ import pytest
 
 from oracle import oracle
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("state_mode")]
 
 from open_spiel_coup_amd import pyspiel, rl_environment  # noqa: E402
 
@@ -246,6 +248,7 @@ def test_slot_ops_rejects_dependent_requests():
     import ctypes
     from open_spiel_coup_amd import _native
     game = pyspiel.load_game("coup")
+    game._device_states = True  # a state on a pool lane
     st = game.new_initial_state()
     pool = st._pool
     env = pool.segs[st._slot[0]]

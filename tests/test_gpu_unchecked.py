@@ -12,7 +12,7 @@ import torch
 
 from oracle import oracle
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("state_mode")]
 
 from open_spiel_coup_amd import pyspiel, rl_environment, vector_env  # noqa: E402
 from open_spiel_coup_amd.env import BatchedCoupEnv  # noqa: E402

@@ -2,7 +2,8 @@
 process (measurement tool only).
 
 Rows:
-  - the State facade on the lane pool, with the device-resident op server
+  - the State facade with host-resident States (the default), and on the
+    lane pool, with the device-resident op server
     (default) and with one launch per op (a second pool built under
     COUP_SERVER=0): child(a) + legal_actions(), clone(), the tensors;
   - batched ops (coup_slot_ops): n children of one node, one action on each
@@ -50,7 +51,15 @@ def _pool_game(server):
             os.environ["COUP_SERVER"] = prev
     game = pyspiel.load_game("coup")
     game._pool = pool
+    game._device_states = True  # States on this pool's lanes
     return game, pool
+
+
+def _host_game():
+    """A game whose States are host-resident (the default since round 4)."""
+    game = pyspiel.load_game("coup")
+    game._device_states = False
+    return game
 
 
 def _opening(game):
@@ -90,6 +99,21 @@ def state_rows(tag, game, n):
             s2 = _opening(game)
         s2.apply_action(s2.legal_actions()[0])
     rows[f"{tag}_apply_action_us"] = _timed(apply_one, n)
+    rng = random.Random(0)
+    s3 = _opening(game)
+
+    def mccfr_node():
+        # outcome_sampling_mccfr.py:81-87 per node: legal_actions,
+        # information_state_string (the info-set key), apply_action
+        nonlocal s3
+        if s3.is_terminal():
+            s3 = _opening(game)
+        legal = s3.legal_actions()
+        if not s3.is_chance_node():
+            s3.information_state_string(s3.current_player())
+        s3.apply_action(rng.choice(legal))
+    rows[f"{tag}_mccfr_node_us"] = _timed(mccfr_node, n)
+    rows[f"{tag}_information_state_string_us"] = _timed(lambda: s3.information_state_string(0), n)
     return rows
 
 
@@ -115,19 +139,19 @@ def raw_rows(tag, game, n):
     return rows
 
 
-def batched_rows(game, n):
+def batched_rows(tag, game, n):
     st = _opening(game)
     rows = {}
     for k in (1, 7, 64, 1024):
         acts = [0] * k
         reps = max(10, n // k)
-        rows[f"children_n{k}_us_per_child"] = _timed(lambda: st.children(acts), reps) / k
-        rows[f"children_n{k}_with_info_state_us_per_child"] = _timed(
+        rows[f"{tag}_children_n{k}_us_per_child"] = _timed(lambda: st.children(acts), reps) / k
+        rows[f"{tag}_children_n{k}_with_info_state_us_per_child"] = _timed(
             lambda: st.children(acts, info_state=True), max(5, reps // 4)) / k
     frontier = [st.clone() for _ in range(1024)]
     t0 = time.perf_counter()
     pyspiel.apply_actions(frontier, [0] * 1024)
-    rows["apply_actions_n1024_us_per_state"] = 1e6 * (time.perf_counter() - t0) / 1024
+    rows[f"{tag}_apply_actions_n1024_us_per_state"] = 1e6 * (time.perf_counter() - t0) / 1024
     return rows
 
 
@@ -188,17 +212,21 @@ def main():
     a = ap.parse_args()
     g_srv, p_srv = _pool_game(True)
     g_launch, p_launch = _pool_game(False)
-    # warm both paths (segments allocated, code paths and the wave started)
+    g_host = _host_game()
+    # warm the paths (segments allocated, code paths and the wave started)
     state_rows("warm_server", g_srv, 50)
     state_rows("warm_launch", g_launch, 50)
+    state_rows("warm_host", g_host, 50)
     samples = {}
     for _ in range(a.rounds):
         rows = {}
+        rows.update(state_rows("host", g_host, a.ops))
         rows.update(state_rows("server", g_srv, a.ops))
         rows.update(state_rows("launch", g_launch, a.ops))
         rows.update(raw_rows("server", g_srv, a.ops))
         rows.update(raw_rows("launch", g_launch, a.ops))
-        rows.update(batched_rows(g_srv, a.ops))
+        rows.update(batched_rows("server", g_srv, a.ops))
+        rows.update(batched_rows("host", g_host, a.ops))
         rows.update(rl_rows(a.ops // 2))
         if not a.no_vector:
             rows.update(vector_env_rows())
