@@ -139,6 +139,7 @@ def test_server_ordered_with_stream_work_on_the_same_lanes(monkeypatch):
         ref.apply_action(a)
         _same(st, ref)
     env = rl_environment.Environment("coup", seed=9)
+    env._game._device_states = True  # its snapshots on pool lanes too
     env.reset()
     for _ in range(5):
         ts = env.get_time_step()
