@@ -33,6 +33,22 @@ RUST_SRC = os.path.join(CSRC, "rust_spiel.cpp")
 RUST_DEPS = [RUST_SRC, os.path.join(ROOT, "include", "coup_rust_abi.h"), os.path.join(ROOT, "include", "coup_mi355x.hpp"),
              os.path.join(ROOT, "include", "coup_mi355x.h")]
 RUST_OUT = os.path.join(HERE, "librust_spiel.so")
+# _coup_host: the CPython binding of the library's host State ops (pyspiel)
+EXT_SRC = os.path.join(CSRC, "host_ext.c")
+
+
+def ext_out():
+    import sysconfig
+    return os.path.join(HERE, "_coup_host" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def ext_command(out=None):
+    """_coup_host: C over the CPython API, linked to libcoup_mi355x.so (found
+    next to it through $ORIGIN)."""
+    import sysconfig
+    return [os.environ.get("CC", "gcc"), "-O2", "-fPIC", "-shared", "-Wall", "-I", sysconfig.get_paths()["include"],
+            "-I", os.path.join(ROOT, "include"), EXT_SRC, "-o", out or ext_out(), "-L", HERE, "-lcoup_mi355x",
+            "-Wl,-rpath,$ORIGIN"]
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("COUP_OFFLOAD_ARCH", "gfx950")
@@ -152,6 +168,11 @@ def build(force=False, verbose=False, repro=False):
         _run_all([[HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT] + objs], verbose)
     if force or not up_to_date(RUST_OUT, RUST_DEPS + [OUT]):
         cmd = rust_command()
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.check_call(cmd)
+    if force or not up_to_date(ext_out(), [EXT_SRC, os.path.join(ROOT, "include", "coup_mi355x.h"), OUT]):
+        cmd = ext_command()
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.check_call(cmd)

@@ -390,52 +390,46 @@ DEVICE_STATES = os.environ.get("COUP_STATE_DEVICE", "0") == "1"
 
 
 class _Host:
-    """The host-resident State ops of libcoup_mi355x.so.  A host state is
-    its 128-byte coup_slot_result (record, history bytes, answers), kept as
-    an immutable bytes object inside its _Result: clones share it."""
+    """The host-resident State ops of libcoup_mi355x.so (coup_host_state_*),
+    through their CPython binding _coup_host (csrc/host_ext.c, linked to the
+    library; ctypes would add ~0.7 us per call).  A host state is its
+    128-byte coup_slot_result (record, history bytes, answers), kept as an
+    immutable bytes object inside its _Result: clones share it."""
 
     def __init__(self):
-        lib = _native.load()
-        self._init = lib.coup_host_state_init
-        self._apply = lib.coup_host_state_apply
-        self._tensors = lib.coup_host_state_tensors
-        self._string = lib.coup_host_state_string
-        self._lock = threading.Lock()
-        self._out = ctypes.create_string_buffer(_native.SLOT_RESULT_BYTES)
+        _native.load()  # torch's HIP runtime, then the library the binding links
+        from . import _coup_host
+        _coup_host.bind(_Result)  # init / apply return _Result objects, built in C
+        self._ext = _coup_host
+        self.apply = _coup_host.apply  # (raw, action, flags) -> _Result
 
     def init(self):
-        with self._lock:
-            _native.check(self._init(self._out))
-            return _parse_result(self._out.raw)
-
-    def apply(self, raw, action, flags):
-        with self._lock:
-            rc = self._apply(raw, action, flags, self._out)
-            if rc:
-                _native.check(rc)
-            return _parse_result(self._out.raw)
+        return self._ext.init()
 
     def string(self, raw, kind, player):
-        """coup_host_state_string: 0 ObservationString, 1
-        InformationStateString, 2 ToString."""
-        buf = ctypes.create_string_buffer(1024)
-        n = self._string(raw, kind, player, buf, 1024)
-        if n < 0:
-            raise SpielError(f"invalid player {player}")
-        if n >= 1024:
-            buf = ctypes.create_string_buffer(n + 1)
-            self._string(raw, kind, player, buf, n + 1)
-        return buf.value.decode()
+        """0 ObservationString, 1 InformationStateString, 2 ToString."""
+        try:
+            return self._ext.string(raw, kind, player)
+        except ValueError:
+            raise SpielError(f"invalid player {player}") from None
 
     def tensors(self, raw, obs, info):
         """[2][98] and / or [2][2492] float32 arrays (None where not asked)."""
         o = np.empty((2, OBS_SIZE), np.float32) if obs else None
         i = np.empty((2, INFO_STATE_SIZE), np.float32) if info else None
-        _native.check(self._tensors(raw, o.ctypes.data if obs else None, i.ctypes.data if info else None))
+        self._ext.tensors(raw, o.ctypes.data if obs else 0, i.ctypes.data if info else 0)
         return o, i
 
 
 _host_ops = None
+
+
+def _tensor_list(row):
+    """One tensor row as the fresh list of floats pyspiel returns
+    (pyspiel.cc's vector<float> cast), built by the library's binding (shared
+    small floats, not tracked by the cyclic GC: rl_environment._float_lists)."""
+    from .rl_environment import _float_lists
+    return _float_lists(row.reshape(1, -1))[0]
 
 
 def _host():
@@ -840,11 +834,11 @@ class CoupState:
 
     def observation_tensor(self, player=None):
         p = self.current_player() if player is None else player
-        return self._query(obs=True)["obs"][p].tolist()
+        return _tensor_list(self._query(obs=True)["obs"][p])
 
     def information_state_tensor(self, player=None):
         p = self.current_player() if player is None else player
-        return self._query(info=True)["info_state"][p].tolist()
+        return _tensor_list(self._query(info=True)["info_state"][p])
 
     def observation_string(self, player=None):
         p = self.current_player() if player is None else player

@@ -98,48 +98,24 @@ def registered_games():
     return pyspiel.registered_games()
 
 
-class _RowLists:
-    """The per-player Python lists of an env's time steps, built by patching
-    the previous step's lists instead of converting every float again.
+_ext = None
 
-    The reference hands out `information_state_tensor(p)` /
-    `observation_tensor(p)` as fresh Python lists (pybind's vector<float> cast,
-    rl_environment.py:243-248): 2 x 2492 new float objects per step under
-    INFORMATION_STATE.  A step changes a handful of them (the new history
-    rows, coins, hands), so this keeps the last rows (numpy) and a private
-    master list per player, writes the entries that differ into the master
-    and returns a copy of it: a pointer copy plus a few float conversions
-    instead of 2492 (numpy tolist ~60 us per row on this container's host,
-    the copy ~9; and the copies' elements are a few shared floats, so a
-    256-env vector step no longer walks ~10^6 freshly allocated objects).
-    Values are equal to tolist's (float(float32) of the same entries); each
-    returned list is the caller's own."""
-    __slots__ = ("rows", "lists")
 
-    def __init__(self):
-        self.rows = None
-        self.lists = None
-
-    def __call__(self, tensors):
-        t = np.asarray(tensors)
-        if self.rows is None or self.rows.shape != t.shape:
-            self.rows = np.array(t, copy=True)
-            self.lists = [r.tolist() for r in self.rows]
-            return [lst.copy() for lst in self.lists]
-        out = []
-        for p in range(t.shape[0]):
-            new, old, master = t[p], self.rows[p], self.lists[p]
-            d = np.flatnonzero(new != old)
-            if d.size > (new.size >> 3):
-                self.lists[p] = master = new.tolist()
-                old[...] = new
-            elif d.size:
-                vals = new[d]
-                for j, v in zip(d.tolist(), vals.tolist()):
-                    master[j] = v
-                old[d] = vals
-            out.append(master.copy())
-        return out
+def _float_lists(rows):
+    """The per-player Python lists of a time step (rl_environment.py:243-248
+    hands out fresh lists of floats) from a [P, n] float32 array, built in C
+    by the library's CPython binding (_coup_host.float_lists): integral
+    values -- every element of both tensors -- share one float object each,
+    and the lists are kept out of the cyclic collector, so a 256-env vector
+    step costs per env what an 8-env one does.  Equal
+    to numpy's tolist element by element; each list is the caller's own."""
+    global _ext
+    if _ext is None:
+        _native.load()
+        from . import _coup_host
+        _ext = _coup_host
+    a = np.ascontiguousarray(rows, dtype=np.float32)
+    return _ext.float_lists(a.ctypes.data, a.shape[0], a.shape[1])
 
 
 def _resolve_seed(seed):
@@ -178,7 +154,6 @@ class Environment:
         self._make_env()
         self._should_reset = True
         self._last = None
-        self._row_lists = _RowLists()
 
     # ------------------------------------------------------------ plumbing
     def _make_env(self):
@@ -263,7 +238,7 @@ class Environment:
         legal_cur = [a for a in range(18) if (mask >> a) & 1] if cur >= 0 else []
         key = "obs" if self._use_observation else "info_state"
         tensors = q[key]
-        obs = {"info_state": self._row_lists(tensors[:self._num_players]),
+        obs = {"info_state": _float_lists(tensors[:self._num_players]),
                "legal_actions": [legal_cur if p == cur else [] for p in range(self._num_players)],
                "current_player": cur,
                "serialized_state": []}

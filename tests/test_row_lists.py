@@ -1,38 +1,51 @@
-"""rl_environment._RowLists: the time steps' per-player lists, patched from
-the previous step's, equal numpy's tolist of the same rows at every step
-(rl_environment.py:243-248 hands out fresh lists), and every returned list is
-the caller's own."""
+"""rl_environment._float_lists (the library's CPython binding,
+_coup_host.float_lists): the time steps' per-player lists equal numpy's
+tolist of the same float32 rows element by element -- one-hots, coin counts,
+and any other value (fractions, negative zero, large values) -- each call
+returns new lists the caller owns, and the lists of floats stay out of the
+cyclic garbage collector (rl_environment.py:243-248 hands out fresh lists)."""
+import gc
+import math
+
 import numpy as np
+import pytest
 
-from open_spiel_coup_amd.rl_environment import _RowLists
+
+def _lists():
+    try:
+        from open_spiel_coup_amd.rl_environment import _float_lists
+        _float_lists(np.zeros((1, 1), np.float32))
+    except (ImportError, OSError) as e:
+        pytest.skip(f"library / binding not built: {e}")
+    return _float_lists
 
 
-def test_patched_lists_equal_tolist_and_are_independent():
+def test_float_lists_equal_tolist():
+    fl = _lists()
     rng = np.random.default_rng(7)
-    rl = _RowLists()
-    rows = np.zeros((2, 2492), dtype=np.float32)
-    kept = []
-    for step in range(300):
-        rows = rows.copy()
-        k = int(rng.choice([0, 1, 3, 40, 2000]))  # few changes, none, and a whole-row rewrite
-        idx = rng.integers(0, rows.shape[1], size=k)
-        rows[rng.integers(0, 2), idx] = rng.integers(0, 13, size=k).astype(np.float32)
-        if step % 50 == 49:
-            rows[:] = 0.0  # reset-like
-        got = rl(rows)
-        assert [type(x) for x in got] == [list, list]
-        assert got == [r.tolist() for r in rows]
-        assert all(type(v) is float for v in got[0][:16])
-        got[0][5] = "caller's"  # mutating a returned list touches nothing else
-        kept.append((rows.copy(), got))
-    for r, got in kept:
-        got[0][5] = float(r[0][5])
-        assert got == [x.tolist() for x in r]
+    for _ in range(50):
+        rows = (rng.random((2, 2492)) < 0.02).astype(np.float32)
+        rows[:, 60:62] = rng.integers(0, 16, size=(2, 2))
+        got = fl(rows)
+        assert got == rows.tolist()
+        assert all(type(v) is float for v in got[0][:100])
+    odd = np.array([[0.0, -0.0, 1.5, 15.0, 16.0, -1.0, 1e30, 3.0]], np.float32)
+    got = fl(odd)[0]
+    assert got == odd[0].tolist()
+    assert math.copysign(1.0, got[1]) == -1.0  # -0.0 keeps its sign
 
 
-def test_shape_change_rebuilds():
-    rl = _RowLists()
-    a = np.arange(6, dtype=np.float32).reshape(2, 3)
-    assert rl(a) == a.tolist()
-    b = np.ones((2, 4), dtype=np.float32)
-    assert rl(b) == b.tolist()
+def test_float_lists_are_fresh_and_untracked():
+    fl = _lists()
+    rows = np.eye(2, 98, dtype=np.float32)
+    a, b = fl(rows), fl(rows)
+    assert a == b and a[0] is not b[0]
+    a[0][0] = "caller's"
+    assert b[0][0] == 1.0 and fl(rows)[0][0] == 1.0
+    assert not gc.is_tracked(b[0]) and gc.is_tracked(b)  # the outer list is an ordinary one
+
+
+def test_float_lists_of_non_contiguous_input():
+    fl = _lists()
+    big = np.arange(4 * 10, dtype=np.float32).reshape(4, 10)
+    assert fl(big[::2]) == big[::2].tolist()

@@ -79,6 +79,8 @@ def main():
             return False
         if fused:
             return "k_rollout" in kn
+        if not want_obs and not want_info and ("k_step_group<" in kn or "12k_step_group" in kn):
+            return True  # the rules-bound step (COUP_STEP_TPL, default 1: k_step_group<1, true>)
         m = (re.search(r"k_step<true, (\d+), \d+, (\d+)(?:, false)?>", kn) or
              re.search(r"k_stepILb1ELi(\d+)ELi\d+ELi(\d+)E", kn))
         return bool(m) and (m.group(1) != "0") == want_obs and (m.group(2) == "2") == want_info
