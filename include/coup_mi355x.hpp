@@ -256,7 +256,7 @@ class Pool {
     const char* e = std::getenv("COUP_SERVER");
     if (!(e && std::atoi(e) == 0)) {
       const char* idle = std::getenv("COUP_SERVER_IDLE_US");
-      if (coup_server_create(idle ? std::atoll(idle) : 20000, &srv_) != COUP_OK) srv_ = nullptr;
+      if (coup_server_create(idle ? std::atoll(idle) : 2000, &srv_) != COUP_OK) srv_ = nullptr;
     }
   }
   ~Pool() {
@@ -312,6 +312,18 @@ inline Pool& ThePool() {
   return p;
 }
 
+// States are host-resident unless COUP_STATE_DEVICE=1 (read once): the
+// library's host build of the lane rules (coup_host_state_*) applies each
+// op on the calling thread instead of a device round trip (DESIGN.md
+// section 12).  A host state has no pool slot (seg < 0).
+inline bool DeviceStates() {
+  static const bool v = [] {
+    const char* e = std::getenv("COUP_STATE_DEVICE");
+    return e && std::atoi(e) == 1;
+  }();
+  return v;
+}
+
 }  // namespace detail
 
 // ---------------------------------------------------------- Game / State
@@ -323,16 +335,28 @@ struct PlayerAction {
   Action action;
 };
 
-// open_spiel::coup::CoupState (coup.h:111-197) on the GPU engine.
+// open_spiel::coup::CoupState (coup.h:111-197) on the MI355X engine: host-
+// resident by default (its coup_slot_result is the state; the library's
+// host rules apply each op), or on a lane of the device pool
+// (COUP_STATE_DEVICE=1; every op a coup_slot_op).  Same results either way.
 class CoupState {
  public:
-  explicit CoupState(const CoupGame* game) : game_(game), slot_(detail::ThePool().Alloc()) {
-    detail::ThePool().Op(slot_, nullptr, -1, COUP_SLOT_INIT, &q_);
+  explicit CoupState(const CoupGame* game) : game_(game) {
+    detail::Pool& pool = detail::ThePool();  // the HIP device is required either way
+    if (!detail::DeviceStates()) {
+      Check(coup_host_state_init(&q_), "coup_host_state_init");
+      return;
+    }
+    slot_ = pool.Alloc();
+    pool.Op(slot_, nullptr, -1, COUP_SLOT_INIT, &q_);
   }
-  // State::Clone (spiel.h:822): a device-side lane copy, no round trip
-  CoupState(const CoupState& o)
-      : game_(o.game_), slot_(detail::ThePool().Alloc()), history_(o.history_), q_(o.q_) {
-    detail::ThePool().Op(slot_, &o.slot_, -1, COUP_SLOT_NO_RESULT, nullptr);
+  // State::Clone (spiel.h:822): the result copied (host), or a device-side
+  // lane copy with no round trip
+  CoupState(const CoupState& o) : game_(o.game_), history_(o.history_), q_(o.q_) {
+    if (!o.Host()) {
+      slot_ = detail::ThePool().Alloc();
+      detail::ThePool().Op(slot_, &o.slot_, -1, COUP_SLOT_NO_RESULT, nullptr);
+    }
   }
   CoupState& operator=(const CoupState&) = delete;
   ~CoupState() { detail::ThePool().Release(slot_); }
@@ -385,7 +409,10 @@ class CoupState {
     const Player p = CurrentPlayer();
     CheckId(a, "ApplyAction");
     coup_slot_result r;
-    detail::ThePool().Op(slot_, nullptr, (int)a, COUP_SLOT_UNCHECKED, &r);
+    if (Host())
+      Check(coup_host_state_apply(&q_, (int)a, COUP_SLOT_UNCHECKED, &r), "coup_host_state_apply");
+    else
+      detail::ThePool().Op(slot_, nullptr, (int)a, COUP_SLOT_UNCHECKED, &r);
     if (!r.ok) detail::ThrowRejected("ApplyAction", a, r);
     q_ = r;
     history_.push_back({p, a});
@@ -402,6 +429,14 @@ class CoupState {
   std::unique_ptr<CoupState> Child(Action a) const {
     const Player p = CurrentPlayer();
     CheckId(a, "Child");
+    if (Host()) {
+      coup_slot_result r;
+      Check(coup_host_state_apply(&q_, (int)a, COUP_SLOT_UNCHECKED, &r), "coup_host_state_apply");
+      if (!r.ok) detail::ThrowRejected("Child", a, r);
+      std::vector<PlayerAction> h = history_;
+      h.push_back({p, a});
+      return std::unique_ptr<CoupState>(new CoupState(game_, detail::Pool::Slot{}, std::move(h), r));
+    }
     detail::Pool& pool = detail::ThePool();
     const detail::Pool::Slot slot = pool.Alloc();
     coup_slot_result r;
@@ -423,6 +458,18 @@ class CoupState {
     const Player p = CurrentPlayer();
     const int32_t rf = COUP_SLOT_UNCHECKED;
     for (Action a : actions) CheckId(a, "Children");
+    if (Host()) {
+      std::vector<std::unique_ptr<CoupState>> out;
+      for (Action a : actions) {
+        coup_slot_result r;
+        Check(coup_host_state_apply(&q_, (int)a, COUP_SLOT_UNCHECKED, &r), "coup_host_state_apply");
+        if (!r.ok) detail::ThrowRejected("Children", a, r);
+        std::vector<PlayerAction> h = history_;
+        h.push_back({p, a});
+        out.emplace_back(new CoupState(game_, detail::Pool::Slot{}, std::move(h), r));
+      }
+      return out;
+    }
     detail::Pool& pool = detail::ThePool();
     std::vector<detail::Pool::Slot> slots;
     for (size_t k = 0; k < actions.size(); ++k) slots.push_back(pool.Alloc());
@@ -464,12 +511,23 @@ class CoupState {
   double PlayerReturn(Player p) const { return Returns()[p]; }
 
   std::vector<float> ObservationTensor(Player p) const {
+    if (Host()) {
+      std::vector<float> both(2 * COUP_OBS_SIZE);
+      Check(coup_host_state_tensors(&q_, both.data(), nullptr), "coup_host_state_tensors");
+      return std::vector<float>(both.begin() + p * COUP_OBS_SIZE, both.begin() + (p + 1) * COUP_OBS_SIZE);
+    }
     std::vector<uint8_t> buf(sizeof(coup_slot_result) + 2 * COUP_OBS_SIZE * 4);
     detail::ThePool().Op(slot_, nullptr, -1, COUP_SLOT_OBS, buf.data());
     const float* both = reinterpret_cast<const float*>(buf.data() + sizeof(coup_slot_result));
     return std::vector<float>(both + p * COUP_OBS_SIZE, both + (p + 1) * COUP_OBS_SIZE);
   }
   std::vector<float> InformationStateTensor(Player p) const {
+    if (Host()) {
+      std::vector<float> both(2 * COUP_INFO_STATE_SIZE);
+      Check(coup_host_state_tensors(&q_, nullptr, both.data()), "coup_host_state_tensors");
+      return std::vector<float>(both.begin() + p * COUP_INFO_STATE_SIZE,
+                                both.begin() + (p + 1) * COUP_INFO_STATE_SIZE);
+    }
     std::vector<uint8_t> buf(sizeof(coup_slot_result) + 2 * COUP_INFO_STATE_SIZE * 4);
     detail::ThePool().Op(slot_, nullptr, -1, COUP_SLOT_INFO, buf.data());
     const float* both = reinterpret_cast<const float*>(buf.data() + sizeof(coup_slot_result));
@@ -506,6 +564,7 @@ class CoupState {
       : game_(game), slot_(slot), history_(std::move(history)), q_(q) {}
   // the result of the last op on this lane (every op refreshes it)
   const coup_slot_result& Q() const { return q_; }
+  bool Host() const { return slot_.seg < 0; }
   // in LegalActions() (ApplyActionWithLegalityCheck)
   bool Legal(Action a) const {
     return a >= 0 && a < COUP_NUM_ACTIONS && ((Q().legal_mask >> a) & 1u) && CurrentPlayer() != kTerminalPlayerId;

@@ -30,6 +30,14 @@ def build_driver(out_dir):
     return exe
 
 
+@pytest.fixture(autouse=True, params=["host", "device"])
+def state_mode(request, monkeypatch):
+    """The C++ layer's States host-resident (default) or on device lanes
+    (COUP_STATE_DEVICE=1), for the driver processes this module starts."""
+    monkeypatch.setenv("COUP_STATE_DEVICE", "1" if request.param == "device" else "0")
+    return request.param
+
+
 @pytest.fixture(scope="module")
 def driver(tmp_path_factory):
     if shutil.which("g++") is None or not os.path.isdir("/opt/rocm/include"):

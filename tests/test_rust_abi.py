@@ -29,6 +29,14 @@ def _declared():
     return sorted(set(re.findall(r"(\w+)\s*\(", text)) - {"defined"})
 
 
+@pytest.fixture(autouse=True, params=["host", "device"])
+def state_mode(request, monkeypatch):
+    """The C++ layer's States host-resident (default) or on device lanes
+    (COUP_STATE_DEVICE=1), for the driver processes this module starts."""
+    monkeypatch.setenv("COUP_STATE_DEVICE", "1" if request.param == "device" else "0")
+    return request.param
+
+
 @pytest.fixture(scope="module")
 def lib():
     from open_spiel_coup_amd import build
