@@ -74,7 +74,8 @@ OPT = {"coup_kernels.hip": "-O3", "coup_nplayer.hip": "-O3"}
 def host_command(obj):
     """coup_host.cpp -> obj: host C++ (g++), the lane rules through the
     csrc/host stand-in of the few HIP names they use."""
-    return [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-fPIC", "-Wall", "-I", HOST_INC, "-I", CSRC, "-I",
+    return [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-fPIC", "-Wall", "-Wno-unknown-pragmas", "-I", HOST_INC,
+            "-I", CSRC, "-I",
             os.path.join(ROOT, "include"), "-c", HOST_SRC, "-o", obj]
 
 
