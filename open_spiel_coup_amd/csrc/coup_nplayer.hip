@@ -230,11 +230,7 @@ __device__ __forceinline__ uint32_t ending_action(const NLane<N>& L) {
 // draw 2N: at most 4 blocks), and the group shares them by cross-lane
 // shuffles, so a reset waits for one Philox instead of up to four in a row.
 // RG = 1 (COUP_NP_RESET_GROUP=1, A/B): one thread deals a reset alone.
-// EARLY: a thread whose lane does not auto-reset this step stores it right
-// after the rules barrier, while the reset phase runs, instead of after the
-// reset barrier (COUP_NP_EARLY_STORE; the reset lanes' owners still store
-// after it).
-template <int N, bool UNIFORM, bool AHEAD, int T = kThreads, bool INLINE = false, int RG = 4, bool EARLY = false>
+template <int N, bool UNIFORM, bool AHEAD, int T = kThreads, bool INLINE = false, int RG = 4>
 #ifdef COUP_WAVE_TRACE
 // the stamps' registers must not cost the traced kernel its 8 blocks per CU
 #define NP_STEP_SORTED_BOUNDS __launch_bounds__(T, 8)
@@ -375,21 +371,6 @@ __global__ NP_STEP_SORTED_BOUNDS void k_step_sorted(StepArgs a) {
   __syncthreads();
   NP_TRACE(a, 5);
 
-  // EARLY: every slot but the resets' is final here (the reset phase writes
-  // only the slots in s_reset, all of step type LAST under auto-reset)
-  bool stored = false;
-  if (EARLY && live) {
-    const uint32_t o = s_out[pos];
-    if (!((((o >> 5) & 3u) == 2u) && a.auto_reset != 0)) {
-      a.sa[i] = s_a[pos];
-      a.sb[i] = s_b[pos];
-      store_step_outputs<N>(a, i, (int)(o & 31u) - 1, (o >> 5) & 3u, (o >> 7) & 7u, (o >> 10) & 7u, s_legal[pos],
-                            (int)(int8_t)(o >> 24));
-      store_episode(a, i, eps, (o >> 5) & 3u, (int32_t)((o >> 14) & 31u) - 16);
-      stored = true;
-    }
-  }
-
   // the auto-resets, packed onto the first threads
   const uint32_t nreset = INLINE ? 0u : s_nreset;
   if (RG == 4) {
@@ -443,7 +424,7 @@ __global__ NP_STEP_SORTED_BOUNDS void k_step_sorted(StepArgs a) {
   NP_TRACE(a, 7);
 
   // phase 3: each thread stores its own lane
-  if (!live || stored) return;
+  if (!live) return;
   a.sa[i] = s_a[pos];
   a.sb[i] = s_b[pos];
   const uint32_t o = s_out[pos];
@@ -1066,16 +1047,12 @@ hipError_t launch_step(const Env& e, const int8_t* actions, const coup_step_outp
         const bool inl = ri ? std::atoi(ri) != 0 : false;
         const char* rg = std::getenv("COUP_NP_RESET_GROUP");  // 1: one thread per reset (A/B)
         const bool single = rg ? std::atoi(rg) == 1 : false;
-        const char* es = std::getenv("COUP_NP_EARLY_STORE");  // 1: non-reset lanes stored before the reset phase
-        const bool early = es ? std::atoi(es) == 1 : false;
         if (actions)
           k_step_sorted<N, false, false, TB><<<g, TB, 0, e.stream>>>(a);
         else if (ahead && inl)
           k_step_sorted<N, true, true, TB, true><<<g, TB, 0, e.stream>>>(a);
         else if (ahead && single)
           k_step_sorted<N, true, true, TB, false, 1><<<g, TB, 0, e.stream>>>(a);
-        else if (ahead && early)
-          k_step_sorted<N, true, true, TB, false, 4, true><<<g, TB, 0, e.stream>>>(a);
         else if (ahead)
           k_step_sorted<N, true, true, TB><<<g, TB, 0, e.stream>>>(a);
         else

@@ -302,32 +302,28 @@ def test_regrouped_step_reset_schedule_invariant(monkeypatch, n_players, lanes):
     threads sharing the Philox blocks (the default), or by one thread
     (COUP_NP_RESET_GROUP=1); and resets dealt where the game ends
     (COUP_NP_RESET_INLINE=1, decisions that end a game drawn ahead as
-    kKeyEnding); and the phase form storing its non-reset lanes before the
-    reset phase (COUP_NP_EARLY_STORE=1).  So does an env alternating the
-    kernels, where a decision parked by one is played by another.  Outputs,
-    records, accumulators."""
+    kKeyEnding).  So does an env alternating the kernels, where a decision
+    parked by one is played by another.  Outputs, records, accumulators."""
     n, steps, seed = 3000, 200, 40 + n_players
     monkeypatch.setenv("COUP_REGROUP", "1")
     monkeypatch.setenv("COUP_NP_SORT_THREADS", lanes)
-    forms = {"phase": ("0", "4", "0"), "single": ("0", "1", "0"), "inline": ("1", "4", "0"),
-             "early": ("0", "4", "1")}
+    forms = {"phase": ("0", "4"), "single": ("0", "1"), "inline": ("1", "4")}
     envs = {knob: BatchedCoupEnv(n, seed=seed, env_id_base=9 << 20, auto_reset=True, obs=False,
                                  num_players=n_players, generic=True, episode_stats=True)
-            for knob in ("phase", "single", "inline", "early", "alt")}
-    cycle = ("phase", "inline", "single", "early")
+            for knob in ("phase", "single", "inline", "alt")}
+    cycle = ("phase", "inline", "single")
     for t in range(steps):
         outs = {}
         for knob, env in envs.items():
-            inline, group, early = forms[knob if knob != "alt" else cycle[t % 4]]
+            inline, group = forms[knob if knob != "alt" else cycle[t % 3]]
             monkeypatch.setenv("COUP_NP_RESET_INLINE", inline)
             monkeypatch.setenv("COUP_NP_RESET_GROUP", group)
-            monkeypatch.setenv("COUP_NP_EARLY_STORE", early)
             outs[knob] = {k: v.clone() for k, v in env.step().items()}
-        for knob in ("single", "inline", "early", "alt"):
+        for knob in ("single", "inline", "alt"):
             for k in ("actions", "rewards", "step_type", "legal_mask", "current_player"):
                 assert torch.equal(outs["phase"][k], outs[knob][k]), (knob, t, k)
             assert torch.equal(envs["phase"].export_state(), envs[knob].export_state()), (knob, t)
-    for knob in ("single", "inline", "early", "alt"):
+    for knob in ("single", "inline", "alt"):
         for x, y in zip(envs["phase"].episode_stats(), envs[knob].episode_stats()):
             assert torch.equal(x, y), knob
     assert int(envs["phase"].episode_stats()[0].sum()) > 100

@@ -27,7 +27,7 @@ sys.path.insert(0, ROOT)
 
 KNOBS = ("COUP_OBS_MODE", "COUP_XCD_REMAP", "COUP_STEP_DYN_LDS", "COUP_REGROUP", "COUP_AHEAD", "COUP_EP_MODE",
          "COUP_NP_SORT_THREADS", "COUP_SORT_THREADS", "COUP_NP_RESET_INLINE", "COUP_TRAJ_STAGE",
-         "COUP_NP_RESET_GROUP", "COUP_STEP_TPL", "COUP_NP_EARLY_STORE")
+         "COUP_NP_RESET_GROUP", "COUP_STEP_TPL")
 
 
 def main():
