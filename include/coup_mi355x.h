@@ -322,6 +322,14 @@ int coup_host_state_apply(const coup_slot_result* in, int action, int flags, cou
 /* ObservationTensor [2][98] and / or InformationStateTensor [2][2492] of
  * both players (either pointer may be NULL; coup.cc:1044-1056). */
 int coup_host_state_tensors(const coup_slot_result* st, float* obs, float* info);
+/* rl_environment's lane ops on a host state (coup_slot_op's COUP_SLOT_RESET /
+ * COUP_SLOT_DEAL semantics): mode COUP_SLOT_INIT starts from the lane
+ * coup_create leaves (in may be NULL), COUP_SLOT_RESET the next episode,
+ * then `action` (< 0: none; COUP_SLOT_UNCHECKED as pyspiel's apply_action),
+ * then COUP_SLOT_DEAL the pending chance deals under the sampling contract of
+ * stream (seed, env_id) -- the draws the env's device lane would use. */
+int coup_host_state_step(const coup_slot_result* in, int action, int mode, uint64_t seed, uint32_t env_id,
+                         coup_slot_result* out);
 /* ObservationString(player) (kind 0), InformationStateString(player) (1) --
  * CoupObserver::StringFrom, coup.cc:290-373 -- or ToString() (2, coup.cc:
  * 945-987) of st into buf (cap bytes, NUL-terminated when it fits).  Returns

@@ -28,6 +28,7 @@ SYMBOLS = (
     "coup_import_history", "coup_error_count", "coup_slot_op", "coup_slot_ops", "coup_measure_step_traffic",
     "coup_server_create", "coup_server_destroy", "coup_attach_server", "coup_server_stats",
     "coup_host_state_init", "coup_host_state_apply", "coup_host_state_tensors", "coup_host_state_string",
+    "coup_host_state_step",
     "coup_write_lane",
 )
 
@@ -118,6 +119,7 @@ def load():
         "coup_host_state_apply": ([ctypes.c_char_p, i32, i32, vp], i32),
         "coup_host_state_tensors": ([ctypes.c_char_p, vp, vp], i32),
         "coup_host_state_string": ([ctypes.c_char_p, i32, i32, vp, i64], i64),
+        "coup_host_state_step": ([ctypes.c_char_p, i32, i32, ctypes.c_uint64, ctypes.c_uint32, vp], i32),
         "coup_write_lane": ([vp, i64, ctypes.c_char_p], i32),
     }
     for name, (args, res) in sig.items():

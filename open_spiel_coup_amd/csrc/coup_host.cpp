@@ -104,6 +104,79 @@ int coup_host_state_apply(const coup_slot_result* in, int action, int flags, cou
   return COUP_OK;
 }
 
+// rl_environment's ops on a host state (the device's COUP_SLOT_RESET /
+// COUP_SLOT_DEAL lane ops, slot_step in coup_kernels.hip, on the host):
+//   mode COUP_SLOT_INIT  -- start from the lane coup_create leaves (episode 0,
+//                           NewInitialState, empty history; `in` may be null)
+//   mode COUP_SLOT_RESET -- the lane's next episode (episode + 1, NewInitialState)
+//   action >= 0          -- State::ApplyAction (COUP_SLOT_UNCHECKED: as pyspiel's)
+//   mode COUP_SLOT_DEAL  -- then the pending chance deals under the sampling
+//                           contract of stream (seed, env_id),
+//                           as rl_environment samples chance (rl_environment.py:369-382)
+// every entry to the history bytes.  A rejected action leaves `in` as it was
+// (the reset included) with ok = 0.  Same draws as the device, so the same
+// games as the env's device lane would play.
+int coup_host_state_step(const coup_slot_result* in, int action, int mode, uint64_t seed, uint32_t env_id,
+                         coup_slot_result* out) {
+  if (!out || (!in && !(mode & COUP_SLOT_INIT))) return COUP_E_INVALID;
+  if (action >= COUP_NUM_ACTIONS) return COUP_E_INVALID;
+  uint8_t hist[kHistoryBytes];
+  Lane L;
+  if (mode & COUP_SLOT_INIT) {
+    std::memset(hist, 0xFF, sizeof(hist));
+    L = initial_lane(0u);
+  } else {
+    std::memcpy(hist, in->history, sizeof(hist));
+    L = unpack(record_of(in));
+  }
+  struct Bytes {
+    uint8_t* b;
+    void record(uint32_t idx, uint32_t entry) {
+      if (idx < kHistoryBytes) b[idx] = (uint8_t)entry;
+    }
+  } rec{hist};
+  if (mode & COUP_SLOT_RESET) {
+    L = initial_lane(L.episode + 1u);
+    L.err = L.episode == 0u ? 1u : 0u;  // the episode counter wrapped (coup_lane.h kEpisodeMask)
+  }
+  if (action >= 0) {
+    const uint32_t x = (uint32_t)action;
+    const uint32_t idx = L.move;
+    const uint32_t entry = is_chance(L) ? hist_deal(x, L.qids & 1u) : hist_decision(x, L.M);
+    NoHistory none;
+    Lane R = L;
+    bool ok;
+    uint32_t unrep = 0u;
+    if (mode & COUP_SLOT_UNCHECKED) {
+      ok = apply_action_unchecked(R, x, none);
+      if (!ok && !is_terminal(L) && !L.err && !is_chance(L)) {
+        Lane T = L;
+        unrep = (ref_decision(T, x) && !representable(T)) ? 1u : 0u;
+      }
+    } else {
+      const uint32_t err_before = R.err;
+      ok = apply_action(R, x, none) && !(R.err && !err_before);
+    }
+    if (!ok) {
+      if (in) {
+        fill_result(unpack(record_of(in)), in->history, 0u, unrep, out);
+      } else {
+        std::memset(hist, 0xFF, sizeof(hist));
+        fill_result(initial_lane(0u), hist, 0u, unrep, out);
+      }
+      return COUP_OK;
+    }
+    L = R;
+    rec.record(idx, entry);
+  }
+  if (mode & COUP_SLOT_DEAL) {
+    Rng rng{(uint32_t)seed, (uint32_t)(seed >> 32), env_id, 0u, make_uint4(0, 0, 0, 0)};
+    resolve_chance(L, rng, rec);
+  }
+  fill_result(L, hist, 1u, 0u, out);
+  return COUP_OK;
+}
+
 // ObservationTensor(p) of both players ([2][98], obs) and / or
 // InformationStateTensor(p) of both players ([2][2492], info) of host state
 // st; either pointer may be null.

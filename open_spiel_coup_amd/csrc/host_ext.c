@@ -10,6 +10,8 @@
  *   init()                          -> (raw, legal_mask, cur_player, terminal, ok, unrepresentable),
  *                                      or after bind a result_type with those keys and ._raw
  *   apply(raw, action, flags)       -> the same for the state after State::ApplyAction
+ *   step(raw, action, mode, seed, env_id) -> the same for rl_environment's reset / step (raw may be None
+ *                                      with mode COUP_SLOT_INIT)
  *   string(raw, kind, player)       -> str (0 ObservationString, 1 InformationStateString, 2 ToString)
  *   tensors(raw, obs_addr, info_addr) -> None (float32 [2][98] / [2][2492] at the addresses, 0 = skip)
  *   float_lists(addr, rows, cols)   -> rows lists of floats (the time steps' tensors)
@@ -110,6 +112,26 @@ static PyObject* py_apply(PyObject* self, PyObject* const* args, Py_ssize_t n) {
   coup_slot_result r;
   if (action < 0 || action >= COUP_NUM_ACTIONS || coup_host_state_apply(st, (int)action, (int)flags, &r) != COUP_OK) {
     PyErr_Format(PyExc_ValueError, "coup_host_state_apply: invalid action %ld", action);
+    return NULL;
+  }
+  return result_tuple(&r);
+}
+
+static PyObject* py_step(PyObject* self, PyObject* const* args, Py_ssize_t n) {
+  (void)self;
+  if (n != 5) {
+    PyErr_SetString(PyExc_TypeError, "step(raw_or_None, action, mode, seed, env_id)");
+    return NULL;
+  }
+  const coup_slot_result* st = NULL;
+  if (args[0] != Py_None && !as_state(args[0], &st)) return NULL;
+  const long action = PyLong_AsLong(args[1]), mode = PyLong_AsLong(args[2]);
+  const unsigned long long seed = PyLong_AsUnsignedLongLongMask(args[3]);
+  const unsigned long env_id = PyLong_AsUnsignedLong(args[4]);
+  if (PyErr_Occurred()) return NULL;
+  coup_slot_result r;
+  if (coup_host_state_step(st, (int)action, (int)mode, (uint64_t)seed, (uint32_t)env_id, &r) != COUP_OK) {
+    PyErr_Format(PyExc_ValueError, "coup_host_state_step: action %ld mode %ld", action, mode);
     return NULL;
   }
   return result_tuple(&r);
@@ -223,6 +245,7 @@ static PyMethodDef kMethods[] = {
     {"float_lists", (PyCFunction)(void (*)(void))py_float_lists, METH_FASTCALL, "float32 rows as lists of floats"},
     {"bind", py_bind, METH_O, "the result class init / apply return"},
     {"init", py_init, METH_NOARGS, "NewInitialState as a host state tuple"},
+    {"step", (PyCFunction)(void (*)(void))py_step, METH_FASTCALL, "rl_environment's reset / step on a host state"},
     {"apply", (PyCFunction)(void (*)(void))py_apply, METH_FASTCALL, "State::ApplyAction on a host state"},
     {"string", (PyCFunction)(void (*)(void))py_string, METH_FASTCALL, "Observation / InformationState / ToString"},
     {"tensors", (PyCFunction)(void (*)(void))py_tensors, METH_FASTCALL, "both players' tensors into buffers"},

@@ -402,6 +402,7 @@ class _Host:
         _coup_host.bind(_Result)  # init / apply return _Result objects, built in C
         self._ext = _coup_host
         self.apply = _coup_host.apply  # (raw, action, flags) -> _Result
+        self.step = _coup_host.step    # (raw or None, action, mode, seed, env_id) -> _Result
 
     def init(self):
         return self._ext.init()
@@ -599,6 +600,22 @@ class CoupState:
                 self._pool.release(self._slot)
         except Exception:
             pass
+
+    @classmethod
+    def _from_host(cls, game, q, history):
+        """Snapshot of a host-resident game (rl_environment.get_state): a host
+        State, or -- for a game whose States live on device lanes -- the
+        record and history written into a new pool lane."""
+        q = q.copy()
+        for k in ("obs", "info_state"):
+            q.pop(k, None)
+        if not game._device_states:
+            return cls(game, _history=history, _host_q=q)
+        pool = game._pool if game._pool is not None else game._bind_pool()
+        slot = pool.alloc()
+        with pool.lock:
+            _native.check(pool.lib.coup_write_lane(pool.handle(slot), slot[1], q._raw))
+        return cls(game, _slot=slot, _q=q, _history=history)
 
     @classmethod
     def _from_env(cls, game, env_handle, lane, history):

@@ -157,6 +157,20 @@ class Environment:
 
     # ------------------------------------------------------------ plumbing
     def _make_env(self):
+        self._hq = None
+        if self._sampler is None and not pyspiel.DEVICE_STATES:
+            # host-resident (round 4): the env's game is a host state, and
+            # reset / step are the library's host build of the device lane
+            # ops (coup_host_state_step: same rules, same Philox deals of
+            # stream (seed, env id 0)), ~1 us instead of a device round trip;
+            # a SyncVectorEnv that adopts the env moves the game to a lane
+            self._env, self._lane, self._owner, self._last = None, 0, None, None
+            # the game's chance stream: (seed, global env id), a 1-lane env's
+            # lane 0 under its own seed until a SyncVectorEnv re-keys it
+            self._hseed, self._env_id = self._seed, 0
+            self._pool = pyspiel._pool(self._device)  # the HIP device is required all the same
+            self._hq = self._host_step(None, -1, _native.SLOT_INIT | _native.SLOT_DEAL)
+            return
         # one lane of a 2-player history env, attached to the device's op
         # server (pyspiel's lane pool): reset and step are one coup_slot_op
         # each (COUP_SLOT_RESET / COUP_SLOT_DEAL) whose 128-byte result and
@@ -178,6 +192,64 @@ class Environment:
         """Play on lane `lane` of `env` (a SyncVectorEnv's shared env, which
         already holds this game's record and history) from now on."""
         self._env, self._lane, self._owner = env, int(lane), owner
+        self._hq = None
+
+    def _host_step(self, raw, action, mode):
+        """coup_host_state_step on the env's host state; with the time
+        step's tensor when the op succeeds."""
+        q = pyspiel._host().step(raw, action, mode, self._hseed, self._env_id)
+        return self._with_tensor(q) if q["ok"] else q
+
+    def _with_tensor(self, q):
+        """q (a host result) with the time step's tensor of both players."""
+        o, i = pyspiel._host().tensors(q._raw, self._use_observation, not self._use_observation)
+        q["obs" if self._use_observation else "info_state"] = o if self._use_observation else i
+        return q
+
+    def _op(self, action, flags):
+        """reset / step / query (action -1, flags 0) of the env's game: on
+        its host state, or as one lane op on its device lane."""
+        if self._hq is not None:
+            if action < 0 and not flags:
+                return self._hq
+            q = self._host_step(self._hq._raw, action, flags)
+            if q["ok"]:
+                self._hq = q
+            return q
+        return self._lane_op(action, flags)
+
+    def _key_stream(self, env_id):
+        """Key this env's chance stream as global env id `env_id` under its
+        seed and start over (tests: an env stepped alone that deals what lane
+        `env_id` of a vector env deals)."""
+        if self._hq is not None:
+            self._hseed, self._env_id = self._seed, int(env_id)
+            self._hq = self._host_step(None, -1, _native.SLOT_INIT | _native.SLOT_DEAL)
+        else:
+            self._env = BatchedCoupEnv(1, seed=self._seed, env_id_base=int(env_id), auto_reset=False, obs=False,
+                                       info_state=False, history=True, device=self._device, unchecked=True)
+            self._pool.attach(self._env)
+            self._lane, self._owner = 0, None
+        self._should_reset, self._last = True, None
+
+    def _host_rekey(self, seed, env_id, owner):
+        """A SyncVectorEnv keeping this host-resident game on the host: its
+        later deals are global env id `env_id`'s under `seed` (what lane
+        `env_id` of an adopting vector env would deal); the game itself is
+        kept."""
+        self._hseed, self._env_id, self._owner = seed, int(env_id), owner
+
+    def _export_lane(self):
+        """The game's record [1, 4] int32 and history [1, 96] uint8, on the
+        device (SyncVectorEnv adoption)."""
+        if self._hq is not None:
+            raw = self._hq._raw
+            dev = torch.device(self._device) if self._device is not None else torch.device("cuda")
+            rec = torch.frombuffer(bytearray(raw[:16]), dtype=torch.int32).view(1, 4).to(dev)
+            hist = torch.frombuffer(bytearray(raw[16:16 + HISTORY_BYTES]), dtype=torch.uint8).view(1, HISTORY_BYTES)
+            return rec, hist.to(dev)
+        j = self._lane
+        return self._env.export_state()[j:j + 1], self._env.export_history()[j:j + 1]
 
     def _lane_op(self, action, flags):
         """reset / step of this env's lane as one coup_slot_op, with the time
@@ -213,6 +285,10 @@ class Environment:
         return m
 
     def _state_view(self):
+        if self._hq is not None:
+            raw = self._hq._raw
+            return (np.frombuffer(raw, np.uint32, 4, 0).copy(),
+                    np.frombuffer(raw, np.uint8, HISTORY_BYTES, 16).copy())
         j = self._lane
         words = self._env.export_state()[j].cpu().numpy().view(np.uint32).reshape(4).copy()
         hist = self._env.export_history()[j].cpu().numpy().reshape(HISTORY_BYTES).copy()
@@ -284,7 +360,7 @@ class Environment:
     def get_time_step(self):
         # an answered query op on the lane (no action): one round trip to the
         # op server instead of a query launch
-        q = self._query() if self._sampler is not None else self._lane_op(-1, 0)
+        q = self._query() if self._sampler is not None else self._op(-1, 0)
         step_type = StepType.LAST if int(q["terminal"]) else StepType.MID
         self._should_reset = step_type == StepType.LAST
         return self._time_step(q, step_type, [float(x) for x in q["rewards"]])
@@ -309,7 +385,7 @@ class Environment:
             # the decision, then the chance deals that follow under the
             # sampling contract, and the time step's answers: one op on the
             # lane (the op server's wave when the pool has one)
-            q = self._lane_op(int(actions[0]), _native.SLOT_DEAL | _native.SLOT_UNCHECKED)
+            q = self._op(int(actions[0]), _native.SLOT_DEAL | _native.SLOT_UNCHECKED)
             if not q["ok"]:
                 # DoApplyAction raised in the reference (coup.cc:490-809), or the
                 # result leaves the packed record (a known gap); the lane is unchanged
@@ -326,7 +402,7 @@ class Environment:
     def reset(self):
         self._should_reset = False
         if self._sampler is None:
-            q = self._lane_op(-1, _native.SLOT_RESET | _native.SLOT_DEAL)
+            q = self._op(-1, _native.SLOT_RESET | _native.SLOT_DEAL)
         else:
             self._env.new_initial_state()
             q = self._sample_external_events()
@@ -371,7 +447,7 @@ class Environment:
 
     @property
     def is_chance_node(self):
-        q = self._query() if self._sampler is not None else self._lane_op(-1, 0)
+        q = self._query() if self._sampler is not None else self._op(-1, 0)
         return int(q["current_player"]) == pyspiel.PlayerId.CHANCE
 
     @property
@@ -382,10 +458,19 @@ class Environment:
     def get_state(self):
         """A pyspiel-shaped CoupState snapshot of the env's lane."""
         words, hist = self._state_view()
+        if self._hq is not None:
+            return pyspiel.CoupState._from_host(self._game, self._hq, self._history_list(words, hist))
         return pyspiel.CoupState._from_env(self._game, self._env._h, self._lane, self._history_list(words, hist))
 
     def set_state(self, new_state):
         assert new_state.get_game() == self.game, "State must have been created by the same game."
+        if self._hq is not None:
+            q = new_state._q.copy()  # the state's record and history (its last answer)
+            for k in ("obs", "info_state"):
+                q.pop(k, None)
+            self._hq = self._with_tensor(q)
+            self._last = None
+            return
         self._env._bind_stream()
         new_state._copy_to_env(self._env._h, self._lane)
         self._last = None  # the cached legal actions no longer describe the lane

@@ -22,6 +22,14 @@ A vector env of at most LANE_OPS_UPTO envs steps them one lane op each
 lane ops' round trips cost less than a launch and a synchronisation.  Both
 forms give the same games (tests/test_gpu_vector_env.py).
 
+Host-resident envs (round 4: an Environment's game is a host state by
+default) are not moved to the device when there are at most HOST_UPTO of
+them: the vector env keeps them on the host and re-keys their chance streams
+as adoption would (env i: global env id i under the first env's seed), so
+the games, deals and time steps are those of the adopted form; each step is
+then the host build of the lane rules per env (~1 us) and the time step's
+lists, which a launch cannot make cheaper.
+
 Envs with a caller-supplied chance sampler (the State API path), envs of
 different games / observation types / devices, or envs already adopted by
 another vector env are stepped in the reference's loop instead.
@@ -30,7 +38,9 @@ Errors: an action outside 0..127 raises SpielError before anything is
 applied.  Actions outside LegalActions() are applied as Environment.step
 applies them (pyspiel's unchecked apply_action); one the reference's
 DoApplyAction would raise on is rejected by its lane (the other envs' actions
-are applied) and raises SpielError after the launch.
+are applied) and raises SpielError after the launch; with the games kept on
+the host, as in the reference's loop, the envs before it are applied and the
+ones after it are not.
 """
 import numpy as np
 import torch
@@ -40,6 +50,7 @@ from .env import BatchedCoupEnv
 
 
 LANE_OPS_UPTO = 2
+HOST_UPTO = 64  # host-resident envs stay on the host up to this many (None: any number, 0: never)
 
 
 class SyncVectorEnv:
@@ -49,8 +60,13 @@ class SyncVectorEnv:
             raise ValueError("Need to call this with a list of rl_environment.Environment objects")
         self.envs = envs
         self._shared = None
+        self._host = False  # host-resident games kept on the host (see the module doc)
         if batched and self._can_batch():
-            self._adopt(self.envs[0]._seed)
+            if all(e._hq is not None for e in envs) and (HOST_UPTO is None or len(envs) <= HOST_UPTO):
+                self._host = True
+                self._rekey_host(self.envs[0]._seed)
+            else:
+                self._adopt(self.envs[0]._seed)
 
     def __len__(self):
         return len(self.envs)
@@ -64,8 +80,9 @@ class SyncVectorEnv:
 
     @property
     def batched(self):
-        """True when one shared env steps every game (see the module doc)."""
-        return self._shared is not None
+        """True when one shared env steps every game, or the host-resident
+        games are stepped on the host under the shared stream (module doc)."""
+        return self._shared is not None or self._host
 
     # ------------------------------------------------------------ adoption
     def _can_batch(self):
@@ -85,8 +102,9 @@ class SyncVectorEnv:
         `seed` (records, histories and each env's pending-reset flag carry
         over), and bind the envs to their lanes."""
         envs = self.envs
-        records = torch.cat([e._env.export_state()[e._lane:e._lane + 1] for e in envs])
-        hist = torch.cat([e._env.export_history()[e._lane:e._lane + 1] for e in envs])
+        lanes = [e._export_lane() for e in envs]  # host-resident games and device lanes alike
+        records = torch.cat([r for r, _ in lanes])
+        hist = torch.cat([h for _, h in lanes])
         shared = BatchedCoupEnv(len(envs), seed=seed, auto_reset=False, obs=False, info_state=False, history=True,
                                 device=envs[0]._device, unchecked=True)  # as each env's own (rl_environment.py)
         shared.import_state(records)
@@ -96,9 +114,16 @@ class SyncVectorEnv:
         for i, e in enumerate(envs):
             e._bind_lane(shared, i, self)
 
+    def _rekey_host(self, seed):
+        for i, e in enumerate(self.envs):
+            e._host_rekey(seed, i, self)
+
     def _rekey(self, seed):
         """Environment.seed() of an adopted env: the shared stream takes the
         new seed, every lane keeps its game."""
+        if self._host:
+            self._rekey_host(seed)
+            return
         for e in self.envs:
             e._owner = None
         self._adopt(seed)
@@ -176,7 +201,8 @@ class SyncVectorEnv:
     # ------------------------------------------------------------ public API
     def step(self, step_outputs, reset_if_done=False):
         """vector_env.py:40-67: returns (time_steps, reward, done, unreset_time_steps)."""
-        if self._shared is None or len(self.envs) <= LANE_OPS_UPTO:
+        one_by_one = self._shared is None or len(self.envs) <= LANE_OPS_UPTO
+        if one_by_one:
             time_steps = [self.envs[i].step([step_outputs[i].action]) for i in range(len(self.envs))]
         else:
             time_steps = self._step_batched(step_outputs)
@@ -184,10 +210,10 @@ class SyncVectorEnv:
         done = [step.last() for step in time_steps]
         unreset_time_steps = time_steps
         if reset_if_done:
-            if self._shared is None:
+            if self._shared is None and not self._host:
                 time_steps = self.reset(envs_to_reset=done)
-            elif len(self.envs) <= LANE_OPS_UPTO:
-                # lane ops: an env that goes on keeps its time step, unless
+            elif one_by_one:
+                # lane ops or host games: an env that goes on keeps its time step, unless
                 # that was a FIRST, which get_time_step reports as MID (as the
                 # reference's reset(envs_to_reset) does)
                 time_steps = [e.reset() if d else (e.get_time_step() if t.first() else t)

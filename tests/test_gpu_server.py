@@ -299,7 +299,7 @@ def test_no_wave_outlives_its_process():
 
 
 @pytest.mark.parametrize("otype", ["info", "obs"])
-def test_environment_lane_ops_equal_batched_steps(otype):
+def test_environment_lane_ops_equal_batched_steps(otype, monkeypatch):
     """rl_environment.Environment's reset and step are single lane ops
     (COUP_SLOT_RESET | COUP_SLOT_DEAL, COUP_SLOT_DEAL; through the op
     server): they deal exactly what coup_reset / coup_step deal on the same
@@ -310,6 +310,7 @@ def test_environment_lane_ops_equal_batched_steps(otype):
     from open_spiel_coup_amd import BatchedCoupEnv
     obs_type = (rl_environment.ObservationType.OBSERVATION if otype == "obs"
                 else rl_environment.ObservationType.INFORMATION_STATE)
+    monkeypatch.setattr(pyspiel, "DEVICE_STATES", True)  # the env's game on a device lane (lane ops)
     env = rl_environment.Environment("coup", seed=123, observation_type=obs_type)
     twin = BatchedCoupEnv(1, seed=123, auto_reset=False, obs=False, history=True)
     assert env._pool.srv is not None

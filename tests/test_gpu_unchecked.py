@@ -243,8 +243,7 @@ def test_sync_vector_env_unchecked_equals_loop():
     # env id i under `seed`), as tests/test_gpu_vector_env.py's _loop_envs
     loop_envs = [rl_environment.Environment("coup", seed=seed) for _ in range(n)]
     for i, e in enumerate(loop_envs):
-        e._env = BatchedCoupEnv(1, seed=seed, env_id_base=i, auto_reset=False, obs=False, history=True,
-                                unchecked=True)
+        e._key_stream(i)
     venv = vector_env.SyncVectorEnv(vec_envs)
     ts_loop = [e.reset() for e in loop_envs]
     ts_vec = venv.reset()

@@ -6,7 +6,9 @@ import torch
 
 from oracle import oracle
 
-pytestmark = pytest.mark.gpu
+# state_mode: host-resident envs (kept on the host by the vector env) and
+# device-lane envs (adopted into one shared env) -- conftest.py
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("state_mode")]
 
 from open_spiel_coup_amd import BatchedCoupEnv, pyspiel, rl_environment, vector_env  # noqa: E402
 
@@ -75,7 +77,7 @@ def _loop_envs(n, seed, obs_type):
     batched SyncVectorEnv (global env id i under `seed`)."""
     envs = [rl_environment.Environment("coup", seed=seed, observation_type=obs_type) for _ in range(n)]
     for i, e in enumerate(envs):
-        e._env = BatchedCoupEnv(1, seed=seed, env_id_base=i, auto_reset=False, obs=False, history=True)
+        e._key_stream(i)
     return envs
 
 
@@ -126,12 +128,14 @@ def test_batched_sync_vector_env_equals_loop(obs_type, n):
     assert lasts > 2 * n  # episodes end (~15 decisions each) and restart
 
 
-def test_adopted_envs_keep_their_games():
+@pytest.mark.parametrize("host_upto", [None, 0], ids=["kept", "adopted"])
+def test_adopted_envs_keep_their_games(host_upto, monkeypatch):
     """After adoption each Environment still plays its own lane: get_state
     replays through the oracle to the last time step; a single env's step,
     set_state and seed act on that lane only; an action DoApplyAction
     raises on (the reference's apply_action has no legality check) raises
     SpielError after the other envs' actions were applied."""
+    monkeypatch.setattr(vector_env, "HOST_UPTO", host_upto)  # 0: host-resident games move to lanes too
     n = 6
     envs = [rl_environment.Environment("coup", seed=100 + i) for i in range(n)]
     envs[2].reset()

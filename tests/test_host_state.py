@@ -173,3 +173,35 @@ def test_host_strings_match_oracle_and_python_forms():
     assert seen > 500
     assert lib.coup_host_state_string(raw, 3, 0, None, 0) == -1
     assert lib.coup_host_state_string(raw, 0, 2, None, 0) == -1
+
+
+def test_host_env_steps_replay_the_oracle_rollout():
+    """coup_host_state_step (rl_environment's reset / step on a host state,
+    the device lane ops' COUP_SLOT_RESET / COUP_SLOT_DEAL): driven with the
+    oracle rollout's own decisions, lanes of several env ids, no auto-reset
+    (LAST, then the next step starts the next episode), the host lanes deal
+    the same cards -- every record equal to the oracle's at the end, and
+    every step type, reward and legal mask on the way."""
+    import ctypes as C
+    lib = _lib()
+    seed, K = 0x1234_5678_9ABC_DEF0, 400
+    out = C.create_string_buffer(RESULT)
+    for env_id in (0, 1, 77, 4096):
+        ref = oracle.rollout(seed=seed, n=1, steps=K, env_id_base=env_id, auto_reset=False)
+        assert lib.coup_host_state_step(None, -1, _native.SLOT_INIT | _native.SLOT_DEAL, seed, env_id, out) == 0
+        raw = out.raw
+        for t in range(K):
+            st = int(ref["step_type"][t][0])
+            if st == 0:  # FIRST: the step after LAST started the next episode
+                mode, a = _native.SLOT_RESET | _native.SLOT_DEAL, -1
+            else:
+                mode, a = _native.SLOT_DEAL | _native.SLOT_UNCHECKED, int(ref["actions"][t][0])
+            assert lib.coup_host_state_step(raw, a, mode, seed, env_id, out) == 0
+            raw = out.raw
+            assert raw[118] == 1, (env_id, t)
+            rec, hist, lm, cp, term, _, _, rew, ret = _fields(raw)
+            assert (2 if term else (0 if st == 0 else 1)) == st, (env_id, t)
+            assert rew[0] == ref["rewards"][t][0][0], (env_id, t)
+            assert (lm & 0xFFFFFFFF) == int(ref["legal"][t][0]), (env_id, t)
+        rec = np.frombuffer(raw, np.uint32, 4, 0)
+        assert rec.tolist() == ref["final_state"][0].tolist(), env_id

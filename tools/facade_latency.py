@@ -156,38 +156,53 @@ def batched_rows(tag, game, n):
 
 
 def rl_rows(n):
-    from open_spiel_coup_amd import rl_environment
+    from open_spiel_coup_amd import pyspiel, rl_environment
     rows = {}
     rng = random.Random(0)  # the caller's pick: ~0.5 us (numpy's choice over a list is ~10x that)
     for otype, tag in ((rl_environment.ObservationType.INFORMATION_STATE, "info"),
                        (rl_environment.ObservationType.OBSERVATION, "obs")):
-        env = rl_environment.Environment("coup", seed=3, observation_type=otype)
-        ts = [env.reset()]
+        for suffix, device in (("", False), ("_device_lane", True)):
+            # default: the host-resident game (round 4); _device_lane: the
+            # game on a device lane (COUP_STATE_DEVICE=1), a round trip per op
+            saved, pyspiel.DEVICE_STATES = pyspiel.DEVICE_STATES, device
+            try:
+                env = rl_environment.Environment("coup", seed=3, observation_type=otype)
+            finally:
+                pyspiel.DEVICE_STATES = saved
+            ts = [env.reset()]
 
-        def step():
-            t = ts[0]
-            p = t.observations["current_player"]
-            ts[0] = env.step([rng.choice(t.observations["legal_actions"][p])]) if not t.last() else env.reset()
-        rows[f"rl_environment_step_{tag}_us"] = _timed(step, n)
-        e1 = env._env
-        rows[f"query_host_{tag}_us"] = _timed(lambda: e1.query_host(obs=tag == "obs", info_state=tag == "info"), n)
+            def step():
+                t = ts[0]
+                p = t.observations["current_player"]
+                ts[0] = env.step([rng.choice(t.observations["legal_actions"][p])]) if not t.last() else env.reset()
+            rows[f"rl_environment_step_{tag}{suffix}_us"] = _timed(step, n)
+            if device:
+                e1 = env._env
+                rows[f"query_host_{tag}_us"] = _timed(
+                    lambda: e1.query_host(obs=tag == "obs", info_state=tag == "info"), n)
     return rows
 
 
 def vector_env_rows(steps=40):
-    """SyncVectorEnv.step(reset_if_done=True) per env step: one shared env
-    (batched) against the reference's loop over the envs."""
+    """SyncVectorEnv.step(reset_if_done=True) per env step: the default
+    (host-resident games kept on the host under the shared stream), the games
+    adopted into one shared device env (vector_env.HOST_UPTO = 0: one launch
+    per step), and the reference's loop over the envs (batched=False)."""
     from open_spiel_coup_amd import rl_environment, vector_env
     rows = {}
     rng = random.Random(1)
     for otype, tag in ((rl_environment.ObservationType.INFORMATION_STATE, "info"),
                        (rl_environment.ObservationType.OBSERVATION, "obs")):
-        for k in (1, 8, 64, 256):
-            for batched in (True, False):
-                if not batched and k > 64:
+        for k in (1, 8, 64, 256, 1024):
+            for form in ("batched", "device", "loop"):
+                if form == "loop" and k > 64:
                     continue
                 envs = [rl_environment.Environment("coup", seed=k, observation_type=otype) for _ in range(k)]
-                venv = vector_env.SyncVectorEnv(envs, batched=batched)
+                saved, vector_env.HOST_UPTO = vector_env.HOST_UPTO, (0 if form == "device" else vector_env.HOST_UPTO)
+                try:
+                    venv = vector_env.SyncVectorEnv(envs, batched=form != "loop")
+                finally:
+                    vector_env.HOST_UPTO = saved
                 ts = venv.reset()
 
                 def run(m, ts):
@@ -200,7 +215,7 @@ def vector_env_rows(steps=40):
                 t0 = time.perf_counter()
                 run(steps, ts)
                 us = 1e6 * (time.perf_counter() - t0) / (steps * k)
-                rows[f"vector_env_{tag}_n{k}_{'batched' if batched else 'loop'}_us_per_env_step"] = us
+                rows[f"vector_env_{tag}_n{k}_{form}_us_per_env_step"] = us
     return rows
 
 
