@@ -202,9 +202,9 @@ static PyObject* py_float_lists(PyObject* self, PyObject* const* args, Py_ssize_
     PyErr_SetString(PyExc_ValueError, "float_lists: bad buffer");
     return NULL;
   }
-  if (!g_small[0])
+  if (!g_small[15]) /* filled in order, the last one only when all succeeded */
     for (int k = 0; k < 16; ++k)
-      if (!(g_small[k] = PyFloat_FromDouble((double)k))) return NULL;
+      if (!g_small[k] && !(g_small[k] = PyFloat_FromDouble((double)k))) return NULL;
   PyObject* out = PyList_New(rows);
   if (!out) return NULL;
   for (Py_ssize_t r = 0; r < rows; ++r) {
