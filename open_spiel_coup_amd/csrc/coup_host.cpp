@@ -17,6 +17,7 @@
 // record, the 96 history bytes and the answers (legal mask, player, ...)
 // that the device ops return, so host and device states convert freely.
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <string>
 
@@ -188,14 +189,25 @@ int coup_host_state_tensors(const coup_slot_result* st, float* obs, float* info)
     for (int g = 0; g < 2 * kObsSize; ++g) obs[g] = obs_pair_at(L, term, g);
   }
   if (info) {
+    // info_f4's values written sparsely: the same prefix words, then zeros
+    // except the prefix's set bits, the two coin counts and one entry per
+    // history row the player saw (a decision, or a deal to that player)
     uint32_t pre[kPreWords];
     info_prefix_to_lds(L, pre);
-    for (uint32_t c = 0; c < (uint32_t)kInfoF4; ++c) {
-      const float4 v = info_f4(pre, st->history, c);
-      info[4 * c + 0] = v.x;
-      info[4 * c + 1] = v.y;
-      info[4 * c + 2] = v.z;
-      info[4 * c + 3] = v.w;
+    std::memset(info, 0, sizeof(float) * 2 * kInfoSize);
+    const uint32_t meta = pre[4], len = std::min<uint32_t>(meta >> 16, (uint32_t)kHist);
+    for (uint32_t p = 0; p < 2; ++p) {
+      float* t = info + p * kInfoSize;
+      const uint64_t prefix = (uint64_t)pre[2 * p] | ((uint64_t)pre[2 * p + 1] << 32);
+      for (int f = 0; f < 60; ++f)
+        if ((prefix >> f) & 1u) t[f] = 1.0f;
+      t[60] = (float)(meta & 0xFFu);
+      t[61] = (float)((meta >> 8) & 0xFFu);
+      for (uint32_t r = 0; r < len; ++r) {
+        const uint32_t e = st->history[r], a = e & 0x1Fu;
+        const bool seen = (e & 0x20u) == 0u || ((e >> 6) & 1u) == p;  // deals: observer's only
+        if (seen && a < 18u) t[62 + 18 * r + a] = 1.0f;
+      }
     }
   }
   return COUP_OK;

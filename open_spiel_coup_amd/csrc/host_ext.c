@@ -13,9 +13,12 @@
  *   step(raw, action, mode, seed, env_id) -> the same for rl_environment's reset / step (raw may be None
  *                                      with mode COUP_SLOT_INIT)
  *   string(raw, kind, player)       -> str (0 ObservationString, 1 InformationStateString, 2 ToString)
- *   tensors(raw, obs_addr, info_addr) -> None (float32 [2][98] / [2][2492] at the addresses, 0 = skip)
- *   float_lists(addr, rows, cols)   -> rows lists of floats (the time steps' tensors)
+ *   tensors(raw, obs, info)         -> None (float32 [2][98] / [2][2492] into obs / info, None = skip)
+ *   float_lists(rows_f32, rows, cols) -> rows lists of floats (the time steps' tensors)
  *
+ * obs, info and rows_f32 are C-contiguous float32 buffers (numpy arrays:
+ * the buffer protocol, no ctypes address lookup per call) or integer
+ * addresses (0 = skip). *
  * raw is the state's 128-byte coup_slot_result (bytes). */
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
@@ -162,18 +165,52 @@ static PyObject* py_string(PyObject* self, PyObject* const* args, Py_ssize_t n) 
   return s;
 }
 
+/* A float32 buffer argument: None or an integer address (0 = none), or a
+ * C-contiguous buffer of at least `floats` elements (released by
+ * release_floats). */
+static int get_floats(PyObject* o, Py_ssize_t floats, int writable, Py_buffer* view, float** out) {
+  view->obj = NULL;
+  *out = NULL;
+  if (o == Py_None) return 1;
+  if (PyLong_Check(o)) {
+    *out = (float*)PyLong_AsVoidPtr(o);
+    return !PyErr_Occurred();
+  }
+  if (PyObject_GetBuffer(o, view, (writable ? PyBUF_WRITABLE : 0) | PyBUF_C_CONTIGUOUS | PyBUF_FORMAT) != 0)
+    return 0;
+  if (view->itemsize != 4 || (view->format && strcmp(view->format, "f") != 0) || view->len < floats * 4) {
+    PyBuffer_Release(view);
+    view->obj = NULL;
+    PyErr_SetString(PyExc_ValueError, "expected a C-contiguous float32 buffer of the tensor's size");
+    return 0;
+  }
+  *out = (float*)view->buf;
+  return 1;
+}
+
+static void release_floats(Py_buffer* view) {
+  if (view->obj) PyBuffer_Release(view);
+}
+
 static PyObject* py_tensors(PyObject* self, PyObject* const* args, Py_ssize_t n) {
   (void)self;
   if (n != 3) {
-    PyErr_SetString(PyExc_TypeError, "tensors(raw, obs_addr, info_addr)");
+    PyErr_SetString(PyExc_TypeError, "tensors(raw, obs, info)");
     return NULL;
   }
   const coup_slot_result* st;
   if (!as_state(args[0], &st)) return NULL;
-  void* obs = PyLong_AsVoidPtr(args[1]);
-  void* info = PyLong_AsVoidPtr(args[2]);
-  if (PyErr_Occurred()) return NULL;
-  if (coup_host_state_tensors(st, (float*)obs, (float*)info) != COUP_OK) {
+  Py_buffer vo, vi;
+  float *obs, *info;
+  if (!get_floats(args[1], 2 * COUP_OBS_SIZE, 1, &vo, &obs)) return NULL;
+  if (!get_floats(args[2], 2 * COUP_INFO_STATE_SIZE, 1, &vi, &info)) {
+    release_floats(&vo);
+    return NULL;
+  }
+  const int rc = coup_host_state_tensors(st, obs, info);
+  release_floats(&vo);
+  release_floats(&vi);
+  if (rc != COUP_OK) {
     PyErr_SetString(PyExc_RuntimeError, "coup_host_state_tensors failed");
     return NULL;
   }
@@ -183,28 +220,58 @@ static PyObject* py_tensors(PyObject* self, PyObject* const* args, Py_ssize_t n)
 /* float_lists(addr, rows, cols): rows x cols contiguous float32 at addr as a
  * list of `rows` Python lists of floats -- the time steps' tensors
  * (rl_environment.py:243-248 hands them out as lists).  Integral values
- * 0..15 (every element of both tensors: one-hots, coin counts) share one
- * float object each, so building and later copying / collecting the lists
+ * 0..15 (every element of both tensors: one-hots, coin counts) share a few
+ * float objects each, so building and later copying / collecting the lists
  * touches a few objects instead of 2 x 2492 fresh ones per env and step;
- * any other value gets its own float, exactly float(x) of the float32. */
-static PyObject* g_small[16];
+ * any other value gets its own float, exactly float(x) of the float32.
+ * Column c takes copy c % kCopies of its value: the reference-count updates
+ * of one list (when built, and again when freed) then form kCopies
+ * independent chains instead of one store-to-load chain through a single
+ * object's count, ~4x faster for an info-state row. */
+enum { kCopies = 8 };
+static PyObject* g_small[16][kCopies];
+
+static PyObject* build_lists(const float* src, Py_ssize_t rows, Py_ssize_t cols);
 
 static PyObject* py_float_lists(PyObject* self, PyObject* const* args, Py_ssize_t n) {
   (void)self;
   if (n != 3) {
-    PyErr_SetString(PyExc_TypeError, "float_lists(addr, rows, cols)");
+    PyErr_SetString(PyExc_TypeError, "float_lists(rows_f32, rows, cols)");
     return NULL;
   }
-  const float* src = (const float*)PyLong_AsVoidPtr(args[0]);
   const Py_ssize_t rows = PyLong_AsSsize_t(args[1]), cols = PyLong_AsSsize_t(args[2]);
   if (PyErr_Occurred()) return NULL;
-  if (!src || rows < 0 || cols < 0) {
+  if (rows < 0 || cols < 0) {
+    PyErr_SetString(PyExc_ValueError, "float_lists: bad shape");
+    return NULL;
+  }
+  Py_buffer view;
+  float* buf;
+  if (!get_floats(args[0], rows * cols, 0, &view, &buf)) return NULL;
+  PyObject* res = build_lists(buf, rows, cols);
+  release_floats(&view);
+  return res;
+}
+
+/* A new reference for a non-zero element of column copy j. */
+static PyObject* element(float v, int j) {
+  const int k = (v >= 0.0f && v < 16.0f) ? (int)v : -1; /* converted only where it fits */
+  if (k >= 0 && (float)k == v && !(v == 0.0f && signbit(v))) {
+    Py_INCREF(g_small[k][j]);
+    return g_small[k][j];
+  }
+  return PyFloat_FromDouble((double)v);
+}
+
+static PyObject* build_lists(const float* src, Py_ssize_t rows, Py_ssize_t cols) {
+  if (!src) {
     PyErr_SetString(PyExc_ValueError, "float_lists: bad buffer");
     return NULL;
   }
-  if (!g_small[15]) /* filled in order, the last one only when all succeeded */
+  if (!g_small[15][kCopies - 1]) /* filled in order, the last one only when all succeeded */
     for (int k = 0; k < 16; ++k)
-      if (!g_small[k] && !(g_small[k] = PyFloat_FromDouble((double)k))) return NULL;
+      for (int j = 0; j < kCopies; ++j)
+        if (!g_small[k][j] && !(g_small[k][j] = PyFloat_FromDouble((double)k))) return NULL;
   PyObject* out = PyList_New(rows);
   if (!out) return NULL;
   for (Py_ssize_t r = 0; r < rows; ++r) {
@@ -214,19 +281,52 @@ static PyObject* py_float_lists(PyObject* self, PyObject* const* args, Py_ssize_
       return NULL;
     }
     const float* x = src + r * cols;
-    for (Py_ssize_t c = 0; c < cols; ++c) {
+    /* +0.0 (most elements) is stored without touching its object: the
+     * references are counted per copy in registers and added once */
+    Py_ssize_t zc[kCopies] = {0};
+    int failed = 0;
+    Py_ssize_t c = 0;
+#define COUP_ONE(J)                                  \
+  {                                                  \
+    const float v = x[c + (J)];                      \
+    uint32_t u;                                      \
+    memcpy(&u, &v, sizeof u);                        \
+    PyObject* o;                                     \
+    if (u == 0u) {                                   \
+      o = g_small[0][(J)];                           \
+      ++zc[(J)];                                     \
+    } else if (!(o = element(v, (J)))) {             \
+      failed = 1;                                    \
+      break;                                         \
+    }                                                \
+    PyList_SET_ITEM(row, c + (J), o);                \
+  }
+    for (; c + kCopies <= cols; c += kCopies) {
+      do {
+        COUP_ONE(0) COUP_ONE(1) COUP_ONE(2) COUP_ONE(3) COUP_ONE(4) COUP_ONE(5) COUP_ONE(6) COUP_ONE(7)
+      } while (0);
+      if (failed) break;
+    }
+    for (; !failed && c < cols; ++c) {
       const float v = x[c];
-      const int k = (int)v;
+      uint32_t u;
+      memcpy(&u, &v, sizeof u);
       PyObject* o;
-      if (v >= 0.0f && v < 16.0f && (float)k == v && !(v == 0.0f && signbit(v))) {
-        o = g_small[k];
-        Py_INCREF(o);
-      } else if (!(o = PyFloat_FromDouble((double)v))) {
-        Py_DECREF(row);
-        Py_DECREF(out);
-        return NULL;
+      if (u == 0u) {
+        o = g_small[0][c % kCopies];
+        ++zc[c % kCopies];
+      } else if (!(o = element(v, (int)(c % kCopies)))) {
+        failed = 1;
+        break;
       }
       PyList_SET_ITEM(row, c, o);
+    }
+#undef COUP_ONE
+    for (int j = 0; j < kCopies; ++j) Py_SET_REFCNT(g_small[0][j], Py_REFCNT(g_small[0][j]) + zc[j]);
+    if (failed) { /* the items set so far hold their references; the rest are NULL */
+      Py_DECREF(row);
+      Py_DECREF(out);
+      return NULL;
     }
     /* a list of floats cannot be part of a reference cycle: keep it out of
      * the cyclic collector, which would otherwise visit its 2492 items in

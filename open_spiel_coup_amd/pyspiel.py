@@ -418,7 +418,7 @@ class _Host:
         """[2][98] and / or [2][2492] float32 arrays (None where not asked)."""
         o = np.empty((2, OBS_SIZE), np.float32) if obs else None
         i = np.empty((2, INFO_STATE_SIZE), np.float32) if info else None
-        self._ext.tensors(raw, o.ctypes.data if obs else 0, i.ctypes.data if info else 0)
+        self._ext.tensors(raw, o, i)
         return o, i
 
 

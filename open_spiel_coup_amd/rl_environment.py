@@ -105,7 +105,7 @@ def _float_lists(rows):
     """The per-player Python lists of a time step (rl_environment.py:243-248
     hands out fresh lists of floats) from a [P, n] float32 array, built in C
     by the library's CPython binding (_coup_host.float_lists): integral
-    values -- every element of both tensors -- share one float object each,
+    values -- every element of both tensors -- share a few float objects,
     and the lists are kept out of the cyclic collector, so a 256-env vector
     step costs per env what an 8-env one does.  Equal
     to numpy's tolist element by element; each list is the caller's own."""
@@ -115,7 +115,7 @@ def _float_lists(rows):
         from . import _coup_host
         _ext = _coup_host
     a = np.ascontiguousarray(rows, dtype=np.float32)
-    return _ext.float_lists(a.ctypes.data, a.shape[0], a.shape[1])
+    return _ext.float_lists(a, a.shape[0], a.shape[1])
 
 
 def _resolve_seed(seed):

@@ -49,3 +49,26 @@ def test_float_lists_of_non_contiguous_input():
     fl = _lists()
     big = np.arange(4 * 10, dtype=np.float32).reshape(4, 10)
     assert fl(big[::2]) == big[::2].tolist()
+
+
+def test_float_lists_reference_counts():
+    """The shared zeros' references are counted in bulk (per column copy,
+    added once per row): building then freeing lists leaves every shared
+    float's count where it was, and a live list holds exactly one reference
+    per element (columns 0, 8, 16, ... share copy 0)."""
+    import sys
+    fl = _lists()
+    z = np.zeros((2, 1003), np.float32)
+    z[1, 5] = 1.0
+    probe_lists = fl(z)
+    zero0, one5 = probe_lists[0][0], probe_lists[1][5]
+    base0, base1 = sys.getrefcount(zero0), sys.getrefcount(one5)
+    for _ in range(5):
+        x = fl(z)
+        del x
+    assert sys.getrefcount(zero0) == base0 and sys.getrefcount(one5) == base1
+    x = fl(z)
+    assert sys.getrefcount(zero0) == base0 + 2 * len(range(0, 1003, 8))
+    assert sys.getrefcount(one5) == base1 + 1
+    del x
+    assert sys.getrefcount(zero0) == base0
