@@ -29,6 +29,7 @@ deal.
 import collections
 import os
 import enum
+import struct
 
 import numpy as np
 import torch
@@ -114,8 +115,31 @@ def _float_lists(rows):
         _native.load()
         from . import _coup_host
         _ext = _coup_host
-    a = np.ascontiguousarray(rows, dtype=np.float32)
-    return _ext.float_lists(a, a.shape[0], a.shape[1])
+    if not (type(rows) is np.ndarray and rows.dtype == np.float32 and rows.flags.c_contiguous):
+        rows = np.ascontiguousarray(rows, dtype=np.float32)
+    return _ext.float_lists(rows, rows.shape[0], rows.shape[1])
+
+
+_LEGAL = {}  # 18-bit mask -> ascending action ids (copied per time step)
+_REWARDS = struct.Struct("<bb")  # coup_slot_result.rewards, at byte 120
+
+
+def _legal_list(mask):
+    """LegalActions() of a mask as a fresh list (the reference's time step
+    holds a new list per step)."""
+    got = _LEGAL.get(mask)
+    if got is None:
+        got = _LEGAL[mask] = tuple(a for a in range(18) if (mask >> a) & 1)
+    return list(got)
+
+
+def _rewards(q):
+    """Rewards() of a result as the time step's list of floats."""
+    raw = getattr(q, "_raw", None)
+    if raw is not None:
+        r0, r1 = _REWARDS.unpack_from(raw, 120)
+        return [float(r0), float(r1)]
+    return [float(x) for x in q["rewards"]]
 
 
 def _resolve_seed(seed):
@@ -202,8 +226,10 @@ class Environment:
 
     def _with_tensor(self, q):
         """q (a host result) with the time step's tensor of both players."""
-        o, i = pyspiel._host().tensors(q._raw, self._use_observation, not self._use_observation)
-        q["obs" if self._use_observation else "info_state"] = o if self._use_observation else i
+        if self._use_observation:
+            q["obs"] = pyspiel._host().tensors(q._raw, True, False)[0]
+        else:
+            q["info_state"] = pyspiel._host().tensors(q._raw, False, True)[1]
         return q
 
     def _op(self, action, flags):
@@ -311,12 +337,15 @@ class Environment:
             # reaches (coup.cc:886, 892, 936), as in the reference's
             # get_time_step (rl_environment.py:243-248)
             raise pyspiel.SpielError("Error in LegalActions(): Invalid action progression")
-        legal_cur = [a for a in range(18) if (mask >> a) & 1] if cur >= 0 else []
-        key = "obs" if self._use_observation else "info_state"
-        tensors = q[key]
-        obs = {"info_state": _float_lists(tensors[:self._num_players]),
-               "legal_actions": [legal_cur if p == cur else [] for p in range(self._num_players)],
-               "current_player": cur,
+        legal_cur = _legal_list(mask) if cur >= 0 else []
+        tensors = q["obs" if self._use_observation else "info_state"]
+        if tensors.shape[0] != self._num_players:
+            tensors = tensors[:self._num_players]
+        if self._num_players == 2:
+            legal = [legal_cur, []] if cur == 0 else ([[], legal_cur] if cur == 1 else [[], []])
+        else:
+            legal = [legal_cur if p == cur else [] for p in range(self._num_players)]
+        obs = {"info_state": _float_lists(tensors), "legal_actions": legal, "current_player": cur,
                "serialized_state": []}
         if self._include_full_state:
             obs["serialized_state"] = pyspiel.serialize_game_and_state(self._game, self.get_state)
@@ -326,7 +355,7 @@ class Environment:
         elif step_type == StepType.LAST:
             discounts = [0.0 for _ in self._discounts]
         self._last = obs
-        return TimeStep(observations=obs, rewards=rewards, discounts=discounts, step_type=step_type)
+        return TimeStep(obs, rewards, discounts, step_type)
 
     def _query(self):
         q = self._env.query_host(obs=self._use_observation, info_state=not self._use_observation)
@@ -363,7 +392,7 @@ class Environment:
         q = self._query() if self._sampler is not None else self._op(-1, 0)
         step_type = StepType.LAST if int(q["terminal"]) else StepType.MID
         self._should_reset = step_type == StepType.LAST
-        return self._time_step(q, step_type, [float(x) for x in q["rewards"]])
+        return self._time_step(q, step_type, _rewards(q))
 
     def step(self, actions):
         assert len(actions) == self.num_actions_per_step, (
@@ -374,11 +403,6 @@ class Environment:
             legal = self._last["legal_actions"][self._last["current_player"]] if self._last else []
             if actions[0] not in legal:
                 raise RuntimeError(f"step() called on illegal action {actions[0]}")
-        # legal per the last time step's mask (which came from the GPU): the
-        # kernel cannot reject it, so the error counter's synchronisation is
-        # skipped
-        cur = self._last["current_player"] if self._last else -1
-        known_legal = cur >= 0 and int(actions[0]) in self._last["legal_actions"][cur]
         if not 0 <= int(actions[0]) < 128:
             raise pyspiel.SpielError(f"illegal action {actions[0]}")  # not an int8 action id
         if self._sampler is None:
@@ -392,7 +416,12 @@ class Environment:
                 raise pyspiel._apply_failed(self._last["current_player"] if self._last else -1, int(actions[0]), q)
             step_type = StepType.LAST if q["terminal"] else StepType.MID
             self._should_reset = step_type == StepType.LAST
-            return self._time_step(q, step_type, [float(x) for x in q["rewards"]])
+            return self._time_step(q, step_type, _rewards(q))
+        # legal per the last time step's mask (which came from the GPU): the
+        # kernel cannot reject it, so the error counter's synchronisation is
+        # skipped
+        cur = self._last["current_player"] if self._last else -1
+        known_legal = cur >= 0 and int(actions[0]) in self._last["legal_actions"][cur]
         self._env.apply_action(self._lane_actions(actions[0]))
         self._sample_external_events()
         if not known_legal and self._env.error_count():
