@@ -232,41 +232,65 @@ int64_t coup_host_state_string(const coup_slot_result* st, int kind, int player,
     return -1;
   const Lane L = unpack(record_of(st));
   const bool recall = kind == 1, all = kind == 2;
+  // appended piece by piece (no printf formatting: ~10-30 calls per string)
   std::string s;
-  s.reserve(512);
-  char line[96];
+  s.reserve(1024);
+  auto put = [&s](const char* t) { s.append(t); };
+  auto putu = [&s](uint32_t v) {
+    char d[10];
+    int n = 0;
+    do {
+      d[n++] = (char)('0' + v % 10u);
+      v /= 10u;
+    } while (v);
+    while (n) s.push_back(d[--n]);
+  };
   if (!all) {
-    std::snprintf(line, sizeof(line), "Observer: P%d\n", player + 1);
-    s += line;
+    put("Observer: P");
+    putu((uint32_t)player + 1u);
+    put("\n");
   }
-  std::snprintf(line, sizeof(line), "Turn: %u\nMove: P%u\n", L.turn, L.M + 1u);
-  s += line;
+  put("Turn: ");
+  putu(L.turn);
+  put("\nMove: P");
+  putu(L.M + 1u);
+  put("\n");
   for (uint32_t p = 0; p < 2; ++p) {
     const uint32_t h = p ? L.h1 : L.h0;
-    std::snprintf(line, sizeof(line), "P%u\n        Card         State\n", p + 1u);
-    s += line;
+    put("P");
+    putu(p + 1u);
+    put("\n        Card         State\n");
     for (uint32_t i = 0; i < 4; ++i) {
       const uint32_t k = nib(h, i);
       if (k == 0xFu) break;
       const bool shown = all || (k & 1u) || p == (uint32_t)player;
-      std::snprintf(line, sizeof(line), "Card %u: %-11s| %s\n", i + 1u, shown ? kCard[k >> 1] : "-", kFace[k & 1u]);
-      s += line;
+      const char* name = shown ? kCard[k >> 1] : "-";
+      put("Card ");
+      putu(i + 1u);
+      put(": ");
+      put(name);
+      const size_t w = std::strlen(name);
+      if (w < 11) s.append(11 - w, ' ');  // %-11s
+      put("| ");
+      put(kFace[k & 1u]);
+      put("\n");
     }
-    std::snprintf(line, sizeof(line), "Coins: %u\n", p ? L.c1 : L.c0);
-    s += line;
+    put("Coins: ");
+    putu(p ? L.c1 : L.c0);
+    put("\n");
     if (recall) {
-      s += "\n";
+      put("\n");
     } else {
       const uint32_t la = p ? L.l1 : L.l0;
-      s += "Last Action: ";
-      s += la == kNoAction ? "None" : kAction[la];
-      s += "\n\n";
+      put("Last Action: ");
+      put(la == kNoAction ? "None" : kAction[la]);
+      put("\n\n");
     }
   }
   if (recall || all) {
     // coup.cc:351-371 (recall): a deal is shown to its receiver only, but the
     // ", " after it depends on its position in the full history
-    s += "Action Sequence: ";
+    put("Action Sequence: ");
     const uint32_t n = L.move < kHistoryBytes ? L.move : kHistoryBytes;
     bool first = true;
     for (uint32_t i = 0; i < n; ++i) {
@@ -274,22 +298,24 @@ int64_t coup_host_state_string(const coup_slot_result* st, int kind, int player,
       const bool deal = (e & 0x20u) != 0u;
       const uint32_t who = (e >> 6) & 1u, a = e & 0x1Fu;
       if (all) {
-        if (!first) s += ", ";
+        if (!first) put(", ");
         first = false;
       }
       if (deal) {
         if (all || who == (uint32_t)player) {
-          s += "PC-";
-          s += kCard[a < 5u ? a : 0u];
-          if (!all && i + 1 < n) s += ", ";
+          put("PC-");
+          put(kCard[a < 5u ? a : 0u]);
+          if (!all && i + 1 < n) put(", ");
         }
       } else {
-        std::snprintf(line, sizeof(line), "P%u-%s", who + 1u, kAction[a < 18u ? a : 0u]);
-        s += line;
-        if (!all && i + 1 < n) s += ", ";
+        put("P");
+        putu(who + 1u);
+        put("-");
+        put(kAction[a < 18u ? a : 0u]);
+        if (!all && i + 1 < n) put(", ");
       }
     }
-    s += "\n";
+    put("\n");
   }
   const int64_t len = (int64_t)s.size();
   if (cap > 0) {
