@@ -185,20 +185,23 @@ def rl_rows(n):
 
 def vector_env_rows(steps=40):
     """SyncVectorEnv.step(reset_if_done=True) per env step: the default
-    (host-resident games kept on the host under the shared stream), the games
-    adopted into one shared device env (vector_env.HOST_UPTO = 0: one launch
-    per step), and the reference's loop over the envs (batched=False)."""
+    (host-resident games kept on the host under the shared stream up to
+    vector_env.HOST_UPTO envs, adopted beyond), the games adopted into one
+    shared device env (HOST_UPTO = 0: one launch per step), kept on the host
+    at any size (HOST_UPTO = None; above the default cut only), and the
+    reference's loop over the envs (batched=False)."""
     from open_spiel_coup_amd import rl_environment, vector_env
     rows = {}
     rng = random.Random(1)
     for otype, tag in ((rl_environment.ObservationType.INFORMATION_STATE, "info"),
                        (rl_environment.ObservationType.OBSERVATION, "obs")):
         for k in (1, 8, 64, 256, 1024):
-            for form in ("batched", "device", "loop"):
-                if form == "loop" and k > 64:
+            for form in ("batched", "device", "host", "loop"):
+                if form == "loop" and k > 64 or form == "host" and k <= vector_env.HOST_UPTO:
                     continue
                 envs = [rl_environment.Environment("coup", seed=k, observation_type=otype) for _ in range(k)]
-                saved, vector_env.HOST_UPTO = vector_env.HOST_UPTO, (0 if form == "device" else vector_env.HOST_UPTO)
+                upto = {"device": 0, "host": None}.get(form, vector_env.HOST_UPTO)
+                saved, vector_env.HOST_UPTO = vector_env.HOST_UPTO, upto
                 try:
                     venv = vector_env.SyncVectorEnv(envs, batched=form != "loop")
                 finally:
