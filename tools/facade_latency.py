@@ -188,7 +188,7 @@ def vector_env_rows(steps=40):
     (host-resident games kept on the host under the shared stream up to
     vector_env.HOST_UPTO envs, adopted beyond), the games adopted into one
     shared device env (HOST_UPTO = 0: one launch per step), kept on the host
-    at any size (HOST_UPTO = None; above the default cut only), and the
+    at any size (HOST_UPTO = None; beyond a finite default cut only), and the
     reference's loop over the envs (batched=False)."""
     from open_spiel_coup_amd import rl_environment, vector_env
     rows = {}
@@ -197,7 +197,8 @@ def vector_env_rows(steps=40):
                        (rl_environment.ObservationType.OBSERVATION, "obs")):
         for k in (1, 8, 64, 256, 1024):
             for form in ("batched", "device", "host", "loop"):
-                if form == "loop" and k > 64 or form == "host" and k <= vector_env.HOST_UPTO:
+                if form == "loop" and k > 64 or form == "host" and (vector_env.HOST_UPTO is None or
+                                                                      k <= vector_env.HOST_UPTO):
                     continue
                 envs = [rl_environment.Environment("coup", seed=k, observation_type=otype) for _ in range(k)]
                 upto = {"device": 0, "host": None}.get(form, vector_env.HOST_UPTO)
