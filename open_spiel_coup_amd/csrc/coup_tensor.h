@@ -72,6 +72,31 @@ __device__ __forceinline__ void obs_row_bits(const Lane& L, bool term, uint64_t&
   }
 }
 
+// obs_row_bits with the observer as a run-time value (the same bits): the
+// split observation writer decodes a lane's two rows on two threads.
+__device__ __forceinline__ void obs_row_bits_rt(const Lane& L, bool term, uint32_t P, uint64_t& lo, uint64_t& hi) {
+  lo = 1ull << P;  // observer one-hot
+#pragma unroll
+  for (uint32_t k = 0; k < 8; ++k) {
+    const uint32_t q = k >> 2, i = k & 3u;
+    const uint32_t n = nib(q ? L.h1 : L.h0, i);
+    const bool exists = n != 0xFu;
+    const bool visible = exists && (q == P || (n & 1u));
+    lo |= (uint64_t)visible << (2u + 20u * q + 5u * i + (n >> 1));
+    lo |= (uint64_t)exists << (44u + 8u * q + 2u * i + (n & 1u));
+  }
+  lo |= (uint64_t)(!term) << (42u + L.M);
+  hi = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < 2; ++q) {
+    const uint32_t a = q ? L.l1 : L.l0;
+    const uint32_t p = 62u + 18u * q + a;
+    const bool has = a != kNoAction;
+    lo |= (uint64_t)(has && p < 64u) << (p & 63u);
+    hi |= (uint64_t)(has && p >= 64u) << ((p - 64u) & 63u);
+  }
+}
+
 // InformationStateTensor layout (see coup_kernels.hip's write_info_wave):
 constexpr int kInfoSize = COUP_INFO_STATE_SIZE;  // 2492
 constexpr int kInfoHalfF4 = kInfoSize / 4;       // 623 float4 per player

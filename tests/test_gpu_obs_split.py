@@ -1,0 +1,87 @@
+"""The split observation step (COUP_OBS_SPLIT, the default from 2^18 lanes):
+the rules step without tensors, then coup::k_obs_sweep writing every lane's
+ObservationTensor pair from the post-step records in address order.  It must
+equal the fused step (k_step<*, kObsWaveBitsSc1>, COUP_OBS_SPLIT=0) bit for
+bit: observations, records, every small output and the episode
+accumulators, at every step -- uniform policy and caller actions (skipped
+lanes, rejected actions, the unchecked env), ragged batches whose last 4 KiB
+chunk is partial, and the headline size.  The oracle side of the same
+observations is tests/test_gpu_headline.py (c3 at 2^20 lanes, now split).
+Reference semantics: ObservationTensor coup.cc:1051-1056, 248-287."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from open_spiel_coup_amd import BatchedCoupEnv  # noqa: E402
+
+KEYS = ("actions", "rewards", "step_type", "legal_mask", "current_player", "obs")
+
+
+def _run(monkeypatch, split, B, steps, seed=5, actions_fn=None, unchecked=False, auto_reset=True):
+    monkeypatch.setenv("COUP_OBS_SPLIT", str(split))
+    env = BatchedCoupEnv(B, seed=seed, auto_reset=auto_reset, obs=True, device="cuda", episode_stats=True,
+                         unchecked=unchecked)
+    outs = []
+    for t in range(steps):
+        o = env.step(actions_fn(env, t) if actions_fn else None)
+        outs.append({k: o[k].cpu().numpy().copy() for k in KEYS})
+    eps, ret = env.episode_stats()
+    res = (outs, env.export_state().cpu().numpy(), eps.cpu().numpy(), ret.cpu().numpy(), env.error_count())
+    env.close()
+    return res
+
+
+def _same(a, b, what):
+    for t, (x, y) in enumerate(zip(a[0], b[0])):
+        for k in KEYS:
+            np.testing.assert_array_equal(x[k], y[k], err_msg=f"{what}: {k} at step {t}")
+    np.testing.assert_array_equal(a[1], b[1], err_msg=f"{what}: records")
+    np.testing.assert_array_equal(a[2], b[2], err_msg=f"{what}: episodes")
+    np.testing.assert_array_equal(a[3], b[3], err_msg=f"{what}: return sums")
+    assert a[4] == b[4], what
+
+
+@pytest.mark.parametrize("B", [3, 1000, 65536 + 77, 1 << 18])
+def test_split_equals_fused_uniform(monkeypatch, B):
+    steps = 40 if B <= 65613 else 12
+    ref = _run(monkeypatch, 0, B, steps)
+    # 1: k_obs_sweep (NT stores), 2: plain stores, 3-7: k_obs_sweep_rows
+    # shapes, 8: the rules kernel stores the words, k_obs_sweep_words expands,
+    # 9-13: more k_obs_sweep_rows shapes
+    for split in range(1, 14):
+        _same(_run(monkeypatch, split, B, steps), ref, f"split {split} B {B}")
+
+
+def test_split_equals_fused_at_headline_size(monkeypatch):
+    """2^20 lanes, the c3 bench size: a few steps, every output compared."""
+    B = 1 << 20
+    ref = _run(monkeypatch, 0, B, 4, seed=9)
+    for split in (1, 8):
+        _same(_run(monkeypatch, split, B, 4, seed=9), ref, f"split {split} 2^20")
+
+
+@pytest.mark.parametrize("unchecked", [False, True], ids=["checked", "unchecked"])
+def test_split_equals_fused_caller_actions(monkeypatch, unchecked):
+    """Caller actions: legal picks, some lanes skipped (-1: the lane and its
+    observation unchanged), some given actions the rules reject."""
+    B = 5003
+
+    def actions(env, t):
+        g = torch.Generator().manual_seed(100 + t)
+        m = env.legal_mask.cpu().to(torch.int64) & 0x3FFFF
+        u = torch.randint(0, 1 << 30, (B,), generator=g)
+        acts = torch.zeros(B, dtype=torch.int64)
+        for lane in range(B):
+            bits = [a for a in range(18) if (int(m[lane]) >> a) & 1]
+            acts[lane] = bits[int(u[lane]) % len(bits)] if bits else 0
+        if t % 4 == 1:
+            acts[::89] = 16  # mostly rejected (ExchangeReturn24 outside an exchange)
+        acts[7::113] = -1
+        return acts
+
+    ref = _run(monkeypatch, 0, B, 20, actions_fn=actions, unchecked=unchecked, auto_reset=False)
+    for split in (1, 8):
+        _same(_run(monkeypatch, split, B, 20, actions_fn=actions, unchecked=unchecked, auto_reset=False), ref,
+              f"caller actions split {split} unchecked={unchecked}")

@@ -71,6 +71,43 @@ __global__ __launch_bounds__(256) void k_expand_pipe(const uint32_t* __restrict_
   }
 }
 
+// Round 4: one block per chunk of S x 256 float4 (S x 4 KiB contiguous), no
+// persistence -- the grid-stride sweep's order, with the <= 22 lanes'
+// bitmaps a chunk needs loaded by its first threads into LDS.  POL: 0 plain,
+// 1 non-temporal, 2 sc1 buffer stores (the fused step's policy).
+template <int S, int POL>
+__global__ __launch_bounds__(256) void k_expand_blk(const uint32_t* __restrict__ rec, v4f* __restrict__ dst,
+                                                    uint32_t lanes) {
+  constexpr uint32_t kMaxLanes = (256u * S + kRowF4 - 1u) / kRowF4 + 1u;
+  __shared__ uint4 bits[2 * kMaxLanes];
+  const uint32_t t = threadIdx.x;
+  const uint32_t nf4 = lanes * kRowF4;
+  const uint32_t x0 = blockIdx.x * 256u * S;
+  const uint32_t o0 = x0 / kRowF4;
+  if (t < 2u * kMaxLanes && o0 + t / 2u < lanes)
+    bits[t] = reinterpret_cast<const uint4*>(rec)[2u * o0 + t];
+  __syncthreads();
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(bits);
+  __amdgpu_buffer_rsrc_t rsrc;
+  if (POL == 2) rsrc = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, (int)(nf4 * 16u), 0x00020000);
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const uint32_t x = x0 + (uint32_t)s * 256u + t;
+    const uint32_t o = x / kRowF4, c = x - o * kRowF4;
+    const uint32_t base = (o - o0) * 8u;
+    const v4f v = expand_f4(w[base + (c >> 3)], w[base + 7u], c);
+    if (POL == 2) {
+      typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), rsrc, (int)(16u * x), 0, 16);
+    } else if (x < nf4) {
+      if (POL == 1)
+        __builtin_nontemporal_store(v, dst + x);
+      else
+        dst[x] = v;
+    }
+  }
+}
+
 #define CK(x)                                                    \
   do {                                                           \
     hipError_t e = (x);                                          \
@@ -124,7 +161,7 @@ int main() {
     return 0;
   };
   char name[96];
-  for (int grid : {512, 1024, 2048}) {
+  for (int grid : {1024}) {
     std::snprintf(name, sizeof name, "expand_pipe_S1_nt_g%d", grid);
     timed(name, [&](int) { k_expand_pipe<1, 1><<<grid, 256, 0, s1>>>(rec, obs, lanes); });
     std::snprintf(name, sizeof name, "expand_pipe_S1_plain_g%d", grid);
@@ -132,6 +169,13 @@ int main() {
     std::snprintf(name, sizeof name, "expand_pipe_S4_plain_g%d", grid);
     timed(name, [&](int) { k_expand_pipe<4, 0><<<grid, 256, 0, s1>>>(rec, obs, lanes); });
   }
+  const uint32_t nf4 = lanes * kRowF4;
+  auto blocks = [&](int S) { return (unsigned)((nf4 + 256u * S - 1u) / (256u * S)); };
+  timed("expand_blk_S1_nt", [&](int) { k_expand_blk<1, 1><<<blocks(1), 256, 0, s1>>>(rec, obs, lanes); });
+  timed("expand_blk_S1_sc1", [&](int) { k_expand_blk<1, 2><<<blocks(1), 256, 0, s1>>>(rec, obs, lanes); });
+  timed("expand_blk_S4_nt", [&](int) { k_expand_blk<4, 1><<<blocks(4), 256, 0, s1>>>(rec, obs, lanes); });
+  timed("expand_blk_S4_sc1", [&](int) { k_expand_blk<4, 2><<<blocks(4), 256, 0, s1>>>(rec, obs, lanes); });
+  timed("expand_blk_S4_plain", [&](int) { k_expand_blk<4, 0><<<blocks(4), 256, 0, s1>>>(rec, obs, lanes); });
   coup_env* bare;
   coup_env* fused;
   CC(coup_create(lanes, 1, 0, COUP_FLAG_AUTO_RESET, &bare));
@@ -152,6 +196,54 @@ int main() {
       k_expand_pipe<1, 0><<<grid, 256, 0, s2>>>(rec, obs, lanes);
     });
   }
+  timed("overlap_bare_step+expand_blk_S4_sc1", [&](int) {
+    coup_step(bare, nullptr, &none);
+    k_expand_blk<4, 2><<<blocks(4), 256, 0, s2>>>(rec, obs, lanes);
+  });
+  timed("overlap_bare_step+expand_blk_S1_nt", [&](int) {
+    coup_step(bare, nullptr, &none);
+    k_expand_blk<1, 1><<<blocks(1), 256, 0, s2>>>(rec, obs, lanes);
+  });
+  // the chunked split step: the batch as C envs of 2^20 / C lanes (the rules
+  // kernel of chunk c), each followed on s2 by the expansion of its obs
+  // chunk, and s1 waiting for the last expansion before the next step (a
+  // step's outputs complete on s1: no overlap across steps)
+  for (int C : {1, 2, 4, 8}) {
+    coup_env* ch[8];
+    hipEvent_t ev[8], done;
+    CK(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+    for (int c = 0; c < C; ++c) {
+      CC(coup_create(lanes / C, 1, (int64_t)c * (lanes / C), COUP_FLAG_AUTO_RESET, &ch[c]));
+      CC(coup_set_stream(ch[c], s1));
+      CC(coup_rollout(ch[c], 256, nullptr));
+      CK(hipEventCreateWithFlags(&ev[c], hipEventDisableTiming));
+    }
+    const uint32_t cl = lanes / C, cf4 = cl * kRowF4;
+    const unsigned cb = (unsigned)((cf4 + 255u) / 256u);
+    std::snprintf(name, sizeof name, "chunked_split_C%d_bare_then_expand_blk_S1_nt", C);
+    timed(name, [&](int) {
+      for (int c = 0; c < C; ++c) {
+        coup_step(ch[c], nullptr, &none);
+        hipEventRecord(ev[c], s1);
+        hipStreamWaitEvent(s2, ev[c], 0);
+        k_expand_blk<1, 1><<<cb, 256, 0, s2>>>(rec + (size_t)c * cl * 8u, obs + (size_t)c * cf4, cl);
+      }
+      hipEventRecord(done, s2);
+      hipStreamWaitEvent(s1, done, 0);
+    });
+    for (int c = 0; c < C; ++c) {
+      CC(coup_destroy(ch[c]));
+      CK(hipEventDestroy(ev[c]));
+    }
+    CK(hipEventDestroy(done));
+  }
+  // the split step on ONE stream (no events): the bare step, then the sweep
+  // expansion of the whole batch
+  timed("seq_bare_then_expand_blk_S1_nt", [&](int) {
+    coup_step(bare, nullptr, &none);
+    k_expand_blk<1, 1><<<blocks(1), 256, 0, s1>>>(rec, obs, lanes);
+  });
+  timed("fused_c3_step_again", [&](int) { coup_step(fused, nullptr, &with_obs); });
   CC(coup_destroy(bare));
   CC(coup_destroy(fused));
   return 0;
