@@ -43,6 +43,10 @@ HBM bytes per launch from the rocprofv3 PMC passes recorded in profiles/
 times coup_measure_step_traffic -- the step's loads and stores in the same
 order with no rules -- over the same buffers: roofline.store_ceiling_ms is
 that ceiling on this box, frac_of_store_ceiling = ceiling / kernel time.
+From 2^20 lanes the observation step is split (coup_obs_split_variant): the
+rules step without tensors, then an address-order observation writer; the
+timed span covers both kernels, and the store ceiling is then the fused
+form's (lane-owned) one, which the split form is not bound by.
 `box` names the GPU box (boxes differ in HBM store rate).
 cpu_baseline: the C oracle (a scalar port of the reference rules, ~14x
 faster than the reference's own C++ on the survey host) on one
@@ -148,6 +152,23 @@ def _np_step_lanes(players):
     if e in ("256", "512", "1024"):
         return int(e)
     return 1024 if players >= 6 else 512
+
+
+_SPLIT_WRITERS = {1: "coup::k_obs_sweep<1>", 2: "coup::k_obs_sweep<0>", 3: "coup::k_obs_sweep_rows<256, 1>",
+                  4: "coup::k_obs_sweep_rows<256, 2>", 5: "coup::k_obs_sweep_rows<128, 1>",
+                  6: "coup::k_obs_sweep_rows<64, 1>", 7: "coup::k_obs_sweep_rows<512, 1>",
+                  8: "coup::k_obs_sweep_words", 9: "coup::k_obs_sweep_rows<256, 3>",
+                  10: "coup::k_obs_sweep_rows<256, 4>", 11: "coup::k_obs_sweep_rows<512, 2>",
+                  12: "coup::k_obs_sweep_rows<128, 4>", 13: "coup::k_obs_sweep_rows<128, 2>",
+                  14: "coup::k_obs_sweep_rows<1024, 2>", 15: "coup::k_obs_sweep_rows<1024, 1>",
+                  16: "coup::k_obs_sweep_rows<512, 3>", 17: "coup::k_obs_sweep_rows<512, 4>"}
+
+
+def obs_split_active(batch):
+    """The split observation step's writer variant coup_step uses for this
+    batch (0: the fused step kernel; COUP_OBS_SPLIT overrides)."""
+    from open_spiel_coup_amd import _native
+    return int(_native.load().coup_obs_split_variant(int(batch)))
 
 
 def _writer(mode_env):
@@ -593,7 +614,12 @@ def main():
         elif with_info:
             kernel = "coup::k_step<true, 0, 256, 2, false>"
         elif with_obs:
-            kernel = "coup::k_step<true, %d, %d, 0, false>" % _writer(os.environ.get("COUP_OBS_MODE"))
+            split = obs_split_active(B) if players == 2 else 0
+            if split:
+                # the rules step without tensors (regrouped from 2^18 lanes) + the writer
+                kernel = "coup::k_step_sorted<true, 512> + " + _SPLIT_WRITERS.get(split, "coup::k_obs_sweep")
+            else:
+                kernel = "coup::k_step<true, %d, %d, 0, false>" % _writer(os.environ.get("COUP_OBS_MODE"))
         else:
             tpl = os.environ.get("COUP_STEP_TPL", "1")
             kernel = ("coup::k_step_group<%s, true>" % tpl if tpl in ("1", "2", "4") else

@@ -403,6 +403,13 @@ int coup_error_count(coup_env* env, int64_t* out);
  * coup_step_outputs (any may be NULL).  Asynchronous on `hip_stream`. */
 int coup_measure_step_traffic(int64_t batch, uint32_t* records, const coup_step_outputs* out, void* hip_stream);
 
+/* Measurement helper: the observation-step form coup_step uses for a batch
+ * of `batch` 2-player lanes with observations and no information state --
+ * 0 the fused step kernel, > 0 the split form's writer variant (the rules
+ * step without tensors, then the observations in address order; DESIGN.md
+ * section 5).  COUP_OBS_SPLIT overrides it. */
+int coup_obs_split_variant(int64_t batch);
+
 #ifdef __cplusplus
 }
 #endif

@@ -2242,11 +2242,15 @@ int obs_mode() {
 }
 
 // COUP_OBS_SPLIT: the observation step as the rules step without tensors
-// plus k_obs_sweep (1), or the fused k_step<*, kObsWaveBitsSc1> (0); by
-// default split from kObsSplitMinLanes lanes.  COUP_OBS_SPLIT=2: split with
-// plain stores (A/B).  Read at every launch.
-constexpr int64_t kObsSplitMinLanes = int64_t(1) << 18;
-constexpr int kObsSplitDefault = 0;  // the fused step until a split variant measures faster (A/B)
+// plus an address-order writer (variant 1..17: k_obs_sweep, its row-decoding
+// shapes k_obs_sweep_rows<T, S>, or k_obs_sweep_words), or the fused
+// k_step<*, kObsWaveBitsSc1> (0).  Default from kObsSplitMinLanes lanes:
+// k_obs_sweep_rows<512, 2> (variant 11), 140.6-146.1 us against 160.2-161.5
+// for the fused step per 2^20-lane step in the same process (calls r04r /
+// r04s, profiles/r04/ab/c3_obs_split_shapes_*.jsonl).  Below 2^20 lanes the
+// fused step stays (the first writer lost there).  Read at every launch.
+constexpr int64_t kObsSplitMinLanes = int64_t(1) << 20;
+constexpr int kObsSplitDefault = 11;
 int obs_split(int64_t n) {
   const char* e = std::getenv("COUP_OBS_SPLIT");
   if (e) return std::atoi(e);
@@ -2683,6 +2687,10 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
         case 11: rows(std::integral_constant<int, 512>(), std::integral_constant<int, 2>()); break;
         case 12: rows(std::integral_constant<int, 128>(), std::integral_constant<int, 4>()); break;
         case 13: rows(std::integral_constant<int, 128>(), std::integral_constant<int, 2>()); break;
+        case 14: rows(std::integral_constant<int, 1024>(), std::integral_constant<int, 2>()); break;
+        case 15: rows(std::integral_constant<int, 1024>(), std::integral_constant<int, 1>()); break;
+        case 16: rows(std::integral_constant<int, 512>(), std::integral_constant<int, 3>()); break;
+        case 17: rows(std::integral_constant<int, 512>(), std::integral_constant<int, 4>()); break;
         default: coup::k_obs_sweep<1><<<g, 256, 0, s>>>(env->state, a.obs, n); break;
       }
       COUP_HIP_TRY(hipGetLastError());
@@ -3437,6 +3445,8 @@ int coup_error_count(coup_env* env, int64_t* out) {
   *out = (int64_t)h;
   return COUP_OK;
 }
+
+int coup_obs_split_variant(int64_t batch) { return batch > 0 ? obs_split(batch) : 0; }
 
 int coup_measure_step_traffic(int64_t batch, uint32_t* records, const coup_step_outputs* out, void* hip_stream) {
   if (batch < 0 || batch > (int64_t(1) << 32)) return fail(COUP_E_INVALID, "coup_measure_step_traffic: bad batch");

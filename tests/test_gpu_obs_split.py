@@ -49,8 +49,8 @@ def test_split_equals_fused_uniform(monkeypatch, B):
     ref = _run(monkeypatch, 0, B, steps)
     # 1: k_obs_sweep (NT stores), 2: plain stores, 3-7: k_obs_sweep_rows
     # shapes, 8: the rules kernel stores the words, k_obs_sweep_words expands,
-    # 9-13: more k_obs_sweep_rows shapes
-    for split in range(1, 14):
+    # 9-17: more k_obs_sweep_rows shapes
+    for split in range(1, 18):
         _same(_run(monkeypatch, split, B, steps), ref, f"split {split} B {B}")
 
 

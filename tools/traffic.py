@@ -56,6 +56,8 @@ def main():
     from bench import CONFIGS
     batch = batch or CONFIGS[cfg][0]
     want_obs, want_info, fused, players = CONFIGS[cfg][1], CONFIGS[cfg][2], CONFIGS[cfg][3], CONFIGS[cfg][6]
+    from bench import obs_split_active
+    split = obs_split_active(batch)
 
     dst = os.path.join(ROOT, "profiles", tag, cfg)
     os.makedirs(dst, exist_ok=True)
@@ -79,6 +81,10 @@ def main():
             return False
         if fused:
             return "k_rollout" in kn
+        if want_obs and not want_info and split:
+            # the split observation step: the rules step without tensors and
+            # the observation writer, two kernels per env step
+            return bool("k_obs_sweep" in kn or "k_step_sorted<true" in kn or "13k_step_sortedILb1E" in kn)
         if not want_obs and not want_info and ("k_step_group<" in kn or "12k_step_group" in kn):
             return True  # the rules-bound step (COUP_STEP_TPL, default 1: k_step_group<1, true>)
         m = (re.search(r"k_step<true, (\d+), \d+, (\d+)(?:, false)?>", kn) or
@@ -91,7 +97,8 @@ def main():
         for r in rows(stats[0]):
             name = r[col(r, "name")]
             if timed_kernel(name):
-                summary["timed_kernel"] = name
+                summary.setdefault("timed_kernels", []).append(name)
+                summary["timed_kernel"] = " + ".join(summary["timed_kernels"])
             if "k_step" in name or "k_rollout" in name or "k_obs" in name:
                 summary.setdefault("kernels", {})[name] = {
                     "calls": int(r[col(r, "calls")]),
@@ -124,31 +131,33 @@ def main():
                             rp = (int(r[col(r, "end", "timestamp")]) - int(r[col(r, "start", "timestamp")])) * 1e-6
                             summary["bench_vs_rocprof_kernel_ms"] = [bench["roofline"]["kernel_ms"], rp]
                             summary["rocprof_compared_dispatch"] = "the timed (last) rollout launch"
-                    elif tk and tk in summary.get("kernels", {}):
-                        # the timed window: the last `steps` dispatches of the
-                        # timed kernel (after the warm-up launches, which
-                        # include the first, cold one)
+                    elif summary.get("timed_kernels"):
+                        # the timed window: the last `steps` env steps' dispatches
+                        # of the timed kernel(s) (after the warm-up launches,
+                        # which include the first, cold one)
+                        tks = set(summary["timed_kernels"])
+                        per_step = len(tks)
                         disp = sorted((r for r in rows(os.path.join(src, "trace", "**", "*kernel_trace.csv"))
-                                       if r[col(r, "kernel", "name")] == tk),
+                                       if r[col(r, "kernel", "name")] in tks),
                                       key=lambda r: int(r[col(r, "start", "timestamp")]))
-                        window = disp[-steps:]
+                        window = disp[-steps * per_step:]
                         if window:
                             mean = sum(int(r[col(r, "end", "timestamp")]) - int(r[col(r, "start", "timestamp")])
-                                       for r in window) / len(window) * 1e-6
+                                       for r in window) / (len(window) / per_step) * 1e-6
                             # the bench times the span of the K launches / K (launch
                             # gaps included: eager launches, or a graph replay); the
                             # trace's first start to last end of the same K dispatches
                             # is that span, its mean dispatch the kernel alone
                             span = (int(window[-1][col(window[-1], "end", "timestamp")]) -
-                                    int(window[0][col(window[0], "start", "timestamp")])) / len(window) * 1e-6
+                                    int(window[0][col(window[0], "start", "timestamp")])) / (len(window) / per_step) * 1e-6
                             rp = span
                             summary["rocprof_mean_dispatch_ms"] = mean
                             summary["rocprof_launch_gap_ms"] = span - mean
                             summary["rocprof_compared_dispatch"] = (f"span of the last {len(window)} dispatches (the "
                                                                     "timed steps) / their count, as the bench times them")
                         else:
-                            rp = summary["kernels"][tk]["avg_ns"] * 1e-6
-                        summary["rocprof_all_dispatch_avg_ms"] = summary["kernels"][tk]["avg_ns"] * 1e-6
+                            rp = sum(summary["kernels"][k]["avg_ns"] for k in tks) * 1e-6
+                        summary["rocprof_all_dispatch_avg_ms"] = sum(summary["kernels"][k]["avg_ns"] for k in tks) * 1e-6
                         summary["bench_vs_rocprof_kernel_ms"] = [bench["roofline"]["kernel_ms"], rp]
 
     # plain bench lines of the same lease, before and after the profiler passes
@@ -171,19 +180,20 @@ def main():
         shutil.copy(os.path.join(src, "box.txt"), os.path.join(dst, "box.txt"))
 
     def counter(kind, cname):
-        vals = []
+        vals = {}
         for r in rows(os.path.join(src, kind, "**", "*counter_collection.csv")):
             kn = r[col(r, "kernel", "name")]
             if not timed_kernel(kn):
                 continue
             if r[col(r, "counter", "name")] != cname:
                 continue
-            vals.append((int(r[col(r, "dispatch")]), float(r[col(r, "counter", "value")])))
+            vals.setdefault(kn, []).append((int(r[col(r, "dispatch")]), float(r[col(r, "counter", "value")])))
         if not vals:
             return None
         if fused:  # the timed launch only (see above)
-            return max(vals)[1]
-        return sum(v for _, v in vals) / len(vals)
+            return sum(max(v)[1] for v in vals.values())
+        # per env step: each timed kernel's mean per dispatch, summed
+        return sum(sum(x for _, x in v) / len(v) for v in vals.values())
 
     fetch_kb = counter("fetch", "FETCH_SIZE")
     write_kb = counter("write", "WRITE_SIZE")
