@@ -157,7 +157,7 @@ def _np_step_lanes(players):
 _SPLIT_WRITERS = {1: "coup::k_obs_sweep<1>", 2: "coup::k_obs_sweep<0>", 3: "coup::k_obs_sweep_rows<256, 1>",
                   4: "coup::k_obs_sweep_rows<256, 2>", 5: "coup::k_obs_sweep_rows<128, 1>",
                   6: "coup::k_obs_sweep_rows<64, 1>", 7: "coup::k_obs_sweep_rows<512, 1>",
-                  8: "coup::k_obs_sweep_words", 9: "coup::k_obs_sweep_rows<256, 3>",
+                  9: "coup::k_obs_sweep_rows<256, 3>",
                   10: "coup::k_obs_sweep_rows<256, 4>", 11: "coup::k_obs_sweep_rows<512, 2>",
                   12: "coup::k_obs_sweep_rows<128, 4>", 13: "coup::k_obs_sweep_rows<128, 2>",
                   14: "coup::k_obs_sweep_rows<1024, 2>", 15: "coup::k_obs_sweep_rows<1024, 1>",

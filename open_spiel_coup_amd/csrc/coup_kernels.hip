@@ -205,20 +205,6 @@ __device__ __forceinline__ void write_obs_wave(float* __restrict__ wave_obs, con
 
 // 8 LDS words of a lane: the 196-bit string (row P1 at bits 0..97, row P2
 // at 98..195) in words 0..6, coins (P1 | P2 << 8) in word 7.
-__device__ __forceinline__ void obs_words(const Lane& L, uint4& x, uint4& y) {
-  const bool term = is_terminal(L);
-  uint64_t a_lo, a_hi, b_lo, b_hi;
-  obs_row_bits<0>(L, term, a_lo, a_hi);
-  obs_row_bits<1>(L, term, b_lo, b_hi);
-  x.x = (uint32_t)a_lo;
-  x.y = (uint32_t)(a_lo >> 32);
-  x.z = (uint32_t)a_hi;
-  x.w = (uint32_t)((a_hi >> 32) & 3u) | (uint32_t)(b_lo << 2);
-  y.x = (uint32_t)(b_lo >> 30);
-  y.y = (uint32_t)(b_lo >> 62) | (uint32_t)(b_hi << 2);
-  y.z = (uint32_t)(b_hi >> 30) & 0xFu;
-  y.w = L.c0 | (L.c1 << 8);
-}
 
 __device__ __forceinline__ void obs_bits_to_lds(const Lane& L, uint32_t* __restrict__ w) {
   const bool term = is_terminal(L);
@@ -467,7 +453,6 @@ struct StepArgs {
   int xcd_remap;   // block -> lane group mapping (xcd_group)
   int unchecked;   // caller actions outside LegalActions go through the reference's unchecked ApplyAction
                    // (COUP_FLAG_UNCHECKED; in-place kernels with caller actions only)
-  uint4* obs_bits; // [B][2] the post-step observation words per lane (split observation step, variant 8)
 #ifdef COUP_WAVE_TRACE
   // measurement builds only (tools/wave_trace.py): per wave, 100 MHz
   // timestamps at entry, end of the step, end of store issue, stores
@@ -477,15 +462,6 @@ struct StepArgs {
 #endif
 };
 
-// The split step's variant 8: the rules kernels store each lane's 8 words
-// (32 bytes) for k_obs_sweep_words.
-__device__ __forceinline__ void store_obs_words(const StepArgs& a, int64_t i, const Lane& L) {
-  if (!a.obs_bits) return;
-  uint4 x, y;
-  obs_words(L, x, y);
-  a.obs_bits[2 * i] = x;
-  a.obs_bits[2 * i + 1] = y;
-}
 
 
 #ifdef COUP_WAVE_TRACE
@@ -786,7 +762,6 @@ __device__ __forceinline__ void step_group_compute(const StepArgs& a, int64_t gr
       step_lane<UNIFORM, kFlow, UNCHECKED>(a, i, L, act, st, rew, ret, none);
     }
     a.state[i] = pack(L);
-    if (OBS == kObsNone) store_obs_words(a, i, L);
     ep_update(a, i, eps, st, ret);
     if (a.actions) a.actions[i] = (int8_t)act;
     if (a.rewards) {
@@ -895,7 +870,6 @@ __global__ __launch_bounds__(256) void k_step_group(StepArgs a) {
   step_lane_rng<UNIFORM, false, false>(a, i, L, act, st, rew, ret, none, rng, q == 0u);  // one count per lane
   if (q != 0u) return;
   a.state[i] = pack(L);
-  store_obs_words(a, i, L);
   ep_update(a, i, eps, st, ret);
   if (a.actions) a.actions[i] = (int8_t)act;
   if (a.rewards) {
@@ -999,39 +973,6 @@ __global__ __launch_bounds__(T) void k_obs_sweep_rows(const uint4* __restrict__ 
     v.w = f[3];
     __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(obs) + x);
   }
-}
-
-// Variant 8 of the split observation step: the expansion from the words the
-// rules kernel stored (a.obs_bits), the probe's fastest shape
-// (tools/split_probe.hip: one block per 4 KiB, non-temporal stores).
-__global__ __launch_bounds__(256) void k_obs_sweep_words(const uint4* __restrict__ words, float* __restrict__ obs,
-                                                         int64_t n) {
-  typedef float v4f __attribute__((ext_vector_type(4)));
-  constexpr uint32_t kLanes = (256u + (uint32_t)kRowF4 - 1u) / (uint32_t)kRowF4 + 1u;  // 7
-  __shared__ uint4 w4[2 * kLanes];
-  const uint32_t t = threadIdx.x;
-  const int64_t x0 = (int64_t)blockIdx.x * 256;
-  const int64_t o0 = x0 / kRowF4;
-  if (t < 2u * kLanes && o0 + (t >> 1) < n) w4[t] = words[2 * o0 + t];
-  __syncthreads();
-  const int64_t x = x0 + t;
-  if (x >= n * kRowF4) return;
-  const uint32_t* bits = reinterpret_cast<const uint32_t*>(w4);
-  const uint32_t rel = (uint32_t)(x0 - o0 * kRowF4) + t;
-  const uint32_t o = rel / (uint32_t)kRowF4, c = rel - o * (uint32_t)kRowF4;
-  const uint32_t word = bits[8u * o + (c >> 3)], coins = bits[8u * o + 7u];
-  const uint32_t nb = word >> (4u * (c & 7u));
-  v4f v;
-  v.x = (float)(nb & 1u);
-  v.y = (float)((nb >> 1) & 1u);
-  v.z = (float)((nb >> 2) & 1u);
-  v.w = (float)((nb >> 3) & 1u);
-  const float c0 = (float)(coins & 0xFFu), c1 = (float)(coins >> 8);
-  v.x = c == 15u ? c0 : v.x;
-  v.y = c == 15u ? c1 : v.y;
-  v.z = c == 39u ? c0 : v.z;
-  v.w = c == 39u ? c1 : v.w;
-  __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(obs) + x);
 }
 
 // coup_measure_step_traffic: the bytes of k_step<*, kObsWaveBitsSc1, 256,
@@ -1280,7 +1221,6 @@ __global__ __launch_bounds__(T, 8) void k_step_sorted(StepArgs a) {
   // phase 3: each thread stores its own lane
   if (!live) return;
   a.state[i] = s_rec[pos];
-  if (a.obs_bits) store_obs_words(a, i, unpack(s_rec[pos]));
   const uint32_t o = s_out[pos];
   const int32_t rew = (int32_t)((o >> 7) & 7u) - 2;
   if (a.actions) a.actions[i] = (int8_t)((int32_t)(o & 31u) - 1);
@@ -2165,8 +2105,6 @@ struct coup_env {
   size_t host_cap;
   uint8_t* host_stage;        // coup_step_host with info_state: device staging of the outputs (grown on demand)
   size_t host_stage_cap;
-  uint4* obs_words = nullptr; // [B][2] observation words of the split step's variant 8 (allocated on first use)
-  bool emit_words = false;    // the next rules step stores them
   bool batch_pending;         // an asynchronous coup_slot_ops may still read the requests
   coup_server* server;        // coup_attach_server: coup_slot_op goes through this resident wave
   bool dirty;                 // work enqueued on `stream` since its last synchronisation
@@ -2243,7 +2181,7 @@ int obs_mode() {
 
 // COUP_OBS_SPLIT: the observation step as the rules step without tensors
 // plus an address-order writer (variant 1..17: k_obs_sweep, its row-decoding
-// shapes k_obs_sweep_rows<T, S>, or k_obs_sweep_words), or the fused
+// shapes k_obs_sweep_rows<T, S>), or the fused
 // k_step<*, kObsWaveBitsSc1> (0).  Default from kObsSplitMinLanes lanes:
 // k_obs_sweep_rows<512, 2> (variant 11), 140.6-146.1 us against 160.2-161.5
 // for the fused step per 2^20-lane step in the same process (calls r04r /
@@ -2467,7 +2405,6 @@ void release(coup_env* env) {
   if (env->batch_scratch) (void)hipHostFree(env->batch_scratch);
   if (env->host_scratch) (void)hipHostFree(env->host_scratch);
   if (env->host_stage) (void)hipFree(env->host_stage);
-  if (env->obs_words) (void)hipFree(env->obs_words);
   delete env;
 }
 
@@ -2630,7 +2567,6 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
   a.err_count = env->err_count;
   a.hist = env->hist;
   a.xcd_remap = xcd_remap();
-  a.obs_bits = env->emit_words ? env->obs_words : nullptr;
 #ifdef COUP_WAVE_TRACE
   a.trace = g_trace;
 #endif
@@ -2662,11 +2598,7 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
       // observations from the post-step records in address order
       coup_step_outputs bare = *out;
       bare.obs = nullptr;
-      if (split == 8 && !env->obs_words)
-        COUP_HIP_TRY(hipMalloc(reinterpret_cast<void**>(&env->obs_words), (size_t)n * 32u));
-      env->emit_words = split == 8;
       const int r = coup_step(env, actions, &bare);
-      env->emit_words = false;
       if (r != COUP_OK) return r;
       const int64_t nf4 = n * coup::kRowF4;
       auto rows = [&](auto tt, auto ss) {
@@ -2681,7 +2613,6 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
         case 5: rows(std::integral_constant<int, 128>(), std::integral_constant<int, 1>()); break;
         case 6: rows(std::integral_constant<int, 64>(), std::integral_constant<int, 1>()); break;
         case 7: rows(std::integral_constant<int, 512>(), std::integral_constant<int, 1>()); break;
-        case 8: coup::k_obs_sweep_words<<<g, 256, 0, s>>>(env->obs_words, a.obs, n); break;
         case 9: rows(std::integral_constant<int, 256>(), std::integral_constant<int, 3>()); break;
         case 10: rows(std::integral_constant<int, 256>(), std::integral_constant<int, 4>()); break;
         case 11: rows(std::integral_constant<int, 512>(), std::integral_constant<int, 2>()); break;
