@@ -1599,6 +1599,48 @@ __global__ __launch_bounds__(kThreads) void k_info_elems(const uint4* __restrict
   reinterpret_cast<float4*>(info)[g] = info_f4(pre, hist + lane * kHist, c);
 }
 
+// The split InformationStateTensor step (COUP_INFO_SPLIT; coup_step): the
+// rules step maintaining the history without tensors, then this kernel
+// writes [B][2][2492] in address order, T x S float4 per block (S passes of
+// T float4).  The <= 2-3 lanes a block touches get their prefix words
+// (info_prefix_to_lds) and 96 history bytes into LDS from its first
+// threads; every thread then decodes its float4s with info_f4, the fused
+// writer's decode (coup_tensor.h), and stores them non-temporally.
+template <int T, int S>
+__global__ __launch_bounds__(T) void k_info_sweep(const uint4* __restrict__ state, const uint8_t* __restrict__ hist,
+                                                  float* __restrict__ info, int64_t n) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  constexpr uint32_t kLanes = ((uint32_t)(T * S) + (uint32_t)kInfoF4 - 1u) / (uint32_t)kInfoF4 + 1u;
+  constexpr uint32_t kHistU4 = (uint32_t)kHist / 16u;  // 6
+  static_assert(kLanes * kHistU4 <= (uint32_t)T, "one history uint4 per thread");
+  __shared__ uint32_t pre[kLanes * kPreWords];
+  __shared__ uint4 h4[kLanes * kHistU4];
+  const uint32_t t = threadIdx.x;
+  const int64_t x0 = (int64_t)blockIdx.x * (T * S);
+  const int64_t o0 = x0 / kInfoF4;
+  if (t < kLanes && o0 + t < n) info_prefix_to_lds(unpack(state[o0 + t]), pre + kPreWords * t);
+  if (t < kLanes * kHistU4 && o0 + t / kHistU4 < n)
+    h4[t] = reinterpret_cast<const uint4*>(hist)[o0 * kHistU4 + t];
+  __syncthreads();
+  const int64_t nf4 = n * kInfoF4;
+  const uint32_t rel0 = (uint32_t)(x0 - o0 * kInfoF4);
+  const uint8_t* hb = reinterpret_cast<const uint8_t*>(h4);
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    const int64_t x = x0 + j * T + t;
+    if (x >= nf4) break;
+    const uint32_t rel = rel0 + (uint32_t)(j * T) + t;
+    const uint32_t o = rel / (uint32_t)kInfoF4, c = rel - o * (uint32_t)kInfoF4;
+    const float4 f = info_f4(pre + kPreWords * o, hb + kHist * o, c);
+    v4f v;
+    v.x = f.x;
+    v.y = f.y;
+    v.z = f.z;
+    v.w = f.w;
+    __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(info) + x);
+  }
+}
+
 // ObservationTensor rows of the requests' lanes (coup_step_host with
 // COUP_HOST_ACTIVE): row l = lane reqs[l].lane, one thread per row.
 __global__ __launch_bounds__(kThreads) void k_obs_lanes(const uint4* __restrict__ state,
@@ -2189,6 +2231,17 @@ int obs_mode() {
 // fused step stays (the first writer lost there).  Read at every launch.
 constexpr int64_t kObsSplitMinLanes = int64_t(1) << 20;
 constexpr int kObsSplitDefault = 11;
+// COUP_INFO_SPLIT: the InformationStateTensor step as the history-keeping
+// rules step plus k_info_sweep<T, S> (1: 512 x 2, 2: 256 x 2, 3: 1024 x 2,
+// 4: 512 x 4, 5: 256 x 4), or the fused k_step<*, kObsNone, 256,
+// kInfoWrite> (0, the default until measured).  Read at every launch.
+int info_split(int64_t n) {
+  const char* e = std::getenv("COUP_INFO_SPLIT");
+  if (e) return std::atoi(e);
+  (void)n;
+  return 0;
+}
+
 int obs_split(int64_t n) {
   const char* e = std::getenv("COUP_OBS_SPLIT");
   if (e) return std::atoi(e);
@@ -2592,6 +2645,31 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
   if (info != coup::kInfoNone && mode != coup::kObsNone) mode = coup::kObsWaveBits;
   hipStream_t s = env->stream;
   const int64_t n = env->batch;
+  if (info == coup::kInfoWrite && mode == coup::kObsNone && n > 0) {
+    if (const int split = info_split(n)) {
+      // the rules step keeping the history (no tensor), then the
+      // InformationStateTensor from the new records and histories
+      coup_step_outputs bare = *out;
+      bare.info_state = nullptr;
+      const int r = coup_step(env, actions, &bare);
+      if (r != COUP_OK) return r;
+      const int64_t nf4 = n * coup::kInfoF4;
+      auto go = [&](auto tt, auto ss) {
+        constexpr int T = decltype(tt)::value, S = decltype(ss)::value;
+        coup::k_info_sweep<T, S><<<(unsigned)((nf4 + T * S - 1) / (T * S)), T, 0, s>>>(env->state, env->hist, a.info,
+                                                                                        n);
+      };
+      switch (split) {
+        case 2: go(std::integral_constant<int, 256>(), std::integral_constant<int, 2>()); break;
+        case 3: go(std::integral_constant<int, 1024>(), std::integral_constant<int, 2>()); break;
+        case 4: go(std::integral_constant<int, 512>(), std::integral_constant<int, 4>()); break;
+        case 5: go(std::integral_constant<int, 256>(), std::integral_constant<int, 4>()); break;
+        default: go(std::integral_constant<int, 512>(), std::integral_constant<int, 2>()); break;
+      }
+      COUP_HIP_TRY(hipGetLastError());
+      return COUP_OK;
+    }
+  }
   if (info == coup::kInfoNone && mode != coup::kObsNone && n > 0) {
     if (const int split = obs_split(n)) {
       // the rules step without tensors (its own kernel choice), then the

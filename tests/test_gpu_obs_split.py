@@ -84,3 +84,39 @@ def test_split_equals_fused_caller_actions(monkeypatch, unchecked):
     for split in (1, 11):
         _same(_run(monkeypatch, split, B, 20, actions_fn=actions, unchecked=unchecked, auto_reset=False), ref,
               f"caller actions split {split} unchecked={unchecked}")
+
+
+INFO_KEYS = ("actions", "rewards", "step_type", "legal_mask", "current_player", "info_state")
+
+
+def _run_info(monkeypatch, split, B, steps, seed=7, actions_fn=None):
+    monkeypatch.setenv("COUP_INFO_SPLIT", str(split))
+    env = BatchedCoupEnv(B, seed=seed, auto_reset=True, obs=False, info_state=True, history=True, device="cuda",
+                         episode_stats=True)
+    outs = []
+    for t in range(steps):
+        o = env.step(actions_fn(env, t) if actions_fn else None)
+        outs.append({k: o[k].cpu().numpy().copy() for k in INFO_KEYS})
+    eps, ret = env.episode_stats()
+    res = (outs, env.export_state().cpu().numpy(), env.export_history().cpu().numpy(), eps.cpu().numpy(),
+           ret.cpu().numpy(), env.error_count())
+    env.close()
+    return res
+
+
+@pytest.mark.parametrize("B", [3, 1000, 4099, 1 << 18])
+def test_info_split_equals_fused(monkeypatch, B):
+    """COUP_INFO_SPLIT: the history-keeping rules step, then k_info_sweep
+    writing the InformationStateTensor (coup.cc:1044-1049) in address order
+    -- every shape equal to the fused writer (k_step<*, 0, 256, kInfoWrite>)
+    bit for bit, with the histories, records and episode words."""
+    steps = 30 if B < (1 << 18) else 4
+    ref = _run_info(monkeypatch, 0, B, steps)
+    for split in (1, 2, 3, 4, 5):
+        got = _run_info(monkeypatch, split, B, steps)
+        for t, (x, y) in enumerate(zip(got[0], ref[0])):
+            for k in INFO_KEYS:
+                np.testing.assert_array_equal(x[k], y[k], err_msg=f"info split {split} B {B}: {k} at step {t}")
+        for i in range(1, 5):
+            np.testing.assert_array_equal(got[i], ref[i], err_msg=f"info split {split} B {B}: part {i}")
+        assert got[5] == ref[5]

@@ -7,7 +7,7 @@ Each positional argument is one variant: a comma-separated list of
 environment settings read by coup_step at launch (COUP_OBS_MODE,
 COUP_XCD_REMAP, COUP_STEP_DYN_LDS, COUP_REGROUP, COUP_AHEAD, COUP_EP_MODE,
 COUP_NP_SORT_THREADS, COUP_NP_RESET_INLINE, COUP_TRAJ_STAGE, COUP_NP_RESET_GROUP,
-COUP_STEP_TPL, COUP_OBS_SPLIT),
+COUP_STEP_TPL, COUP_OBS_SPLIT, COUP_INFO_SPLIT),
 plus STATS=0/1 (bind the per-episode accumulators, coup_step_outputs.
 episodes / return_sum; default 1, as bench.py) and CEIL=1 (time
 coup_measure_step_traffic -- the step's traffic with no rules -- instead of
@@ -27,7 +27,7 @@ sys.path.insert(0, ROOT)
 
 KNOBS = ("COUP_OBS_MODE", "COUP_XCD_REMAP", "COUP_STEP_DYN_LDS", "COUP_REGROUP", "COUP_AHEAD", "COUP_EP_MODE",
          "COUP_NP_SORT_THREADS", "COUP_SORT_THREADS", "COUP_NP_RESET_INLINE", "COUP_TRAJ_STAGE",
-         "COUP_NP_RESET_GROUP", "COUP_STEP_TPL", "COUP_OBS_SPLIT")
+         "COUP_NP_RESET_GROUP", "COUP_STEP_TPL", "COUP_OBS_SPLIT", "COUP_INFO_SPLIT")
 
 
 def main():
