@@ -171,6 +171,16 @@ def obs_split_active(batch):
     return int(_native.load().coup_obs_split_variant(int(batch)))
 
 
+_INFO_WRITERS = {1: "coup::k_info_sweep<512, 2>", 2: "coup::k_info_sweep<256, 2>", 3: "coup::k_info_sweep<1024, 2>",
+                 4: "coup::k_info_sweep<512, 4>", 5: "coup::k_info_sweep<256, 4>"}
+
+
+def info_split_active(batch):
+    """The split InformationStateTensor step's writer variant (0: fused)."""
+    from open_spiel_coup_amd import _native
+    return int(_native.load().coup_info_split_variant(int(batch)))
+
+
 def _writer(mode_env):
     """(ObsMode template value, block size) of the step kernel that
     coup_step launches for COUP_OBS_MODE (default 9; csrc/coup_kernels.hip)."""
@@ -612,7 +622,9 @@ def main():
         elif fused:
             kernel = "coup::k_rollout" + sorted_
         elif with_info:
-            kernel = "coup::k_step<true, 0, 256, 2, false>"
+            isplit = info_split_active(B)
+            kernel = ("coup::k_step<true, 0, 256, 1, false> + " + _INFO_WRITERS.get(isplit, "coup::k_info_sweep")
+                      if isplit else "coup::k_step<true, 0, 256, 2, false>")
         elif with_obs:
             split = obs_split_active(B) if players == 2 else 0
             if split:

@@ -410,6 +410,11 @@ int coup_measure_step_traffic(int64_t batch, uint32_t* records, const coup_step_
  * section 5).  COUP_OBS_SPLIT overrides it. */
 int coup_obs_split_variant(int64_t batch);
 
+/* The same for the InformationStateTensor step (2-player lanes with the
+ * information state and no observations): 0 the fused step kernel, > 0 the
+ * split form's k_info_sweep shape.  COUP_INFO_SPLIT overrides it. */
+int coup_info_split_variant(int64_t batch);
+
 #ifdef __cplusplus
 }
 #endif

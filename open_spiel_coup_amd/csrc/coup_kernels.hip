@@ -3457,6 +3457,8 @@ int coup_error_count(coup_env* env, int64_t* out) {
 
 int coup_obs_split_variant(int64_t batch) { return batch > 0 ? obs_split(batch) : 0; }
 
+int coup_info_split_variant(int64_t batch) { return batch > 0 ? info_split(batch) : 0; }
+
 int coup_measure_step_traffic(int64_t batch, uint32_t* records, const coup_step_outputs* out, void* hip_stream) {
   if (batch < 0 || batch > (int64_t(1) << 32)) return fail(COUP_E_INVALID, "coup_measure_step_traffic: bad batch");
   if (!records) return fail(COUP_E_INVALID, "coup_measure_step_traffic: records is null");

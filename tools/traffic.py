@@ -56,8 +56,9 @@ def main():
     from bench import CONFIGS
     batch = batch or CONFIGS[cfg][0]
     want_obs, want_info, fused, players = CONFIGS[cfg][1], CONFIGS[cfg][2], CONFIGS[cfg][3], CONFIGS[cfg][6]
-    from bench import obs_split_active
+    from bench import info_split_active, obs_split_active
     split = obs_split_active(batch)
+    isplit = info_split_active(batch)
 
     dst = os.path.join(ROOT, "profiles", tag, cfg)
     os.makedirs(dst, exist_ok=True)
@@ -81,6 +82,11 @@ def main():
             return False
         if fused:
             return "k_rollout" in kn
+        if want_info and not want_obs and isplit:
+            # the split InformationStateTensor step: the history-keeping
+            # rules step and k_info_sweep
+            m = re.search(r"k_step<true, 0, \d+, 1(?:, false)?>", kn) or re.search(r"k_stepILb1ELi0ELi\d+ELi1E", kn)
+            return bool("k_info_sweep" in kn or m)
         if want_obs and not want_info and split:
             # the split observation step: the rules step without tensors and
             # the observation writer, two kernels per env step
