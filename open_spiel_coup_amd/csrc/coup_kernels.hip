@@ -1618,7 +1618,22 @@ __global__ __launch_bounds__(T) void k_info_sweep(const uint4* __restrict__ stat
   const uint32_t t = threadIdx.x;
   const int64_t x0 = (int64_t)blockIdx.x * (T * S);
   const int64_t o0 = x0 / kInfoF4;
-  if (t < kLanes && o0 + t < n) info_prefix_to_lds(unpack(state[o0 + t]), pre + kPreWords * t);
+  if (t < 2u * kLanes && o0 + (t >> 1) < n) {
+    // info_prefix_to_lds's words, one observer row per thread, 32-bit
+    // values only (its uint2 form gave wrong prefix bits in this kernel)
+    const Lane L = unpack(state[o0 + (t >> 1)]);
+    const uint32_t p = t & 1u;
+    uint64_t lo, hi;
+    obs_row_bits_rt(L, is_terminal(L), p, lo, hi);
+    const uint64_t m62 = (1ull << 62) - 1ull;  // drop the observation's last_action bits
+    uint32_t* w = pre + kPreWords * (t >> 1);
+    w[2u * p] = (uint32_t)lo;
+    w[2u * p + 1u] = (uint32_t)((lo & m62) >> 32);
+    if (p == 0u) {
+      w[4] = L.c0 | (L.c1 << 8) | (L.move << 16);
+      w[5] = 0u;
+    }
+  }
   if (t < kLanes * kHistU4 && o0 + t / kHistU4 < n)
     h4[t] = reinterpret_cast<const uint4*>(hist)[o0 * kHistU4 + t];
   __syncthreads();
@@ -2234,12 +2249,14 @@ constexpr int kObsSplitDefault = 11;
 // COUP_INFO_SPLIT: the InformationStateTensor step as the history-keeping
 // rules step plus k_info_sweep<T, S> (1: 512 x 2, 2: 256 x 2, 3: 1024 x 2,
 // 4: 512 x 4, 5: 256 x 4), or the fused k_step<*, kObsNone, 256,
-// kInfoWrite> (0, the default until measured).  Read at every launch.
+// kInfoWrite> (0).  Default from 2^18 lanes (c3i's batch): 1024 x 2, 837 us
+// against 978 us for the fused step in the same process (call r04v,
+// profiles/r04/ab/c3i_info_split_shapes.jsonl).  Read at every launch.
+constexpr int64_t kInfoSplitMinLanes = int64_t(1) << 18;
 int info_split(int64_t n) {
   const char* e = std::getenv("COUP_INFO_SPLIT");
   if (e) return std::atoi(e);
-  (void)n;
-  return 0;
+  return n >= kInfoSplitMinLanes ? 3 : 0;
 }
 
 int obs_split(int64_t n) {
