@@ -105,7 +105,7 @@ def main():
             if timed_kernel(name):
                 summary.setdefault("timed_kernels", []).append(name)
                 summary["timed_kernel"] = " + ".join(summary["timed_kernels"])
-            if "k_step" in name or "k_rollout" in name or "k_obs" in name:
+            if "k_step" in name or "k_rollout" in name or "k_obs" in name or "k_info" in name:
                 summary.setdefault("kernels", {})[name] = {
                     "calls": int(r[col(r, "calls")]),
                     "avg_ns": float(r[col(r, "average")]),
