@@ -665,7 +665,12 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kernel,
                          "kernel_ms": launch_ms, "bytes_per_launch": bytes_per_launch,
                          "store_ceiling_ms": ceiling_ms,
-                         "frac_of_store_ceiling": (ceiling_ms / launch_ms) if ceiling_ms else None},
+                         "frac_of_store_ceiling": (ceiling_ms / launch_ms) if ceiling_ms else None,
+                         # the ceiling is the fused (lane-owned) store pattern's; the split step
+                         # writes in address order and is not bound by it
+                         "store_ceiling_form": ("fused" if ceiling_ms else None),
+                         "step_form": ("split" if (with_obs and players == 2 and obs_split_active(B)) or
+                                       (with_info and info_split_active(B)) else "fused")},
             "episodes": {"finished": ep_total, "mean_return_p0": ret_total / max(ep_total, 1),
                          "collective": ("all_gather [world*B] int16 (return sum << 8 | episodes per lane)"
                                         if width == 2 else
