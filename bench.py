@@ -161,8 +161,7 @@ _SPLIT_WRITERS = {1: "coup::k_obs_sweep<1>", 2: "coup::k_obs_sweep<0>", 3: "coup
                   10: "coup::k_obs_sweep_rows<256, 4>", 11: "coup::k_obs_sweep_rows<512, 2>",
                   12: "coup::k_obs_sweep_rows<128, 4>", 13: "coup::k_obs_sweep_rows<128, 2>",
                   14: "coup::k_obs_sweep_rows<1024, 2>", 15: "coup::k_obs_sweep_rows<1024, 1>",
-                  16: "coup::k_obs_sweep_rows<512, 3>", 17: "coup::k_obs_sweep_rows<512, 4>",
-                  18: "coup::k_obs_sweep_rows<512, 2, false>", 19: "coup::k_obs_sweep_rows<256, 2, false>"}
+                  16: "coup::k_obs_sweep_rows<512, 3>", 17: "coup::k_obs_sweep_rows<512, 4>"}
 
 
 def obs_split_active(batch):
@@ -173,8 +172,7 @@ def obs_split_active(batch):
 
 
 _INFO_WRITERS = {1: "coup::k_info_sweep<512, 2>", 2: "coup::k_info_sweep<256, 2>", 3: "coup::k_info_sweep<1024, 2>",
-                 4: "coup::k_info_sweep<512, 4>", 5: "coup::k_info_sweep<256, 4>",
-                 6: "coup::k_info_sweep<1024, 2, false>"}
+                 4: "coup::k_info_sweep<512, 4>", 5: "coup::k_info_sweep<256, 4>"}
 
 
 def info_split_active(batch):

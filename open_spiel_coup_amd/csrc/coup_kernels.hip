@@ -929,7 +929,7 @@ __global__ __launch_bounds__(256) void k_obs_sweep(const uint4* __restrict__ sta
 // block writing T x S float4 contiguous (S passes of T float4), every lane
 // decoded on two threads (one observer row each, obs_row_bits_rt) into LDS
 // as 4 words per row, each float then picked by row and bit.
-template <int T, int S, bool NT = true>
+template <int T, int S>
 __global__ __launch_bounds__(T) void k_obs_sweep_rows(const uint4* __restrict__ state, float* __restrict__ obs,
                                                       int64_t n) {
   typedef float v4f __attribute__((ext_vector_type(4)));
@@ -971,10 +971,7 @@ __global__ __launch_bounds__(T) void k_obs_sweep_rows(const uint4* __restrict__ 
     v.y = f[1];
     v.z = f[2];
     v.w = f[3];
-    if (NT)
-      __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(obs) + x);
-    else
-      reinterpret_cast<v4f*>(obs)[x] = v;
+    __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(obs) + x);
   }
 }
 
@@ -1609,7 +1606,7 @@ __global__ __launch_bounds__(kThreads) void k_info_elems(const uint4* __restrict
 // (info_prefix_to_lds) and 96 history bytes into LDS from its first
 // threads; every thread then decodes its float4s with info_f4, the fused
 // writer's decode (coup_tensor.h), and stores them non-temporally.
-template <int T, int S, bool NT = true>
+template <int T, int S>
 __global__ __launch_bounds__(T) void k_info_sweep(const uint4* __restrict__ state, const uint8_t* __restrict__ hist,
                                                   float* __restrict__ info, int64_t n) {
   typedef float v4f __attribute__((ext_vector_type(4)));
@@ -1655,10 +1652,7 @@ __global__ __launch_bounds__(T) void k_info_sweep(const uint4* __restrict__ stat
     v.y = f.y;
     v.z = f.z;
     v.w = f.w;
-    if (NT)
-      __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(info) + x);
-    else
-      reinterpret_cast<v4f*>(info)[x] = v;
+    __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(info) + x);
   }
 }
 
@@ -2687,10 +2681,6 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
         case 3: go(std::integral_constant<int, 1024>(), std::integral_constant<int, 2>()); break;
         case 4: go(std::integral_constant<int, 512>(), std::integral_constant<int, 4>()); break;
         case 5: go(std::integral_constant<int, 256>(), std::integral_constant<int, 4>()); break;
-        case 6:  // plain stores (A/B)
-          coup::k_info_sweep<1024, 2, false><<<(unsigned)((nf4 + 2047) / 2048), 1024, 0, s>>>(env->state, env->hist,
-                                                                                               a.info, n);
-          break;
         default: go(std::integral_constant<int, 512>(), std::integral_constant<int, 2>()); break;
       }
       COUP_HIP_TRY(hipGetLastError());
@@ -2727,12 +2717,6 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
         case 15: rows(std::integral_constant<int, 1024>(), std::integral_constant<int, 1>()); break;
         case 16: rows(std::integral_constant<int, 512>(), std::integral_constant<int, 3>()); break;
         case 17: rows(std::integral_constant<int, 512>(), std::integral_constant<int, 4>()); break;
-        case 18:  // plain stores (A/B)
-          coup::k_obs_sweep_rows<512, 2, false><<<(unsigned)((nf4 + 1023) / 1024), 512, 0, s>>>(env->state, a.obs, n);
-          break;
-        case 19:
-          coup::k_obs_sweep_rows<256, 2, false><<<(unsigned)((nf4 + 511) / 512), 256, 0, s>>>(env->state, a.obs, n);
-          break;
         default: coup::k_obs_sweep<1><<<g, 256, 0, s>>>(env->state, a.obs, n); break;
       }
       COUP_HIP_TRY(hipGetLastError());
