@@ -171,6 +171,15 @@ def obs_split_active(batch):
     return int(_native.load().coup_obs_split_variant(int(batch)))
 
 
+def pipelined_active(batch, players, graph):
+    """Whether the timed steps run as the pipelined split step: uniform steps
+    recorded through coup_step_many (the graph path) on a 2-player env whose
+    split step uses the shipped writer (variant 11), COUP_PIPE not 0
+    (mirrors coup_kernels.hip `pipelined`)."""
+    return (graph and players == 2 and obs_split_active(batch) == 11 and
+            os.environ.get("COUP_PIPE", "1").strip() not in ("0", ""))
+
+
 _INFO_WRITERS = {1: "coup::k_info_sweep<512, 2>", 2: "coup::k_info_sweep<256, 2>", 3: "coup::k_info_sweep<1024, 2>",
                  4: "coup::k_info_sweep<512, 4>", 5: "coup::k_info_sweep<256, 4>"}
 
@@ -501,6 +510,12 @@ def main():
     if not fused and (args.graph == "on" or (args.graph == "auto" and cfg in GRAPH_AUTO)):
         for _ in range(args.warmup):
             env.step()
+        # the warm-up's episodes out of the packed word before the capture
+        # reserves the timed steps' room in it (warm-up + K > 63
+        # folded an int16 word and the collate below refused it)
+        env.clear_episode_stats()
+        # uniform steps are recorded through coup_step_many: from 2^20 lanes
+        # with observations the pipelined split step (k_step_obs_pipe)
         graph = env.capture_steps(args.steps)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))]
     elif fused:
@@ -515,6 +530,7 @@ def main():
     else:
         for _ in range(args.warmup):
             env.step()
+        env.clear_episode_stats()  # as above: the warm-up never folds the timed steps' word
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))]
         if with_info:  # no rollout on a history env; a c3i step is ~1 ms, its launch latency noise
             gate = lambda: None  # noqa: E731
@@ -627,7 +643,10 @@ def main():
                       if isplit else "coup::k_step<true, 0, 256, 2, false>")
         elif with_obs:
             split = obs_split_active(B) if players == 2 else 0
-            if split:
+            if pipelined_active(B, players, graph is not None):
+                # one launch per step: the rules of step t + 1 beside the writer of step t
+                kernel = "coup::k_step_obs_pipe<512, 2>"
+            elif split:
                 # the rules step without tensors (regrouped from 2^18 lanes) + the writer
                 kernel = "coup::k_step_sorted<true, 512> + " + _SPLIT_WRITERS.get(split, "coup::k_obs_sweep")
             else:
@@ -669,7 +688,8 @@ def main():
                          # the ceiling is the fused (lane-owned) store pattern's; the split step
                          # writes in address order and is not bound by it
                          "store_ceiling_form": ("fused" if ceiling_ms else None),
-                         "step_form": ("split" if (with_obs and players == 2 and obs_split_active(B)) or
+                         "step_form": ("pipelined" if with_obs and pipelined_active(B, players, graph is not None)
+                                       else "split" if (with_obs and players == 2 and obs_split_active(B)) or
                                        (with_info and info_split_active(B)) else "fused")},
             "episodes": {"finished": ep_total, "mean_return_p0": ret_total / max(ep_total, 1),
                          "collective": ("all_gather [world*B] int16 (return sum << 8 | episodes per lane)"

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define COUP_ABI_VERSION 11
+#define COUP_ABI_VERSION 12
 
 #define COUP_NUM_PLAYERS 2          /* coup.h:42 */
 #define COUP_MAX_PLAYERS 6          /* N-player extension */
@@ -244,17 +244,32 @@ int coup_step_host(coup_env* env, const int8_t* actions, int want, void* host_ou
 size_t coup_step_host_layout(int64_t batch, int num_players, int want, size_t* off);
 
 /* `steps` uniform-random env steps per lane (the coup_step of actions ==
- * NULL, with the env's auto-reset setting) in ONE launch, the state kept in
- * registers, every step's outputs stored: out's actions / rewards /
- * step_type / legal_mask / cur_player point to [steps][B][...] buffers
- * (slice t = step t, laid out as coup_step's [B][...]); episodes /
- * return_sum are [B] accumulators as in coup_step.  obs / info_state must
- * be NULL, and the env must not keep histories (COUP_E_INVALID).  Results
- * equal `steps` coup_step calls -- the trajectory a learner collects
- * (rl_environment.py:282-322 per step), without the per-step launch and
- * record round trip.  From 2^18 lanes the lanes are regrouped by decision
- * every step, with the same results. */
+ * NULL, with the env's auto-reset setting), every step's outputs stored:
+ * out's actions / rewards / step_type / legal_mask / cur_player (and obs /
+ * info_state) point to [steps][B][...] buffers (slice t = step t, laid out
+ * as coup_step's [B][...]); episodes / return_sum / episode_word are [B]
+ * accumulators as in coup_step.  Results equal `steps` coup_step calls --
+ * the trajectory a learner collects (rl_environment.py:282-322 per step).
+ * Without tensors: ONE launch, the state kept in registers (the env must not
+ * keep histories, COUP_E_INVALID), lanes regrouped by decision every step
+ * from 2^18 lanes.  With obs: the pipelined split step
+ * of coup_step_many where it applies (from 2^20 lanes), else one coup_step
+ * per slice; info_state needs COUP_FLAG_HISTORY and takes coup_step per
+ * slice. */
 int coup_step_trajectory(coup_env* env, int64_t steps, const coup_step_outputs* out);
+
+/* `steps` calls of coup_step(env, NULL, out) -- uniform-random policy, every
+ * step writing the same output buffers -- as one call, with the same results
+ * (outputs of the last step, records, accumulators).  For the split
+ * observation step (2-player lanes with obs and no history, from 2^20 lanes:
+ * coup_obs_split_variant) the steps are pipelined: launch m runs the rules of
+ * step m beside the observation writer of step m - 1 (k_step_obs_pipe; the
+ * records alternate between two buffers), so the ~30 us rules kernel no
+ * longer sits between two writers.  Every other env
+ * loops over coup_step.  COUP_PIPE=0 at coup_create turns the pipeline off
+ * (A/B).  May be captured into a HIP graph (no allocation, no
+ * synchronisation). */
+int coup_step_many(coup_env* env, int64_t steps, const coup_step_outputs* out);
 
 /* `steps` uniform-random env steps per lane in one launch, state kept in
  * registers (auto-reset always on); per-lane statistics are accumulated

@@ -11,7 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # COUP_LIB_PATH: load another build of the same library (A/B timing of two
 # builds, tools/ab_builds.sh); there is still no fallback
 LIB_PATH = os.environ.get("COUP_LIB_PATH") or os.path.join(HERE, "libcoup_mi355x.so")
-ABI_VERSION = 11
+ABI_VERSION = 12
 FLAG_AUTO_RESET, FLAG_HISTORY, FLAG_GENERIC, FLAG_UNCHECKED = 1, 2, 4, 8
 MAX_PLAYERS = 6
 HISTORY_BYTES = 96
@@ -22,7 +22,7 @@ COUP_OK, COUP_E_INVALID, COUP_E_HIP, COUP_E_LANES = 0, 1, 2, 3
 SYMBOLS = (
     "coup_abi_version", "coup_last_error", "coup_create", "coup_create_ex", "coup_destroy",
     "coup_set_stream", "coup_batch", "coup_num_players", "coup_state_bytes", "coup_reset", "coup_step", "coup_rollout",
-    "coup_step_trajectory", "coup_step_host", "coup_step_host_layout",
+    "coup_step_trajectory", "coup_step_many", "coup_step_host", "coup_step_host_layout",
     "coup_new_initial_state", "coup_apply_action", "coup_query",
     "coup_export_state", "coup_import_state", "coup_export_history",
     "coup_import_history", "coup_error_count", "coup_slot_op", "coup_slot_ops", "coup_measure_step_traffic", "coup_obs_split_variant",
@@ -99,6 +99,7 @@ def load():
         "coup_step": ([vp, vp, ctypes.POINTER(StepOutputs)], i32),
         "coup_rollout": ([vp, i64, ctypes.POINTER(RolloutStats)], i32),
         "coup_step_trajectory": ([vp, i64, ctypes.POINTER(StepOutputs)], i32),
+        "coup_step_many": ([vp, i64, ctypes.POINTER(StepOutputs)], i32),
         "coup_step_host": ([vp, vp, i32, vp], i32),
         "coup_step_host_layout": ([i64, i32, i32, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_size_t),
         "coup_new_initial_state": ([vp, vp], i32),

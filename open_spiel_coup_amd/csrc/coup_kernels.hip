@@ -930,15 +930,24 @@ __global__ __launch_bounds__(256) void k_obs_sweep(const uint4* __restrict__ sta
 // decoded on two threads (one observer row each, obs_row_bits_rt) into LDS
 // as 4 words per row, each float then picked by row and bit.
 template <int T, int S>
-__global__ __launch_bounds__(T) void k_obs_sweep_rows(const uint4* __restrict__ state, float* __restrict__ obs,
-                                                      int64_t n) {
+struct ObsSweepLds {
+  static constexpr uint32_t kLanes = ((uint32_t)(T * S) + (uint32_t)kRowF4 - 1u) / (uint32_t)kRowF4 + 1u;
+  alignas(16) uint32_t rows[kLanes * 8];  // lane, row: lo.x lo.y hi.x hi.y
+  uint32_t coins[kLanes];
+};
+
+// Block `blk` of the writer (T threads): float4s [blk T S, (blk + 1) T S) of
+// the [n][2][98] buffer from the records `state`.
+template <int T, int S>
+__device__ __forceinline__ void obs_sweep_rows_block(const uint4* __restrict__ state, float* __restrict__ obs,
+                                                     int64_t n, uint32_t blk, ObsSweepLds<T, S>& lds) {
   typedef float v4f __attribute__((ext_vector_type(4)));
-  constexpr uint32_t kLanes = ((uint32_t)(T * S) + (uint32_t)kRowF4 - 1u) / (uint32_t)kRowF4 + 1u;
+  constexpr uint32_t kLanes = ObsSweepLds<T, S>::kLanes;
   static_assert(2 * kLanes <= T, "two decoding threads per lane");
-  __shared__ uint32_t rows[kLanes * 8];   // lane, row: lo.x lo.y hi.x hi.y
-  __shared__ uint32_t coins[kLanes];
+  uint32_t* rows = lds.rows;
+  uint32_t* coins = lds.coins;
   const uint32_t t = threadIdx.x;
-  const int64_t x0 = (int64_t)blockIdx.x * (T * S);
+  const int64_t x0 = (int64_t)blk * (T * S);
   const int64_t o0 = x0 / kRowF4;
   if (t < 2u * kLanes && o0 + (t >> 1) < n) {
     const Lane L = unpack(state[o0 + (t >> 1)]);
@@ -973,6 +982,13 @@ __global__ __launch_bounds__(T) void k_obs_sweep_rows(const uint4* __restrict__ 
     v.w = f[3];
     __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(obs) + x);
   }
+}
+
+template <int T, int S>
+__global__ __launch_bounds__(T) void k_obs_sweep_rows(const uint4* __restrict__ state, float* __restrict__ obs,
+                                                      int64_t n) {
+  __shared__ ObsSweepLds<T, S> lds;
+  obs_sweep_rows_block<T, S>(state, obs, n, blockIdx.x, lds);
 }
 
 // coup_measure_step_traffic: the bytes of k_step<*, kObsWaveBitsSc1, 256,
@@ -1119,19 +1135,34 @@ __device__ __forceinline__ uint32_t regroup_key(const Lane& L, uint32_t x) {
 // decision and resolves the deals; finished lanes are listed and dealt their
 // next episode by the block's first threads.  Phase 3: each thread stores
 // its own lane's record and outputs, coalesced.  Same results as k_step.
-template <bool UNIFORM, int T = kThreads>
-__global__ __launch_bounds__(T, 8) void k_step_sorted(StepArgs a) {
+template <int T>
+struct SortStepLds {
+  uint4 rec[T];
+  uint32_t meta[T];   // slot -> owner thread | key << kO | st << kO + 5
+  uint32_t out[T];    // slot -> act + 1 | st << 5 | (rew + 2) << 7 | (ret + 2) << 10 | cp << 24
+  uint32_t legal[T];  // slot -> post-step legal mask
+  uint32_t reset[T];  // slots whose lane auto-resets
+  alignas(16) uint32_t bin[32];  // read as uint4 by bins_below
+  uint32_t nreset;
+};
+
+// Block `blk` of the regrouped step: lanes [blk T, (blk + 1) T) read from
+// a.state and written to rec_out (a.state itself, or the other record buffer
+// of the pipelined step, coup_step_many).
+template <bool UNIFORM, int T>
+__device__ __forceinline__ void step_sorted_block(const StepArgs& a, uint32_t blk, uint4* rec_out,
+                                                  SortStepLds<T>& lds) {
   static_assert((T & (T - 1)) == 0 && T >= 64 && T <= 1024, "power-of-two block of whole waves");
   constexpr uint32_t kO = T <= 256 ? 8u : 10u;  // owner-thread bits of s_meta
-  __shared__ uint4 s_rec[T];
-  __shared__ uint32_t s_meta[T];   // slot -> owner thread | key << kO | st << kO + 5
-  __shared__ uint32_t s_out[T];    // slot -> act + 1 | st << 5 | (rew + 2) << 7 | (ret + 2) << 10 | cp << 24
-  __shared__ uint32_t s_legal[T];  // slot -> post-step legal mask
-  __shared__ uint32_t s_reset[T];  // slots whose lane auto-resets
-  __shared__ uint32_t s_bin[32];
-  __shared__ uint32_t s_nreset;
+  uint4* s_rec = lds.rec;
+  uint32_t* s_meta = lds.meta;
+  uint32_t* s_out = lds.out;
+  uint32_t* s_legal = lds.legal;
+  uint32_t* s_reset = lds.reset;
+  uint32_t* s_bin = lds.bin;
+  uint32_t& s_nreset = lds.nreset;
   const uint32_t t = threadIdx.x;
-  const int64_t base = (int64_t)blockIdx.x * T;
+  const int64_t base = (int64_t)blk * T;
   const int64_t i = base + t;
   const bool live = i < a.n;
   if (t < 32u) s_bin[t] = 0u;
@@ -1220,7 +1251,7 @@ __global__ __launch_bounds__(T, 8) void k_step_sorted(StepArgs a) {
 
   // phase 3: each thread stores its own lane
   if (!live) return;
-  a.state[i] = s_rec[pos];
+  rec_out[i] = s_rec[pos];
   const uint32_t o = s_out[pos];
   const int32_t rew = (int32_t)((o >> 7) & 7u) - 2;
   if (a.actions) a.actions[i] = (int8_t)((int32_t)(o & 31u) - 1);
@@ -1232,6 +1263,55 @@ __global__ __launch_bounds__(T, 8) void k_step_sorted(StepArgs a) {
   if (a.legal) a.legal[i] = s_legal[pos];
   if (a.cur_player) a.cur_player[i] = (int8_t)(o >> 24);
   ep_update(a, i, eps, (o >> 5) & 3u, (int32_t)((o >> 10) & 7u) - 2);
+}
+
+template <bool UNIFORM, int T = kThreads>
+__global__ __launch_bounds__(T, 8) void k_step_sorted(StepArgs a) {
+  __shared__ SortStepLds<T> lds;
+  step_sorted_block<UNIFORM, T>(a, blockIdx.x, a.state, lds);
+}
+
+// The pipelined split observation step (coup_step_many; DESIGN.md section
+// 5): ONE launch holds the rules blocks of step t+1 (step_sorted_block,
+// uniform policy: records rules_in -> rules_out) and the observation-writer
+// blocks of step t (obs_sweep_rows_block over the records rules_in, the
+// post-step records of step t).  The two read the same records and write
+// disjoint buffers, so no block waits for another; the rules no longer sit
+// on the path between two writers.  Rules block k sits at block position
+// k * stride (stride >= 1, k < rules_blocks), every other position is the
+// next writer block in address order, so the rules spread over the first
+// positions of the launch while the writer sweeps the buffer.  With
+// rules_blocks == 0 or writer_blocks == 0 the launch is one role only (the
+// pipeline's first and last launches).
+struct PipeArgs {
+  StepArgs a;               // the rules step; a.state = its input records (rules_in)
+  uint4* rules_out;         // its output records: a.state (in place) or the other buffer
+  const uint4* obs_state;   // the writer's records
+  float* obs;               // [n][2][98]
+  uint32_t rules_blocks, writer_blocks, stride;
+};
+
+template <int T, int S>
+__global__ __launch_bounds__(T, 8) void k_step_obs_pipe(PipeArgs p) {
+  __shared__ union PipeLds {
+    SortStepLds<T> rules;
+    ObsSweepLds<T, S> writer;
+  } lds;
+  const uint32_t b = blockIdx.x;
+  uint32_t role_rules, idx;
+  if (p.writer_blocks == 0u) {
+    role_rules = 1u, idx = b;
+  } else if (p.rules_blocks == 0u) {
+    role_rules = 0u, idx = b;
+  } else {
+    const uint32_t k = b / p.stride;
+    role_rules = (b == k * p.stride && k < p.rules_blocks) ? 1u : 0u;
+    idx = role_rules ? k : b - min(k + 1u, p.rules_blocks);
+  }
+  if (role_rules)
+    step_sorted_block<true, T>(p.a, idx, p.rules_out, lds.rules);
+  else
+    obs_sweep_rows_block<T, S>(p.obs_state, p.obs, p.a.n, idx, lds.writer);
 }
 
 // The decision key of a lane at a decision node: the uniform policy's draw,
@@ -2166,6 +2246,9 @@ struct coup_env {
   coup_server* server;        // coup_attach_server: coup_slot_op goes through this resident wave
   bool dirty;                 // work enqueued on `stream` since its last synchronisation
   hipEvent_t stream_event;    // coup_set_stream: orders a new stream after the old one's pending work
+  uint4* state2;              // 2 players: the second record buffer of the pipelined step (coup_step_many)
+  int pipe;                   // coup_step_many pipelines the split observation step (COUP_PIPE, read at create)
+  double pipe_span;           // rules blocks spread over this fraction of a pipelined launch (COUP_PIPE_SPAN)
 };
 
 // coup_server (coup_mi355x.h; kernel coup::k_server).  The ring, the control
@@ -2264,6 +2347,14 @@ int obs_split(int64_t n) {
   if (e) return std::atoi(e);
   return n >= kObsSplitMinLanes ? kObsSplitDefault : 0;
 }
+
+// The pipelined form of the split step (coup_step_many,
+// coup::k_step_obs_pipe): the shipped split kernels' bodies, the regrouped
+// 512-lane rules step and the 512 x 2 writer (variant 11).
+constexpr int kPipeT = 512, kPipeS = 2;
+// rules blocks spread over the first kPipeSpanDefault of a pipelined
+// launch's block positions (COUP_PIPE_SPAN, read at coup_create)
+constexpr double kPipeSpanDefault = 0.85;
 
 // COUP_XCD_REMAP=0 turns off the XCD-aware block -> lane group mapping of
 // the step kernel (coup::xcd_group; A/B measurements).
@@ -2469,6 +2560,7 @@ namespace {
 
 void release(coup_env* env) {
   (void)hipFree(env->state);
+  (void)hipFree(env->state2);
   (void)hipFree(env->hist);
   (void)hipFree(env->err_count);
   if (env->slot_scratch) (void)hipHostFree(env->slot_scratch);
@@ -2531,8 +2623,20 @@ int coup_create_ex(int64_t batch, uint64_t seed, uint32_t env_id_base, int flags
   env->host_stage_cap = 0;
   env->server = nullptr;
   env->dirty = false;
+  env->stream_event = nullptr;
+  env->state2 = nullptr;
+  {
+    const char* e = std::getenv("COUP_PIPE");
+    env->pipe = e ? std::atoi(e) : 1;
+    const char* f = std::getenv("COUP_PIPE_SPAN");
+    const double v = f ? std::atof(f) : kPipeSpanDefault;
+    env->pipe_span = (v > 0.0 && v <= 1.0) ? v : kPipeSpanDefault;
+  }
   const size_t lanes = (size_t)(batch > 0 ? batch : 1);
   hipError_t e = hipMalloc(&env->state, lanes * sizeof(uint4) * (generic ? 2 : 1));
+  // the pipelined step's second record buffer (allocated here: coup_step_many
+  // may be captured into a HIP graph, where no allocation may happen)
+  if (e == hipSuccess && !generic) e = hipMalloc(&env->state2, lanes * sizeof(uint4));
   if (e == hipSuccess) e = hipMalloc(&env->err_count, sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemset(env->err_count, 0, sizeof(uint32_t));
   if (e == hipSuccess && (flags & COUP_FLAG_HISTORY)) {
@@ -2620,6 +2724,12 @@ uint64_t* coup_debug_get_trace() { return g_trace; }
 int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out) {
   COUP_CHECK_ENV(env);
   if (env->batch == 0) return COUP_OK;
+  {
+    // the accumulators are checked here for both engines (the N-player
+    // launch relies on it)
+    coup::EpAcc ep;
+    if (const char* why = coup::ep_acc_of(out, ep)) return fail(COUP_E_INVALID, std::string("coup_step: ") + why);
+  }
   COUP_TRY(launching(env));
   if (env->generic) {
     if (out && out->info_state) return fail(COUP_E_INVALID, "coup_step: info_state is 2-player only");
@@ -2821,6 +2931,10 @@ int coup_rollout(coup_env* env, int64_t steps, const coup_rollout_stats* stats) 
   COUP_CHECK_ENV(env);
   if (steps < 0) return fail(COUP_E_INVALID, "coup_rollout: negative steps");
   if (env->hist) return fail(COUP_E_INVALID, "coup_rollout: not available on an env with COUP_FLAG_HISTORY");
+  if (stats) {
+    coup::EpAcc ep;  // checked for both engines (the N-player launch relies on it)
+    if (const char* why = coup::ep_acc_of(stats, ep)) return fail(COUP_E_INVALID, std::string("coup_rollout: ") + why);
+  }
   if (env->batch == 0 || steps == 0) return COUP_OK;
   COUP_TRY(launching(env));
   if (env->generic) return np_result(coup::np::launch_rollout(np_env(env), steps, stats), "coup_rollout");
@@ -2966,14 +3080,136 @@ int coup_step_host(coup_env* env, const int8_t* actions, int want, void* host_ou
   return COUP_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// coup_step_many / coup_step_trajectory with observations: can the steps
+// run as the pipelined split step?  Uniform policy, 2 players, no history,
+// observations and no information state, and the split step with the
+// shipped writer is this batch's form (from 2^20 lanes, or COUP_OBS_SPLIT).
+bool pipelined(const coup_env* env, const coup_step_outputs* out) {
+  return env->pipe != 0 && !env->generic && !env->hist && env->state2 && out && out->obs && !out->info_state &&
+         obs_split(env->batch) == kObsSplitDefault;
+}
+
+// Output slice t of a [steps][B][...] coup_step_outputs (the accumulators
+// are [B] and not sliced).
+coup_step_outputs slice_outputs(const coup_step_outputs& o, int64_t B, int64_t P, int64_t t) {
+  coup_step_outputs s = o;
+  if (o.actions) s.actions = o.actions + t * B;
+  if (o.rewards) s.rewards = o.rewards + t * B * P;
+  if (o.step_type) s.step_type = o.step_type + t * B;
+  if (o.legal_mask) s.legal_mask = o.legal_mask + t * B;
+  if (o.cur_player) s.cur_player = o.cur_player + t * B;
+  if (o.obs) s.obs = o.obs + t * B * P * 49 * P;  // [B][P][49 P] (98 per player at P = 2)
+  if (o.info_state) s.info_state = o.info_state + t * B * 2 * COUP_INFO_STATE_SIZE;
+  return s;
+}
+
+// `steps` uniform split steps as steps + 1 launches of k_step_obs_pipe:
+// launch m runs the rules of step m (m < steps) beside the observation
+// writer of step m - 1 (m >= 1).  Both read the records after step m - 1;
+// the rules write the records of step m to the other buffer, so the
+// records ping-pong between env->state and env->state2.  With an odd step
+// count the first rules launch (no writer beside it) runs in place, so the
+// last records always land in env->state.  Results -- outputs, records,
+// accumulators -- equal `steps` coup_step calls; `slices`: step t's outputs
+// go to slice t of [steps][B][...] buffers, else every step overwrites out's.
+int step_many_pipelined(coup_env* env, int64_t steps, const coup_step_outputs* out, bool slices) {
+  const int64_t n = env->batch;
+  coup::PipeArgs p;
+  std::memset(&p, 0, sizeof(p));
+  coup::StepArgs& a = p.a;
+  a.n = n;
+  a.seed_lo = (uint32_t)env->seed;
+  a.seed_hi = (uint32_t)(env->seed >> 32);
+  a.env_id_base = env->env_id_base;
+  a.auto_reset = (env->flags & COUP_FLAG_AUTO_RESET) ? 1 : 0;
+  a.err_count = env->err_count;
+  (void)coup::ep_acc_of(out, a.ep);  // validated by the caller
+  const uint32_t R = (uint32_t)((n + kPipeT - 1) / kPipeT);
+  const uint32_t W = (uint32_t)((n * coup::kRowF4 + kPipeT * kPipeS - 1) / (kPipeT * kPipeS));
+  uint4* const X = env->state;
+  uint4* const Y = env->state2;
+  uint4* cur = X;  // the records after the last rules launch
+  for (int64_t m = 0; m <= steps; ++m) {
+    const bool rules = m < steps, writer = m >= 1;
+    uint4* next = cur;
+    if (rules) {
+      const coup_step_outputs o = slices ? slice_outputs(*out, n, 2, m) : *out;
+      a.state = cur;
+      a.actions = o.actions;
+      a.rewards = o.rewards;
+      a.step_type = o.step_type;
+      a.legal = o.legal_mask;
+      a.cur_player = o.cur_player;
+      next = (m == 0 && (steps & 1)) ? cur : (cur == X ? Y : X);
+      p.rules_out = next;
+    }
+    p.rules_blocks = rules ? R : 0u;
+    p.writer_blocks = writer ? W : 0u;
+    p.obs_state = cur;
+    p.obs = writer ? out->obs + (slices ? (m - 1) * n * 2 * COUP_OBS_SIZE : 0) : nullptr;
+    const uint32_t total = p.rules_blocks + p.writer_blocks;
+    p.stride = (rules && writer) ? std::max<uint32_t>(1u, (uint32_t)(env->pipe_span * total / R)) : 1u;
+    coup::k_step_obs_pipe<kPipeT, kPipeS><<<total, kPipeT, 0, env->stream>>>(p);
+    COUP_HIP_TRY(hipGetLastError());
+    cur = next;
+  }
+  if (cur != X) return fail(COUP_E_HIP, "coup_step_many: internal error (records left in the second buffer)");
+  return COUP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int coup_step_many(coup_env* env, int64_t steps, const coup_step_outputs* out) {
+  COUP_CHECK_ENV(env);
+  if (steps < 0) return fail(COUP_E_INVALID, "coup_step_many: negative steps");
+  if (out && out->info_state && !env->hist)
+    return fail(COUP_E_INVALID, "coup_step_many: info_state needs an env created with COUP_FLAG_HISTORY");
+  {
+    coup::EpAcc ep;
+    if (const char* why = coup::ep_acc_of(out, ep)) return fail(COUP_E_INVALID, std::string("coup_step_many: ") + why);
+  }
+  if (env->batch == 0 || steps == 0) return COUP_OK;
+  if (pipelined(env, out)) {
+    COUP_TRY(launching(env));
+    return step_many_pipelined(env, steps, out, false);
+  }
+  for (int64_t k = 0; k < steps; ++k) COUP_TRY(coup_step(env, nullptr, out));
+  return COUP_OK;
+}
+
 int coup_step_trajectory(coup_env* env, int64_t steps, const coup_step_outputs* out) {
   COUP_CHECK_ENV(env);
   if (steps < 0) return fail(COUP_E_INVALID, "coup_step_trajectory: negative steps");
+  if (out && (out->obs || out->info_state)) {
+    // with tensors: the pipelined split step where it applies (from 2^20
+    // lanes), else one coup_step per slice.  (A one-launch form writing obs
+    // every step measured slower than per-step launches: 196 vs 162 us per
+    // 2^20-lane step)
+    if (out->info_state && !env->hist)
+      return fail(COUP_E_INVALID, "coup_step_trajectory: info_state needs an env created with COUP_FLAG_HISTORY");
+    {
+      coup::EpAcc ep;
+      if (const char* why = coup::ep_acc_of(out, ep))
+        return fail(COUP_E_INVALID, std::string("coup_step_trajectory: ") + why);
+    }
+    if (env->batch == 0 || steps == 0) return COUP_OK;
+    if (pipelined(env, out)) {
+      COUP_TRY(launching(env));
+      return step_many_pipelined(env, steps, out, true);
+    }
+    for (int64_t t = 0; t < steps; ++t) {
+      const coup_step_outputs o = slice_outputs(*out, env->batch, env->players, t);
+      COUP_TRY(coup_step(env, nullptr, &o));
+    }
+    return COUP_OK;
+  }
   if (env->hist) return fail(COUP_E_INVALID, "coup_step_trajectory: not available on an env with COUP_FLAG_HISTORY");
-  // (a 2-player form writing obs every step measured slower than per-step
-  // launches: 196 vs 162 us per 2^20-lane step)
-  if (out && (out->obs || out->info_state))
-    return fail(COUP_E_INVALID, "coup_step_trajectory: obs / info_state are written by coup_step only");
   {
     coup::EpAcc ep;
     if (const char* why = coup::ep_acc_of(out, ep))

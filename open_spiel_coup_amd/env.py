@@ -315,12 +315,24 @@ class BatchedCoupEnv:
             self._ep_fold = None
             self._ep_steps = 0
 
+    def step_many(self, steps):
+        """`steps` uniform-policy env steps as one call (coup_step_many): the
+        same results as `steps` step() calls -- the output buffers hold the
+        last step's outputs.  From 2^20 lanes with observations the steps
+        are pipelined (the rules of step t + 1 beside the observation writer
+        of step t)."""
+        self._bind_stream()
+        self._ep_reserve(int(steps))
+        _native.check(self.lib.coup_step_many(self._h, int(steps), ctypes.byref(self._out)))
+
     def capture_steps(self, steps, actions=None):
         """Record `steps` batched env steps (uniform policy, or the fixed
         `actions` tensor every step) as one HIP graph; `graph.replay()` then
         runs them with a single launch, writing the usual output buffers.
         Removes the per-step host overhead where a step's kernel is short
-        (small B).  The env must outlive the graph."""
+        (small B).  Uniform steps are recorded through coup_step_many (the
+        pipelined split step where it applies).  The env must outlive the
+        graph."""
         a = None
         if actions is not None:
             actions = actions.to(device=self.device, dtype=torch.int8).contiguous()
@@ -332,8 +344,11 @@ class BatchedCoupEnv:
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.graph(g, stream=side):
             self._bind_stream()
-            for _ in range(int(steps)):
-                _native.check(self.lib.coup_step(self._h, a, ctypes.byref(self._out)))
+            if a is None:
+                _native.check(self.lib.coup_step_many(self._h, int(steps), ctypes.byref(self._out)))
+            else:
+                for _ in range(int(steps)):
+                    _native.check(self.lib.coup_step(self._h, a, ctypes.byref(self._out)))
         torch.cuda.current_stream(self.device).wait_stream(side)
         self._bind_stream()
         return g
@@ -360,11 +375,11 @@ class BatchedCoupEnv:
                                       "info_state")], *self._ep_fields())
 
     def _fused_trajectory(self, buf):
-        """Whether coup_step_trajectory can write `buf` in one launch: no
-        observation / info-state tensors, no history.  (A one-launch form
-        with observations measured slower than per-step launches at 2^20
-        lanes)"""
-        return not self.history and "obs" not in buf and "info_state" not in buf
+        """Whether coup_step_trajectory takes `buf` in one call: always with
+        tensors (the library pipelines the split observation step from 2^20
+        lanes, else runs one coup_step per slice); without them only on an
+        env without history (its one-launch kernels keep none)."""
+        return "obs" in buf or "info_state" in buf or not self.history
 
     def _trajectory_outputs(self, buf):
         return _native.StepOutputs(*[_addr(buf[k]) if k in buf else None for k in
@@ -373,10 +388,12 @@ class BatchedCoupEnv:
 
     def collect_trajectory(self, steps, buf=None):
         """`steps` uniform-policy env steps whose outputs land in slice t of
-        [T, B, ...] device buffers (trajectory_buffers); returns them.  Without
-        observation tensors or history the T steps run as ONE launch
-        (coup_step_trajectory, state in registers); otherwise one coup_step
-        per slice.  Same results either way."""
+        [T, B, ...] device buffers (trajectory_buffers); returns them.  One
+        coup_step_trajectory call: without tensors or history ONE launch
+        (state in registers); with observations the pipelined split step from
+        2^20 lanes, else one coup_step per slice inside the library.  A
+        history env without tensors takes one coup_step per slice here.  Same
+        results either way."""
         buf = buf if buf is not None else self.trajectory_buffers(steps)
         self._bind_stream()
         self._ep_reserve(int(steps))
@@ -393,7 +410,7 @@ class BatchedCoupEnv:
         """collect_trajectory(steps, buf) as a zero-argument callable that only
         enqueues the one coup_step_trajectory launch (timing loops)."""
         if not self._fused_trajectory(buf):
-            raise ValueError("coup_step_trajectory writes no obs / info_state and needs an env without history")
+            raise ValueError("coup_step_trajectory without tensors needs an env without history")
         self._bind_stream()
         out = self._trajectory_outputs(buf)
         fn, h, k, ref = self.lib.coup_step_trajectory, self._h, int(steps), ctypes.byref(out)

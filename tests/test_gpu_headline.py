@@ -1,21 +1,25 @@
 """The bench's own kernels at the bench's own sizes, against the oracle.
 
-bench.py's c3 line (the BASELINE metric) runs k_step<true, 9, 256, 0> --
-the branch-form transition (apply_decision_v1) with the wave-cooperative
-sc1 observation writer -- over 2^20 lanes: settle through the fused rollout,
-W warm-up steps, then K steps replayed from one HIP graph
-(BatchedCoupEnv.capture_steps).  c3i runs k_step<true, 0, 256, 2> (history +
-InformationStateTensor) over 2^18 lanes with eager launches.  The oracle
-cannot afford 2^20 lanes per step, but lanes are independent and keyed by
-their global env id, so three 256-lane slices --
-the start, an odd offset in the middle, the end -- are checked against the
-oracle run on those env ids alone, at every timed step: actions, rewards,
-step types, legal masks, current players, both tensors of every lane, and
-the full 16-byte records (word 3: turn_number_ and episode bits, the word the
-code-generation hazard of DESIGN.md section 12 corrupted) and per-episode
-accumulators at the phase boundaries.  Reference semantics: coup.cc:248-287
-(ObservationTensor), :230-245 (InformationStateTensor), :522-808 (the
-transition)."""
+bench.py's c3 line (the BASELINE metric) runs the split observation step
+over 2^20 lanes: settle through the fused rollout, W warm-up steps, then K
+steps replayed from one HIP graph (BatchedCoupEnv.capture_steps), which
+records coup_step_many -- the pipelined form, k_step_obs_pipe<512, 2>: the
+regrouped rules of step t + 1 (k_step_sorted's body, the branch-form
+transition apply_decision_v1) beside the address-order observation writer
+of step t (k_obs_sweep_rows' body).  Its timed region keeps only the last
+step's tensors, so the same launches also run as a trajectory whose every
+step lands in its own [T][B][2][98] slice, checked step by step.  c3i runs
+the history-keeping rules step and k_info_sweep<1024, 2> over 2^18 lanes
+with eager launches.  The oracle cannot afford 2^20 lanes per step, but
+lanes are independent and keyed by their global env id (DESIGN.md section
+4), so three 256-lane slices -- the start, an odd offset in the middle, the
+end -- are checked against the oracle run on those env ids alone, at every
+timed step: actions, rewards, step types, legal masks, current players,
+both tensors of every lane, and the full 16-byte records (word 3:
+turn_number_ and episode bits, the word the code-generation hazard of
+DESIGN.md section 12 corrupted) and per-episode accumulators at the phase
+boundaries.  Reference semantics: coup.cc:248-287 (ObservationTensor),
+:230-245 (InformationStateTensor), :522-808 (the transition)."""
 import numpy as np
 import pytest
 import torch
@@ -86,14 +90,16 @@ def _check_records(env, B, seed, steps, stats_from=None):
 def test_c3_headline_kernel_full_batch_slices_match_oracle():
     """bench.py --config c3 at its size: 2^20 lanes, obs x2, settle 256 +
     warm-up 5, then K = 20 eager coup_step launches, K = 20 replays of a
-    1-step graph (each step checked), and one replay of a K = 20-step graph
-    (bench.py's timed region; its last step and the records checked)."""
-    B, seed, settle, warm, K = 1 << 20, 1, 256, 5, 20
+    1-step graph (each step checked), one replay of a K = 20-step graph
+    (bench.py's timed region, the pipelined coup_step_many; its last step and
+    the records checked), and the same pipeline as a TK-step trajectory with
+    every step's observations in their own slice (each step checked)."""
+    B, seed, settle, warm, K, TK = 1 << 20, 1, 256, 5, 20, 10
     # the bench's accumulators: the packed int16 word at K = 20 (bench.payload_width)
     env = BatchedCoupEnv(B, seed=seed, env_id_base=0, auto_reset=True, obs=True,
                          episode_stats=bench.episode_stats_mode(bench.payload_width(2, K, B)))
     assert env.episode_word_bytes == 2
-    total = settle + warm + 3 * K
+    total = settle + warm + 3 * K + TK
     refs = {k: oracle.rollout(seed=seed, n=256, steps=total, env_id_base=k, auto_reset=True, want_obs=True)
             for k in _slices(B)}
     env.rollout(settle)
@@ -122,6 +128,19 @@ def test_c3_headline_kernel_full_batch_slices_match_oracle():
     t += K
     for k, ref in refs.items():
         _check_step(o, ref, t - 1, k, "obs")
+    _check_records(env, B, seed, t, stats_from=settle + warm)
+    # the pipelined launches with a slice per step (coup_step_trajectory):
+    # every step's tensors, not only the last (the packed word has taken 60
+    # steps of replays its reserve count did not see: fold it first)
+    env.fold_episode_stats()
+    buf = env.collect_trajectory(TK)
+    torch.cuda.synchronize()
+    for s in range(TK):
+        o_s = {name: buf[name][s] for name in ("actions", "rewards", "step_type", "legal_mask", "obs")}
+        for k, ref in refs.items():
+            _check_step(o_s, ref, t, k, "obs")
+        t += 1
+    del buf
     _check_records(env, B, seed, t, stats_from=settle + warm)
     assert t == total
     assert env.error_count() == 0

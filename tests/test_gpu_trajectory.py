@@ -70,21 +70,34 @@ def test_trajectory_graph_and_full_batch(players):
     assert torch.equal(a.episodes, b.episodes) and torch.equal(a.return_sum, b.return_sum)
 
 
-def test_trajectory_rejects_what_it_cannot_write():
-    env = BatchedCoupEnv(64, seed=1, obs=True)
-    buf = env.trajectory_buffers(4)
-    out = _native.StepOutputs(*[buf[k].data_ptr() if k in buf else None for k in
-                                ("actions", "rewards", "step_type", "legal_mask", "current_player", "obs",
-                                 "info_state")], None, None)
-    assert env.lib.coup_step_trajectory(env._h, 4, ctypes.byref(out)) == _native.COUP_E_INVALID
-    hist = BatchedCoupEnv(64, seed=1, obs=False, info_state=True)
-    hb = hist.trajectory_buffers(4)
-    assert "info_state" in hb and not hist._fused_trajectory(hb)
+def test_trajectory_with_tensors_and_refusals():
+    """With observation / information-state slices coup_step_trajectory runs
+    one coup_step per slice inside the library (the pipelined split step
+    from 2^20 lanes: tests/test_gpu_pipeline.py), equal to stepping slice by
+    slice; a history env without tensors and negative steps are refused."""
+    kw = dict(seed=1, obs=True, episode_stats=True)
+    env, ref = BatchedCoupEnv(64, **kw), BatchedCoupEnv(64, **kw)
+    buf, rb = env.trajectory_buffers(4), ref.trajectory_buffers(4)
+    assert env._fused_trajectory(buf)
+    env.collect_trajectory(4, buf)
+    _stepped(ref, 4, rb)
+    for k in KEYS + ("obs",):
+        assert torch.equal(buf[k], rb[k]), k
+    assert torch.equal(env.export_state(), ref.export_state())
+    hist = BatchedCoupEnv(64, seed=1, obs=False, info_state=True, episode_stats=True)
+    href = BatchedCoupEnv(64, seed=1, obs=False, info_state=True, episode_stats=True)
+    hb, hr = hist.trajectory_buffers(4), href.trajectory_buffers(4)
+    assert "info_state" in hb and hist._fused_trajectory(hb)
+    hist.collect_trajectory(4, hb)
+    _stepped(href, 4, hr)
+    for k in KEYS + ("info_state",):
+        assert torch.equal(hb[k], hr[k]), k
     assert hist.lib.coup_step_trajectory(hist._h, 4, None) == _native.COUP_E_INVALID
     assert env.lib.coup_step_trajectory(env._h, -1, None) == _native.COUP_E_INVALID
-    # with obs the Python API falls back to one coup_step per slice
-    env.collect_trajectory(4, buf)
-    assert (buf["step_type"] <= 2).all()
+    bad = _native.StepOutputs(buf["actions"].data_ptr(), None, None, None, None, None, None,
+                              env.episodes.data_ptr(), None, None, 0)  # episodes without return_sum
+    assert env.lib.coup_step_trajectory(env._h, 4, ctypes.byref(bad)) == _native.COUP_E_INVALID
+    assert env.lib.coup_step_many(env._h, 4, ctypes.byref(bad)) == _native.COUP_E_INVALID
 
 
 @pytest.mark.parametrize("n", [1501, 1502, 1503, 2048])

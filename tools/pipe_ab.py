@@ -1,0 +1,84 @@
+"""Same-process A/B of the c3 step forms in the driver's own form (a HIP
+graph of K uniform steps, the packed int16 episode word, 2^20 lanes after
+the settle), variants interleaved round-robin.
+
+    python tools/pipe_ab.py [--batch B] [--steps K] [--rounds R] NAME:VAR=VAL[,...] ...
+
+Each positional argument is one env created with those environment settings
+(knobs read at coup_create, e.g. COUP_PIPE, COUP_PIPE_SPAN; or per launch,
+e.g. COUP_OBS_SPLIT) and captured with BatchedCoupEnv.capture_steps(K).
+Default variants: the fused step, the serial split step (COUP_PIPE=0) and
+the pipelined step at three spreads of its rules blocks.  Prints one JSON
+line per variant: median / min us per env step.  Measurement tool only.
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+DEFAULT = ["fused:COUP_OBS_SPLIT=0", "serial:COUP_PIPE=0", "pipe85:COUP_PIPE_SPAN=0.85",
+           "pipe60:COUP_PIPE_SPAN=0.6", "pipe100:COUP_PIPE_SPAN=1.0"]
+KNOBS = ("COUP_PIPE", "COUP_PIPE_SPAN", "COUP_OBS_SPLIT", "COUP_OBS_MODE")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=1 << 20)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=9)
+    ap.add_argument("--settle", type=int, default=256)
+    ap.add_argument("variants", nargs="*")
+    a = ap.parse_args()
+    import torch
+
+    import bench
+    from open_spiel_coup_amd import BatchedCoupEnv
+    variants = a.variants or DEFAULT
+    envs, graphs = {}, {}
+    for v in variants:
+        name, _, kvs = v.partition(":")
+        for k in KNOBS:
+            os.environ.pop(k, None)
+        for kv in kvs.split(","):
+            if kv:
+                k, val = kv.split("=")
+                os.environ[k] = val
+        env = BatchedCoupEnv(a.batch, seed=1, auto_reset=True, obs=True, device="cuda:0",
+                             episode_stats=bench.episode_stats_mode(bench.payload_width(2, a.steps, a.batch)))
+        env.rollout(a.settle)
+        for _ in range(5):
+            env.step()
+        env.clear_episode_stats()
+        graphs[name] = env.capture_steps(a.steps)
+        envs[name] = env
+    for k in KNOBS:
+        os.environ.pop(k, None)
+    stream = torch.cuda.current_stream()
+    times = {n: [] for n in graphs}
+    for _ in range(a.rounds):
+        for name, g in graphs.items():
+            envs[name].clear_episode_stats()
+            g.replay()  # warm
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            envs[name].clear_episode_stats()
+            e0.record(stream)
+            g.replay()
+            e1.record(stream)
+            e1.synchronize()
+            times[name].append(e0.elapsed_time(e1) * 1e3 / a.steps)
+    for name, env in envs.items():
+        assert env.error_count() == 0, name
+    bytes_step = 824 * a.batch
+    for name, t in times.items():
+        med = statistics.median(t)
+        print(json.dumps({"variant": name, "median_us": round(med, 2), "min_us": round(min(t), 2),
+                          "frac_of_spec": round(bytes_step / (med * 1e-6) / 8e12, 4),
+                          "all_us": [round(x, 2) for x in t]}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -56,9 +56,15 @@ def main():
     from bench import CONFIGS
     batch = batch or CONFIGS[cfg][0]
     want_obs, want_info, fused, players = CONFIGS[cfg][1], CONFIGS[cfg][2], CONFIGS[cfg][3], CONFIGS[cfg][6]
-    from bench import info_split_active, obs_split_active
+    from bench import info_split_active, obs_split_active, pipelined_active
     split = obs_split_active(batch)
     isplit = info_split_active(batch)
+    # the pipelined split step (coup_step_many recorded in the bench's graph):
+    # K + 1 dispatches of ONE kernel per K steps -- the rules of step 1 alone,
+    # K - 1 launches of rules(t + 1) beside writer(t), the writer of step K alone
+    pipe = bool(want_obs and not want_info and not fused and players == 2 and
+                pipelined_active(batch, players, "--graph" not in args or "off" not in args))
+    dispatches_per_window = steps + 1 if pipe else None
 
     dst = os.path.join(ROOT, "profiles", tag, cfg)
     os.makedirs(dst, exist_ok=True)
@@ -87,6 +93,8 @@ def main():
             # rules step and k_info_sweep
             m = re.search(r"k_step<true, 0, \d+, 1(?:, false)?>", kn) or re.search(r"k_stepILb1ELi0ELi\d+ELi1E", kn)
             return bool("k_info_sweep" in kn or m)
+        if pipe:
+            return "k_step_obs_pipe" in kn or "15k_step_obs_pipe" in kn
         if want_obs and not want_info and split:
             # the split observation step: the rules step without tensors and
             # the observation writer, two kernels per env step
@@ -97,6 +105,20 @@ def main():
              re.search(r"k_stepILb1ELi(\d+)ELi\d+ELi(\d+)E", kn))
         return bool(m) and (m.group(1) != "0") == want_obs and (m.group(2) == "2") == want_info
 
+    def kernel_bytes_per_lane(kn, role=None):
+        """Algorithmic bytes per lane of one dispatch of timed kernel kn
+        (40 B of rules traffic per lane-step, 784 B of
+        ObservationTensor, 19,936 B of InformationStateTensor plus 2 x 96 B
+        of history for the history-keeping rules step)."""
+        total = CONFIGS[cfg][4]
+        if pipe:
+            return {"rules": 40, "writer": total - 40}.get(role, total)
+        if want_obs and split:
+            return total - 40 if "k_obs_sweep" in kn else 40
+        if want_info and isplit:
+            return 2 * 2492 * 4 if "k_info_sweep" in kn else total - 2 * 2492 * 4
+        return total
+
     stats = glob.glob(os.path.join(src, "trace", "**", "*kernel_stats.csv"), recursive=True)
     if stats:
         shutil.copy(stats[0], os.path.join(dst, "kernel_stats.csv"))
@@ -106,9 +128,12 @@ def main():
                 summary.setdefault("timed_kernels", []).append(name)
                 summary["timed_kernel"] = " + ".join(summary["timed_kernels"])
             if "k_step" in name or "k_rollout" in name or "k_obs" in name or "k_info" in name:
-                summary.setdefault("kernels", {})[name] = {
+                # rocprof's --stats over EVERY dispatch of the process (settle,
+                # warm-up and the cold first call included): not the steady
+                # state -- per_kernel below is
+                summary.setdefault("kernels_all_dispatches", {})[name] = {
                     "calls": int(r[col(r, "calls")]),
-                    "avg_ns": float(r[col(r, "average")]),
+                    "avg_ns_all_dispatches": float(r[col(r, "average")]),
                 }
 
     # the bench line printed by the traced command itself (trace.log): its
@@ -146,24 +171,53 @@ def main():
                         disp = sorted((r for r in rows(os.path.join(src, "trace", "**", "*kernel_trace.csv"))
                                        if r[col(r, "kernel", "name")] in tks),
                                       key=lambda r: int(r[col(r, "start", "timestamp")]))
-                        window = disp[-steps * per_step:]
+                        window = disp[-(dispatches_per_window or steps * per_step):]
+                        dur = lambda r: int(r[col(r, "end", "timestamp")]) - int(r[col(r, "start", "timestamp")])  # noqa: E731
                         if window:
-                            mean = sum(int(r[col(r, "end", "timestamp")]) - int(r[col(r, "start", "timestamp")])
-                                       for r in window) / (len(window) / per_step) * 1e-6
-                            # the bench times the span of the K launches / K (launch
-                            # gaps included: eager launches, or a graph replay); the
-                            # trace's first start to last end of the same K dispatches
-                            # is that span, its mean dispatch the kernel alone
+                            mean = sum(dur(r) for r in window) / steps * 1e-6
+                            # the bench times the span of the K steps' launches / K
+                            # (launch gaps included: eager launches, or a graph
+                            # replay); the trace's first start to last end of the
+                            # same dispatches is that span, their summed durations
+                            # per step the kernels alone
                             span = (int(window[-1][col(window[-1], "end", "timestamp")]) -
-                                    int(window[0][col(window[0], "start", "timestamp")])) / (len(window) / per_step) * 1e-6
+                                    int(window[0][col(window[0], "start", "timestamp")])) / steps * 1e-6
                             rp = span
-                            summary["rocprof_mean_dispatch_ms"] = mean
+                            summary["rocprof_kernel_time_per_step_ms"] = mean
                             summary["rocprof_launch_gap_ms"] = span - mean
                             summary["rocprof_compared_dispatch"] = (f"span of the last {len(window)} dispatches (the "
-                                                                    "timed steps) / their count, as the bench times them")
+                                                                    f"{steps} timed steps) / {steps}, as the bench times "
+                                                                    "them")
+                            # every timed kernel's steady-state
+                            # mean over the timed dispatches only, its own
+                            # algorithmic bytes and roofline fraction, and a check
+                            # that the means sum to the span
+                            groups = {}
+                            for j, r in enumerate(window):
+                                kn = r[col(r, "kernel", "name")]
+                                if pipe:
+                                    role = ("rules" if j == 0 else "writer" if j == len(window) - 1 else
+                                            "rules+writer")
+                                    key = f"{kn} [{role}]"
+                                else:
+                                    role, key = None, kn
+                                groups.setdefault(key, (kn, role, []))[2].append(dur(r))
+                            per_kernel, step_sum = {}, 0.0
+                            for key, (kn, role, ds) in groups.items():
+                                m_ns = sum(ds) / len(ds)
+                                b = kernel_bytes_per_lane(kn, role if role != "rules+writer" else None) * batch
+                                per_kernel[key] = {"dispatches": len(ds), "mean_us": m_ns * 1e-3,
+                                                   "min_us": min(ds) * 1e-3, "max_us": max(ds) * 1e-3,
+                                                   "bytes": b, "achieved_gbs": b / m_ns,
+                                                   "frac": b / m_ns / 8000.0}
+                                step_sum += sum(ds)
+                            summary["per_kernel"] = per_kernel
+                            summary["per_kernel_sum_check"] = {
+                                "sum_of_means_per_step_us": step_sum / steps * 1e-3, "span_per_step_us": span * 1e3,
+                                "pct": 100.0 * (step_sum / steps * 1e-6 - span) / span,
+                                "ok_within_2pct": abs(step_sum / steps * 1e-6 - span) <= 0.02 * span}
                         else:
-                            rp = sum(summary["kernels"][k]["avg_ns"] for k in tks) * 1e-6
-                        summary["rocprof_all_dispatch_avg_ms"] = sum(summary["kernels"][k]["avg_ns"] for k in tks) * 1e-6
+                            rp = sum(summary["kernels_all_dispatches"][k]["avg_ns_all_dispatches"] for k in tks) * 1e-6
                         summary["bench_vs_rocprof_kernel_ms"] = [bench["roofline"]["kernel_ms"], rp]
 
     # plain bench lines of the same lease, before and after the profiler passes
@@ -198,8 +252,11 @@ def main():
             return None
         if fused:  # the timed launch only (see above)
             return sum(max(v)[1] for v in vals.values())
-        # per env step: each timed kernel's mean per dispatch, summed
-        return sum(sum(x for _, x in v) / len(v) for v in vals.values())
+        # per env step: the timed steps' dispatches (the last K per kernel, or
+        # the pipeline's last K + 1), summed, / K
+        allv = sorted(x for v in vals.values() for x in v)
+        n = dispatches_per_window or steps * len(vals)
+        return sum(x for _, x in allv[-n:]) / steps
 
     fetch_kb = counter("fetch", "FETCH_SIZE")
     write_kb = counter("write", "WRITE_SIZE")
