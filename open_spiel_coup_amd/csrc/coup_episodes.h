@@ -22,6 +22,14 @@
 
 namespace coup {
 
+// A lane's accumulator value as two scalars.  Not an int2: HIP's int2 is a
+// <2 x i32> IR vector, and <2 x i32> values carried through the rules'
+// divergent control flow are the shape the AMDGPU backend lowers wrong
+// (DESIGN.md section 12); a struct of two ints is split into two scalars.
+struct EpVal {
+  int32_t x, y;
+};
+
 struct EpAcc {
   int32_t* count;      // pair form
   int32_t* ret;
@@ -31,19 +39,19 @@ struct EpAcc {
   __device__ __forceinline__ bool on() const { return count != nullptr || word != nullptr; }
 
   // The lane's current value: (episodes, return sum), or (word, 0) packed.
-  __device__ __forceinline__ int2 load(int64_t i) const {
+  __device__ __forceinline__ EpVal load(int64_t i) const {
     if (word)
-      return make_int2(word_bytes == 2 ? (int32_t) static_cast<const int16_t*>(word)[i]
-                                       : static_cast<const int32_t*>(word)[i],
-                       0);
-    if (count) return make_int2(count[i], ret[i]);
-    return make_int2(0, 0);
+      return EpVal{word_bytes == 2 ? (int32_t) static_cast<const int16_t*>(word)[i]
+                                   : static_cast<const int32_t*>(word)[i],
+                   0};
+    if (count) return EpVal{count[i], ret[i]};
+    return EpVal{0, 0};
   }
 
   // Store `prev` (a load()) plus `eps` episodes whose returns sum to `r`.
   // Unsigned arithmetic: the packed word is (return_sum * 2^S + episodes)
   // modulo 2^(8 * word_bytes).
-  __device__ __forceinline__ void store(int64_t i, int2 prev, int32_t eps, int32_t r) const {
+  __device__ __forceinline__ void store(int64_t i, EpVal prev, int32_t eps, int32_t r) const {
     if (word) {
       const uint32_t w = (uint32_t)prev.x + ((uint32_t)r << (4 * word_bytes)) + (uint32_t)eps;
       if (word_bytes == 2)

@@ -88,7 +88,7 @@ int coup_host_state_apply(const coup_slot_result* in, int action, int flags, cou
   uint32_t unrep = 0u;
   if (flags & COUP_SLOT_UNCHECKED) {
     ok = apply_action_unchecked(R, x, none);
-    if (!ok && !is_terminal(L) && !L.err && !is_chance(L)) {
+    if (!ok && x < (uint32_t)COUP_NUM_ACTIONS && !is_terminal(L) && !L.err && !is_chance(L)) {
       Lane T = L;
       unrep = (ref_decision(T, x) && !representable(T)) ? 1u : 0u;
     }
@@ -120,7 +120,10 @@ int coup_host_state_apply(const coup_slot_result* in, int action, int flags, cou
 int coup_host_state_step(const coup_slot_result* in, int action, int mode, uint64_t seed, uint32_t env_id,
                          coup_slot_result* out) {
   if (!out || (!in && !(mode & COUP_SLOT_INIT))) return COUP_E_INVALID;
-  if (action >= COUP_NUM_ACTIONS) return COUP_E_INVALID;
+  // 18..127: a rejected action (ok = 0, state unchanged), as the device lane
+  // op reports it (DoApplyAction raises: coup.cc:493, :806); past an int8 id
+  // the argument itself is invalid
+  if (action > 127) return COUP_E_INVALID;
   uint8_t hist[kHistoryBytes];
   Lane L;
   if (mode & COUP_SLOT_INIT) {
@@ -150,7 +153,7 @@ int coup_host_state_step(const coup_slot_result* in, int action, int mode, uint6
     uint32_t unrep = 0u;
     if (mode & COUP_SLOT_UNCHECKED) {
       ok = apply_action_unchecked(R, x, none);
-      if (!ok && !is_terminal(L) && !L.err && !is_chance(L)) {
+      if (!ok && x < (uint32_t)COUP_NUM_ACTIONS && !is_terminal(L) && !L.err && !is_chance(L)) {
         Lane T = L;
         unrep = (ref_decision(T, x) && !representable(T)) ? 1u : 0u;
       }

@@ -367,8 +367,7 @@ __device__ __forceinline__ void write_info_wave(float* __restrict__ wave_info, c
     const uint32_t len = meta >> 16;
     v4f w = {0.0f, 0.0f, 0.0f, 0.0f};
     if (f0 < 62 + 18 * (int)len) {
-      const uint2 pw = reinterpret_cast<const uint2*>(po)[p];
-      const uint64_t prefix = (uint64_t)pw.x | ((uint64_t)pw.y << 32);
+      const uint64_t prefix = (uint64_t)po[2u * p] | ((uint64_t)po[2u * p + 1u] << 32);  // 32-bit loads
       // history rows touched by elements f0..f0+3 (t = f - 62; two rows at most)
       const int t0 = f0 - 62;
       const uint32_t r0 = t0 < 0 ? 0u : (uint32_t)t0 / 18u;
@@ -634,11 +633,11 @@ __device__ __forceinline__ void step_lane(const StepArgs& a, int64_t i, Lane& L,
 // 163.9 -- the ~7% of lanes that finish scatter their stores over most lines,
 // and those partial-line writes cost more than full-line ones.  The packed
 // int16 word (round 4) moves 2 bytes per lane each way instead of 8.
-__device__ __forceinline__ int2 ep_prefetch(const StepArgs& a, int64_t i, bool active) {
-  return active ? a.ep.load(i) : make_int2(0, 0);
+__device__ __forceinline__ EpVal ep_prefetch(const StepArgs& a, int64_t i, bool active) {
+  return active ? a.ep.load(i) : EpVal{0, 0};
 }
 
-__device__ __forceinline__ void ep_update(const StepArgs& a, int64_t i, int2 e, uint32_t st, int32_t ret) {
+__device__ __forceinline__ void ep_update(const StepArgs& a, int64_t i, EpVal e, uint32_t st, int32_t ret) {
   const bool last = st == COUP_STEP_LAST;
   a.ep.store(i, e, last ? 1 : 0, last ? ret : 0);
 }
@@ -737,7 +736,7 @@ __device__ __forceinline__ void step_group_compute(const StepArgs& a, int64_t gr
   const int64_t wleft = a.n - wave0;
   const uint32_t wave_valid = wleft >= 64 ? 64u : (wleft > 0 ? (uint32_t)wleft : 0u);  // wave-uniform
   uint8_t* hist_wave = lds.hist + wl * kHist;
-  const int2 eps = ep_prefetch(a, i, active);
+  const EpVal eps = ep_prefetch(a, i, active);
   if (INFO != kInfoNone) {
     if (wave_valid) wave_hist_copy<true>(a.hist + wave0 * kHist, hist_wave, wave_valid);
     wave_sync();
@@ -832,7 +831,7 @@ __global__ __launch_bounds__(256) void k_step_group(StepArgs a) {
   const int64_t i = (int64_t)blockIdx.x * kLanes + threadIdx.x / TPL;
   const bool active = i < a.n;
   const uint4 rec = active ? a.state[i] : pack(initial_lane(0u));
-  const int2 eps = ep_prefetch(a, i, active && q == 0u);
+  const EpVal eps = ep_prefetch(a, i, active && q == 0u);
   Lane L = unpack(rec);
   const uint32_t id = lane_stream_id(a.env_id_base, i);
   const uint32_t b = L.move >> 2, ep = L.episode, ep1 = (L.episode + 1u) & kEpisodeMask;
@@ -1172,7 +1171,7 @@ __device__ __forceinline__ void step_sorted_block(const StepArgs& a, uint32_t bl
   // phase 1: up to the decision (step_lane)
   Lane L = initial_lane(0u);
   uint32_t key = kKeyDead, st = COUP_STEP_MID;
-  const int2 eps = ep_prefetch(a, i, live);
+  const EpVal eps = ep_prefetch(a, i, live);
   if (live) {
     L = unpack(a.state[i]);
     Rng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, i), 0u, make_uint4(0, 0, 0, 0)};
@@ -1618,7 +1617,7 @@ template <bool OBS, bool INFO>
 __global__ __launch_bounds__(kThreads) void k_query(QueryArgs a) {
   __shared__ uint32_t bits[OBS ? kThreads * 8 : 1];
   __shared__ uint8_t hist[INFO ? kThreads * kHist : 16];
-  __shared__ uint32_t pre[INFO ? kThreads * kPreWords : 1];
+  __shared__ __attribute__((aligned(16))) uint32_t pre[INFO ? kThreads * kPreWords : 1];
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   const bool active = i < a.n;
   const uint32_t wl = threadIdx.x & ~63u;
@@ -1693,7 +1692,7 @@ __global__ __launch_bounds__(T) void k_info_sweep(const uint4* __restrict__ stat
   constexpr uint32_t kLanes = ((uint32_t)(T * S) + (uint32_t)kInfoF4 - 1u) / (uint32_t)kInfoF4 + 1u;
   constexpr uint32_t kHistU4 = (uint32_t)kHist / 16u;  // 6
   static_assert(kLanes * kHistU4 <= (uint32_t)T, "one history uint4 per thread");
-  __shared__ uint32_t pre[kLanes * kPreWords];
+  __shared__ __attribute__((aligned(16))) uint32_t pre[kLanes * kPreWords];
   __shared__ uint4 h4[kLanes * kHistU4];
   const uint32_t t = threadIdx.x;
   const int64_t x0 = (int64_t)blockIdx.x * (T * S);
@@ -1854,6 +1853,12 @@ __device__ COUP_SLOT_FN uint32_t slot_step(uint4 w, uint32_t x, uint32_t mode, u
     L.err = L.episode == 0u ? 1u : 0u;  // counter wrap (coup_lane.h kEpisodeMask)
   }
   RegHistory rec;
+  if (x != 0xFFu && x >= 18u) {
+    // an int8 action id outside 0..17: DoApplyAction raises (coup.cc:493,
+    // :806) -- rejected, the lane untouched, the reset included
+    *out = w;
+    return 0u;
+  }
   if (x < 18u) {
     const uint32_t idx = L.move;
     const uint32_t entry = is_chance(L) ? hist_deal(x, L.qids & 1u) : hist_decision(x, L.M);
@@ -3355,7 +3360,9 @@ int coup_slot_op(coup_env* env, int64_t lane, const coup_env* src_env, int64_t s
       return fail(COUP_E_INVALID, "coup_slot_op: src_env needs COUP_FLAG_HISTORY (2 players)");
     if (src_lane < 0 || src_lane >= src_env->batch) return fail(COUP_E_INVALID, "coup_slot_op: src_lane out of range");
   }
-  if (action < -1 || action >= COUP_NUM_ACTIONS) return fail(COUP_E_INVALID, "coup_slot_op: action out of range");
+  // 18..127 reach the transition, which rejects them (result.ok = 0: the
+  // reference's DoApplyAction raises, coup.cc:493, :806), as on the host
+  if (action < -1 || action > 127) return fail(COUP_E_INVALID, "coup_slot_op: action out of range");
   const bool result = !(flags & COUP_SLOT_NO_RESULT);
   if (result && !host_out) return fail(COUP_E_INVALID, "coup_slot_op: host_out is null");
   const bool obs = result && (flags & COUP_SLOT_OBS), info = result && (flags & COUP_SLOT_INFO);
@@ -3479,7 +3486,7 @@ int coup_slot_ops(coup_env* env, int64_t n, const coup_slot_req* reqs, const cou
     if (r.lane < 0 || r.lane >= env->batch) return fail(COUP_E_INVALID, "coup_slot_ops: lane out of range");
     if (r.flags & ~(COUP_SLOT_INIT | COUP_SLOT_UNCHECKED))
       return fail(COUP_E_INVALID, "coup_slot_ops: request flags other than INIT / UNCHECKED");
-    if (r.action < -1 || r.action >= COUP_NUM_ACTIONS) return fail(COUP_E_INVALID, "coup_slot_ops: action out of range");
+    if (r.action < -1 || r.action > 127) return fail(COUP_E_INVALID, "coup_slot_ops: action out of range");
     if (r.src_lane >= 0) {
       if (!src_env) return fail(COUP_E_INVALID, "coup_slot_ops: a request copies but src_env is null");
       if (r.src_lane >= src_env->batch) return fail(COUP_E_INVALID, "coup_slot_ops: src_lane out of range");

@@ -95,9 +95,9 @@ struct StepArgs {
 // (coalesced; unchanged unless the episode ended), so no wave waits on a late
 // load and no line is written partially (as the 2-player kernels,
 // coup_kernels.hip ep_update).
-__device__ __forceinline__ int2 load_episode(const StepArgs& a, int64_t i) { return a.ep.load(i); }
+__device__ __forceinline__ EpVal load_episode(const StepArgs& a, int64_t i) { return a.ep.load(i); }
 
-__device__ __forceinline__ void store_episode(const StepArgs& a, int64_t i, int2 e, uint32_t st, int32_t ret0) {
+__device__ __forceinline__ void store_episode(const StepArgs& a, int64_t i, EpVal e, uint32_t st, int32_t ret0) {
   const bool last = st == 2u;
   a.ep.store(i, e, last ? 1 : 0, last ? ret0 : 0);
 }
@@ -146,7 +146,7 @@ __global__ __launch_bounds__(kThreads) void k_step(StepArgs a) {
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= a.n) return;
   NLane<N> L = unpack<N>(a.sa[i], a.sb[i]);
-  const int2 eps = load_episode(a, i);
+  const EpVal eps = load_episode(a, i);
   NRng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, i), 0u, make_uint4(0, 0, 0, 0)};
   int act;
   uint32_t st, rl, rc;
@@ -262,7 +262,7 @@ __global__ NP_STEP_SORTED_BOUNDS void k_step_sorted(StepArgs a) {
   NLane<N> L;
   uint32_t key = kKeyDead, st = 0u;
   bool error = false, raw = false;
-  const int2 eps = live ? load_episode(a, i) : make_int2(0, 0);
+  const EpVal eps = live ? load_episode(a, i) : EpVal{0, 0};
   uint4 ra = make_uint4(0u, 0u, 0u, 0u), rb = ra;
   if (live) {
     ra = a.sa[i];

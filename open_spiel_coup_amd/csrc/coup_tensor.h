@@ -110,8 +110,12 @@ __device__ __forceinline__ void info_prefix_to_lds(const Lane& L, uint32_t* __re
   obs_row_bits<0>(L, term, a_lo, a_hi);
   obs_row_bits<1>(L, term, b_lo, b_hi);
   const uint64_t m62 = (1ull << 62) - 1ull;  // drop the observation's last_action bits
-  reinterpret_cast<uint2*>(pre)[0] = make_uint2((uint32_t)a_lo, (uint32_t)((a_lo & m62) >> 32));
-  reinterpret_cast<uint2*>(pre)[1] = make_uint2((uint32_t)b_lo, (uint32_t)((b_lo & m62) >> 32));
+  // 32-bit stores only: the uint2 form (a <2 x i32> value) gave wrong prefix
+  // bits in k_info_sweep
+  pre[0] = (uint32_t)a_lo;
+  pre[1] = (uint32_t)((a_lo & m62) >> 32);
+  pre[2] = (uint32_t)b_lo;
+  pre[3] = (uint32_t)((b_lo & m62) >> 32);
   pre[4] = L.c0 | (L.c1 << 8) | (L.move << 16);
   pre[5] = 0;
 }

@@ -113,7 +113,7 @@ static PyObject* py_apply(PyObject* self, PyObject* const* args, Py_ssize_t n) {
   const long action = PyLong_AsLong(args[1]), flags = PyLong_AsLong(args[2]);
   if (PyErr_Occurred()) return NULL;
   coup_slot_result r;
-  if (action < 0 || action >= COUP_NUM_ACTIONS || coup_host_state_apply(st, (int)action, (int)flags, &r) != COUP_OK) {
+  if (action < 0 || action > 127 || coup_host_state_apply(st, (int)action, (int)flags, &r) != COUP_OK) {
     PyErr_Format(PyExc_ValueError, "coup_host_state_apply: invalid action %ld", action);
     return NULL;
   }
@@ -133,7 +133,8 @@ static PyObject* py_step(PyObject* self, PyObject* const* args, Py_ssize_t n) {
   const unsigned long env_id = PyLong_AsUnsignedLong(args[4]);
   if (PyErr_Occurred()) return NULL;
   coup_slot_result r;
-  if (coup_host_state_step(st, (int)action, (int)mode, (uint64_t)seed, (uint32_t)env_id, &r) != COUP_OK) {
+  if (action < -1 || action > 127 ||
+      coup_host_state_step(st, (int)action, (int)mode, (uint64_t)seed, (uint32_t)env_id, &r) != COUP_OK) {
     PyErr_Format(PyExc_ValueError, "coup_host_state_step: action %ld mode %ld", action, mode);
     return NULL;
   }
@@ -231,15 +232,21 @@ static PyObject* py_tensors(PyObject* self, PyObject* const* args, Py_ssize_t n)
 enum { kCopies = 8 };
 static PyObject* g_small[16][kCopies];
 
-static PyObject* build_lists(const float* src, Py_ssize_t rows, Py_ssize_t cols);
+static PyObject* build_lists(const float* src, Py_ssize_t rows, Py_ssize_t cols, int untrack);
 
+/* float_lists(rows_f32, rows, cols[, untrack = 1]).  untrack = 0 keeps the
+ * rows in the cyclic collector (the pyspiel State tensor accessors: one row,
+ * an ordinary list a caller may grow into a cycle); 1 leaves them out of it
+ * (rl_environment time steps: the facade's documented contract, see
+ * build_lists). */
 static PyObject* py_float_lists(PyObject* self, PyObject* const* args, Py_ssize_t n) {
   (void)self;
-  if (n != 3) {
-    PyErr_SetString(PyExc_TypeError, "float_lists(rows_f32, rows, cols)");
+  if (n != 3 && n != 4) {
+    PyErr_SetString(PyExc_TypeError, "float_lists(rows_f32, rows, cols[, untrack])");
     return NULL;
   }
   const Py_ssize_t rows = PyLong_AsSsize_t(args[1]), cols = PyLong_AsSsize_t(args[2]);
+  const long untrack = n == 4 ? PyLong_AsLong(args[3]) : 1;
   if (PyErr_Occurred()) return NULL;
   if (rows < 0 || cols < 0) {
     PyErr_SetString(PyExc_ValueError, "float_lists: bad shape");
@@ -248,7 +255,7 @@ static PyObject* py_float_lists(PyObject* self, PyObject* const* args, Py_ssize_
   Py_buffer view;
   float* buf;
   if (!get_floats(args[0], rows * cols, 0, &view, &buf)) return NULL;
-  PyObject* res = build_lists(buf, rows, cols);
+  PyObject* res = build_lists(buf, rows, cols, untrack != 0);
   release_floats(&view);
   return res;
 }
@@ -263,7 +270,7 @@ static PyObject* element(float v, int j) {
   return PyFloat_FromDouble((double)v);
 }
 
-static PyObject* build_lists(const float* src, Py_ssize_t rows, Py_ssize_t cols) {
+static PyObject* build_lists(const float* src, Py_ssize_t rows, Py_ssize_t cols, int untrack) {
   if (!src) {
     PyErr_SetString(PyExc_ValueError, "float_lists: bad buffer");
     return NULL;
@@ -322,7 +329,14 @@ static PyObject* build_lists(const float* src, Py_ssize_t rows, Py_ssize_t cols)
       PyList_SET_ITEM(row, c, o);
     }
 #undef COUP_ONE
+#ifndef Py_GIL_DISABLED
+    /* under the GIL the counts are plain integers: add each copy's at once */
     for (int j = 0; j < kCopies; ++j) Py_SET_REFCNT(g_small[0][j], Py_REFCNT(g_small[0][j]) + zc[j]);
+#else
+    /* free-threaded builds split reference counts: one Py_INCREF per item */
+    for (int j = 0; j < kCopies; ++j)
+      for (Py_ssize_t q = 0; q < zc[j]; ++q) Py_INCREF(g_small[0][j]);
+#endif
     if (failed) { /* the items set so far hold their references; the rest are NULL */
       Py_DECREF(row);
       Py_DECREF(out);
@@ -334,8 +348,9 @@ static PyObject* build_lists(const float* src, Py_ssize_t rows, Py_ssize_t cols)
      * lists alive across collections: +60% per env step, measured).  As
      * CPython does for tuples and dicts of atomic values; a caller that later
      * puts a container into such a list and builds a cycle through it only
-     * leaves that cycle to be freed by hand. */
-    PyObject_GC_UnTrack(row);
+     * leaves that cycle to be freed by hand (documented on
+     * rl_environment.Environment; the State accessors pass untrack = 0). */
+    if (untrack) PyObject_GC_UnTrack(row);
     PyList_SET_ITEM(out, r, row);
   }
   return out;

@@ -427,12 +427,12 @@ _host_ops = None
 
 def _tensor_list(row):
     """One tensor row as the fresh list of floats pyspiel returns
-    (pyspiel.cc's vector<float> cast), built by the library's binding (shared
-    small floats, not tracked by the cyclic GC: rl_environment._float_lists)."""
-    if row.dtype == np.float32 and row.flags.c_contiguous:
-        return _host()._ext.float_lists(row, 1, row.size)[0]
-    from .rl_environment import _float_lists
-    return _float_lists(row.reshape(1, -1))[0]
+    (pyspiel.cc's vector<float> cast), built by the library's binding from
+    shared small floats.  An ordinary list: it stays tracked by the cyclic
+    GC (only rl_environment's time-step lists are untracked, the contract
+    documented on rl_environment.Environment)."""
+    row = np.ascontiguousarray(row, dtype=np.float32)
+    return _host()._ext.float_lists(row, 1, row.size, 0)[0]
 
 
 def _host():

@@ -109,7 +109,11 @@ def _float_lists(rows):
     values -- every element of both tensors -- share a few float objects,
     and the lists are kept out of the cyclic collector, so a 256-env vector
     step costs per env what an 8-env one does.  Equal
-    to numpy's tolist element by element; each list is the caller's own."""
+    to numpy's tolist element by element; each list is the caller's own.
+    Contract: these lists are not tracked by the cyclic collector (a list of
+    floats cannot be in a cycle; CPython untracks tuples and dicts of atomic
+    values the same way), so a caller that puts a container into one and
+    closes a reference cycle through it must break that cycle itself."""
     global _ext
     if _ext is None:
         _native.load()

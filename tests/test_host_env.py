@@ -107,6 +107,16 @@ def test_environment_seeds_and_states():
         assert c.get_state.history() == st.history()
     with pytest.raises(pyspiel.SpielError):
         c.step([200])  # not an action id
+    # an int8 id past the action space: DoApplyAction raises
+    # (coup.cc:806), so SpielError -- a RuntimeError, not the binding's
+    # ValueError -- and the game unchanged
+    before = c.get_state.history()
+    for x in (18, 20, 127):
+        with pytest.raises(pyspiel.SpielError):
+            c.step([x])
+        assert c.get_state.history() == before
+    q = pyspiel._host()._ext.step(c._hq._raw, 20, _native.SLOT_DEAL | _native.SLOT_UNCHECKED, 1, 0)
+    assert not q["ok"]
     # seed() restarts the env on its own new stream: seed 6's first deal
     a.seed(6)
     assert a.step([0]).first()

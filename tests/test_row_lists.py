@@ -45,6 +45,15 @@ def test_float_lists_are_fresh_and_untracked():
     assert not gc.is_tracked(b[0]) and gc.is_tracked(b)  # the outer list is an ordinary one
 
 
+def test_state_tensor_rows_stay_tracked():
+    """pyspiel State tensors are ordinary lists: untrack = 0
+    keeps them in the cyclic collector, equal to tolist."""
+    from open_spiel_coup_amd import _coup_host
+    rows = np.eye(1, 98, dtype=np.float32)
+    t = _coup_host.float_lists(rows, 1, 98, 0)[0]
+    assert gc.is_tracked(t) and t == rows[0].tolist()
+
+
 def test_float_lists_of_non_contiguous_input():
     fl = _lists()
     big = np.arange(4 * 10, dtype=np.float32).reshape(4, 10)
