@@ -400,18 +400,50 @@ def _free_port():
         return so.getsockname()[1]
 
 
+def visible_gpus(sysfs="/sys/class/kfd/kfd/topology/nodes", env=None):
+    """GPUs this process may use, counted without touching the GPU or
+    importing torch (torch.cuda.device_count() falls back
+    to hipGetDeviceCount, which initialises HIP, when amdsmi fails): the KFD
+    topology nodes with a non-zero simd_count (CPU nodes have none),
+    narrowed by ROCR_VISIBLE_DEVICES, then HIP_VISIBLE_DEVICES /
+    CUDA_VISIBLE_DEVICES (comma-separated lists; an empty list hides every
+    GPU; entries past the physical count are dropped, as the runtime does)."""
+    import glob
+    env = os.environ if env is None else env
+    n = 0
+    for prop in glob.glob(os.path.join(sysfs, "*", "properties")):
+        try:
+            with open(prop) as f:
+                for ln in f:
+                    k, _, v = ln.partition(" ")
+                    if k == "simd_count" and int(v) > 0:
+                        n += 1
+                        break
+        except (OSError, ValueError):
+            continue
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = env.get(var)
+        if v is None:
+            continue
+        ids = [x for x in v.split(",") if x.strip()]
+        n = min(n, len(ids))
+        if var != "ROCR_VISIBLE_DEVICES":
+            break  # HIP_VISIBLE_DEVICES, if set, wins over CUDA_VISIBLE_DEVICES
+    return n
+
+
 def launch_ranks(n, argv, backend="nccl", script=None):
     """--gpus N > 1 without torchrun: start N rank processes of `script`
     (this file) with `argv` and the torchrun environment (RANK, LOCAL_RANK,
     WORLD_SIZE, MASTER_ADDR / MASTER_PORT on 127.0.0.1), one GPU each.  This
-    process never initialises the GPU (torch.cuda.device_count() does not on
-    ROCm) and execs nothing: the ranks are child processes.  Relays rank 0's
-    JSON line; returns non-zero if any rank fails (the others are then
-    stopped) or rank 0 prints no line."""
+    process never initialises the GPU -- it counts GPUs from the KFD
+    topology (visible_gpus) and does not import torch -- and execs nothing:
+    the ranks are child processes.  Relays rank 0's JSON line; returns
+    non-zero if any rank fails (the others are then stopped) or rank 0
+    prints no line."""
     script = script or os.path.abspath(__file__)
     if backend == "nccl":
-        import torch
-        vis = torch.cuda.device_count()
+        vis = visible_gpus()
         if n > vis:
             print(f"bench.py: --gpus {n} with nccl needs {n} visible GPUs, found {vis}", file=sys.stderr)
             return 2

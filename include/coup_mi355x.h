@@ -193,6 +193,12 @@ int coup_create(int64_t batch, uint64_t seed, uint32_t env_id_base, int flags, c
  * DESIGN.md section 11 has the extension's rules).  Synchronous. */
 int coup_create_ex(int64_t batch, uint64_t seed, uint32_t env_id_base, int flags, int num_players, coup_env** out);
 int coup_destroy(coup_env* env);
+/* Re-read the env's dispatch knobs from the environment variables
+ * coup_create reads them from (COUP_OBS_SPLIT, COUP_INFO_SPLIT,
+ * COUP_REGROUP, COUP_PIPE, COUP_PIPE_SPAN; in a measurement build also the
+ * A/B variant knobs): for tests and A/B runs that switch one existing env
+ * between forms.  Launches never read the environment themselves. */
+int coup_reload_knobs(coup_env* env);
 /* Use this HIP stream (hipStream_t, may be NULL = default) for later calls. */
 int coup_set_stream(coup_env* env, void* hip_stream);
 int64_t coup_batch(const coup_env* env);
@@ -429,6 +435,14 @@ int coup_obs_split_variant(int64_t batch);
  * information state and no observations): 0 the fused step kernel, > 0 the
  * split form's k_info_sweep shape.  COUP_INFO_SPLIT overrides it. */
 int coup_info_split_variant(int64_t batch);
+
+/* What this build of the library holds: 0 the product (the shipped kernels
+ * only), COUP_BUILD_AB_VARIANTS a measurement build that also instantiates
+ * every measured-and-rejected kernel variant, selected by environment
+ * variables read at coup_create (build.py writes it to
+ * build/ab/libcoup_mi355x.so for A/B runs and their equality tests). */
+#define COUP_BUILD_AB_VARIANTS 1
+int coup_build_flags(void);
 
 #ifdef __cplusplus
 }

@@ -17,16 +17,17 @@ MAX_PLAYERS = 6
 HISTORY_BYTES = 96
 
 COUP_OK, COUP_E_INVALID, COUP_E_HIP, COUP_E_LANES = 0, 1, 2, 3
+BUILD_AB_VARIANTS = 1  # coup_build_flags: a measurement build with every A/B variant
 
 # Every symbol declared in include/coup_mi355x.h
 SYMBOLS = (
-    "coup_abi_version", "coup_last_error", "coup_create", "coup_create_ex", "coup_destroy",
+    "coup_abi_version", "coup_last_error", "coup_create", "coup_create_ex", "coup_destroy", "coup_reload_knobs",
     "coup_set_stream", "coup_batch", "coup_num_players", "coup_state_bytes", "coup_reset", "coup_step", "coup_rollout",
     "coup_step_trajectory", "coup_step_many", "coup_step_host", "coup_step_host_layout",
     "coup_new_initial_state", "coup_apply_action", "coup_query",
     "coup_export_state", "coup_import_state", "coup_export_history",
     "coup_import_history", "coup_error_count", "coup_slot_op", "coup_slot_ops", "coup_measure_step_traffic", "coup_obs_split_variant",
-    "coup_info_split_variant",
+    "coup_info_split_variant", "coup_build_flags",
     "coup_server_create", "coup_server_destroy", "coup_attach_server", "coup_server_stats",
     "coup_host_state_init", "coup_host_state_apply", "coup_host_state_tensors", "coup_host_state_string",
     "coup_host_state_step",
@@ -91,6 +92,7 @@ def load():
         "coup_create": ([i64, ctypes.c_uint64, ctypes.c_uint32, i32, ctypes.POINTER(vp)], i32),
         "coup_create_ex": ([i64, ctypes.c_uint64, ctypes.c_uint32, i32, i32, ctypes.POINTER(vp)], i32),
         "coup_destroy": ([vp], i32),
+        "coup_reload_knobs": ([vp], i32),
         "coup_set_stream": ([vp, vp], i32),
         "coup_batch": ([vp], i64),
         "coup_num_players": ([vp], i32),
@@ -115,6 +117,7 @@ def load():
         "coup_measure_step_traffic": ([i64, vp, ctypes.POINTER(StepOutputs), vp], i32),
         "coup_obs_split_variant": ([i64], i32),
         "coup_info_split_variant": ([i64], i32),
+        "coup_build_flags": ([], i32),
         "coup_server_create": ([i64, ctypes.POINTER(vp)], i32),
         "coup_server_destroy": ([vp], i32),
         "coup_attach_server": ([vp, vp], i32),

@@ -3,7 +3,12 @@
     python -m open_spiel_coup_amd.build [--force] [--verbose]
 
   libcoup_mi355x.so   the kernels and the C ABI (include/coup_mi355x.h), hipcc
-                      for gfx950;
+                      for gfx950: the shipped kernels only;
+  build/variants/libcoup_mi355x.so
+                      the same with -DCOUP_AB_VARIANTS: every measured and
+                      rejected kernel variant too, chosen by environment
+                      variables at coup_create (csrc/coup_knobs.h) -- A/B
+                      runs and their equality tests (COUP_LIB_PATH);
   librust_spiel.so    the reference's per-state C ABI (rust_open_spiel.h,
                       include/coup_rust_abi.h) over it, host C++ (g++), so the
                       reference's Rust crate links it as `dylib=rust_spiel`.
@@ -25,10 +30,14 @@ SOURCES = [os.path.join(CSRC, "coup_kernels.hip"), os.path.join(CSRC, "coup_npla
 HOST_SRC = os.path.join(CSRC, "coup_host.cpp")
 HOST_INC = os.path.join(CSRC, "host")
 DEPS = SOURCES + [os.path.join(CSRC, h) for h in ("coup_lane.h", "coup_nlane.h", "coup_np.h", "coup_regroup.h", "coup_episodes.h",
-                                                 "coup_tensor.h")] + [
+                                                 "coup_tensor.h", "coup_knobs.h")] + [
     os.path.join(ROOT, "include", "coup_mi355x.h"), HOST_SRC, os.path.join(HOST_INC, "hip", "hip_runtime.h")]
 OUT = os.path.join(HERE, "libcoup_mi355x.so")
 OBJ_DIR = os.path.join(ROOT, "build", "obj")  # git-ignored (build/)
+# the measurement build (every A/B variant; csrc/coup_knobs.h)
+VARIANTS_OUT = os.path.join(ROOT, "build", "variants", "libcoup_mi355x.so")
+VARIANTS_OBJ_DIR = os.path.join(OBJ_DIR, "variants")
+VARIANTS_DEFINE = "COUP_AB_VARIANTS"
 RUST_SRC = os.path.join(CSRC, "rust_spiel.cpp")
 RUST_DEPS = [RUST_SRC, os.path.join(ROOT, "include", "coup_rust_abi.h"), os.path.join(ROOT, "include", "coup_mi355x.hpp"),
              os.path.join(ROOT, "include", "coup_mi355x.h")]
@@ -143,30 +152,38 @@ def _run_all(cmds, verbose=False):
         raise subprocess.CalledProcessError(1, failed[0])
 
 
-def build(force=False, verbose=False, repro=False):
+def build(force=False, verbose=False, repro=False, variants=True):
     """libcoup_mi355x.so (its two HIP sources compiled concurrently, then
-    linked), librust_spiel.so, and with `repro` the section-12 reproducer in
-    the same batch of compiler processes."""
-    jobs, objs = [], []
+    linked), with `variants` the measurement build beside it
+    (build/variants/), librust_spiel.so, and with `repro` the section-12
+    reproducer, in one batch of compiler processes."""
+    jobs, links = [], []
     lib_stale = force or not up_to_date()
-    if lib_stale:
-        os.makedirs(OBJ_DIR, exist_ok=True)
+    var_stale = variants and (force or not up_to_date(VARIANTS_OUT))
+    if lib_stale or var_stale:
+        jobs.append(host_command(HOST_OBJ))
+    for stale, odir, out, defines in ((lib_stale, OBJ_DIR, OUT, ()),
+                                      (var_stale, VARIANTS_OBJ_DIR, VARIANTS_OUT, (VARIANTS_DEFINE,))):
+        if not stale:
+            continue
+        os.makedirs(odir, exist_ok=True)
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        objs = []
         for src in SOURCES:
-            obj = os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
+            obj = os.path.join(odir, os.path.basename(src) + ".o")
             objs.append(obj)
             cmd = [HIPCC, f"--offload-arch={ARCH}", OPT[os.path.basename(src)], NO_SLP, "-std=c++17", "-fPIC", "-Wall", "-I",
-                   os.path.join(ROOT, "include"), "-c", src, "-o", obj]
+                   os.path.join(ROOT, "include"), "-c", src, "-o", obj] + [f"-D{d}" for d in defines]
             if verbose:
                 cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
             jobs.append(cmd)
-        objs.append(HOST_OBJ)
-        jobs.append(host_command(HOST_OBJ))
+        links.append([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs + [HOST_OBJ])
     if repro and (force or not up_to_date(REPRO_OUT, [REPRO_SRC] + DEPS)):
         os.makedirs(os.path.dirname(REPRO_OUT), exist_ok=True)
         jobs.append(repro_command())
     _run_all(jobs, verbose)
-    if lib_stale:
-        _run_all([[HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT] + objs], verbose)
+    if links:
+        _run_all(links, verbose)
     if force or not up_to_date(RUST_OUT, RUST_DEPS + [OUT]):
         cmd = rust_command()
         if verbose:
@@ -186,6 +203,7 @@ def main():
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--out", default=None, help="measurement builds: write the library elsewhere")
     ap.add_argument("--define", action="append", default=[], help="measurement builds: e.g. COUP_WAVE_TRACE")
+    ap.add_argument("--no-variants", action="store_true", help="skip the A/B-variant measurement build")
     a = ap.parse_args()
     if a.out or a.define:
         out = os.path.abspath(a.out or OUT)
@@ -194,7 +212,7 @@ def main():
         subprocess.check_call(command(a.verbose, out, a.define))
         print(out)
         return
-    print(build(force=a.force, verbose=a.verbose))
+    print(build(force=a.force, verbose=a.verbose, variants=not a.no_variants))
 
 
 if __name__ == "__main__":

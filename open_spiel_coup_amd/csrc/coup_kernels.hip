@@ -2252,8 +2252,7 @@ struct coup_env {
   bool dirty;                 // work enqueued on `stream` since its last synchronisation
   hipEvent_t stream_event;    // coup_set_stream: orders a new stream after the old one's pending work
   uint4* state2;              // 2 players: the second record buffer of the pipelined step (coup_step_many)
-  int pipe;                   // coup_step_many pipelines the split observation step (COUP_PIPE, read at create)
-  double pipe_span;           // rules blocks spread over this fraction of a pipelined launch (COUP_PIPE_SPAN)
+  coup::Knobs knobs;          // dispatch knobs, read once at coup_create (coup_knobs.h)
 };
 
 // coup_server (coup_mi355x.h; kernel coup::k_server).  The ring, the control
@@ -2312,71 +2311,81 @@ int fail(int code, const std::string& msg) {
 #define COUP_CHECK_ENV(env) \
   if (!(env)) return fail(COUP_E_INVALID, "null coup_env")
 
-// COUP_OBS_MODE=1..9 overrides the observation writer (A/B measurements;
-// the modes are listed at coup::ObsMode).  Default 9: wave-cooperative
-// bitmap, sc1 (write-through) buffer stores -- 1-4 us per 2^20-lane step
-// faster than the non-temporal stores of mode 4 in every same-process A/B
-// (tools/ab_step.py).
-constexpr int kDefaultObsMode = 9;
-int obs_mode() {
-  const char* e = std::getenv("COUP_OBS_MODE");
-  const int m = e ? std::atoi(e) : kDefaultObsMode;
-  return (m >= 1 && m <= 9) ? m : kDefaultObsMode;
+// The fused step's observation writer: mode 9 (coup::ObsMode), the
+// wave-cooperative bitmap with sc1 (write-through) buffer stores -- 1-4 us
+// per 2^20-lane step faster than the non-temporal stores of mode 4 in every
+// same-process A/B (tools/ab_step.py).  Measurement
+// builds take COUP_OBS_MODE=1..9 (the modes at coup::ObsMode).
+int obs_mode(const coup::Knobs& k) {
+#ifdef COUP_AB_VARIANTS
+  return k.obs_mode;
+#else
+  (void)k;
+  return coup::kObsWaveBitsSc1;
+#endif
 }
 
-// COUP_OBS_SPLIT: the observation step as the rules step without tensors
-// plus an address-order writer (variant 1..17: k_obs_sweep, its row-decoding
-// shapes k_obs_sweep_rows<T, S>), or the fused
-// k_step<*, kObsWaveBitsSc1> (0).  Default from kObsSplitMinLanes lanes:
-// k_obs_sweep_rows<512, 2> (variant 11), 140.6-146.1 us against 160.2-161.5
-// for the fused step per 2^20-lane step in the same process (calls r04r /
-// r04s, profiles/r04/ab/c3_obs_split_shapes_*.jsonl).  Below 2^20 lanes the
-// fused step stays (the first writer lost there).  Read at every launch.
+// The observation step of n lanes: the split form from kObsSplitMinLanes
+// lanes -- the rules step without tensors plus k_obs_sweep_rows<512, 2>
+// (variant 11) in address order, 140.6-146.1 us against 160.2-161.5 for the
+// fused step per 2^20-lane step in the same process (calls r04r / r04s,
+// profiles/r04/ab/c3_obs_split_shapes_*.jsonl) -- else the fused
+// k_step<*, kObsWaveBitsSc1> (0; the split form lost below 2^20 lanes).
+// COUP_OBS_SPLIT forces 0 or 11 (measurement builds: the rejected writer
+// shapes 1..17).
 constexpr int64_t kObsSplitMinLanes = int64_t(1) << 20;
-constexpr int kObsSplitDefault = 11;
-// COUP_INFO_SPLIT: the InformationStateTensor step as the history-keeping
-// rules step plus k_info_sweep<T, S> (1: 512 x 2, 2: 256 x 2, 3: 1024 x 2,
-// 4: 512 x 4, 5: 256 x 4), or the fused k_step<*, kObsNone, 256,
-// kInfoWrite> (0).  Default from 2^18 lanes (c3i's batch): 1024 x 2, 837 us
-// against 978 us for the fused step in the same process (call r04v,
-// profiles/r04/ab/c3i_info_split_shapes.jsonl).  Read at every launch.
-constexpr int64_t kInfoSplitMinLanes = int64_t(1) << 18;
-int info_split(int64_t n) {
-  const char* e = std::getenv("COUP_INFO_SPLIT");
-  if (e) return std::atoi(e);
-  return n >= kInfoSplitMinLanes ? 3 : 0;
+int obs_split(const coup::Knobs& k, int64_t n) {
+  const int v = k.obs_split >= 0 ? k.obs_split : (n >= kObsSplitMinLanes ? coup::kObsSplitDefault : 0);
+#ifdef COUP_AB_VARIANTS
+  return v;
+#else
+  return v == 0 ? 0 : coup::kObsSplitDefault;
+#endif
 }
-
-int obs_split(int64_t n) {
-  const char* e = std::getenv("COUP_OBS_SPLIT");
-  if (e) return std::atoi(e);
-  return n >= kObsSplitMinLanes ? kObsSplitDefault : 0;
+// The InformationStateTensor step: from 2^18 lanes (c3i's batch) the
+// history-keeping rules step plus k_info_sweep<1024, 2> (variant 3), 837 us
+// against 978 us for the fused step in the same process (call r04v,
+// profiles/r04/ab/c3i_info_split_shapes.jsonl); else the fused
+// k_step<*, kObsNone, 256, kInfoWrite> (0).  COUP_INFO_SPLIT forces 0 or 3
+// (measurement builds: the shapes 1..5).
+constexpr int64_t kInfoSplitMinLanes = int64_t(1) << 18;
+int info_split(const coup::Knobs& k, int64_t n) {
+  const int v = k.info_split >= 0 ? k.info_split : (n >= kInfoSplitMinLanes ? coup::kInfoSplitDefault : 0);
+#ifdef COUP_AB_VARIANTS
+  return v;
+#else
+  return v == 0 ? 0 : coup::kInfoSplitDefault;
+#endif
 }
 
 // The pipelined form of the split step (coup_step_many,
 // coup::k_step_obs_pipe): the shipped split kernels' bodies, the regrouped
 // 512-lane rules step and the 512 x 2 writer (variant 11).
 constexpr int kPipeT = 512, kPipeS = 2;
-// rules blocks spread over the first kPipeSpanDefault of a pipelined
-// launch's block positions (COUP_PIPE_SPAN, read at coup_create)
-constexpr double kPipeSpanDefault = 0.85;
 
-// COUP_XCD_REMAP=0 turns off the XCD-aware block -> lane group mapping of
-// the step kernel (coup::xcd_group; A/B measurements).
-int xcd_remap() {
-  const char* e = std::getenv("COUP_XCD_REMAP");
-  return e ? (std::atoi(e) != 0) : 1;
+// The XCD-aware block -> lane group mapping of the fused step (coup::
+// xcd_group; measurement builds: COUP_XCD_REMAP=0 turns it off).
+int xcd_remap(const coup::Knobs& k) {
+#ifdef COUP_AB_VARIANTS
+  return k.xcd_remap;
+#else
+  (void)k;
+  return 1;
+#endif
 }
 
-// COUP_STEP_TPL: threads per lane of the rules-bound in-place step
-// (coup::k_step_group; 0 = k_step).  Default 1: the Philox blocks computed
-// ahead with ILP, 7.08 -> 6.95 us per c2 step; 2 and 4 lanes' threads per
-// lane measured 7.59 and 9.74 us (profiles/r04/ab/c2_tpl.jsonl).  Read at
-// every launch (A/B in one process).
-int step_tpl() {
-  const char* e = std::getenv("COUP_STEP_TPL");
-  const int v = e ? std::atoi(e) : 1;
-  return (v == 1 || v == 2 || v == 4) ? v : 0;
+// Threads per lane of the rules-bound in-place step (coup::k_step_group):
+// 1, the Philox blocks computed ahead with ILP, 7.08 -> 6.95 us per c2 step;
+// 2 and 4 threads per lane measured 7.59 and 9.74 us
+// (profiles/r04/ab/c2_tpl.jsonl) and k_step (0) 7.08: measurement builds
+// take COUP_STEP_TPL=0/2/4.
+int step_tpl(const coup::Knobs& k) {
+#ifdef COUP_AB_VARIANTS
+  return k.step_tpl;
+#else
+  (void)k;
+  return 1;
+#endif
 }
 
 // Blocks of the step kernel: one per group of T lanes.
@@ -2401,6 +2410,7 @@ coup::np::Env np_env(const coup_env* env) {
   e.auto_reset = (env->flags & COUP_FLAG_AUTO_RESET) ? 1 : 0;
   e.err_count = env->err_count;
   e.stream = env->stream;
+  e.knobs = env->knobs;
   return e;
 }
 
@@ -2630,13 +2640,7 @@ int coup_create_ex(int64_t batch, uint64_t seed, uint32_t env_id_base, int flags
   env->dirty = false;
   env->stream_event = nullptr;
   env->state2 = nullptr;
-  {
-    const char* e = std::getenv("COUP_PIPE");
-    env->pipe = e ? std::atoi(e) : 1;
-    const char* f = std::getenv("COUP_PIPE_SPAN");
-    const double v = f ? std::atof(f) : kPipeSpanDefault;
-    env->pipe_span = (v > 0.0 && v <= 1.0) ? v : kPipeSpanDefault;
-  }
+  env->knobs = coup::read_knobs();
   const size_t lanes = (size_t)(batch > 0 ? batch : 1);
   hipError_t e = hipMalloc(&env->state, lanes * sizeof(uint4) * (generic ? 2 : 1));
   // the pipelined step's second record buffer (allocated here: coup_step_many
@@ -2680,6 +2684,12 @@ int coup_destroy(coup_env* env) {
   if (env->stream_event) (void)hipEventDestroy(env->stream_event);
   release(env);
   if (e1 != hipSuccess) return fail(COUP_E_HIP, "coup_destroy: HIP error while releasing the env");
+  return COUP_OK;
+}
+
+int coup_reload_knobs(coup_env* env) {
+  COUP_CHECK_ENV(env);
+  env->knobs = coup::read_knobs();
   return COUP_OK;
 }
 
@@ -2751,13 +2761,17 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
   a.actions_in = actions;
   a.err_count = env->err_count;
   a.hist = env->hist;
-  a.xcd_remap = xcd_remap();
+  a.xcd_remap = xcd_remap(env->knobs);
 #ifdef COUP_WAVE_TRACE
   a.trace = g_trace;
 #endif
-  // COUP_STEP_DYN_LDS: extra LDS per block, to cap blocks per CU (A/B only)
-  const char* dl = std::getenv("COUP_STEP_DYN_LDS");
-  const unsigned dyn_lds = dl ? (unsigned)std::atoi(dl) : 0u;
+#ifdef COUP_AB_VARIANTS
+  // COUP_STEP_DYN_LDS: extra LDS per block of the fused step, to cap blocks
+  // per CU (measurement builds)
+  const unsigned dyn_lds = (unsigned)env->knobs.dyn_lds;
+#else
+  const unsigned dyn_lds = 0u;
+#endif
   if (out) {
     a.actions = out->actions;
     a.rewards = out->rewards;
@@ -2773,12 +2787,12 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
   const bool uniform = actions == nullptr;
   a.unchecked = (!uniform && (env->flags & COUP_FLAG_UNCHECKED)) ? 1 : 0;
   const int info = a.info ? coup::kInfoWrite : (a.hist ? coup::kInfoHistory : coup::kInfoNone);
-  int mode = a.obs == nullptr ? coup::kObsNone : obs_mode();
+  int mode = a.obs == nullptr ? coup::kObsNone : obs_mode(env->knobs);
   if (info != coup::kInfoNone && mode != coup::kObsNone) mode = coup::kObsWaveBits;
   hipStream_t s = env->stream;
   const int64_t n = env->batch;
   if (info == coup::kInfoWrite && mode == coup::kObsNone && n > 0) {
-    if (const int split = info_split(n)) {
+    if (const int split = info_split(env->knobs, n)) {
       // the rules step keeping the history (no tensor), then the
       // InformationStateTensor from the new records and histories
       coup_step_outputs bare = *out;
@@ -2791,6 +2805,7 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
         coup::k_info_sweep<T, S><<<(unsigned)((nf4 + T * S - 1) / (T * S)), T, 0, s>>>(env->state, env->hist, a.info,
                                                                                         n);
       };
+#ifdef COUP_AB_VARIANTS
       switch (split) {
         case 2: go(std::integral_constant<int, 256>(), std::integral_constant<int, 2>()); break;
         case 3: go(std::integral_constant<int, 1024>(), std::integral_constant<int, 2>()); break;
@@ -2798,12 +2813,16 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
         case 5: go(std::integral_constant<int, 256>(), std::integral_constant<int, 4>()); break;
         default: go(std::integral_constant<int, 512>(), std::integral_constant<int, 2>()); break;
       }
+#else
+      (void)split;
+      go(std::integral_constant<int, 1024>(), std::integral_constant<int, 2>());  // variant 3
+#endif
       COUP_HIP_TRY(hipGetLastError());
       return COUP_OK;
     }
   }
   if (info == coup::kInfoNone && mode != coup::kObsNone && n > 0) {
-    if (const int split = obs_split(n)) {
+    if (const int split = obs_split(env->knobs, n)) {
       // the rules step without tensors (its own kernel choice), then the
       // observations from the post-step records in address order
       coup_step_outputs bare = *out;
@@ -2815,6 +2834,7 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
         constexpr int T = decltype(tt)::value, S = decltype(ss)::value;
         coup::k_obs_sweep_rows<T, S><<<(unsigned)((nf4 + T * S - 1) / (T * S)), T, 0, s>>>(env->state, a.obs, n);
       };
+#ifdef COUP_AB_VARIANTS
       const unsigned g = (unsigned)((nf4 + 255) / 256);
       switch (split) {
         case 2: coup::k_obs_sweep<0><<<g, 256, 0, s>>>(env->state, a.obs, n); break;
@@ -2834,13 +2854,15 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
         case 17: rows(std::integral_constant<int, 512>(), std::integral_constant<int, 4>()); break;
         default: coup::k_obs_sweep<1><<<g, 256, 0, s>>>(env->state, a.obs, n); break;
       }
+#else
+      (void)split;
+      rows(std::integral_constant<int, 512>(), std::integral_constant<int, 2>());  // variant 11
+#endif
       COUP_HIP_TRY(hipGetLastError());
       return COUP_OK;
     }
   }
-  if (info == coup::kInfoNone && mode == coup::kObsNone && !a.unchecked && coup::regroup_lanes(n)) {
-    // COUP_SORT_THREADS: lanes per regrouping block (A/B; coup_regroup.h)
-    const int lanes = coup::sort_lanes("COUP_SORT_THREADS", coup::kStepSortLanes);
+  if (info == coup::kInfoNone && mode == coup::kObsNone && !a.unchecked && coup::regroup_lanes(env->knobs, n)) {
     auto go = [&](auto tb) {
       constexpr int TB = decltype(tb)::value;
       const unsigned g = (unsigned)((n + TB - 1) / TB);
@@ -2849,18 +2871,24 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
       else
         coup::k_step_sorted<false, TB><<<g, TB, 0, s>>>(a);
     };
+#ifdef COUP_AB_VARIANTS
+    // COUP_SORT_THREADS: lanes per regrouping block
+    const int lanes = coup::sort_lanes(env->knobs.sort_lanes, coup::kStepSortLanes);
     if (lanes == 512)
       go(std::integral_constant<int, 512>());
     else if (lanes == 1024)
       go(std::integral_constant<int, 1024>());
     else
       go(std::integral_constant<int, 256>());
+#else
+    go(std::integral_constant<int, coup::kStepSortLanes>());
+#endif
     COUP_HIP_TRY(hipGetLastError());
     return COUP_OK;
   }
   if (info == coup::kInfoNone && mode == coup::kObsNone && !a.unchecked) {
-    // COUP_STEP_TPL=1/2/4: the group-Philox step (coup::k_step_group; A/B)
-    const int tpl = step_tpl();
+    // the group-Philox step (coup::k_step_group), TPL threads per lane
+    const int tpl = step_tpl(env->knobs);
     if (tpl) {
       auto go = [&](auto tp) {
         constexpr int TP = decltype(tp)::value;
@@ -2870,31 +2898,41 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
         else
           coup::k_step_group<TP, false><<<g, 256, 0, s>>>(a);
       };
+#ifdef COUP_AB_VARIANTS
       if (tpl == 4)
         go(std::integral_constant<int, 4>());
       else if (tpl == 2)
         go(std::integral_constant<int, 2>());
       else
+#endif
         go(std::integral_constant<int, 1>());
       COUP_HIP_TRY(hipGetLastError());
       return COUP_OK;
     }
   }
 #define COUP_LAUNCH_STEP(U, M, T, I) launch_step<U, M, T, I>(env, a, n, dyn_lds, s)
+#ifdef COUP_AB_VARIANTS
+#define COUP_LAUNCH_NO_INFO(U)                                                                       \
+  switch (mode) {                                                                                    \
+    case 0: COUP_LAUNCH_STEP(U, coup::kObsNone, 256, coup::kInfoNone); break;                        \
+    case 1: COUP_LAUNCH_STEP(U, coup::kObsLaneRows, 256, coup::kInfoNone); break;                    \
+    case 2: COUP_LAUNCH_STEP(U, coup::kObsWave, 256, coup::kInfoNone); break;                        \
+    case 3: COUP_LAUNCH_STEP(U, coup::kObsWaveNT, 256, coup::kInfoNone); break;                      \
+    case 5: COUP_LAUNCH_STEP(U, coup::kObsBlockBits, 256, coup::kInfoNone); break;                   \
+    case 6: COUP_LAUNCH_STEP(U, coup::kObsBlockBits, 1024, coup::kInfoNone); break;                  \
+    case 7: COUP_LAUNCH_STEP(U, coup::kObsBlockBitsNT, 1024, coup::kInfoNone); break;                \
+    case 8: COUP_LAUNCH_STEP(U, coup::kObsWaveBitsPlain, 256, coup::kInfoNone); break;               \
+    default: COUP_LAUNCH_STEP(U, coup::kObsWaveBitsSc1, 256, coup::kInfoNone); break;                \
+    case 4: COUP_LAUNCH_STEP(U, coup::kObsWaveBits, 256, coup::kInfoNone); break;                    \
+  }
+#else
+  // the product: without tensors the sorted / group steps above took every
+  // checked launch, so what is left writes observations with writer 9
+#define COUP_LAUNCH_NO_INFO(U) COUP_LAUNCH_STEP(U, coup::kObsWaveBitsSc1, 256, coup::kInfoNone);
+#endif
 #define COUP_LAUNCH_MODES(U)                                                                         \
   if (info == coup::kInfoNone) {                                                                     \
-    switch (mode) {                                                                                  \
-      case 0: COUP_LAUNCH_STEP(U, coup::kObsNone, 256, coup::kInfoNone); break;                      \
-      case 1: COUP_LAUNCH_STEP(U, coup::kObsLaneRows, 256, coup::kInfoNone); break;                  \
-      case 2: COUP_LAUNCH_STEP(U, coup::kObsWave, 256, coup::kInfoNone); break;                      \
-      case 3: COUP_LAUNCH_STEP(U, coup::kObsWaveNT, 256, coup::kInfoNone); break;                    \
-      case 5: COUP_LAUNCH_STEP(U, coup::kObsBlockBits, 256, coup::kInfoNone); break;                 \
-      case 6: COUP_LAUNCH_STEP(U, coup::kObsBlockBits, 1024, coup::kInfoNone); break;                \
-      case 7: COUP_LAUNCH_STEP(U, coup::kObsBlockBitsNT, 1024, coup::kInfoNone); break;              \
-      case 8: COUP_LAUNCH_STEP(U, coup::kObsWaveBitsPlain, 256, coup::kInfoNone); break;             \
-      default: COUP_LAUNCH_STEP(U, coup::kObsWaveBitsSc1, 256, coup::kInfoNone); break;              \
-      case 4: COUP_LAUNCH_STEP(U, coup::kObsWaveBits, 256, coup::kInfoNone); break;                  \
-    }                                                                                                \
+    COUP_LAUNCH_NO_INFO(U)                                                                           \
   } else if (info == coup::kInfoHistory) {                                                           \
     if (mode == 0) COUP_LAUNCH_STEP(U, coup::kObsNone, 256, coup::kInfoHistory);                     \
     else COUP_LAUNCH_STEP(U, coup::kObsWaveBits, 256, coup::kInfoHistory);                           \
@@ -2927,6 +2965,7 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
     COUP_LAUNCH_MODES(false)
   }
 #undef COUP_LAUNCH_MODES
+#undef COUP_LAUNCH_NO_INFO
 #undef COUP_LAUNCH_STEP
   COUP_HIP_TRY(hipGetLastError());
   return COUP_OK;
@@ -2956,13 +2995,18 @@ int coup_rollout(coup_env* env, int64_t steps, const coup_rollout_stats* stats) 
     if (const char* why = coup::ep_acc_of(stats, a.ep)) return fail(COUP_E_INVALID, std::string("coup_rollout: ") + why);
     a.length_sum = stats->length_sum;
   }
-  if (coup::regroup_lanes(env->batch)) {
+  if (coup::regroup_lanes(env->knobs, env->batch)) {
     const int64_t n = env->batch;
-    switch (coup::sort_lanes("COUP_SORT_THREADS", coup::kRolloutSortLanes)) {
+#ifdef COUP_AB_VARIANTS
+    switch (coup::sort_lanes(env->knobs.sort_lanes, coup::kRolloutSortLanes)) {
       case 256: coup::k_rollout_sorted<256><<<grid_for(n), 256, 0, env->stream>>>(a); break;
       case 512: coup::k_rollout_sorted<512><<<(unsigned)((n + 511) / 512), 512, 0, env->stream>>>(a); break;
       default: coup::k_rollout_sorted<1024><<<(unsigned)((n + 1023) / 1024), 1024, 0, env->stream>>>(a); break;
     }
+#else
+    constexpr int TB = coup::kRolloutSortLanes;
+    coup::k_rollout_sorted<TB><<<(unsigned)((n + TB - 1) / TB), TB, 0, env->stream>>>(a);
+#endif
   } else
     coup::k_rollout<<<grid_for(env->batch), coup::kThreads, 0, env->stream>>>(a);
   COUP_HIP_TRY(hipGetLastError());
@@ -3094,8 +3138,8 @@ namespace {
 // observations and no information state, and the split step with the
 // shipped writer is this batch's form (from 2^20 lanes, or COUP_OBS_SPLIT).
 bool pipelined(const coup_env* env, const coup_step_outputs* out) {
-  return env->pipe != 0 && !env->generic && !env->hist && env->state2 && out && out->obs && !out->info_state &&
-         obs_split(env->batch) == kObsSplitDefault;
+  return env->knobs.pipe != 0 && !env->generic && !env->hist && env->state2 && out && out->obs &&
+         !out->info_state && obs_split(env->knobs, env->batch) == coup::kObsSplitDefault;
 }
 
 // Output slice t of a [steps][B][...] coup_step_outputs (the accumulators
@@ -3157,7 +3201,7 @@ int step_many_pipelined(coup_env* env, int64_t steps, const coup_step_outputs* o
     p.obs_state = cur;
     p.obs = writer ? out->obs + (slices ? (m - 1) * n * 2 * COUP_OBS_SIZE : 0) : nullptr;
     const uint32_t total = p.rules_blocks + p.writer_blocks;
-    p.stride = (rules && writer) ? std::max<uint32_t>(1u, (uint32_t)(env->pipe_span * total / R)) : 1u;
+    p.stride = (rules && writer) ? std::max<uint32_t>(1u, (uint32_t)(env->knobs.pipe_span * total / R)) : 1u;
     coup::k_step_obs_pipe<kPipeT, kPipeS><<<total, kPipeT, 0, env->stream>>>(p);
     COUP_HIP_TRY(hipGetLastError());
     cur = next;
@@ -3241,14 +3285,19 @@ int coup_step_trajectory(coup_env* env, int64_t steps, const coup_step_outputs* 
   }
   (void)coup::ep_acc_of(out, a.ep);
   const int64_t n = env->batch;
-  if (coup::regroup_lanes(n)) {
-    switch (coup::sort_lanes("COUP_SORT_THREADS", coup::kRolloutSortLanes)) {
+  if (coup::regroup_lanes(env->knobs, n)) {
+#ifdef COUP_AB_VARIANTS
+    switch (coup::sort_lanes(env->knobs.sort_lanes, coup::kRolloutSortLanes)) {
       case 256: coup::k_trajectory_sorted<256><<<grid_for(n), 256, 0, env->stream>>>(a, steps); break;
       case 512: coup::k_trajectory_sorted<512><<<(unsigned)((n + 511) / 512), 512, 0, env->stream>>>(a, steps); break;
       default:
         coup::k_trajectory_sorted<1024><<<(unsigned)((n + 1023) / 1024), 1024, 0, env->stream>>>(a, steps);
         break;
     }
+#else
+    constexpr int TB = coup::kRolloutSortLanes;
+    coup::k_trajectory_sorted<TB><<<(unsigned)((n + TB - 1) / TB), TB, 0, env->stream>>>(a, steps);
+#endif
   } else {
     coup::k_step_trajectory<<<grid_for(n), coup::kThreads, 0, env->stream>>>(a, steps);
   }
@@ -3715,9 +3764,17 @@ int coup_error_count(coup_env* env, int64_t* out) {
   return COUP_OK;
 }
 
-int coup_obs_split_variant(int64_t batch) { return batch > 0 ? obs_split(batch) : 0; }
+int coup_obs_split_variant(int64_t batch) { return batch > 0 ? obs_split(coup::read_knobs(), batch) : 0; }
 
-int coup_info_split_variant(int64_t batch) { return batch > 0 ? info_split(batch) : 0; }
+int coup_info_split_variant(int64_t batch) { return batch > 0 ? info_split(coup::read_knobs(), batch) : 0; }
+
+int coup_build_flags(void) {
+#ifdef COUP_AB_VARIANTS
+  return COUP_BUILD_AB_VARIANTS;
+#else
+  return 0;
+#endif
+}
 
 int coup_measure_step_traffic(int64_t batch, uint32_t* records, const coup_step_outputs* out, void* hip_stream) {
   if (batch < 0 || batch > (int64_t(1) << 32)) return fail(COUP_E_INVALID, "coup_measure_step_traffic: bad batch");
@@ -3727,7 +3784,7 @@ int coup_measure_step_traffic(int64_t batch, uint32_t* records, const coup_step_
   std::memset(&a, 0, sizeof(a));
   a.state = reinterpret_cast<uint4*>(records);
   a.n = batch;
-  a.xcd_remap = xcd_remap();
+  a.xcd_remap = xcd_remap(coup::read_knobs());
   if (out) {
     a.actions = out->actions;
     a.rewards = out->rewards;

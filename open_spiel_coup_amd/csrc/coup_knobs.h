@@ -1,0 +1,100 @@
+// coup_knobs.h -- host-side dispatch knobs of an env, read ONCE at
+// coup_create from environment variables (not at every launch).
+//
+// The product library instantiates only the shipped kernels; its knobs pick
+// between shipped forms (the fused or split observation step, regrouping,
+// the pipelined split step).  A measurement build (-DCOUP_AB_VARIANTS:
+// `python -m open_spiel_coup_amd.build` also writes it to
+// build/ab/libcoup_mi355x.so) adds every variant that was measured and
+// rejected, selected by the knobs marked "measurement
+// builds" below, for same-process A/B runs (tools/ab_step.py,
+// tools/pipe_ab.py) and their equality tests (tests/ab_variants/, run by
+// tests/test_gpu_ab_variants.py with COUP_LIB_PATH at that build).
+#pragma once
+
+#include <stdint.h>
+
+#include <cstdlib>
+
+namespace coup {
+
+// The split observation step's shipped writer (k_obs_sweep_rows<512, 2>)
+// and the split InformationStateTensor step's (k_info_sweep<1024, 2>).
+constexpr int kObsSplitDefault = 11;
+constexpr int kInfoSplitDefault = 3;
+// rules blocks spread over the first kPipeSpanDefault of a pipelined
+// launch's block positions (COUP_PIPE_SPAN)
+constexpr double kPipeSpanDefault = 0.85;
+
+struct Knobs {
+  // -- every build
+  int obs_split = -1;   // COUP_OBS_SPLIT: -1 by batch (from 2^20 lanes), 0 fused, 11 the shipped writer
+  int info_split = -1;  // COUP_INFO_SPLIT: -1 by batch (from 2^18 lanes), 0 fused, 3 the shipped writer
+  int regroup = -1;     // COUP_REGROUP: -1 by batch (from 2^18 lanes), 0 / 1 forced
+  int pipe = 1;         // COUP_PIPE: coup_step_many pipelines the split observation step
+  double pipe_span = kPipeSpanDefault;  // COUP_PIPE_SPAN in (0, 1]
+  // -- measurement builds (-DCOUP_AB_VARIANTS); the product ignores them
+  int obs_mode = 9;       // COUP_OBS_MODE 1..9: the fused step's observation writer
+  int xcd_remap = 1;      // COUP_XCD_REMAP: XCD-aware block -> lane-group mapping of the fused step
+  int step_tpl = 1;       // COUP_STEP_TPL 0 / 1 / 2 / 4: threads per lane of the rules-bound step
+  int dyn_lds = 0;        // COUP_STEP_DYN_LDS: extra dynamic LDS per block of the fused step
+  int sort_lanes = 0;     // COUP_SORT_THREADS 256 / 512 / 1024 (0: each kernel's default)
+  int np_sort_lanes = 0;  // COUP_NP_SORT_THREADS
+  int np_ahead = 1;       // COUP_AHEAD: the 6-player step draws the next decision ahead
+  int np_reset_inline = 0;  // COUP_NP_RESET_INLINE
+  int np_reset_group = 0;   // COUP_NP_RESET_GROUP (1: one thread per reset)
+  int np_traj_stage = 1;    // COUP_TRAJ_STAGE
+  int np_scan = 1;          // COUP_NP_SCAN
+};
+
+inline int knob_int(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
+
+inline Knobs read_knobs() {
+  Knobs k;
+  k.obs_split = knob_int("COUP_OBS_SPLIT", -1);
+  k.info_split = knob_int("COUP_INFO_SPLIT", -1);
+  k.regroup = knob_int("COUP_REGROUP", -1);
+  k.pipe = knob_int("COUP_PIPE", 1);
+  if (const char* f = std::getenv("COUP_PIPE_SPAN")) {
+    const double v = std::atof(f);
+    if (v > 0.0 && v <= 1.0) k.pipe_span = v;
+  }
+#ifdef COUP_AB_VARIANTS
+  k.obs_mode = knob_int("COUP_OBS_MODE", 9);
+  if (k.obs_mode < 1 || k.obs_mode > 9) k.obs_mode = 9;
+  k.xcd_remap = knob_int("COUP_XCD_REMAP", 1) != 0;
+  k.step_tpl = knob_int("COUP_STEP_TPL", 1);
+  if (k.step_tpl != 1 && k.step_tpl != 2 && k.step_tpl != 4) k.step_tpl = 0;
+  k.dyn_lds = knob_int("COUP_STEP_DYN_LDS", 0);
+  k.sort_lanes = knob_int("COUP_SORT_THREADS", 0);
+  k.np_sort_lanes = knob_int("COUP_NP_SORT_THREADS", 0);
+  k.np_ahead = knob_int("COUP_AHEAD", 1) != 0;
+  k.np_reset_inline = knob_int("COUP_NP_RESET_INLINE", 0) != 0;
+  k.np_reset_group = knob_int("COUP_NP_RESET_GROUP", 0);
+  k.np_traj_stage = knob_int("COUP_TRAJ_STAGE", 1);
+  k.np_scan = knob_int("COUP_NP_SCAN", 1) != 0;
+#endif
+  return k;
+}
+
+// Regroup a launch of n lanes by decision?  Measured on MI355X
+// (tools/ab_step.py): the sort's barriers and LDS
+// round trips cost more than the divergence they remove below ~4 waves per
+// SIMD (2^18 lanes on 256 CUs) and win above it (2-player rollout 2^20:
+// 20.5 -> 18.6 us per step; 6-player 2^20: step 56.8 -> 43.0, rollout 41.5
+// -> 29.1).  COUP_REGROUP forces it off / on (tests, A/B).
+constexpr int64_t kRegroupMinLanes = int64_t{1} << 18;
+inline bool regroup_lanes(const Knobs& k, int64_t n) {
+  return k.regroup >= 0 ? k.regroup != 0 : n >= kRegroupMinLanes;
+}
+
+// Lanes per regrouping block: the kernel's default, or (measurement builds)
+// 256 / 512 / 1024 from the knob.
+inline int sort_lanes(int knob, int dflt) {
+  return (knob == 256 || knob == 512 || knob == 1024) ? knob : dflt;
+}
+
+}  // namespace coup

@@ -7,6 +7,7 @@
 #include <stdint.h>
 
 #include "coup_episodes.h"
+#include "coup_knobs.h"
 #include "coup_mi355x.h"
 
 namespace coup {
@@ -22,6 +23,7 @@ struct Env {
   int auto_reset;
   uint32_t* err_count;
   hipStream_t stream;
+  Knobs knobs;  // the env's dispatch knobs (coup_knobs.h), read at coup_create
 };
 
 // mode 0: episode 0, mode 1: next episode; deal: resolve the initial deals

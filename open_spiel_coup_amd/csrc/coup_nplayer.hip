@@ -1034,19 +1034,18 @@ hipError_t launch_step(const Env& e, const int8_t* actions, const coup_step_outp
   return dispatch(e.players, [&](auto np) {
     constexpr int N = decltype(np)::value;
     const unsigned grid = grid_for(e.n, kThreads);
-    if (regroup_lanes(e.n)) {
-      const char* ah = std::getenv("COUP_AHEAD");  // 0: no decision drawn ahead (A/B)
-      const bool ahead = ah ? std::atoi(ah) != 0 : true;
+    if (regroup_lanes(e.knobs, e.n)) {
+#ifdef COUP_AB_VARIANTS
+      // measurement builds: the rejected schedules of DESIGN.md section 5
+      // (no decision drawn ahead; COUP_NP_RESET_INLINE=1, resets dealt where
+      // the game ends, 34.07 vs 35.01 us per 2^20-lane step in one process,
+      // profiles/r03/ab/np_reset_inline.jsonl; COUP_NP_RESET_GROUP=1, one
+      // thread per reset) and block sizes (COUP_NP_SORT_THREADS)
+      const bool ahead = e.knobs.np_ahead != 0, inl = e.knobs.np_reset_inline != 0;
+      const bool single = e.knobs.np_reset_group == 1;
       auto go = [&](auto lanes) {
         constexpr int TB = decltype(lanes)::value;
         const unsigned g = grid_for(e.n, TB);
-        // COUP_NP_RESET_INLINE=1: resets dealt where the game ends (kKeyEnding),
-        // measured slower than the reset phase (34.07 vs 35.01 us per 2^20-lane
-        // step, same process: profiles/r03/ab/np_reset_inline.jsonl); A/B only
-        const char* ri = std::getenv("COUP_NP_RESET_INLINE");
-        const bool inl = ri ? std::atoi(ri) != 0 : false;
-        const char* rg = std::getenv("COUP_NP_RESET_GROUP");  // 1: one thread per reset (A/B)
-        const bool single = rg ? std::atoi(rg) == 1 : false;
         if (actions)
           k_step_sorted<N, false, false, TB><<<g, TB, 0, e.stream>>>(a);
         else if (ahead && inl)
@@ -1058,11 +1057,21 @@ hipError_t launch_step(const Env& e, const int8_t* actions, const coup_step_outp
         else
           k_step_sorted<N, true, false, TB><<<g, TB, 0, e.stream>>>(a);
       };
-      switch (sort_lanes("COUP_NP_SORT_THREADS", step_sort_lanes(N))) {
+      switch (sort_lanes(e.knobs.np_sort_lanes, step_sort_lanes(N))) {
         case 256: go(std::integral_constant<int, 256>()); break;
         case 1024: go(std::integral_constant<int, 1024>()); break;
         default: go(std::integral_constant<int, 512>()); break;
       }
+#else
+      // the shipped schedule: decision drawn ahead, resets dealt by 4-thread
+      // groups, step_sort_lanes(N) lanes per block
+      constexpr int TB = step_sort_lanes(N);
+      const unsigned g = grid_for(e.n, TB);
+      if (actions)
+        k_step_sorted<N, false, false, TB><<<g, TB, 0, e.stream>>>(a);
+      else
+        k_step_sorted<N, true, true, TB><<<g, TB, 0, e.stream>>>(a);
+#endif
     } else if (actions) {
       k_step<N, false><<<grid, kThreads, 0, e.stream>>>(a);
     } else {
@@ -1092,20 +1101,23 @@ hipError_t launch_trajectory(const Env& e, int64_t steps, const coup_step_output
   }
   return dispatch(e.players, [&](auto np) {
     constexpr int N = decltype(np)::value;
-    if (regroup_lanes(e.n)) {
-      switch (sort_lanes("COUP_NP_SORT_THREADS", kRolloutSortLanes)) {
+    if (regroup_lanes(e.knobs, e.n)) {
+#ifdef COUP_AB_VARIANTS
+      switch (sort_lanes(e.knobs.np_sort_lanes, kRolloutSortLanes)) {
         case 256: k_trajectory_sorted<N, 256><<<grid_for(e.n, 256), 256, 0, e.stream>>>(a, steps); break;
         case 512: k_trajectory_sorted<N, 512><<<grid_for(e.n, 512), 512, 0, e.stream>>>(a, steps); break;
-        default: {
-          // COUP_TRAJ_STAGE=0: the round-2 stores (A/B, 1024-lane blocks)
-          const char* st = std::getenv("COUP_TRAJ_STAGE");
-          if (st && std::atoi(st) == 0)
+        default:
+          // COUP_TRAJ_STAGE=0: the round-2 stores (1024-lane blocks)
+          if (e.knobs.np_traj_stage == 0)
             k_trajectory_sorted<N, 1024, 0><<<grid_for(e.n, 1024), 1024, 0, e.stream>>>(a, steps);
           else
             k_trajectory_sorted<N, 1024><<<grid_for(e.n, 1024), 1024, 0, e.stream>>>(a, steps);
           break;
-        }
       }
+#else
+      k_trajectory_sorted<N, kRolloutSortLanes><<<grid_for(e.n, kRolloutSortLanes), kRolloutSortLanes, 0, e.stream>>>(
+          a, steps);
+#endif
     } else {
       k_step_trajectory<N><<<grid_for(e.n, kThreads), kThreads, 0, e.stream>>>(a, steps);
     }
@@ -1130,17 +1142,21 @@ hipError_t launch_rollout(const Env& e, int64_t steps, const coup_rollout_stats*
   return dispatch(e.players, [&](auto np) {
     constexpr int N = decltype(np)::value;
     const unsigned grid = grid_for(e.n, kThreads);
-    if (regroup_lanes(e.n)) {
-      switch (sort_lanes("COUP_NP_SORT_THREADS", kRolloutSortLanes)) {
+    if (regroup_lanes(e.knobs, e.n)) {
+#ifdef COUP_AB_VARIANTS
+      switch (sort_lanes(e.knobs.np_sort_lanes, kRolloutSortLanes)) {
         case 512: k_rollout_sorted<N, 512><<<grid_for(e.n, 512), 512, 0, e.stream>>>(a); break;
         case 256: k_rollout_sorted<N, 256><<<grid, 256, 0, e.stream>>>(a); break;
         default:
-          if (!np_scan_mode())  // COUP_NP_SCAN=0: the per-lane bin prefix (A/B)
+          if (!e.knobs.np_scan)  // COUP_NP_SCAN=0: the per-lane bin prefix
             k_rollout_sorted<N, 1024, false><<<grid_for(e.n, 1024), 1024, 0, e.stream>>>(a);
           else
             k_rollout_sorted<N, 1024><<<grid_for(e.n, 1024), 1024, 0, e.stream>>>(a);
           break;
       }
+#else
+      k_rollout_sorted<N, kRolloutSortLanes><<<grid_for(e.n, kRolloutSortLanes), kRolloutSortLanes, 0, e.stream>>>(a);
+#endif
     } else {
       k_rollout<N><<<grid, kThreads, 0, e.stream>>>(a);
     }

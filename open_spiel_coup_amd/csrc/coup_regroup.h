@@ -12,7 +12,6 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include <cstdlib>
 
 namespace coup {
 
@@ -52,33 +51,7 @@ __device__ __forceinline__ uint32_t bins_below(const uint32_t* bin, uint32_t key
   return below;
 }
 
-// COUP_NP_SCAN: 1 (default) the N-player rollout's per-wave scan
-// (wave_bins_below), 0 its round-2 per-lane sums (A/B runs).
-inline uint32_t np_scan_mode() {
-  const char* e = std::getenv("COUP_NP_SCAN");
-  return e ? (uint32_t)(std::atoi(e) != 0) : 1u;
-}
-
-// Host side: regroup a launch of n lanes?  Measured on MI355X (tools/ab_step.py,
-// DESIGN.md section 5): the sort's barriers and LDS round trips cost more
-// than the divergence they remove below ~4 waves per SIMD (2^18 lanes on 256
-// CUs) and win above it (2-player rollout 2^20: 20.5 -> 18.6 us per step;
-// 6-player 2^20: step 56.8 -> 43.0, rollout 41.5 -> 29.1).  COUP_REGROUP=0/1
-// forces it off/on (A/B runs and tests).
-constexpr int64_t kRegroupMinLanes = int64_t{1} << 18;
-
-inline bool regroup_lanes(int64_t n) {
-  const char* e = std::getenv("COUP_REGROUP");
-  if (e) return std::atoi(e) != 0;
-  return n >= kRegroupMinLanes;
-}
-
-// Lanes per regrouping block: `dflt`, or 256 / 512 / 1024 from environment
-// variable `var` (A/B runs; every size gives the same results).
-inline int sort_lanes(const char* var, int dflt) {
-  const char* s = std::getenv(var);
-  const int v = s ? std::atoi(s) : dflt;
-  return (v == 256 || v == 512 || v == 1024) ? v : dflt;
-}
+// The host-side choice of regrouping and block sizes is coup_knobs.h's
+// (regroup_lanes, sort_lanes), read once per env at coup_create.
 
 }  // namespace coup

@@ -147,6 +147,12 @@ class BatchedCoupEnv:
             _native.check(self.lib.coup_set_stream(self._h, ctypes.c_void_p(s)))
             self._bound_stream = s
 
+    def reload_knobs(self):
+        """Re-read the dispatch knobs (COUP_OBS_SPLIT, COUP_REGROUP, ...) from
+        the environment: coup_create reads them once, launches never do
+        (tests and A/B runs switching this env between forms)."""
+        _native.check(self.lib.coup_reload_knobs(self._h))
+
     def close(self):
         if self._h:
             self.lib.coup_destroy(self._h)

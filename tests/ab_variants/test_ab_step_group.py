@@ -1,13 +1,16 @@
-"""The c2 kernel, coup::k_step_group<1>: the rules-bound step (65,536 lanes:
-one wave per SIMD) with the three Philox blocks one step can need computed
-ahead with ILP (PrefRng), against the oracle at c2's batch and against the
-regrouped step (k_step_sorted, COUP_REGROUP=1: another kernel, the same
-sampling contract) on ragged batches, caller actions (legal, illegal:
-counted once per lane, skipped lanes) and rl_environment semantics
-(auto_reset off).  Its rejected 2- and 4-thread forms and the plain k_step
-are held equal in tests/ab_variants/test_ab_step_group.py (measurement
-build).  Reference semantics: coup.cc:490-809 (the transition),
-random_agent.py:29-42 with spiel.cc:258-294 (the draws)."""
+"""Measurement build (tests/ab_variants/conftest.py).
+
+coup::k_step_group (COUP_STEP_TPL = 1 / 2 / 4): the rules-bound step with
+the Philox blocks one step can need computed ahead by the lane's thread
+group (PrefRng) and traded by DPP (TPL 1, the default, computes them in
+one thread with ILP), against the plain k_step (COUP_STEP_TPL=0) and the
+oracle.  Same sampling contract, so the same games: every
+output of every step, the records and the episode accumulators are equal,
+at c2's batch (65,536 lanes: one wave per SIMD) and ragged batches whose
+last group is partial.  Caller actions (legal, illegal: counted once per
+lane) and rl_environment semantics (auto_reset off, LAST then reset) too.
+Reference semantics: coup.cc:490-809 (the transition), random_agent.py:29-42
+with spiel.cc:258-294 (the draws)."""
 import numpy as np
 import pytest
 import torch
@@ -21,8 +24,8 @@ from open_spiel_coup_amd import BatchedCoupEnv  # noqa: E402
 KEYS = ("actions", "rewards", "step_type", "legal_mask", "current_player")
 
 
-def _run(monkeypatch, regroup, B, steps, seed=3, auto_reset=True, actions_fn=None, env_id_base=0):
-    monkeypatch.setenv("COUP_REGROUP", str(regroup))  # 0: k_step_group<1>, 1: k_step_sorted
+def _run(monkeypatch, tpl, B, steps, seed=3, auto_reset=True, actions_fn=None, env_id_base=0):
+    monkeypatch.setenv("COUP_STEP_TPL", str(tpl))  # 0: k_step
     env = BatchedCoupEnv(B, seed=seed, auto_reset=auto_reset, obs=False, device="cuda", episode_stats=True,
                          env_id_base=env_id_base)
     outs = []
@@ -49,15 +52,18 @@ def _same(a, b, what):
 
 
 @pytest.mark.parametrize("B", [65536, 65536 + 77, 1000, 3])
-def test_group_step_equals_regrouped_step(monkeypatch, B):
-    _same(_run(monkeypatch, 0, B, 80), _run(monkeypatch, 1, B, 80), f"B {B}")
+def test_group_step_equals_k_step_uniform(monkeypatch, B):
+    ref = _run(monkeypatch, 0, B, 80)
+    for tpl in (1, 2, 4):
+        _same(_run(monkeypatch, tpl, B, 80), ref, f"TPL {tpl} B {B}")
 
 
-def test_group_step_equals_oracle_slices(monkeypatch):
-    """k_step_group<1> at c2's batch against the oracle directly, on three
-    256-lane slices at every step."""
+@pytest.mark.parametrize("tpl", [1, 4])
+def test_group_step_equals_oracle_slices(monkeypatch, tpl):
+    """k_step_group at c2's batch (TPL 1: the default c2 kernel) against the
+    oracle directly, on three 256-lane slices at every step."""
     B, K = 65536, 60
-    outs, rec, _, _, err = _run(monkeypatch, 0, B, K, seed=11)
+    outs, rec, _, _, err = _run(monkeypatch, tpl, B, K, seed=11)
     assert err == 0
     for k in (0, B // 2 + 77, B - 256):
         ref = oracle.rollout(seed=11, n=256, steps=K, env_id_base=k)
@@ -73,9 +79,9 @@ def test_group_step_equals_oracle_slices(monkeypatch):
 
 def test_group_step_caller_actions_and_errors(monkeypatch):
     """Caller actions: a legal pick per lane from the last legal mask, with
-    some lanes given an illegal action (left unchanged, counted once) and
-    some skipped (-1); no auto reset (rl_environment: LAST, then a reset on
-    the next step)."""
+    some lanes given an illegal action (left unchanged, counted once per
+    lane even though four threads play it) and some skipped (-1); no auto
+    reset (rl_environment: LAST, then a reset on the next step)."""
     B = 4099
 
     def actions(env, t):
@@ -91,12 +97,18 @@ def test_group_step_caller_actions_and_errors(monkeypatch):
         acts[5::211] = -1
         return acts
 
-    ref = _run(monkeypatch, 1, B, 24, auto_reset=False, actions_fn=actions)
+    ref = _run(monkeypatch, 0, B, 24, auto_reset=False, actions_fn=actions)
     assert ref[4] > 0
-    _same(_run(monkeypatch, 0, B, 24, auto_reset=False, actions_fn=actions), ref, "caller actions")
+    for tpl in (1, 2, 4):
+        _same(_run(monkeypatch, tpl, B, 24, auto_reset=False, actions_fn=actions), ref, f"caller TPL {tpl}")
 
 
-def test_group_step_env_id_base(monkeypatch):
-    """Lanes keyed by env_id_base + i (a rank's shard)."""
-    _same(_run(monkeypatch, 0, 2048, 30, env_id_base=123457), _run(monkeypatch, 1, 2048, 30, env_id_base=123457),
-          "env_id_base")
+def test_group_step_env_id_base_and_default_kernel(monkeypatch):
+    """Lanes keyed by env_id_base + i (a rank's shard), and an out-of-range
+    value selects k_step."""
+    ref = _run(monkeypatch, 0, 2048, 30, env_id_base=123457)
+    _same(_run(monkeypatch, 4, 2048, 30, env_id_base=123457), ref, "env_id_base")
+    monkeypatch.setenv("COUP_STEP_TPL", "3")
+    env = BatchedCoupEnv(64, seed=3, obs=False, device="cuda")
+    env.step()
+    assert env.error_count() == 0

@@ -53,11 +53,51 @@ def test_gpus_disagreeing_with_world_size_exits_nonzero():
     assert "disagrees with WORLD_SIZE=1" in r.stderr
 
 
+def _fake_kfd(tmp_path, simd_counts):
+    root = tmp_path / "nodes"
+    for i, c in enumerate(simd_counts):
+        d = root / str(i)
+        d.mkdir(parents=True)
+        (d / "properties").write_text(f"cpu_cores_count {0 if c else 16}\nsimd_count {c}\narray_count 32\n")
+    return str(root)
+
+
+def test_visible_gpus_from_kfd_topology(tmp_path):
+    """The launcher's GPU count: KFD nodes with SIMDs,
+    narrowed by ROCR_VISIBLE_DEVICES and HIP / CUDA_VISIBLE_DEVICES."""
+    root = _fake_kfd(tmp_path, [0, 1024, 1024, 1024, 0])  # 2 CPU nodes, 3 GPUs
+    assert bench.visible_gpus(root, env={}) == 3
+    assert bench.visible_gpus(root, env={"HIP_VISIBLE_DEVICES": "0,2"}) == 2
+    assert bench.visible_gpus(root, env={"CUDA_VISIBLE_DEVICES": "1"}) == 1
+    assert bench.visible_gpus(root, env={"HIP_VISIBLE_DEVICES": "0,1", "CUDA_VISIBLE_DEVICES": "0"}) == 2
+    assert bench.visible_gpus(root, env={"ROCR_VISIBLE_DEVICES": "GPU-aaaa,GPU-bbbb"}) == 2
+    assert bench.visible_gpus(root, env={"ROCR_VISIBLE_DEVICES": "0,1", "HIP_VISIBLE_DEVICES": "1"}) == 1
+    assert bench.visible_gpus(root, env={"HIP_VISIBLE_DEVICES": ""}) == 0
+    assert bench.visible_gpus(root, env={"HIP_VISIBLE_DEVICES": "0,1,2,3,4,5"}) == 3
+    assert bench.visible_gpus(str(tmp_path / "absent"), env={}) == 0
+
+
+def test_launcher_parent_never_imports_torch(tmp_path):
+    """The parent of `bench.py --gpus N` starts its ranks without importing
+    torch (so it cannot initialise HIP before it starts the children): run
+    the launcher in a fresh interpreter with fake ranks and check sys.modules
+    there, for both backends' paths."""
+    code = (
+        "import sys; sys.path.insert(0, %r); import bench\n"
+        "rc = bench.launch_ranks(2, ['--gpus', '2', '--batch', '10'], backend='gloo', script=%r)\n"
+        "n = bench.visible_gpus()\n"
+        "assert rc == 0, rc\n"
+        "assert 'torch' not in sys.modules, 'the launcher imported torch'\n"
+        "print('ok', n)\n") % (ROOT, FAKE)
+    r = subprocess.run([sys.executable, "-c", code], env=_env(), capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr
+    assert "ok" in r.stdout
+
+
 def test_gpus_beyond_visible_devices_exits_nonzero():
     """nccl (RCCL) runs one rank per GPU: more ranks than visible GPUs is an
     error before any rank starts (this container has none)."""
-    import torch
-    n = torch.cuda.device_count() + 1
+    n = bench.visible_gpus() + 1
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(max(n, 2))], env=_env(),
                        capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and not r.stdout.strip()

@@ -146,6 +146,87 @@ def test_device_builds_turn_the_slp_vectorizer_off(monkeypatch):
     monkeypatch.setattr(b.subprocess, "check_call", lambda cmd, *a, **k: cmds.append(cmd))
     b.build(force=True, repro=True)
     device = [c for c in cmds if c[0] == b.HIPCC and any(str(x).endswith(".hip") for x in c)]
-    assert len(device) == 3  # the two product sources and the reproducer
+    assert len(device) == 5  # the two product sources, their measurement build and the reproducer
     assert all(b.NO_SLP in c for c in device)
     assert b.NO_SLP in b.command() and b.NO_SLP in b.repro_command()
+
+
+# The kernels the product library ships: the A/B
+# variants measured and rejected in rounds 1-4 live in the measurement
+# build only (build/variants/, -DCOUP_AB_VARIANTS; csrc/coup_knobs.h).
+_SHIPPED_2P = """
+coup::k_info_elems coup::k_measure_traffic coup::k_obs_lanes coup::k_reset coup::k_rollout coup::k_server
+coup::k_step_trajectory coup::np::k_export coup::np::k_import |
+void coup::k_apply<false> | void coup::k_apply<true> | void coup::k_info_sweep<1024, 2> |
+void coup::k_obs_sweep_rows<512, 2> | void coup::k_query<false, false> | void coup::k_query<false, true> |
+void coup::k_query<true, false> | void coup::k_query<true, true> | void coup::k_rollout_sorted<1024> |
+void coup::k_slot<false> | void coup::k_slot<true> | void coup::k_slot_batch<false> | void coup::k_slot_batch<true> |
+void coup::k_step<false, 0, 256, 0, true> | void coup::k_step<false, 0, 256, 1, false> |
+void coup::k_step<false, 0, 256, 1, true> | void coup::k_step<false, 0, 256, 2, false> |
+void coup::k_step<false, 0, 256, 2, true> | void coup::k_step<false, 4, 256, 1, false> |
+void coup::k_step<false, 4, 256, 1, true> | void coup::k_step<false, 4, 256, 2, false> |
+void coup::k_step<false, 4, 256, 2, true> | void coup::k_step<false, 9, 256, 0, false> |
+void coup::k_step<false, 9, 256, 0, true> | void coup::k_step<true, 0, 256, 1, false> |
+void coup::k_step<true, 0, 256, 2, false> | void coup::k_step<true, 4, 256, 1, false> |
+void coup::k_step<true, 4, 256, 2, false> | void coup::k_step<true, 9, 256, 0, false> |
+void coup::k_step_group<1, false> | void coup::k_step_group<1, true> | void coup::k_step_obs_pipe<512, 2> |
+void coup::k_step_sorted<false, 512> | void coup::k_step_sorted<true, 512> | void coup::k_trajectory_sorted<1024>
+"""
+
+
+def _shipped_kernels():
+    words = _SHIPPED_2P.split("|")
+    names = set()
+    for w in words:
+        w = " ".join(w.split())
+        if w.startswith("coup::"):  # the plain (non-template) kernels
+            names.update(w.split())
+        elif w:
+            names.add(w)
+    for n in range(2, 7):
+        tb = 1024 if n >= 6 else 512
+        names.update(f"void coup::np::{k}<{n}>" for k in ("k_apply", "k_obs", "k_query", "k_reset", "k_rollout",
+                                                          "k_step_trajectory"))
+        names.update({f"void coup::np::k_step<{n}, false>", f"void coup::np::k_step<{n}, true>",
+                      f"void coup::np::k_rollout_sorted<{n}, 1024, true>",
+                      f"void coup::np::k_trajectory_sorted<{n}, 1024, 1>",
+                      f"void coup::np::k_step_sorted<{n}, false, false, {tb}, false, 4>",
+                      f"void coup::np::k_step_sorted<{n}, true, true, {tb}, false, 4>"})
+    return names
+
+
+def _kernel_handles(path):
+    """Kernel handle symbols of a HIP library (the host-side stubs the
+    runtime registers, one per instantiated __global__), demangled without
+    their parameter lists."""
+    import subprocess
+    out = subprocess.run(["nm", path], capture_output=True, text=True, check=True).stdout
+    mangled = [ln.split()[2] for ln in out.splitlines()
+               if len(ln.split()) == 3 and ln.split()[1] in "DV" and re.match(r"_ZN4coup(2np)?\d+k_", ln.split()[2])]
+    dem = subprocess.run(["c++filt"], input="\n".join(mangled), capture_output=True, text=True, check=True).stdout
+    return {ln.split("(")[0] for ln in dem.splitlines() if ln}
+
+
+def test_product_library_ships_only_the_shipped_kernels():
+    build.build()
+    got = _kernel_handles(_native.LIB_PATH)
+    want = _shipped_kernels()
+    assert got == want, {"unexpected": sorted(got - want), "missing": sorted(want - got)}
+    lib = ctypes.CDLL(_native.LIB_PATH)
+    assert lib.coup_build_flags() == 0
+
+
+def test_measurement_build_holds_the_variants():
+    """build() also writes the A/B-variant build; it holds every shipped
+    kernel and the rejected ones (a sample named here)."""
+    build.build()
+    got = _kernel_handles(build.VARIANTS_OUT)
+    assert _shipped_kernels() <= got
+    for k in ("void coup::k_obs_sweep<1>", "void coup::k_obs_sweep_rows<256, 2>", "void coup::k_step_group<4, true>",
+              "void coup::k_step<true, 1, 256, 0, false>", "void coup::k_step_sorted<true, 1024>",
+              "void coup::k_info_sweep<512, 2>", "void coup::np::k_step_sorted<6, true, true, 1024, true, 4>",
+              "void coup::np::k_rollout_sorted<6, 1024, false>", "void coup::np::k_trajectory_sorted<6, 1024, 0>"):
+        assert k in got, k
+    lib = ctypes.CDLL(build.VARIANTS_OUT)
+    lib.coup_build_flags.restype = ctypes.c_int
+    assert lib.coup_build_flags() == _native.BUILD_AB_VARIANTS

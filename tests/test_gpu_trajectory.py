@@ -105,14 +105,15 @@ def test_trajectory_with_tensors_and_refusals():
 def test_regrouped_trajectory_store_forms(monkeypatch, n, players):
     """The regrouped N-player trajectory stages each step's outputs by lane
     and stores them from each lane's home thread (default) or where the lane
-    is played (COUP_TRAJ_STAGE=0), on ragged batches (slices not 4-lane
-    aligned) and whole ones: both equal coup_step launched once per step."""
+    is played (COUP_TRAJ_STAGE=0: the measurement build,
+    tests/ab_variants/test_ab_trajectory.py), on ragged batches (slices not
+    4-lane aligned) and whole ones: equal to coup_step launched once per step."""
     monkeypatch.setenv("COUP_REGROUP", "1")
     T = 40
     kw = dict(seed=7 + n, env_id_base=5 << 20, auto_reset=True, obs=False, num_players=players, episode_stats=True)
     ref = BatchedCoupEnv(n, **kw)
     br = _stepped(ref, T, ref.trajectory_buffers(T))
-    for form in ("1", "0"):
+    for form in ("1",):
         monkeypatch.setenv("COUP_TRAJ_STAGE", form)
         env = BatchedCoupEnv(n, **kw)
         bf = env.collect_trajectory(T)
