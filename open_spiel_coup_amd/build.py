@@ -114,6 +114,17 @@ REPRO_SRC = os.path.join(ROOT, "tools", "slot_inline_repro.hip")
 REPRO_OUT = os.path.join(ROOT, "build", "slot_inline_repro")
 
 
+INFO_REPRO_SRC = os.path.join(ROOT, "tools", "info_prefix_repro.hip")
+INFO_REPRO_OUT = os.path.join(ROOT, "build", "info_prefix_repro")
+
+
+def info_repro_command():
+    """The uint2-prefix reproducer of round 4's k_info_sweep sighting
+    (tests/test_gpu_codegen_hazard.py), with the product's device flags."""
+    return [HIPCC, f"--offload-arch={ARCH}", "-O3", NO_SLP, "-std=c++17", "-I", os.path.join(ROOT, "include"),
+            "-I", CSRC, INFO_REPRO_SRC, "-o", INFO_REPRO_OUT]
+
+
 def build_repro(force=False):
     """The k_slot miscompile reproducer (investigation tool, DESIGN.md
     section 12; tests/test_gpu_codegen_hazard.py runs it on the GPU)."""
@@ -181,6 +192,9 @@ def build(force=False, verbose=False, repro=False, variants=True):
     if repro and (force or not up_to_date(REPRO_OUT, [REPRO_SRC] + DEPS)):
         os.makedirs(os.path.dirname(REPRO_OUT), exist_ok=True)
         jobs.append(repro_command())
+    if repro and (force or not up_to_date(INFO_REPRO_OUT, [INFO_REPRO_SRC] + DEPS)):
+        os.makedirs(os.path.dirname(INFO_REPRO_OUT), exist_ok=True)
+        jobs.append(info_repro_command())
     _run_all(jobs, verbose)
     if links:
         _run_all(links, verbose)

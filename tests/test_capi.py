@@ -146,9 +146,9 @@ def test_device_builds_turn_the_slp_vectorizer_off(monkeypatch):
     monkeypatch.setattr(b.subprocess, "check_call", lambda cmd, *a, **k: cmds.append(cmd))
     b.build(force=True, repro=True)
     device = [c for c in cmds if c[0] == b.HIPCC and any(str(x).endswith(".hip") for x in c)]
-    assert len(device) == 5  # the two product sources, their measurement build and the reproducer
+    assert len(device) == 6  # the two product sources, their measurement build and the two reproducers
     assert all(b.NO_SLP in c for c in device)
-    assert b.NO_SLP in b.command() and b.NO_SLP in b.repro_command()
+    assert b.NO_SLP in b.command() and b.NO_SLP in b.repro_command() and b.NO_SLP in b.info_repro_command()
 
 
 # The kernels the product library ships: the A/B

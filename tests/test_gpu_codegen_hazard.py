@@ -42,3 +42,27 @@ def test_shipped_slot_form_matches_per_lane_rules():
     print("\ninlined k_slot copies, mismatching records of 20000:", counts)
     # built without the SLP vectorizer, the inlined shapes compile right too
     assert all(c == 0 for c in counts.values()), counts
+
+
+INFO_EXE = os.path.join(ROOT, "build", "info_prefix_repro")
+
+
+def test_info_prefix_forms_against_the_reference_writer():
+    """Round 4's second sighting: the split
+    InformationStateTensor writer with its prefix words stored as uint2
+    (<2 x i32>) LDS stores gave a few lanes in 1000 wrong observer bits.
+    build/info_prefix_repro (tools/info_prefix_repro.hip) writes 100,000
+    generated states' tensors with that first form (k_sweep_uint2, three
+    block shapes) and with the shipped one (k_sweep_rows, 32-bit stores),
+    against a one-thread-per-float4 reference (k_info_elems' decode).  The
+    shipped form must match on every lane; the uint2 form's count is
+    printed (it is not shipped: info_prefix_to_lds stores 32-bit words)."""
+    if not os.path.exists(INFO_EXE):
+        pytest.fail("build/info_prefix_repro missing: run __graft_entry__.build()")
+    out = subprocess.run([INFO_EXE, "100000"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    lines = {d["kernel"]: d for d in (json.loads(x) for x in out.stdout.splitlines() if x.startswith("{"))}
+    print("\n" + "\n".join(json.dumps(v) for v in lines.values()))
+    shipped = [v for k, v in lines.items() if k.startswith("k_sweep_rows")]
+    assert shipped and all(v["mismatching_lanes"] == 0 for v in shipped), shipped
+    assert all(v["terminal_lanes"] > 0 for v in lines.values())  # finished games are in the sample

@@ -1,7 +1,7 @@
 # Round 5, first call: the pipelined split observation step (coup_step_many,
 # k_step_obs_pipe) -- its equality tests and the c3 headline check against the
 # oracle, then a same-process A/B of the step forms in the driver's form, the
-# driver's bench line, and the c3 profile (trace + PMC passes).
+# driver's bench line, smoke(), and the c3 profile (trace + PMC passes).
 set -u
 D=gpurun_out/r05a
 mkdir -p $D
@@ -13,5 +13,7 @@ timeout -k 10 300 python -u tools/pipe_ab.py > $D/pipe_ab.jsonl 2> $D/pipe_ab.er
 cat $D/pipe_ab.jsonl
 timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > $D/bench_c3.json 2> $D/bench_c3.err || { tail -20 $D/bench_c3.err; exit 1; }
 cat $D/bench_c3.json
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $D/smoke.log 2>&1 || { tail -20 $D/smoke.log; exit 1; }
+tail -1 $D/smoke.log
 timeout -k 10 900 bash tools/profile_gpu.sh r05 c3 > $D/profile.log 2>&1 || { tail -30 $D/profile.log; exit 1; }
 tail -5 $D/profile.log
