@@ -39,14 +39,17 @@ return sums (the collation of SURVEY.md 8(e)).
 roofline: algorithmic bytes per launch over the step
 kernel's average duration from HIP events on the launch stream; traffic:
 HBM bytes per launch from the rocprofv3 PMC passes recorded in profiles/
-(null if absent).  For the 2-player step configs the same process then
-times coup_measure_step_traffic -- the step's loads and stores in the same
-order with no rules -- over the same buffers: roofline.store_ceiling_ms is
-that ceiling on this box, frac_of_store_ceiling = ceiling / kernel time.
-From 2^20 lanes the observation step is split (coup_obs_split_variant): the
-rules step without tensors, then an address-order observation writer; the
-timed span covers both kernels, and the store ceiling is then the fused
-form's (lane-owned) one, which the split form is not bound by.
+(null if absent).  From 2^20 lanes the observation step is split
+(coup_obs_split_variant: the rules step without tensors, then an
+address-order observation writer) and its K timed steps are pipelined
+(coup_step_many: the rules of step t + 1 run in the launch that writes step
+t's observations); c3i's InformationStateTensor step is split from 2^18
+lanes.  The same process then times the writer's store ceiling on this box:
+for the split / pipelined steps coup_measure_store_sweep -- the same
+address-order grid over the same tensor buffer, stores only -- and for the
+fused step coup_measure_step_traffic (its loads and stores with no rules);
+roofline.store_ceiling_ms is that ceiling, frac_of_store_ceiling = ceiling /
+kernel time, store_ceiling_form says which.
 `box` names the GPU box (boxes differ in HBM store rate).
 cpu_baseline: the C oracle (a scalar port of the reference rules, ~14x
 faster than the reference's own C++ on the survey host) on one
@@ -364,6 +367,36 @@ def _time_traffic_ceiling(env, steps, stream):
     return a.elapsed_time(b) / steps
 
 
+def _time_sweep_ceiling(buf, nf4, threads, passes, steps, stream):
+    """Average duration of coup_measure_store_sweep -- the split writers'
+    address-order store grid with no decode -- over the tensor buffer `buf`
+    (nf4 float4), K launches replayed from one HIP graph like the steps."""
+    import ctypes
+    import torch
+    from open_spiel_coup_amd import _native
+    lib = _native.load()
+
+    def launch(s):
+        _native.check(lib.coup_measure_store_sweep(ctypes.c_void_p(buf.data_ptr()), int(nf4), threads, passes, 0,
+                                                   ctypes.c_void_p(s)))
+
+    for _ in range(3):
+        launch(stream.cuda_stream)
+    g = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream(buf.device)
+    side.wait_stream(stream)
+    with torch.cuda.graph(g, stream=side):
+        for _ in range(steps):
+            launch(side.cuda_stream)
+    stream.wait_stream(side)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(stream)
+    g.replay()
+    b.record(stream)
+    b.synchronize()
+    return a.elapsed_time(b) / steps
+
+
 def _calibrate_gate(env, stream):
     """Steps of an untimed rollout (the gate) that keep the GPU busy for
     twice the host's enqueue latency of one fused rollout (event record +
@@ -640,9 +673,21 @@ def main():
     collective_ms_ranks = [float(x) for x in
                            D.collate(torch.tensor([collective_ms], dtype=torch.float64, device=dev), force=force)]
     errors = env.error_count()
-    ceiling_ms = None
-    if players == 2 and not fused and not with_info:
-        ceiling_ms = _time_traffic_ceiling(env, args.steps, stream)
+    # the store ceiling of the step's writer, timed in this process on this
+    # box: the split / pipelined steps' address-order writers against a
+    # store-only sweep of their tensor buffer with the same grid; the fused
+    # step against its own loads and stores with no rules
+    ceiling_ms, ceiling_form = None, None
+    if players == 2 and not fused:
+        if with_obs and obs_split_active(B):
+            ceiling_ms = _time_sweep_ceiling(env.obs, B * 49, 512, 2, args.steps, stream)
+            ceiling_form = "sweep: [B][2][98] fp32 stores in address order, 512 x 2 grid, no decode"
+        elif with_info and info_split_active(B):
+            ceiling_ms = _time_sweep_ceiling(env.info_state, B * 1246, 1024, 2, args.steps, stream)
+            ceiling_form = "sweep: [B][2][2492] fp32 stores in address order, 1024 x 2 grid, no decode"
+        elif not with_info:
+            ceiling_ms = _time_traffic_ceiling(env, args.steps, stream)
+            ceiling_form = "fused: the fused step's loads and stores, no rules"
 
     if rank == 0:
         bytes_per_launch = bytes_per_lane * B * (args.steps if fused else 1)
@@ -717,9 +762,7 @@ def main():
                          "kernel_ms": launch_ms, "bytes_per_launch": bytes_per_launch,
                          "store_ceiling_ms": ceiling_ms,
                          "frac_of_store_ceiling": (ceiling_ms / launch_ms) if ceiling_ms else None,
-                         # the ceiling is the fused (lane-owned) store pattern's; the split step
-                         # writes in address order and is not bound by it
-                         "store_ceiling_form": ("fused" if ceiling_ms else None),
+                         "store_ceiling_form": ceiling_form,
                          "step_form": ("pipelined" if with_obs and pipelined_active(B, players, graph is not None)
                                        else "split" if (with_obs and players == 2 and obs_split_active(B)) or
                                        (with_info and info_split_active(B)) else "fused")},

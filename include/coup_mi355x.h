@@ -424,6 +424,17 @@ int coup_error_count(coup_env* env, int64_t* out);
  * coup_step_outputs (any may be NULL).  Asynchronous on `hip_stream`. */
 int coup_measure_step_traffic(int64_t batch, uint32_t* records, const coup_step_outputs* out, void* hip_stream);
 
+/* Measurement helper: the split writers' store pattern with no decode --
+ * n_float4 float4 of the device buffer dst written in address order by
+ * blocks of `threads` threads, `passes` float4 per thread (the grid of
+ * k_obs_sweep_rows<512, 2> / k_info_sweep<1024, 2>: threads x passes =
+ * 512 x 2 or 1024 x 2; a measurement build takes more shapes, and with
+ * `resident` a grid-stride form from a resident grid), non-temporal.  Its
+ * duration is those writers' store ceiling on the box at hand (bench.py:
+ * roofline.store_ceiling_ms of the split and pipelined steps).
+ * Asynchronous on `hip_stream`; the buffer's contents are a pattern. */
+int coup_measure_store_sweep(float* dst, int64_t n_float4, int threads, int passes, int resident, void* hip_stream);
+
 /* Measurement helper: the observation-step form coup_step uses for a batch
  * of `batch` 2-player lanes with observations and no information state --
  * 0 the fused step kernel, > 0 the split form's writer variant (the rules

@@ -26,7 +26,7 @@ SYMBOLS = (
     "coup_step_trajectory", "coup_step_many", "coup_step_host", "coup_step_host_layout",
     "coup_new_initial_state", "coup_apply_action", "coup_query",
     "coup_export_state", "coup_import_state", "coup_export_history",
-    "coup_import_history", "coup_error_count", "coup_slot_op", "coup_slot_ops", "coup_measure_step_traffic", "coup_obs_split_variant",
+    "coup_import_history", "coup_error_count", "coup_slot_op", "coup_slot_ops", "coup_measure_step_traffic", "coup_measure_store_sweep", "coup_obs_split_variant",
     "coup_info_split_variant", "coup_build_flags",
     "coup_server_create", "coup_server_destroy", "coup_attach_server", "coup_server_stats",
     "coup_host_state_init", "coup_host_state_apply", "coup_host_state_tensors", "coup_host_state_string",
@@ -115,6 +115,7 @@ def load():
         "coup_slot_op": ([vp, i64, vp, i64, i32, i32, vp], i32),
         "coup_slot_ops": ([vp, i64, ctypes.POINTER(SlotReq), vp, i32, vp], i32),
         "coup_measure_step_traffic": ([i64, vp, ctypes.POINTER(StepOutputs), vp], i32),
+        "coup_measure_store_sweep": ([vp, i64, i32, i32, i32, vp], i32),
         "coup_obs_split_variant": ([i64], i32),
         "coup_info_split_variant": ([i64], i32),
         "coup_build_flags": ([], i32),

@@ -1028,6 +1028,47 @@ __global__ __launch_bounds__(kThreads, 8) void k_measure_traffic(StepArgs a) {
   }
 }
 
+// coup_measure_store_sweep: the split writers' store pattern with no
+// decode -- block b writes float4s [b T S, (b + 1) T S) of a buffer of
+// nf4 float4 in S passes of T (the grid shape of k_obs_sweep_rows<T, S> /
+// k_info_sweep<T, S>), non-temporal, as they do.  Its duration is the
+// writers' store ceiling on the box at hand (bench.py: roofline.
+// store_ceiling_ms of the split / pipelined steps).  The value stored is
+// the float4's index bits (no all-zero lines).
+template <int T, int S>
+__global__ __launch_bounds__(T) void k_store_sweep(float* __restrict__ dst, int64_t nf4) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  const int64_t x0 = (int64_t)blockIdx.x * (T * S) + threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    const int64_t x = x0 + j * T;
+    if (x >= nf4) break;
+    const float f = __int_as_float((int)(x & 0x3FFFFF));  // small denormals: a pattern, never read
+    v4f v = {f, f, f, f};
+    __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(dst) + x);
+  }
+}
+
+#ifdef COUP_AB_VARIANTS
+// measurement builds: the same stores from a resident grid, each block
+// looping over chunks of T S float4 (grid-stride), without a wave launch
+// per chunk
+template <int T, int S>
+__global__ __launch_bounds__(T) void k_store_sweep_resident(float* __restrict__ dst, int64_t nf4) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  for (int64_t c = blockIdx.x; c * (T * S) < nf4; c += gridDim.x) {
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      const int64_t x = c * (T * S) + j * T + threadIdx.x;
+      if (x >= nf4) break;
+      const float f = __int_as_float((int)(x & 0x3FFFFF));
+      v4f v = {f, f, f, f};
+      __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(dst) + x);
+    }
+  }
+}
+#endif
+
 struct RolloutArgs {
   uint4* state;
   int64_t n;
@@ -3796,6 +3837,41 @@ int coup_measure_step_traffic(int64_t batch, uint32_t* records, const coup_step_
   coup::k_measure_traffic<<<grid_for(batch), coup::kThreads, 0, (hipStream_t)hip_stream>>>(a);
   COUP_HIP_TRY(hipGetLastError());
   return COUP_OK;
+}
+
+int coup_measure_store_sweep(float* dst, int64_t n_float4, int threads, int passes, int resident, void* hip_stream) {
+  if (!dst || n_float4 < 0) return fail(COUP_E_INVALID, "coup_measure_store_sweep: bad buffer");
+  if (n_float4 == 0) return COUP_OK;
+  hipStream_t s = (hipStream_t)hip_stream;
+  auto go = [&](auto tt, auto ss) -> int {
+    constexpr int T = decltype(tt)::value, S = decltype(ss)::value;
+    const int64_t blocks = (n_float4 + T * S - 1) / (T * S);
+    if (resident) {
+#ifdef COUP_AB_VARIANTS
+      int dev = 0, cus = 0;
+      COUP_HIP_TRY(hipGetDevice(&dev));
+      COUP_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+      const int64_t grid = std::min<int64_t>(blocks, (int64_t)cus * (2048 / T));
+      coup::k_store_sweep_resident<T, S><<<(unsigned)grid, T, 0, s>>>(dst, n_float4);
+#else
+      return fail(COUP_E_INVALID, "coup_measure_store_sweep: the resident form is a measurement build's");
+#endif
+    } else {
+      coup::k_store_sweep<T, S><<<(unsigned)blocks, T, 0, s>>>(dst, n_float4);
+    }
+    COUP_HIP_TRY(hipGetLastError());
+    return COUP_OK;
+  };
+  // the shipped writers' shapes: 512 x 2 (observations), 1024 x 2 (info state)
+  if (threads == 512 && passes == 2) return go(std::integral_constant<int, 512>(), std::integral_constant<int, 2>());
+  if (threads == 1024 && passes == 2) return go(std::integral_constant<int, 1024>(), std::integral_constant<int, 2>());
+#ifdef COUP_AB_VARIANTS
+  if (threads == 256 && passes == 2) return go(std::integral_constant<int, 256>(), std::integral_constant<int, 2>());
+  if (threads == 512 && passes == 4) return go(std::integral_constant<int, 512>(), std::integral_constant<int, 4>());
+  if (threads == 1024 && passes == 4) return go(std::integral_constant<int, 1024>(), std::integral_constant<int, 4>());
+  if (threads == 1024 && passes == 8) return go(std::integral_constant<int, 1024>(), std::integral_constant<int, 8>());
+#endif
+  return fail(COUP_E_INVALID, "coup_measure_store_sweep: shape not in this build");
 }
 
 }  // extern "C"

@@ -60,11 +60,12 @@ def _check_step(o, ref, t, k, obs_key):
         np.testing.assert_array_equal(_np(o["info_state"][sl]), ref["info"][t], err_msg=msg)
 
 
-def _check_records(env, B, seed, steps, stats_from=None):
+def _check_records(env, B, seed, steps, stats_from=None, cur_player=None):
     """Full records (and, with stats_from, the per-episode accumulators since
-    step `stats_from`) of the three slices after `steps` steps."""
+    step `stats_from`) of the three slices after `steps` steps; cur_player:
+    the last step's current players (default: the env's output buffer)."""
     words = _np(env.export_state()).astype(np.uint32)
-    cur = _np(env.cur_player)
+    cur = _np(env.cur_player if cur_player is None else cur_player)
     hist = _np(env.export_history()) if env.history else None
     for k in _slices(B):
         ref = oracle.rollout(seed=seed, n=256, steps=steps, env_id_base=k, auto_reset=True, want_trajectory=False)
@@ -140,8 +141,9 @@ def test_c3_headline_kernel_full_batch_slices_match_oracle():
         for k, ref in refs.items():
             _check_step(o_s, ref, t, k, "obs")
         t += 1
+    last_cur = buf["current_player"][TK - 1].clone()
     del buf
-    _check_records(env, B, seed, t, stats_from=settle + warm)
+    _check_records(env, B, seed, t, stats_from=settle + warm, cur_player=last_cur)
     assert t == total
     assert env.error_count() == 0
 
