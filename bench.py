@@ -41,11 +41,12 @@ kernel's average duration from HIP events on the launch stream; traffic:
 HBM bytes per launch from the rocprofv3 PMC passes recorded in profiles/
 (null if absent).  From 2^20 lanes the observation step is split
 (coup_obs_split_variant: the rules step without tensors, then an
-address-order observation writer) and its K timed steps are pipelined
-(coup_step_many: the rules of step t + 1 run in the launch that writes step
-t's observations); c3i's InformationStateTensor step is split from 2^18
-lanes.  The same process then times the writer's store ceiling on this box:
-for the split / pipelined steps coup_measure_store_sweep -- the same
+address-order observation writer) and its K timed steps run as coup_step_many's
+rules-trajectory form (chunks of up to 8 steps as one regrouped rules launch
+that keeps the records in registers and stores every step's records, then
+the writer once per step); c3i's InformationStateTensor step is split from
+2^18 lanes.  The same process then times the writer's store ceiling on this
+box: for the split steps coup_measure_store_sweep -- the same
 address-order grid over the same tensor buffer, stores only -- and for the
 fused step coup_measure_step_traffic (its loads and stores with no rules);
 roofline.store_ceiling_ms is that ceiling, frac_of_store_ceiling = ceiling /
@@ -174,13 +175,37 @@ def obs_split_active(batch):
     return int(_native.load().coup_obs_split_variant(int(batch)))
 
 
-def pipelined_active(batch, players, graph):
-    """Whether the timed steps run as the pipelined split step: uniform steps
-    recorded through coup_step_many (the graph path) on a 2-player env whose
-    split step uses the shipped writer (variant 11), COUP_PIPE not 0
-    (mirrors coup_kernels.hip `pipelined`)."""
-    return (graph and players == 2 and obs_split_active(batch) == 11 and
-            os.environ.get("COUP_PIPE", "1").strip() not in ("0", ""))
+TRAJ_CHUNK_MAX = 8  # coup::kTrajChunkMax
+
+
+def step_many_form(batch, players, graph):
+    """The form coup_step_many gives the timed steps (uniform steps recorded
+    through it: the graph path) on a 2-player env whose split step uses the
+    shipped writer (variant 11) -- "rules-trajectory" (COUP_PIPE=1, the
+    default: chunks of COUP_TRAJ_CHUNK steps as one regrouped rules launch
+    plus a writer launch per step; needs the regrouped rules), "pipelined"
+    (COUP_PIPE=2, measurement builds: rules(t + 1) beside writer(t) in one
+    launch) -- or None (per-step launches).  Mirrors coup_kernels.hip
+    `many_form`."""
+    if not (graph and players == 2 and obs_split_active(batch) == 11):
+        return None
+    v = os.environ.get("COUP_PIPE", "1").strip()
+    if v == "0":
+        return None
+    if v == "2":
+        from open_spiel_coup_amd import _native
+        if _native.load().coup_build_flags() & _native.BUILD_AB_VARIANTS:
+            return "pipelined"
+    return "rules-trajectory" if _regrouped(batch) else None
+
+
+def traj_chunk():
+    """COUP_TRAJ_CHUNK as coup::read_knobs clamps it."""
+    try:
+        c = int(os.environ.get("COUP_TRAJ_CHUNK", TRAJ_CHUNK_MAX))
+    except ValueError:
+        c = TRAJ_CHUNK_MAX
+    return c if 1 <= c <= TRAJ_CHUNK_MAX else TRAJ_CHUNK_MAX
 
 
 _INFO_WRITERS = {1: "coup::k_info_sweep<512, 2>", 2: "coup::k_info_sweep<256, 2>", 3: "coup::k_info_sweep<1024, 2>",
@@ -580,7 +605,7 @@ def main():
         # folded an int16 word and the collate below refused it)
         env.clear_episode_stats()
         # uniform steps are recorded through coup_step_many: from 2^20 lanes
-        # with observations the pipelined split step (k_step_obs_pipe)
+        # with observations its rules-trajectory split step
         graph = env.capture_steps(args.steps)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))]
     elif fused:
@@ -681,10 +706,10 @@ def main():
     if players == 2 and not fused:
         if with_obs and obs_split_active(B):
             ceiling_ms = _time_sweep_ceiling(env.obs, B * 49, 512, 2, args.steps, stream)
-            ceiling_form = "sweep: [B][2][98] fp32 stores in address order, 512 x 2 grid, no decode"
+            ceiling_form = "sweep: [B][2][98] fp32 stores in address order, 512 x 2 grid, no decode, tensor-like data"
         elif with_info and info_split_active(B):
             ceiling_ms = _time_sweep_ceiling(env.info_state, B * 1246, 1024, 2, args.steps, stream)
-            ceiling_form = "sweep: [B][2][2492] fp32 stores in address order, 1024 x 2 grid, no decode"
+            ceiling_form = "sweep: [B][2][2492] fp32 stores in address order, 1024 x 2 grid, no decode, tensor-like data"
         elif not with_info:
             ceiling_ms = _time_traffic_ceiling(env, args.steps, stream)
             ceiling_form = "fused: the fused step's loads and stores, no rules"
@@ -720,9 +745,13 @@ def main():
                       if isplit else "coup::k_step<true, 0, 256, 2, false>")
         elif with_obs:
             split = obs_split_active(B) if players == 2 else 0
-            if pipelined_active(B, players, graph is not None):
+            form = step_many_form(B, players, graph is not None)
+            if form == "pipelined":
                 # one launch per step: the rules of step t + 1 beside the writer of step t
                 kernel = "coup::k_step_obs_pipe<512, 2>"
+            elif form:
+                # one rules-trajectory launch per chunk of steps + the writer per step
+                kernel = "coup::k_trajectory_sorted<1024, true> + " + _SPLIT_WRITERS.get(split, "coup::k_obs_sweep")
             elif split:
                 # the rules step without tensors (regrouped from 2^18 lanes) + the writer
                 kernel = "coup::k_step_sorted<true, 512> + " + _SPLIT_WRITERS.get(split, "coup::k_obs_sweep")
@@ -763,8 +792,8 @@ def main():
                          "store_ceiling_ms": ceiling_ms,
                          "frac_of_store_ceiling": (ceiling_ms / launch_ms) if ceiling_ms else None,
                          "store_ceiling_form": ceiling_form,
-                         "step_form": ("pipelined" if with_obs and pipelined_active(B, players, graph is not None)
-                                       else "split" if (with_obs and players == 2 and obs_split_active(B)) or
+                         "step_form": ((with_obs and step_many_form(B, players, graph is not None))
+                                       or "split" if (with_obs and players == 2 and obs_split_active(B)) or
                                        (with_info and info_split_active(B)) else "fused")},
             "episodes": {"finished": ep_total, "mean_return_p0": ret_total / max(ep_total, 1),
                          "collective": ("all_gather [world*B] int16 (return sum << 8 | episodes per lane)"

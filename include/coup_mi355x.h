@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define COUP_ABI_VERSION 12
+#define COUP_ABI_VERSION 13
 
 #define COUP_NUM_PLAYERS 2          /* coup.h:42 */
 #define COUP_MAX_PLAYERS 6          /* N-player extension */
@@ -429,11 +429,15 @@ int coup_measure_step_traffic(int64_t batch, uint32_t* records, const coup_step_
  * blocks of `threads` threads, `passes` float4 per thread (the grid of
  * k_obs_sweep_rows<512, 2> / k_info_sweep<1024, 2>: threads x passes =
  * 512 x 2 or 1024 x 2; a measurement build takes more shapes, and with
- * `resident` a grid-stride form from a resident grid), non-temporal.  Its
- * duration is those writers' store ceiling on the box at hand (bench.py:
- * roofline.store_ceiling_ms of the split and pipelined steps).
- * Asynchronous on `hip_stream`; the buffer's contents are a pattern. */
-int coup_measure_store_sweep(float* dst, int64_t n_float4, int threads, int passes, int resident, void* hip_stream);
+ * COUP_SWEEP_RESIDENT in `mode` a grid-stride form from a resident grid),
+ * non-temporal.  Its duration is those writers' store ceiling on the box at
+ * hand (bench.py: roofline.store_ceiling_ms of the split steps).  The data:
+ * tensor-like (0.0 with a 1.0 in one float of 32), or with
+ * COUP_SWEEP_INDEX_BITS every float the float4's index bits (HBM store time
+ * depends on the data).  Asynchronous on `hip_stream`. */
+#define COUP_SWEEP_RESIDENT 1
+#define COUP_SWEEP_INDEX_BITS 2
+int coup_measure_store_sweep(float* dst, int64_t n_float4, int threads, int passes, int mode, void* hip_stream);
 
 /* Measurement helper: the observation-step form coup_step uses for a batch
  * of `batch` 2-player lanes with observations and no information state --

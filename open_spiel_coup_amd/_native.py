@@ -11,13 +11,14 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # COUP_LIB_PATH: load another build of the same library (A/B timing of two
 # builds, tools/ab_builds.sh); there is still no fallback
 LIB_PATH = os.environ.get("COUP_LIB_PATH") or os.path.join(HERE, "libcoup_mi355x.so")
-ABI_VERSION = 12
+ABI_VERSION = 13
 FLAG_AUTO_RESET, FLAG_HISTORY, FLAG_GENERIC, FLAG_UNCHECKED = 1, 2, 4, 8
 MAX_PLAYERS = 6
 HISTORY_BYTES = 96
 
 COUP_OK, COUP_E_INVALID, COUP_E_HIP, COUP_E_LANES = 0, 1, 2, 3
 BUILD_AB_VARIANTS = 1  # coup_build_flags: a measurement build with every A/B variant
+SWEEP_RESIDENT, SWEEP_INDEX_BITS = 1, 2  # coup_measure_store_sweep mode bits
 
 # Every symbol declared in include/coup_mi355x.h
 SYMBOLS = (

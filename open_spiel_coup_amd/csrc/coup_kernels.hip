@@ -1033,19 +1033,32 @@ __global__ __launch_bounds__(kThreads, 8) void k_measure_traffic(StepArgs a) {
 // nf4 float4 in S passes of T (the grid shape of k_obs_sweep_rows<T, S> /
 // k_info_sweep<T, S>), non-temporal, as they do.  Its duration is the
 // writers' store ceiling on the box at hand (bench.py: roofline.
-// store_ceiling_ms of the split / pipelined steps).  The value stored is
-// the float4's index bits (no all-zero lines).
-template <int T, int S>
-__global__ __launch_bounds__(T) void k_store_sweep(float* __restrict__ dst, int64_t nf4) {
+// store_ceiling_ms of the split steps).  The values stored: like the
+// tensors' (0.0 with a 1.0 in one float of 32: one-hot ObservationTensor /
+// InformationStateTensor fields), or with `bits` the float4's index bits in
+// every float (no all-zero lines; round 5a's form, measured 3-12 % slower
+// than the tensor-like data on the same buffer: HBM store time depends on
+// the data, profiles/r05/sweep).
+__device__ inline void sweep_store(float* dst, int64_t x, bool bits) {
   typedef float v4f __attribute__((ext_vector_type(4)));
+  v4f v;
+  if (bits) {
+    const float f = __int_as_float((int)(x & 0x3FFFFF));  // small denormals: a pattern, never read
+    v = v4f{f, f, f, f};
+  } else {
+    v = v4f{(x & 7) == 0 ? 1.0f : 0.0f, 0.0f, 0.0f, 0.0f};
+  }
+  __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(dst) + x);
+}
+
+template <int T, int S>
+__global__ __launch_bounds__(T) void k_store_sweep(float* __restrict__ dst, int64_t nf4, int bits) {
   const int64_t x0 = (int64_t)blockIdx.x * (T * S) + threadIdx.x;
 #pragma unroll
   for (int j = 0; j < S; ++j) {
     const int64_t x = x0 + j * T;
     if (x >= nf4) break;
-    const float f = __int_as_float((int)(x & 0x3FFFFF));  // small denormals: a pattern, never read
-    v4f v = {f, f, f, f};
-    __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(dst) + x);
+    sweep_store(dst, x, bits != 0);
   }
 }
 
@@ -1054,16 +1067,13 @@ __global__ __launch_bounds__(T) void k_store_sweep(float* __restrict__ dst, int6
 // looping over chunks of T S float4 (grid-stride), without a wave launch
 // per chunk
 template <int T, int S>
-__global__ __launch_bounds__(T) void k_store_sweep_resident(float* __restrict__ dst, int64_t nf4) {
-  typedef float v4f __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(T) void k_store_sweep_resident(float* __restrict__ dst, int64_t nf4, int bits) {
   for (int64_t c = blockIdx.x; c * (T * S) < nf4; c += gridDim.x) {
 #pragma unroll
     for (int j = 0; j < S; ++j) {
       const int64_t x = c * (T * S) + j * T + threadIdx.x;
       if (x >= nf4) break;
-      const float f = __int_as_float((int)(x & 0x3FFFFF));
-      v4f v = {f, f, f, f};
-      __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(dst) + x);
+      sweep_store(dst, x, bits != 0);
     }
   }
 }
@@ -1456,9 +1466,19 @@ __global__ __launch_bounds__(T, 8) void k_rollout_sorted(RolloutArgs a) {
 // that finished with auto-reset keeps kKeyReset, and the next step's reset
 // group deals its new episode and completes the finished step's legal mask
 // and player; kKeyFirst restarts a lane that is terminal as a step starts).
-// Results equal coup_step's, step for step.
-template <int T>
-__global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t steps) {
+// Results equal coup_step's, step for step.  Step s's outputs go to offset
+// s * x.stride of the output buffers (x.stride = B: [steps][B] slices; 0:
+// every step overwrites them, the last step's stay).  REC: also every
+// step's post-step record (after an auto-reset) to x.rec[s * B + lane] --
+// the records the observation writer of step s reads (coup_step_many's
+// rules-trajectory form).
+struct TrajOut {
+  uint4* rec;      // REC: [steps][B] post-step records
+  int64_t stride;  // output offset per step: B or 0
+};
+
+template <int T, bool REC = false>
+__global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t steps, TrajOut x) {
   static_assert((T & (T - 1)) == 0 && T >= 64 && T <= 1024, "power-of-two block of whole waves");
   constexpr uint32_t kO = T <= 256 ? 8u : 10u;  // lane bits of s_meta
   __shared__ uint4 s_rec[T];
@@ -1501,7 +1521,8 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
     L = unpack(s_rec[t]);
     const int64_t li = base + lane;
     if (li >= a.n) continue;  // past the batch
-    const int64_t o = s * a.n + li;
+    const int64_t o = s * x.stride + li;
+    uint4* const rec_s = REC ? x.rec + s * a.n + li : nullptr;  // step s's record of the lane
     rng.env_id = lane_stream_id(a.env_id_base, li);
     rng.blk_tag = 0u;
     // a new episode and a live lane after resolve_chance are at decision
@@ -1514,14 +1535,16 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
       if (a.step_type) a.step_type[o] = (uint8_t)COUP_STEP_FIRST;
       if (a.legal) a.legal[o] = legal;
       if (a.cur_player) a.cur_player[o] = (int8_t)L.M;
+      if (REC) *rec_s = pack(L);
       key = regroup_key(L, sample_action(legal, rng.draw(L.episode, L.move)));
       continue;
     }
     if (key == kKeyReset) {  // finished in step s - 1 with auto-reset (vector_env.py:62-65)
       L = new_episode(L.episode + 1u, rng, none);
       const uint32_t legal = decision_mask(L);
-      if (a.legal) a.legal[o - a.n] = legal;
-      if (a.cur_player) a.cur_player[o - a.n] = (int8_t)L.M;
+      if (a.legal) a.legal[o - x.stride] = legal;
+      if (a.cur_player) a.cur_player[o - x.stride] = (int8_t)L.M;
+      if (REC) *(rec_s - a.n) = pack(L);  // step s - 1's record, after its auto-reset
       key = regroup_key(L, sample_action(legal, rng.draw(L.episode, L.move)));
     }
     if (key == kKeyDead) {  // no legal decision: coup_step's rejected step
@@ -1531,16 +1554,17 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
       if (a.step_type) a.step_type[o] = (uint8_t)COUP_STEP_MID;
       if (a.legal) a.legal[o] = legal_mask(L);
       if (a.cur_player) a.cur_player[o] = (int8_t)current_player(L);
+      if (REC) *rec_s = pack(L);
       continue;
     }
-    const uint32_t x = key_action(key);
+    const uint32_t act = key_action(key);
     const uint32_t err_before = L.err;
-    apply_decision_v1(L, x);  // regrouped: the branch form, as k_rollout_sorted
+    apply_decision_v1(L, act);  // regrouped: the branch form, as k_rollout_sorted
     L.move += 1u;
     resolve_chance(L, rng);
     errs += (L.err && !err_before) ? 1u : 0u;
     const bool term = is_terminal(L);
-    if (a.actions) a.actions[o] = (int8_t)x;
+    if (a.actions) a.actions[o] = (int8_t)act;
     if (a.rewards) reinterpret_cast<uint16_t*>(a.rewards)[o] = (uint16_t)((uint8_t)L.r0 | ((uint8_t)(-L.r0) << 8));
     if (a.step_type) a.step_type[o] = (uint8_t)(term ? COUP_STEP_LAST : COUP_STEP_MID);
     if (term) {
@@ -1553,18 +1577,21 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
       key = kKeyFirst;
       if (a.legal) a.legal[o] = 0u;  // terminal: no legal actions, kTerminalPlayerId
       if (a.cur_player) a.cur_player[o] = (int8_t)-4;
+      if (REC) *rec_s = pack(L);
       continue;
     }
     const uint32_t legal = decision_mask(L);
     if (a.legal) a.legal[o] = legal;
     if (a.cur_player) a.cur_player[o] = (int8_t)L.M;
+    if (REC) *rec_s = pack(L);
     if (s + 1 < steps) key = regroup_key(L, sample_action(legal, rng.draw(L.episode, L.move)));
   }
   if (key == kKeyReset && base + lane < a.n) {  // finished on the last step
     L = new_episode(L.episode + 1u, rng, none);
-    const int64_t o = (steps - 1) * a.n + base + lane;
+    const int64_t o = (steps - 1) * x.stride + base + lane;
     if (a.legal) a.legal[o] = decision_mask(L);
     if (a.cur_player) a.cur_player[o] = (int8_t)L.M;
+    if (REC) x.rec[(steps - 1) * a.n + base + lane] = pack(L);
   }
   __syncthreads();
   s_rec[lane] = pack(L);
@@ -2292,7 +2319,8 @@ struct coup_env {
   coup_server* server;        // coup_attach_server: coup_slot_op goes through this resident wave
   bool dirty;                 // work enqueued on `stream` since its last synchronisation
   hipEvent_t stream_event;    // coup_set_stream: orders a new stream after the old one's pending work
-  uint4* state2;              // 2 players: the second record buffer of the pipelined step (coup_step_many)
+  uint4* traj_rec;            // 2 players: [kTrajChunkMax][B] records of coup_step_many's rules trajectories
+  uint4* state2;              // = traj_rec: the second record buffer of the merged pipelined step
   coup::Knobs knobs;          // dispatch knobs, read once at coup_create (coup_knobs.h)
 };
 
@@ -2399,10 +2427,12 @@ int info_split(const coup::Knobs& k, int64_t n) {
 #endif
 }
 
-// The pipelined form of the split step (coup_step_many,
+#ifdef COUP_AB_VARIANTS
+// The merged pipelined form of the split step (coup_step_many kManyPipe,
 // coup::k_step_obs_pipe): the shipped split kernels' bodies, the regrouped
 // 512-lane rules step and the 512 x 2 writer (variant 11).
 constexpr int kPipeT = 512, kPipeS = 2;
+#endif
 
 // The XCD-aware block -> lane group mapping of the fused step (coup::
 // xcd_group; measurement builds: COUP_XCD_REMAP=0 turns it off).
@@ -2616,7 +2646,7 @@ namespace {
 
 void release(coup_env* env) {
   (void)hipFree(env->state);
-  (void)hipFree(env->state2);
+  (void)hipFree(env->traj_rec);
   (void)hipFree(env->hist);
   (void)hipFree(env->err_count);
   if (env->slot_scratch) (void)hipHostFree(env->slot_scratch);
@@ -2680,13 +2710,17 @@ int coup_create_ex(int64_t batch, uint64_t seed, uint32_t env_id_base, int flags
   env->server = nullptr;
   env->dirty = false;
   env->stream_event = nullptr;
+  env->traj_rec = nullptr;
   env->state2 = nullptr;
   env->knobs = coup::read_knobs();
   const size_t lanes = (size_t)(batch > 0 ? batch : 1);
   hipError_t e = hipMalloc(&env->state, lanes * sizeof(uint4) * (generic ? 2 : 1));
-  // the pipelined step's second record buffer (allocated here: coup_step_many
+  // coup_step_many's per-step record buffer (allocated here: coup_step_many
   // may be captured into a HIP graph, where no allocation may happen)
-  if (e == hipSuccess && !generic) e = hipMalloc(&env->state2, lanes * sizeof(uint4));
+  if (e == hipSuccess && !generic) {
+    e = hipMalloc(&env->traj_rec, lanes * sizeof(uint4) * coup::kTrajChunkMax);
+    env->state2 = env->traj_rec;
+  }
   if (e == hipSuccess) e = hipMalloc(&env->err_count, sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemset(env->err_count, 0, sizeof(uint32_t));
   if (e == hipSuccess && (flags & COUP_FLAG_HISTORY)) {
@@ -3174,13 +3208,17 @@ int coup_step_host(coup_env* env, const int8_t* actions, int want, void* host_ou
 
 namespace {
 
-// coup_step_many / coup_step_trajectory with observations: can the steps
-// run as the pipelined split step?  Uniform policy, 2 players, no history,
-// observations and no information state, and the split step with the
-// shipped writer is this batch's form (from 2^20 lanes, or COUP_OBS_SPLIT).
-bool pipelined(const coup_env* env, const coup_step_outputs* out) {
-  return env->knobs.pipe != 0 && !env->generic && !env->hist && env->state2 && out && out->obs &&
-         !out->info_state && obs_split(env->knobs, env->batch) == coup::kObsSplitDefault;
+// coup_step_many / coup_step_trajectory with observations: which form of
+// the split step runs them?  Uniform policy, 2 players, no history,
+// observations and no information state, the split step with the shipped
+// writer is this batch's form (from 2^20 lanes, or COUP_OBS_SPLIT) and the
+// rules regroup (from 2^18): COUP_PIPE's form (kManyTraj by default), else
+// kManySerial (one coup_step per step).
+int many_form(const coup_env* env, const coup_step_outputs* out) {
+  if (env->generic || env->hist || !env->traj_rec || !out || !out->obs || out->info_state) return coup::kManySerial;
+  if (obs_split(env->knobs, env->batch) != coup::kObsSplitDefault) return coup::kManySerial;
+  if (env->knobs.pipe == coup::kManyTraj && !coup::regroup_lanes(env->knobs, env->batch)) return coup::kManySerial;
+  return env->knobs.pipe;
 }
 
 // Output slice t of a [steps][B][...] coup_step_outputs (the accumulators
@@ -3197,27 +3235,71 @@ coup_step_outputs slice_outputs(const coup_step_outputs& o, int64_t B, int64_t P
   return s;
 }
 
-// `steps` uniform split steps as steps + 1 launches of k_step_obs_pipe:
-// launch m runs the rules of step m (m < steps) beside the observation
-// writer of step m - 1 (m >= 1).  Both read the records after step m - 1;
-// the rules write the records of step m to the other buffer, so the
-// records ping-pong between env->state and env->state2.  With an odd step
-// count the first rules launch (no writer beside it) runs in place, so the
-// last records always land in env->state.  Results -- outputs, records,
-// accumulators -- equal `steps` coup_step calls; `slices`: step t's outputs
-// go to slice t of [steps][B][...] buffers, else every step overwrites out's.
-int step_many_pipelined(coup_env* env, int64_t steps, const coup_step_outputs* out, bool slices) {
-  const int64_t n = env->batch;
-  coup::PipeArgs p;
-  std::memset(&p, 0, sizeof(p));
-  coup::StepArgs& a = p.a;
-  a.n = n;
+coup::StepArgs uniform_args(const coup_env* env, const coup_step_outputs* out) {
+  coup::StepArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.state = env->state;
+  a.n = env->batch;
   a.seed_lo = (uint32_t)env->seed;
   a.seed_hi = (uint32_t)(env->seed >> 32);
   a.env_id_base = env->env_id_base;
   a.auto_reset = (env->flags & COUP_FLAG_AUTO_RESET) ? 1 : 0;
   a.err_count = env->err_count;
   (void)coup::ep_acc_of(out, a.ep);  // validated by the caller
+  return a;
+}
+
+// kManyTraj: `steps` uniform split steps in chunks of up to
+// knobs.traj_chunk steps.  A chunk is ONE launch of the regrouped rules
+// trajectory (k_trajectory_sorted<1024, true>: the records stay in registers
+// from step to step, one record load and one LDS regroup setup per chunk
+// instead of per step) that also stores every step's post-step records to
+// env->traj_rec[s], then one k_obs_sweep_rows<512, 2> launch per step
+// writing step s's observations from them.  Results -- outputs, records,
+// accumulators -- equal `steps` coup_step calls; `slices`: step t's outputs
+// go to slice t of [steps][B][...] buffers, else every step overwrites out's.
+int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, bool slices) {
+  const int64_t n = env->batch;
+  constexpr int TB = coup::kRolloutSortLanes;
+  const int64_t chunk = env->knobs.traj_chunk;
+  const int64_t nf4 = n * coup::kRowF4;
+  const unsigned wgrid = (unsigned)((nf4 + 1023) / 1024);  // 512 threads x 2 passes
+  for (int64_t t0 = 0; t0 < steps; t0 += chunk) {
+    const int64_t c = std::min(chunk, steps - t0);
+    const coup_step_outputs o = slices ? slice_outputs(*out, n, 2, t0) : *out;
+    coup::StepArgs a = uniform_args(env, out);
+    a.actions = o.actions;
+    a.rewards = o.rewards;
+    a.step_type = o.step_type;
+    a.legal = o.legal_mask;
+    a.cur_player = o.cur_player;
+    coup::k_trajectory_sorted<TB, true><<<(unsigned)((n + TB - 1) / TB), TB, 0, env->stream>>>(
+        a, c, coup::TrajOut{env->traj_rec, slices ? n : 0});
+    COUP_HIP_TRY(hipGetLastError());
+    for (int64_t s = 0; s < c; ++s) {
+      float* obs = out->obs + (slices ? (t0 + s) * n * 2 * COUP_OBS_SIZE : 0);
+      coup::k_obs_sweep_rows<512, 2><<<wgrid, 512, 0, env->stream>>>(env->traj_rec + s * n, obs, n);
+      COUP_HIP_TRY(hipGetLastError());
+    }
+  }
+  return COUP_OK;
+}
+
+#ifdef COUP_AB_VARIANTS
+// kManyPipe (measurement builds): `steps` uniform split steps as steps + 1
+// launches of k_step_obs_pipe:
+// launch m runs the rules of step m (m < steps) beside the observation
+// writer of step m - 1 (m >= 1).  Both read the records after step m - 1;
+// the rules write the records of step m to the other buffer, so the
+// records ping-pong between env->state and env->state2.  With an odd step
+// count the first rules launch (no writer beside it) runs in place, so the
+// last records always land in env->state.  Results equal kManyTraj's.
+int step_many_pipelined(coup_env* env, int64_t steps, const coup_step_outputs* out, bool slices) {
+  const int64_t n = env->batch;
+  coup::PipeArgs p;
+  std::memset(&p, 0, sizeof(p));
+  coup::StepArgs& a = p.a;
+  a = uniform_args(env, out);
   const uint32_t R = (uint32_t)((n + kPipeT - 1) / kPipeT);
   const uint32_t W = (uint32_t)((n * coup::kRowF4 + kPipeT * kPipeS - 1) / (kPipeT * kPipeS));
   uint4* const X = env->state;
@@ -3250,6 +3332,7 @@ int step_many_pipelined(coup_env* env, int64_t steps, const coup_step_outputs* o
   if (cur != X) return fail(COUP_E_HIP, "coup_step_many: internal error (records left in the second buffer)");
   return COUP_OK;
 }
+#endif
 
 }  // namespace
 
@@ -3265,9 +3348,12 @@ int coup_step_many(coup_env* env, int64_t steps, const coup_step_outputs* out) {
     if (const char* why = coup::ep_acc_of(out, ep)) return fail(COUP_E_INVALID, std::string("coup_step_many: ") + why);
   }
   if (env->batch == 0 || steps == 0) return COUP_OK;
-  if (pipelined(env, out)) {
-    COUP_TRY(launching(env));
-    return step_many_pipelined(env, steps, out, false);
+  switch (many_form(env, out)) {
+    case coup::kManyTraj: COUP_TRY(launching(env)); return step_many_traj(env, steps, out, false);
+#ifdef COUP_AB_VARIANTS
+    case coup::kManyPipe: COUP_TRY(launching(env)); return step_many_pipelined(env, steps, out, false);
+#endif
+    default: break;
   }
   for (int64_t k = 0; k < steps; ++k) COUP_TRY(coup_step(env, nullptr, out));
   return COUP_OK;
@@ -3277,10 +3363,11 @@ int coup_step_trajectory(coup_env* env, int64_t steps, const coup_step_outputs* 
   COUP_CHECK_ENV(env);
   if (steps < 0) return fail(COUP_E_INVALID, "coup_step_trajectory: negative steps");
   if (out && (out->obs || out->info_state)) {
-    // with tensors: the pipelined split step where it applies (from 2^20
-    // lanes), else one coup_step per slice.  (A one-launch form writing obs
-    // every step measured slower than per-step launches: 196 vs 162 us per
-    // 2^20-lane step)
+    // with tensors: coup_step_many's rules-trajectory form where it applies
+    // (from 2^20 lanes), else one coup_step per slice.  (A one-launch form
+    // writing obs every step inside the rules kernel measured slower than
+    // per-step launches: 196 vs 162 us per 2^20-lane step, DESIGN.md
+    // section 5.)
     if (out->info_state && !env->hist)
       return fail(COUP_E_INVALID, "coup_step_trajectory: info_state needs an env created with COUP_FLAG_HISTORY");
     {
@@ -3289,9 +3376,12 @@ int coup_step_trajectory(coup_env* env, int64_t steps, const coup_step_outputs* 
         return fail(COUP_E_INVALID, std::string("coup_step_trajectory: ") + why);
     }
     if (env->batch == 0 || steps == 0) return COUP_OK;
-    if (pipelined(env, out)) {
-      COUP_TRY(launching(env));
-      return step_many_pipelined(env, steps, out, true);
+    switch (many_form(env, out)) {
+      case coup::kManyTraj: COUP_TRY(launching(env)); return step_many_traj(env, steps, out, true);
+#ifdef COUP_AB_VARIANTS
+      case coup::kManyPipe: COUP_TRY(launching(env)); return step_many_pipelined(env, steps, out, true);
+#endif
+      default: break;
     }
     for (int64_t t = 0; t < steps; ++t) {
       const coup_step_outputs o = slice_outputs(*out, env->batch, env->players, t);
@@ -3329,15 +3419,17 @@ int coup_step_trajectory(coup_env* env, int64_t steps, const coup_step_outputs* 
   if (coup::regroup_lanes(env->knobs, n)) {
 #ifdef COUP_AB_VARIANTS
     switch (coup::sort_lanes(env->knobs.sort_lanes, coup::kRolloutSortLanes)) {
-      case 256: coup::k_trajectory_sorted<256><<<grid_for(n), 256, 0, env->stream>>>(a, steps); break;
-      case 512: coup::k_trajectory_sorted<512><<<(unsigned)((n + 511) / 512), 512, 0, env->stream>>>(a, steps); break;
+      case 256: coup::k_trajectory_sorted<256><<<grid_for(n), 256, 0, env->stream>>>(a, steps, {nullptr, n}); break;
+      case 512:
+        coup::k_trajectory_sorted<512><<<(unsigned)((n + 511) / 512), 512, 0, env->stream>>>(a, steps, {nullptr, n});
+        break;
       default:
-        coup::k_trajectory_sorted<1024><<<(unsigned)((n + 1023) / 1024), 1024, 0, env->stream>>>(a, steps);
+        coup::k_trajectory_sorted<1024><<<(unsigned)((n + 1023) / 1024), 1024, 0, env->stream>>>(a, steps, {nullptr, n});
         break;
     }
 #else
     constexpr int TB = coup::kRolloutSortLanes;
-    coup::k_trajectory_sorted<TB><<<(unsigned)((n + TB - 1) / TB), TB, 0, env->stream>>>(a, steps);
+    coup::k_trajectory_sorted<TB><<<(unsigned)((n + TB - 1) / TB), TB, 0, env->stream>>>(a, steps, {nullptr, n});
 #endif
   } else {
     coup::k_step_trajectory<<<grid_for(n), coup::kThreads, 0, env->stream>>>(a, steps);
@@ -3839,10 +3931,14 @@ int coup_measure_step_traffic(int64_t batch, uint32_t* records, const coup_step_
   return COUP_OK;
 }
 
-int coup_measure_store_sweep(float* dst, int64_t n_float4, int threads, int passes, int resident, void* hip_stream) {
+int coup_measure_store_sweep(float* dst, int64_t n_float4, int threads, int passes, int mode, void* hip_stream) {
   if (!dst || n_float4 < 0) return fail(COUP_E_INVALID, "coup_measure_store_sweep: bad buffer");
+  if (mode & ~(COUP_SWEEP_RESIDENT | COUP_SWEEP_INDEX_BITS))
+    return fail(COUP_E_INVALID, "coup_measure_store_sweep: unknown mode bits");
   if (n_float4 == 0) return COUP_OK;
   hipStream_t s = (hipStream_t)hip_stream;
+  const bool resident = (mode & COUP_SWEEP_RESIDENT) != 0;
+  const int bits = (mode & COUP_SWEEP_INDEX_BITS) ? 1 : 0;
   auto go = [&](auto tt, auto ss) -> int {
     constexpr int T = decltype(tt)::value, S = decltype(ss)::value;
     const int64_t blocks = (n_float4 + T * S - 1) / (T * S);
@@ -3852,12 +3948,12 @@ int coup_measure_store_sweep(float* dst, int64_t n_float4, int threads, int pass
       COUP_HIP_TRY(hipGetDevice(&dev));
       COUP_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
       const int64_t grid = std::min<int64_t>(blocks, (int64_t)cus * (2048 / T));
-      coup::k_store_sweep_resident<T, S><<<(unsigned)grid, T, 0, s>>>(dst, n_float4);
+      coup::k_store_sweep_resident<T, S><<<(unsigned)grid, T, 0, s>>>(dst, n_float4, bits);
 #else
       return fail(COUP_E_INVALID, "coup_measure_store_sweep: the resident form is a measurement build's");
 #endif
     } else {
-      coup::k_store_sweep<T, S><<<(unsigned)blocks, T, 0, s>>>(dst, n_float4);
+      coup::k_store_sweep<T, S><<<(unsigned)blocks, T, 0, s>>>(dst, n_float4, bits);
     }
     COUP_HIP_TRY(hipGetLastError());
     return COUP_OK;

@@ -3,7 +3,7 @@
 //
 // The product library instantiates only the shipped kernels; its knobs pick
 // between shipped forms (the fused or split observation step, regrouping,
-// the pipelined split step).  A measurement build (-DCOUP_AB_VARIANTS:
+// coup_step_many's serial or rules-trajectory split step).  A measurement build (-DCOUP_AB_VARIANTS:
 // `python -m open_spiel_coup_amd.build` also writes it to
 // build/ab/libcoup_mi355x.so) adds every variant that was measured and
 // rejected, selected by the knobs marked "measurement
@@ -22,6 +22,14 @@ namespace coup {
 // and the split InformationStateTensor step's (k_info_sweep<1024, 2>).
 constexpr int kObsSplitDefault = 11;
 constexpr int kInfoSplitDefault = 3;
+// coup_step_many's forms of the split observation step (COUP_PIPE): each
+// step's rules then its writer (kManySerial); chunks of up to kTrajChunkMax
+// steps as ONE regrouped rules-trajectory launch writing every step's
+// records, then a writer launch per step (kManyTraj, shipped); the rules of
+// step t + 1 beside the writer of step t in one launch (kManyPipe,
+// measurement builds: measured slower).
+constexpr int kManySerial = 0, kManyTraj = 1, kManyPipe = 2;
+constexpr int kTrajChunkMax = 8;
 // rules blocks spread over the first kPipeSpanDefault of a pipelined
 // launch's block positions (COUP_PIPE_SPAN)
 constexpr double kPipeSpanDefault = 0.85;
@@ -31,8 +39,8 @@ struct Knobs {
   int obs_split = -1;   // COUP_OBS_SPLIT: -1 by batch (from 2^20 lanes), 0 fused, 11 the shipped writer
   int info_split = -1;  // COUP_INFO_SPLIT: -1 by batch (from 2^18 lanes), 0 fused, 3 the shipped writer
   int regroup = -1;     // COUP_REGROUP: -1 by batch (from 2^18 lanes), 0 / 1 forced
-  int pipe = 1;         // COUP_PIPE: coup_step_many pipelines the split observation step
-  double pipe_span = kPipeSpanDefault;  // COUP_PIPE_SPAN in (0, 1]
+  int pipe = kManyTraj;  // COUP_PIPE: coup_step_many's form of the split step (kMany*)
+  int traj_chunk = kTrajChunkMax;  // COUP_TRAJ_CHUNK 1..kTrajChunkMax: steps per rules-trajectory launch
   // -- measurement builds (-DCOUP_AB_VARIANTS); the product ignores them
   int obs_mode = 9;       // COUP_OBS_MODE 1..9: the fused step's observation writer
   int xcd_remap = 1;      // COUP_XCD_REMAP: XCD-aware block -> lane-group mapping of the fused step
@@ -45,6 +53,7 @@ struct Knobs {
   int np_reset_group = 0;   // COUP_NP_RESET_GROUP (1: one thread per reset)
   int np_traj_stage = 1;    // COUP_TRAJ_STAGE
   int np_scan = 1;          // COUP_NP_SCAN
+  double pipe_span = kPipeSpanDefault;  // COUP_PIPE_SPAN in (0, 1] (kManyPipe)
 };
 
 inline int knob_int(const char* name, int dflt) {
@@ -57,12 +66,15 @@ inline Knobs read_knobs() {
   k.obs_split = knob_int("COUP_OBS_SPLIT", -1);
   k.info_split = knob_int("COUP_INFO_SPLIT", -1);
   k.regroup = knob_int("COUP_REGROUP", -1);
-  k.pipe = knob_int("COUP_PIPE", 1);
+  k.pipe = knob_int("COUP_PIPE", kManyTraj);
+  if (k.pipe != kManySerial && k.pipe != kManyPipe) k.pipe = kManyTraj;
+  k.traj_chunk = knob_int("COUP_TRAJ_CHUNK", kTrajChunkMax);
+  if (k.traj_chunk < 1 || k.traj_chunk > kTrajChunkMax) k.traj_chunk = kTrajChunkMax;
+#ifdef COUP_AB_VARIANTS
   if (const char* f = std::getenv("COUP_PIPE_SPAN")) {
     const double v = std::atof(f);
     if (v > 0.0 && v <= 1.0) k.pipe_span = v;
   }
-#ifdef COUP_AB_VARIANTS
   k.obs_mode = knob_int("COUP_OBS_MODE", 9);
   if (k.obs_mode < 1 || k.obs_mode > 9) k.obs_mode = 9;
   k.xcd_remap = knob_int("COUP_XCD_REMAP", 1) != 0;
@@ -76,6 +88,8 @@ inline Knobs read_knobs() {
   k.np_reset_group = knob_int("COUP_NP_RESET_GROUP", 0);
   k.np_traj_stage = knob_int("COUP_TRAJ_STAGE", 1);
   k.np_scan = knob_int("COUP_NP_SCAN", 1) != 0;
+#else
+  if (k.pipe == kManyPipe) k.pipe = kManyTraj;  // the merged launch ships in measurement builds only
 #endif
   return k;
 }

@@ -324,9 +324,10 @@ class BatchedCoupEnv:
     def step_many(self, steps):
         """`steps` uniform-policy env steps as one call (coup_step_many): the
         same results as `steps` step() calls -- the output buffers hold the
-        last step's outputs.  From 2^20 lanes with observations the steps
-        are pipelined (the rules of step t + 1 beside the observation writer
-        of step t)."""
+        last step's outputs.  From 2^20 lanes with observations the rules of
+        up to 8 steps run as one regrouped trajectory launch storing every
+        step's records, then the observation writer once per step (DESIGN.md
+        section 5)."""
         self._bind_stream()
         self._ep_reserve(int(steps))
         _native.check(self.lib.coup_step_many(self._h, int(steps), ctypes.byref(self._out)))
@@ -337,7 +338,7 @@ class BatchedCoupEnv:
         runs them with a single launch, writing the usual output buffers.
         Removes the per-step host overhead where a step's kernel is short
         (small B).  Uniform steps are recorded through coup_step_many (the
-        pipelined split step where it applies).  The env must outlive the
+        rules-trajectory split step where it applies).  The env must outlive the
         graph."""
         a = None
         if actions is not None:
@@ -382,8 +383,8 @@ class BatchedCoupEnv:
 
     def _fused_trajectory(self, buf):
         """Whether coup_step_trajectory takes `buf` in one call: always with
-        tensors (the library pipelines the split observation step from 2^20
-        lanes, else runs one coup_step per slice); without them only on an
+        tensors (the library's rules-trajectory split observation step from
+        2^20 lanes, else one coup_step per slice); without them only on an
         env without history (its one-launch kernels keep none)."""
         return "obs" in buf or "info_state" in buf or not self.history
 
@@ -396,8 +397,8 @@ class BatchedCoupEnv:
         """`steps` uniform-policy env steps whose outputs land in slice t of
         [T, B, ...] device buffers (trajectory_buffers); returns them.  One
         coup_step_trajectory call: without tensors or history ONE launch
-        (state in registers); with observations the pipelined split step from
-        2^20 lanes, else one coup_step per slice inside the library.  A
+        (state in registers); with observations the rules-trajectory split
+        step from 2^20 lanes, else one coup_step per slice inside the library.  A
         history env without tensors takes one coup_step per slice here.  Same
         results either way."""
         buf = buf if buf is not None else self.trajectory_buffers(steps)

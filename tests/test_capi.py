@@ -62,6 +62,22 @@ def test_create_ex_validates_players_and_flags():
     assert L.coup_num_players(None) == -1 and L.coup_state_bytes(None) == -1
 
 
+def test_store_sweep_validates_before_launching():
+    """coup_measure_store_sweep refuses unknown mode bits, a product build's
+    resident form and shapes outside the build before any HIP call."""
+    L = _native.load()
+    fake = ctypes.c_void_p(4096)  # never dereferenced: every call below fails first
+    assert L.coup_measure_store_sweep(fake, 64, 512, 2, 4, None) == _native.COUP_E_INVALID
+    assert b"mode" in L.coup_last_error()
+    assert L.coup_measure_store_sweep(None, 64, 512, 2, 0, None) == _native.COUP_E_INVALID
+    assert L.coup_measure_store_sweep(fake, 64, 384, 2, 0, None) == _native.COUP_E_INVALID
+    assert b"shape" in L.coup_last_error()
+    assert L.coup_measure_store_sweep(fake, 0, 512, 2, _native.SWEEP_INDEX_BITS, None) == _native.COUP_OK
+    if not L.coup_build_flags() & _native.BUILD_AB_VARIANTS:
+        assert L.coup_measure_store_sweep(fake, 64, 512, 2, _native.SWEEP_RESIDENT, None) == _native.COUP_E_INVALID
+        assert b"measurement build" in L.coup_last_error()
+
+
 def test_create_fails_loudly_without_gpu():
     import torch
     if torch.cuda.is_available():
@@ -169,8 +185,9 @@ void coup::k_step<false, 4, 256, 2, true> | void coup::k_step<false, 9, 256, 0, 
 void coup::k_step<false, 9, 256, 0, true> | void coup::k_step<true, 0, 256, 1, false> |
 void coup::k_step<true, 0, 256, 2, false> | void coup::k_step<true, 4, 256, 1, false> |
 void coup::k_step<true, 4, 256, 2, false> | void coup::k_step<true, 9, 256, 0, false> |
-void coup::k_step_group<1, false> | void coup::k_step_group<1, true> | void coup::k_step_obs_pipe<512, 2> |
-void coup::k_step_sorted<false, 512> | void coup::k_step_sorted<true, 512> | void coup::k_trajectory_sorted<1024> |
+void coup::k_step_group<1, false> | void coup::k_step_group<1, true> |
+void coup::k_step_sorted<false, 512> | void coup::k_step_sorted<true, 512> |
+void coup::k_trajectory_sorted<1024, false> | void coup::k_trajectory_sorted<1024, true> |
 void coup::k_store_sweep<512, 2> | void coup::k_store_sweep<1024, 2>
 """
 
@@ -225,7 +242,7 @@ def test_measurement_build_holds_the_variants():
     assert _shipped_kernels() <= got
     for k in ("void coup::k_obs_sweep<1>", "void coup::k_obs_sweep_rows<256, 2>", "void coup::k_step_group<4, true>",
               "void coup::k_step<true, 1, 256, 0, false>", "void coup::k_step_sorted<true, 1024>",
-              "void coup::k_info_sweep<512, 2>", "void coup::np::k_step_sorted<6, true, true, 1024, true, 4>",
+              "void coup::k_info_sweep<512, 2>", "void coup::k_step_obs_pipe<512, 2>", "void coup::np::k_step_sorted<6, true, true, 1024, true, 4>",
               "void coup::np::k_rollout_sorted<6, 1024, false>", "void coup::np::k_trajectory_sorted<6, 1024, 0>"):
         assert k in got, k
     lib = ctypes.CDLL(build.VARIANTS_OUT)

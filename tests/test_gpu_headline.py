@@ -3,10 +3,11 @@
 bench.py's c3 line (the BASELINE metric) runs the split observation step
 over 2^20 lanes: settle through the fused rollout, W warm-up steps, then K
 steps replayed from one HIP graph (BatchedCoupEnv.capture_steps), which
-records coup_step_many -- the pipelined form, k_step_obs_pipe<512, 2>: the
-regrouped rules of step t + 1 (k_step_sorted's body, the branch-form
-transition apply_decision_v1) beside the address-order observation writer
-of step t (k_obs_sweep_rows' body).  Its timed region keeps only the last
+records coup_step_many -- the rules-trajectory form: chunks of up to 8
+steps as one regrouped rules-trajectory launch (k_trajectory_sorted<1024,
+true>, the branch-form transition apply_decision_v1) storing every step's
+records, then the address-order observation writer k_obs_sweep_rows<512, 2>
+once per step.  Its timed region keeps only the last
 step's tensors, so the same launches also run as a trajectory whose every
 step lands in its own [T][B][2][98] slice, checked step by step.  c3i runs
 the history-keeping rules step and k_info_sweep<1024, 2> over 2^18 lanes
@@ -92,8 +93,8 @@ def test_c3_headline_kernel_full_batch_slices_match_oracle():
     """bench.py --config c3 at its size: 2^20 lanes, obs x2, settle 256 +
     warm-up 5, then K = 20 eager coup_step launches, K = 20 replays of a
     1-step graph (each step checked), one replay of a K = 20-step graph
-    (bench.py's timed region, the pipelined coup_step_many; its last step and
-    the records checked), and the same pipeline as a TK-step trajectory with
+    (bench.py's timed region, coup_step_many's rules-trajectory form; its last
+    step and the records checked), and the same form as a TK-step trajectory with
     every step's observations in their own slice (each step checked)."""
     B, seed, settle, warm, K, TK = 1 << 20, 1, 256, 5, 20, 10
     # the bench's accumulators: the packed int16 word at K = 20 (bench.payload_width)
@@ -130,7 +131,7 @@ def test_c3_headline_kernel_full_batch_slices_match_oracle():
     for k, ref in refs.items():
         _check_step(o, ref, t - 1, k, "obs")
     _check_records(env, B, seed, t, stats_from=settle + warm)
-    # the pipelined launches with a slice per step (coup_step_trajectory):
+    # the rules-trajectory form with a slice per step (coup_step_trajectory):
     # every step's tensors, not only the last (the packed word has taken 60
     # steps of replays its reserve count did not see: fold it first)
     env.fold_episode_stats()

@@ -1,0 +1,134 @@
+"""coup_step_many / coup_step_trajectory with observations in the
+rules-trajectory form (COUP_PIPE=1, the default):
+chunks of up to COUP_TRAJ_CHUNK steps run as ONE regrouped rules-trajectory
+launch (k_trajectory_sorted<1024, true>) that also stores every step's
+post-step records, then one k_obs_sweep_rows<512, 2> launch per step reading
+them.  It must equal coup_step launched once per step (COUP_PIPE=0: the
+split step's two kernels per step) bit for bit -- the last step's outputs,
+the records, the episode accumulators and the error count -- for every
+chunk length (a chunk ending mid-call, episodes ending on a chunk's last
+step), ragged batches, graph capture, and as a trajectory with every step's
+observations in [T][B][2][98] slices.  The oracle side at the bench size is
+tests/test_gpu_headline.py.  Reference semantics: ObservationTensor
+coup.cc:1051-1056, 248-287; the transition coup.cc:522-808;
+rl_environment.py:243-248 (both players' tensors every step)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from open_spiel_coup_amd import BatchedCoupEnv, _native  # noqa: E402
+
+KEYS = ("actions", "rewards", "step_type", "legal_mask", "current_player", "obs")
+
+
+def _env(monkeypatch, B, traj, seed, chunk=None, word=False):
+    monkeypatch.setenv("COUP_OBS_SPLIT", "11")  # the shipped writer at every size (the default from 2^20)
+    monkeypatch.setenv("COUP_REGROUP", "1")     # the regrouped rules at every size (the default from 2^18)
+    monkeypatch.setenv("COUP_PIPE", "1" if traj else "0")
+    if chunk is None:
+        monkeypatch.delenv("COUP_TRAJ_CHUNK", raising=False)
+    else:
+        monkeypatch.setenv("COUP_TRAJ_CHUNK", str(chunk))
+    return BatchedCoupEnv(B, seed=seed, auto_reset=True, obs=True, episode_stats=2 if word else True)
+
+
+def _state(env):
+    out = {k: v.cpu().numpy().copy() for k, v in
+           (("actions", env.actions), ("rewards", env.rewards), ("step_type", env.step_type),
+            ("legal_mask", env.legal_mask), ("current_player", env.cur_player), ("obs", env.obs))}
+    eps, ret = env.episode_stats()
+    return out, env.export_state().cpu().numpy(), eps.cpu().numpy(), ret.cpu().numpy()
+
+
+def _same(a, b, what):
+    for k in KEYS:
+        np.testing.assert_array_equal(a[0][k], b[0][k], err_msg=f"{what}: {k}")
+    np.testing.assert_array_equal(a[1], b[1], err_msg=f"{what}: records")
+    np.testing.assert_array_equal(a[2], b[2], err_msg=f"{what}: episodes")
+    np.testing.assert_array_equal(a[3], b[3], err_msg=f"{what}: return sums")
+
+
+@pytest.mark.parametrize("B", [3, 1000, 65536 + 77, (1 << 18) + 5])
+def test_step_many_equals_stepping(monkeypatch, B):
+    seed = 11
+    many, ref = _env(monkeypatch, B, True, seed), _env(monkeypatch, B, False, seed)
+    for K in (1, 2, 5, 8, 3, 17):  # below, at and above one chunk, one call after the other on the same env
+        many.step_many(K)
+        for _ in range(K):
+            ref.step()
+        _same(_state(many), _state(ref), f"B {B} after K={K}")
+    assert many.error_count() == ref.error_count() == 0
+
+
+@pytest.mark.parametrize("chunk", [1, 3, 8])
+def test_chunk_length_invariant(monkeypatch, chunk):
+    """How the steps split into rules-trajectory launches changes no result
+    (episodes that end on a chunk's last step reset in the next launch)."""
+    B, seed = 70001, 3
+    many, ref = _env(monkeypatch, B, True, seed, chunk=chunk), _env(monkeypatch, B, False, seed)
+    many.step_many(23)
+    for _ in range(23):
+        ref.step()
+    _same(_state(many), _state(ref), f"chunk {chunk}")
+
+
+def test_graph_capture_and_packed_word(monkeypatch):
+    """capture_steps records coup_step_many (bench.py's timed region); two
+    replays equal 2 K eager steps, the packed int16 episode word included."""
+    B, seed, K = 50000, 21, 9
+    many, ref = _env(monkeypatch, B, True, seed, word=True), _env(monkeypatch, B, False, seed, word=True)
+    for _ in range(3):
+        many.step()
+        ref.step()
+    many.clear_episode_stats()
+    ref.clear_episode_stats()
+    g = many.capture_steps(K)
+    g.replay()
+    g.replay()
+    torch.cuda.synchronize()
+    for _ in range(2 * K):
+        ref.step()
+    assert torch.equal(many.episode_word, ref.episode_word)
+    _same(_state(many), _state(ref), "graph")
+
+
+@pytest.mark.parametrize("B,T", [(1000, 12), (1 << 20, 10)])
+def test_trajectory_slices_every_step(monkeypatch, B, T):
+    """coup_step_trajectory with observations through the rules-trajectory
+    form: every step's outputs in its slice, equal to one coup_step per
+    slice."""
+    seed = 17
+    many, ref = _env(monkeypatch, B, True, seed), _env(monkeypatch, B, False, seed)
+    for env in (many, ref):
+        env.rollout(30)
+    bp = many.collect_trajectory(T)
+    br = ref.trajectory_buffers(T)
+    ref._bind_stream()
+    for t in range(T):
+        _native.check(ref.lib.coup_step(ref._h, None, ctypes.byref(ref._slice_outputs(br, t))))
+    for k in KEYS:
+        assert torch.equal(bp[k], br[k]), k
+    assert torch.equal(many.export_state(), ref.export_state())
+    for a, b in zip(many.episode_stats(), ref.episode_stats()):
+        assert torch.equal(a, b)
+
+
+def test_default_form_by_batch(monkeypatch):
+    """Without COUP_OBS_SPLIT / COUP_REGROUP the rules-trajectory form
+    applies from 2^20 lanes (the split step's size); below it coup_step_many
+    loops over the fused step."""
+    for k in ("COUP_OBS_SPLIT", "COUP_REGROUP", "COUP_PIPE", "COUP_TRAJ_CHUNK"):
+        monkeypatch.delenv(k, raising=False)
+    lib = _native.load()
+    assert lib.coup_obs_split_variant(1 << 20) == 11
+    assert lib.coup_obs_split_variant((1 << 20) - 1) == 0
+    a = BatchedCoupEnv(4096, seed=2, obs=True)
+    b = BatchedCoupEnv(4096, seed=2, obs=True)
+    a.step_many(4)
+    for _ in range(4):
+        b.step()
+    assert torch.equal(a.obs, b.obs) and torch.equal(a.export_state(), b.export_state())

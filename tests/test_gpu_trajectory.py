@@ -72,8 +72,8 @@ def test_trajectory_graph_and_full_batch(players):
 
 def test_trajectory_with_tensors_and_refusals():
     """With observation / information-state slices coup_step_trajectory runs
-    one coup_step per slice inside the library (the pipelined split step
-    from 2^20 lanes: tests/test_gpu_pipeline.py), equal to stepping slice by
+    one coup_step per slice inside the library (the rules-trajectory split
+    step from 2^20 lanes: tests/test_gpu_step_many.py), equal to stepping slice by
     slice; a history env without tensors and negative steps are refused."""
     kw = dict(seed=1, obs=True, episode_stats=True)
     env, ref = BatchedCoupEnv(64, **kw), BatchedCoupEnv(64, **kw)

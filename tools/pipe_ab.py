@@ -5,11 +5,13 @@ the settle), variants interleaved round-robin.
     python tools/pipe_ab.py [--batch B] [--steps K] [--rounds R] NAME:VAR=VAL[,...] ...
 
 Each positional argument is one env created with those environment settings
-(knobs read at coup_create, e.g. COUP_PIPE, COUP_PIPE_SPAN; or per launch,
-e.g. COUP_OBS_SPLIT) and captured with BatchedCoupEnv.capture_steps(K).
-Default variants: the fused step, the serial split step (COUP_PIPE=0) and
-the pipelined step at three spreads of its rules blocks.  Prints one JSON
-line per variant: median / min us per env step.  Measurement tool only.
+(knobs read at coup_create, e.g. COUP_PIPE, COUP_TRAJ_CHUNK, COUP_PIPE_SPAN)
+and captured with BatchedCoupEnv.capture_steps(K).  Default variants: the
+fused step, the serial split step (COUP_PIPE=0), the rules-trajectory form
+(COUP_PIPE=1, the default) at chunks of 8 / 4 / 2 / 1 steps, and with the
+measurement build (COUP_LIB_PATH=build/variants/libcoup_mi355x.so) the
+merged pipelined step (COUP_PIPE=2).  Prints one JSON line per variant:
+median / min us per env step.  Measurement tool only.
 """
 import argparse
 import json
@@ -20,9 +22,10 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-DEFAULT = ["fused:COUP_OBS_SPLIT=0", "serial:COUP_PIPE=0", "pipe85:COUP_PIPE_SPAN=0.85",
-           "pipe60:COUP_PIPE_SPAN=0.6", "pipe100:COUP_PIPE_SPAN=1.0"]
-KNOBS = ("COUP_PIPE", "COUP_PIPE_SPAN", "COUP_OBS_SPLIT", "COUP_OBS_MODE")
+DEFAULT = ["fused:COUP_OBS_SPLIT=0", "serial:COUP_PIPE=0", "traj8:COUP_PIPE=1", "traj4:COUP_TRAJ_CHUNK=4",
+           "traj2:COUP_TRAJ_CHUNK=2", "traj1:COUP_TRAJ_CHUNK=1"]
+AB_ONLY = ["pipe85:COUP_PIPE=2,COUP_PIPE_SPAN=0.85"]
+KNOBS = ("COUP_PIPE", "COUP_PIPE_SPAN", "COUP_TRAJ_CHUNK", "COUP_OBS_SPLIT", "COUP_OBS_MODE")
 
 
 def main():
@@ -36,8 +39,9 @@ def main():
     import torch
 
     import bench
-    from open_spiel_coup_amd import BatchedCoupEnv
-    variants = a.variants or DEFAULT
+    from open_spiel_coup_amd import BatchedCoupEnv, _native
+    ab = bool(_native.load().coup_build_flags() & _native.BUILD_AB_VARIANTS)
+    variants = a.variants or (DEFAULT + (AB_ONLY if ab else []))
     envs, graphs = {}, {}
     for v in variants:
         name, _, kvs = v.partition(":")

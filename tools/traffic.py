@@ -56,15 +56,19 @@ def main():
     from bench import CONFIGS
     batch = batch or CONFIGS[cfg][0]
     want_obs, want_info, fused, players = CONFIGS[cfg][1], CONFIGS[cfg][2], CONFIGS[cfg][3], CONFIGS[cfg][6]
-    from bench import info_split_active, obs_split_active, pipelined_active
+    from bench import info_split_active, obs_split_active, step_many_form, traj_chunk
     split = obs_split_active(batch)
     isplit = info_split_active(batch)
-    # the pipelined split step (coup_step_many recorded in the bench's graph):
-    # K + 1 dispatches of ONE kernel per K steps -- the rules of step 1 alone,
-    # K - 1 launches of rules(t + 1) beside writer(t), the writer of step K alone
-    pipe = bool(want_obs and not want_info and not fused and players == 2 and
-                pipelined_active(batch, players, "--graph" not in args or "off" not in args))
-    dispatches_per_window = steps + 1 if pipe else None
+    many = (step_many_form(batch, players, "--graph" not in args or "off" not in args)
+            if want_obs and not want_info and not fused and players == 2 else None)
+    # coup_step_many recorded in the bench's graph.  The merged pipelined
+    # step: K + 1 dispatches of ONE kernel per K steps -- the rules of step 1
+    # alone, K - 1 launches of rules(t + 1) beside writer(t), the writer of
+    # step K alone.  The rules-trajectory step: ceil(K / chunk) rules
+    # launches of up to `chunk` steps each and K writer launches.
+    pipe = many == "pipelined"
+    chunks = -(-steps // traj_chunk()) if many == "rules-trajectory" else None
+    dispatches_per_window = steps + 1 if pipe else steps + chunks if chunks else None
 
     dst = os.path.join(ROOT, "profiles", tag, cfg)
     os.makedirs(dst, exist_ok=True)
@@ -95,6 +99,9 @@ def main():
             return bool("k_info_sweep" in kn or m)
         if pipe:
             return "k_step_obs_pipe" in kn or "15k_step_obs_pipe" in kn
+        if chunks:
+            return bool("k_obs_sweep" in kn or re.search(r"k_trajectory_sorted<\d+, true>", kn) or
+                        re.search(r"19k_trajectory_sortedILi\d+ELb1E", kn))
         if want_obs and not want_info and split:
             # the split observation step: the rules step without tensors and
             # the observation writer, two kernels per env step
@@ -113,6 +120,8 @@ def main():
         total = CONFIGS[cfg][4]
         if pipe:
             return {"rules": 40, "writer": total - 40}.get(role, total)
+        if chunks and "trajectory_sorted" in kn:
+            return 40 * steps / chunks  # the rules of the chunk's steps (mean steps per launch)
         if want_obs and split:
             return total - 40 if "k_obs_sweep" in kn else 40
         if want_info and isplit:
