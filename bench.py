@@ -29,7 +29,10 @@ A "step" is one batched env step over all B lanes; value = env-steps/s of
 the whole job (N x B x K / max-over-ranks wall time).  Before the W warmup
 steps, --settle (default 256) untimed steps run through the fused rollout so
 the lanes are spread over game phases as in a long run (a freshly reset batch
-is in lock-step, and its first steps diverge less).  Multi-GPU: one
+is in lock-step, and its first steps diverge less); after them, untimed
+repeats of the timed K steps for --power-warm-ms (default 40 ms of GPU time)
+bring the GPU from its idle power state to the one sustained load runs in
+(tools/dpm_probe.py; reported as power_warm).  Multi-GPU: one
 process per GPU (torchrun), global env ids sharded by rank, no collective
 inside the step loop; every step accumulates, per lane, the episodes that
 end and player 0's Returns() of each (coup.cc:1016-1032), and the timed
@@ -237,6 +240,12 @@ def parse():
                     help="untimed env steps run first through the fused rollout (same trajectories as "
                          "coup_step), so the timed steps see the steady-state mix of game phases rather "
                          "than 2^20 lanes that all started together (not for info-state configs)")
+    ap.add_argument("--power-warm-ms", type=float, default=40.0,
+                    help="after the warm-up, untimed repeats of the timed K steps (the same graph replay, "
+                         "fused launch or eager steps) until about this much GPU time has passed: the GPU "
+                         "leaves its idle power state only under sustained load (tools/dpm_probe.py: the "
+                         "c3 graph 151 us per step after idle gaps, 135.7 under sustained load; DESIGN.md "
+                         "section 5); 0 turns it off")
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--seed", type=int, default=1)
@@ -641,6 +650,31 @@ def main():
     # one collation outside the timed region: RCCL sets up its all-gather
     # channels lazily, and HIP loads torch's stack kernel on first use
     D.collate(episode_payload(), force=force)
+
+    def unit():  # the timed region's K steps, untimed
+        if graph is not None:
+            graph.replay()
+        elif fused:
+            timed()
+        else:
+            for _ in range(args.steps):
+                env.step()
+
+    # power warm-up: sustained load right before the timed region, so it
+    # starts in the power state it runs in (the accumulators are cleared
+    # below; the env advances, as in the warm-up)
+    power_warm_steps, power_warm_ms = 0, 0.0
+    if args.power_warm_ms > 0:
+        tw = time.perf_counter()
+        unit()
+        torch.cuda.synchronize()
+        one_ms = (time.perf_counter() - tw) * 1e3
+        reps = min(int(args.power_warm_ms / max(one_ms, 1e-3)), 1000)
+        for _ in range(reps):
+            unit()
+        torch.cuda.synchronize()
+        power_warm_steps = (reps + 1) * args.steps
+        power_warm_ms = (time.perf_counter() - tw) * 1e3
     if stats is not None:
         for t in stats.values():
             t.zero_()
@@ -774,6 +808,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "settle_steps": args.settle if not with_info else 0,
+            "power_warm": {"steps": power_warm_steps, "ms": power_warm_ms},
             "ms_per_step": elapsed * 1e3 / args.steps,
             "higher_is_better": True,
             "scaling": "weak",

@@ -255,7 +255,7 @@ def test_slot_ops_rejects_dependent_requests():
     R = _native.SlotReq
     host = (ctypes.c_uint8 * (128 * 4))()
     for reqs in ([R(5, -1, -1, 0), R(5, -1, -1, 0)], [R(6, 7, -1, 0), R(7, -1, -1, 0)],
-                 [R(1 << 20, -1, -1, 0)], [R(3, -1, 18, 0)]):
+                 [R(1 << 20, -1, -1, 0)], [R(3, -1, 128, 0)], [R(3, -1, -2, 0)]):
         arr = (R * len(reqs))(*reqs)
         rc = pool.lib.coup_slot_ops(env._h, len(reqs), arr, env._h, 0, host)
         assert rc == _native.COUP_E_INVALID, pool.lib.coup_last_error()
