@@ -121,7 +121,8 @@ def test_bench_two_ranks_gloo(config):
     # play identical games): the gathered totals match
     one = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "1", "--config", config,
                           "--steps", "8", "--warmup", "2", "--power-warm-ms", "0", "--settle", "16",
-                          "--batch", str(2 * batch), "--no-cpu-baseline"], capture_output=True, text=True, timeout=110, cwd=ROOT)
+                          "--batch", str(2 * batch), "--no-cpu-baseline"], capture_output=True, text=True,
+                         timeout=110, cwd=ROOT)
     assert one.returncode == 0, one.stderr[-2000:]
     single = json.loads([ln for ln in one.stdout.splitlines() if ln.startswith("{")][-1])
     assert single["config"]["hip_graph"] and rec["config"]["hip_graph"]
