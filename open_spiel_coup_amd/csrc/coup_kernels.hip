@@ -2320,7 +2320,10 @@ struct coup_env {
   bool dirty;                 // work enqueued on `stream` since its last synchronisation
   hipEvent_t stream_event;    // coup_set_stream: orders a new stream after the old one's pending work
   uint4* traj_rec;            // 2 players: [kTrajChunkMax][B] records of coup_step_many's rules trajectories
+                              // ([2][kTrajChunkMax][B] once the overlapped form's resources exist)
   uint4* state2;              // = traj_rec: the second record buffer of the merged pipelined step
+  hipStream_t aux;            // kManyOverlap: the rules trajectories' stream (null until needed)
+  hipEvent_t ev_fork, ev_rules[2], ev_writers[2];  // kManyOverlap's fork / chunk events
   coup::Knobs knobs;          // dispatch knobs, read once at coup_create (coup_knobs.h)
 };
 
@@ -2647,6 +2650,11 @@ namespace {
 void release(coup_env* env) {
   (void)hipFree(env->state);
   (void)hipFree(env->traj_rec);
+  if (env->aux) {
+    (void)hipStreamDestroy(env->aux);
+    for (hipEvent_t ev : {env->ev_fork, env->ev_rules[0], env->ev_rules[1], env->ev_writers[0], env->ev_writers[1]})
+      if (ev) (void)hipEventDestroy(ev);
+  }
   (void)hipFree(env->hist);
   (void)hipFree(env->err_count);
   if (env->slot_scratch) (void)hipHostFree(env->slot_scratch);
@@ -2654,6 +2662,38 @@ void release(coup_env* env) {
   if (env->host_scratch) (void)hipHostFree(env->host_scratch);
   if (env->host_stage) (void)hipFree(env->host_stage);
   delete env;
+}
+
+// coup_step_many's overlapped form (kManyOverlap): a second stream for the
+// rules trajectories, the fork / chunk events, and the record buffer grown
+// to two chunks.  Created at coup_create where the form applies, else at the
+// first call that needs them outside a graph capture.
+int overlap_resources(coup_env* env) {
+  if (env->aux) return COUP_OK;
+  const size_t lanes = (size_t)(env->batch > 0 ? env->batch : 1);
+  uint4* rec = nullptr;
+  hipError_t e = hipMalloc(&rec, lanes * sizeof(uint4) * 2 * coup::kTrajChunkMax);
+  if (e != hipSuccess) return fail(COUP_E_HIP, std::string("coup_step_many: ") + hipGetErrorString(e));
+  hipStream_t aux = nullptr;
+  hipEvent_t ev[5] = {};
+  e = hipStreamCreateWithFlags(&aux, hipStreamNonBlocking);
+  for (int i = 0; i < 5 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
+  if (e != hipSuccess) {
+    for (hipEvent_t x : ev)
+      if (x) (void)hipEventDestroy(x);
+    if (aux) (void)hipStreamDestroy(aux);
+    (void)hipFree(rec);
+    return fail(COUP_E_HIP, std::string("coup_step_many: ") + hipGetErrorString(e));
+  }
+  (void)hipFree(env->traj_rec);  // synchronises: no launch in flight still reads it
+  env->traj_rec = env->state2 = rec;
+  env->aux = aux;
+  env->ev_fork = ev[0];
+  env->ev_rules[0] = ev[1];
+  env->ev_rules[1] = ev[2];
+  env->ev_writers[0] = ev[3];
+  env->ev_writers[1] = ev[4];
+  return COUP_OK;
 }
 
 }  // namespace
@@ -2712,6 +2752,8 @@ int coup_create_ex(int64_t batch, uint64_t seed, uint32_t env_id_base, int flags
   env->stream_event = nullptr;
   env->traj_rec = nullptr;
   env->state2 = nullptr;
+  env->aux = nullptr;
+  env->ev_fork = env->ev_rules[0] = env->ev_rules[1] = env->ev_writers[0] = env->ev_writers[1] = nullptr;
   env->knobs = coup::read_knobs();
   const size_t lanes = (size_t)(batch > 0 ? batch : 1);
   hipError_t e = hipMalloc(&env->state, lanes * sizeof(uint4) * (generic ? 2 : 1));
@@ -2736,6 +2778,12 @@ int coup_create_ex(int64_t batch, uint64_t seed, uint32_t env_id_base, int flags
     e = hipStreamSynchronize(env->stream);
     if (e != hipSuccess) rc = fail(COUP_E_HIP, std::string("coup_create: ") + hipGetErrorString(e));
   }
+  // the overlapped coup_step_many's stream, events and second record
+  // buffer, where the split observation step applies (a graph capture cannot
+  // create them later)
+  if (rc == COUP_OK && !generic && (batch >= kObsSplitMinLanes || env->knobs.obs_split > 0) &&
+      env->knobs.pipe == coup::kManyOverlap)
+    rc = overlap_resources(env);
   if (rc != COUP_OK) {
     release(env);
     return rc;
@@ -3217,7 +3265,9 @@ namespace {
 int many_form(const coup_env* env, const coup_step_outputs* out) {
   if (env->generic || env->hist || !env->traj_rec || !out || !out->obs || out->info_state) return coup::kManySerial;
   if (obs_split(env->knobs, env->batch) != coup::kObsSplitDefault) return coup::kManySerial;
-  if (env->knobs.pipe == coup::kManyTraj && !coup::regroup_lanes(env->knobs, env->batch)) return coup::kManySerial;
+  if ((env->knobs.pipe == coup::kManyTraj || env->knobs.pipe == coup::kManyOverlap) &&
+      !coup::regroup_lanes(env->knobs, env->batch))
+    return coup::kManySerial;
   return env->knobs.pipe;
 }
 
@@ -3258,14 +3308,28 @@ coup::StepArgs uniform_args(const coup_env* env, const coup_step_outputs* out) {
 // writing step s's observations from them.  Results -- outputs, records,
 // accumulators -- equal `steps` coup_step calls; `slices`: step t's outputs
 // go to slice t of [steps][B][...] buffers, else every step overwrites out's.
-int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, bool slices) {
+// `overlap` (kManyOverlap): the rules trajectories run on env->aux, chunk
+// c + 1's beside chunk c's writers on env->stream, the records alternating
+// between two chunk buffers; events order each writer chunk after its rules
+// and each rules chunk after the writers that last read its buffer.  The
+// stream joins back (the writers wait for the last rules chunk), so the call
+// is one fork / join of env->stream, capturable into a HIP graph.
+int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, bool slices, bool overlap) {
   const int64_t n = env->batch;
   constexpr int TB = coup::kRolloutSortLanes;
   const int64_t chunk = env->knobs.traj_chunk;
   const int64_t nf4 = n * coup::kRowF4;
   const unsigned wgrid = (unsigned)((nf4 + 1023) / 1024);  // 512 threads x 2 passes
-  for (int64_t t0 = 0; t0 < steps; t0 += chunk) {
+  const hipStream_t S = env->stream, R = overlap ? env->aux : env->stream;
+  if (overlap) {
+    COUP_HIP_TRY(hipEventRecord(env->ev_fork, S));
+    COUP_HIP_TRY(hipStreamWaitEvent(R, env->ev_fork, 0));
+  }
+  int64_t k = 0;  // chunk index
+  for (int64_t t0 = 0; t0 < steps; t0 += chunk, ++k) {
     const int64_t c = std::min(chunk, steps - t0);
+    const int b = (int)(k & 1);
+    uint4* const rec = env->traj_rec + (overlap ? b * coup::kTrajChunkMax * n : 0);
     const coup_step_outputs o = slices ? slice_outputs(*out, n, 2, t0) : *out;
     coup::StepArgs a = uniform_args(env, out);
     a.actions = o.actions;
@@ -3273,16 +3337,31 @@ int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, b
     a.step_type = o.step_type;
     a.legal = o.legal_mask;
     a.cur_player = o.cur_player;
-    coup::k_trajectory_sorted<TB, true><<<(unsigned)((n + TB - 1) / TB), TB, 0, env->stream>>>(
-        a, c, coup::TrajOut{env->traj_rec, slices ? n : 0});
+    if (overlap && k >= 2) COUP_HIP_TRY(hipStreamWaitEvent(R, env->ev_writers[b], 0));
+    coup::k_trajectory_sorted<TB, true><<<(unsigned)((n + TB - 1) / TB), TB, 0, R>>>(
+        a, c, coup::TrajOut{rec, slices ? n : 0});
     COUP_HIP_TRY(hipGetLastError());
+    if (overlap) {
+      COUP_HIP_TRY(hipEventRecord(env->ev_rules[b], R));
+      COUP_HIP_TRY(hipStreamWaitEvent(S, env->ev_rules[b], 0));
+    }
     for (int64_t s = 0; s < c; ++s) {
       float* obs = out->obs + (slices ? (t0 + s) * n * 2 * COUP_OBS_SIZE : 0);
-      coup::k_obs_sweep_rows<512, 2><<<wgrid, 512, 0, env->stream>>>(env->traj_rec + s * n, obs, n);
+      coup::k_obs_sweep_rows<512, 2><<<wgrid, 512, 0, S>>>(rec + s * n, obs, n);
       COUP_HIP_TRY(hipGetLastError());
     }
+    if (overlap) COUP_HIP_TRY(hipEventRecord(env->ev_writers[b], S));
   }
   return COUP_OK;
+}
+
+// kManyOverlap's resources, or false where they cannot be made now (a graph
+// capture on env->stream: the call then runs as kManyTraj, same results).
+bool overlap_ready(coup_env* env) {
+  if (env->aux) return true;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(env->stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return false;
+  return overlap_resources(env) == COUP_OK;
 }
 
 #ifdef COUP_AB_VARIANTS
@@ -3349,7 +3428,10 @@ int coup_step_many(coup_env* env, int64_t steps, const coup_step_outputs* out) {
   }
   if (env->batch == 0 || steps == 0) return COUP_OK;
   switch (many_form(env, out)) {
-    case coup::kManyTraj: COUP_TRY(launching(env)); return step_many_traj(env, steps, out, false);
+    case coup::kManyTraj: COUP_TRY(launching(env)); return step_many_traj(env, steps, out, false, false);
+    case coup::kManyOverlap:
+      COUP_TRY(launching(env));
+      return step_many_traj(env, steps, out, false, overlap_ready(env));
 #ifdef COUP_AB_VARIANTS
     case coup::kManyPipe: COUP_TRY(launching(env)); return step_many_pipelined(env, steps, out, false);
 #endif
@@ -3377,7 +3459,10 @@ int coup_step_trajectory(coup_env* env, int64_t steps, const coup_step_outputs* 
     }
     if (env->batch == 0 || steps == 0) return COUP_OK;
     switch (many_form(env, out)) {
-      case coup::kManyTraj: COUP_TRY(launching(env)); return step_many_traj(env, steps, out, true);
+      case coup::kManyTraj: COUP_TRY(launching(env)); return step_many_traj(env, steps, out, true, false);
+      case coup::kManyOverlap:
+        COUP_TRY(launching(env));
+        return step_many_traj(env, steps, out, true, overlap_ready(env));
 #ifdef COUP_AB_VARIANTS
       case coup::kManyPipe: COUP_TRY(launching(env)); return step_many_pipelined(env, steps, out, true);
 #endif

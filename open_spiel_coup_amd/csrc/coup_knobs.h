@@ -25,10 +25,12 @@ constexpr int kInfoSplitDefault = 3;
 // coup_step_many's forms of the split observation step (COUP_PIPE): each
 // step's rules then its writer (kManySerial); chunks of up to kTrajChunkMax
 // steps as ONE regrouped rules-trajectory launch writing every step's
-// records, then a writer launch per step (kManyTraj, shipped); the rules of
-// step t + 1 beside the writer of step t in one launch (kManyPipe,
-// measurement builds: measured slower).
-constexpr int kManySerial = 0, kManyTraj = 1, kManyPipe = 2;
+// records, then a writer launch per step (kManyTraj); the same with the
+// rules trajectory of chunk c + 1 on a second stream beside the writers of
+// chunk c, the records double-buffered (kManyOverlap); the rules of step
+// t + 1 beside the writer of step t in one launch (kManyPipe, measurement
+// builds: measured slower).
+constexpr int kManySerial = 0, kManyTraj = 1, kManyPipe = 2, kManyOverlap = 3;
 constexpr int kTrajChunkMax = 8;
 // rules blocks spread over the first kPipeSpanDefault of a pipelined
 // launch's block positions (COUP_PIPE_SPAN)
@@ -67,7 +69,7 @@ inline Knobs read_knobs() {
   k.info_split = knob_int("COUP_INFO_SPLIT", -1);
   k.regroup = knob_int("COUP_REGROUP", -1);
   k.pipe = knob_int("COUP_PIPE", kManyTraj);
-  if (k.pipe != kManySerial && k.pipe != kManyPipe) k.pipe = kManyTraj;
+  if (k.pipe != kManySerial && k.pipe != kManyPipe && k.pipe != kManyOverlap) k.pipe = kManyTraj;
   k.traj_chunk = knob_int("COUP_TRAJ_CHUNK", kTrajChunkMax);
   if (k.traj_chunk < 1 || k.traj_chunk > kTrajChunkMax) k.traj_chunk = kTrajChunkMax;
 #ifdef COUP_AB_VARIANTS

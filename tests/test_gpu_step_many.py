@@ -1,5 +1,7 @@
 """coup_step_many / coup_step_trajectory with observations in the
-rules-trajectory form (COUP_PIPE=1, the default):
+rules-trajectory forms: COUP_PIPE=1 on the env's
+stream, COUP_PIPE=3 with the rules trajectories on a second stream beside
+the previous chunk's writers (records double-buffered, events between):
 chunks of up to COUP_TRAJ_CHUNK steps run as ONE regrouped rules-trajectory
 launch (k_trajectory_sorted<1024, true>) that also stores every step's
 post-step records, then one k_obs_sweep_rows<512, 2> launch per step reading
@@ -25,10 +27,14 @@ from open_spiel_coup_amd import BatchedCoupEnv, _native  # noqa: E402
 KEYS = ("actions", "rewards", "step_type", "legal_mask", "current_player", "obs")
 
 
+FORMS = ["1", "3"]  # COUP_PIPE: the rules trajectory on the env's stream / overlapped on a second stream
+
+
 def _env(monkeypatch, B, traj, seed, chunk=None, word=False):
+    """traj: a COUP_PIPE form ("1" / "3"), or False for per-step coup_step."""
     monkeypatch.setenv("COUP_OBS_SPLIT", "11")  # the shipped writer at every size (the default from 2^20)
     monkeypatch.setenv("COUP_REGROUP", "1")     # the regrouped rules at every size (the default from 2^18)
-    monkeypatch.setenv("COUP_PIPE", "1" if traj else "0")
+    monkeypatch.setenv("COUP_PIPE", traj if traj else "0")
     if chunk is None:
         monkeypatch.delenv("COUP_TRAJ_CHUNK", raising=False)
     else:
@@ -52,10 +58,11 @@ def _same(a, b, what):
     np.testing.assert_array_equal(a[3], b[3], err_msg=f"{what}: return sums")
 
 
+@pytest.mark.parametrize("form", FORMS)
 @pytest.mark.parametrize("B", [3, 1000, 65536 + 77, (1 << 18) + 5])
-def test_step_many_equals_stepping(monkeypatch, B):
+def test_step_many_equals_stepping(monkeypatch, B, form):
     seed = 11
-    many, ref = _env(monkeypatch, B, True, seed), _env(monkeypatch, B, False, seed)
+    many, ref = _env(monkeypatch, B, form, seed), _env(monkeypatch, B, False, seed)
     for K in (1, 2, 5, 8, 3, 17):  # below, at and above one chunk, one call after the other on the same env
         many.step_many(K)
         for _ in range(K):
@@ -64,26 +71,34 @@ def test_step_many_equals_stepping(monkeypatch, B):
     assert many.error_count() == ref.error_count() == 0
 
 
+@pytest.mark.parametrize("form", FORMS)
 @pytest.mark.parametrize("chunk", [1, 3, 8])
-def test_chunk_length_invariant(monkeypatch, chunk):
+def test_chunk_length_invariant(monkeypatch, chunk, form):
     """How the steps split into rules-trajectory launches changes no result
     (episodes that end on a chunk's last step reset in the next launch)."""
     B, seed = 70001, 3
-    many, ref = _env(monkeypatch, B, True, seed, chunk=chunk), _env(monkeypatch, B, False, seed)
+    many, ref = _env(monkeypatch, B, form, seed, chunk=chunk), _env(monkeypatch, B, False, seed)
     many.step_many(23)
     for _ in range(23):
         ref.step()
     _same(_state(many), _state(ref), f"chunk {chunk}")
 
 
-def test_graph_capture_and_packed_word(monkeypatch):
+@pytest.mark.parametrize("form", FORMS)
+@pytest.mark.parametrize("chunk", [2, 8])
+def test_graph_capture_and_packed_word(monkeypatch, form, chunk):
     """capture_steps records coup_step_many (bench.py's timed region); two
-    replays equal 2 K eager steps, the packed int16 episode word included."""
+    replays equal 2 K eager steps, the packed int16 episode word included.
+    The overlapped form's second stream joins the capture (its resources
+    made by the eager steps before it)."""
     B, seed, K = 50000, 21, 9
-    many, ref = _env(monkeypatch, B, True, seed, word=True), _env(monkeypatch, B, False, seed, word=True)
+    many = _env(monkeypatch, B, form, seed, chunk=chunk, word=True)
+    ref = _env(monkeypatch, B, False, seed, word=True)
     for _ in range(3):
         many.step()
         ref.step()
+    many.step_many(1)  # makes the overlapped form's stream and buffers outside the capture
+    ref.step()
     many.clear_episode_stats()
     ref.clear_episode_stats()
     g = many.capture_steps(K)
@@ -96,13 +111,14 @@ def test_graph_capture_and_packed_word(monkeypatch):
     _same(_state(many), _state(ref), "graph")
 
 
-@pytest.mark.parametrize("B,T", [(1000, 12), (1 << 20, 10)])
-def test_trajectory_slices_every_step(monkeypatch, B, T):
+@pytest.mark.parametrize("form", FORMS)
+@pytest.mark.parametrize("B,T", [(1000, 12), (1 << 20, 10), (1 << 20, 21)])
+def test_trajectory_slices_every_step(monkeypatch, B, T, form):
     """coup_step_trajectory with observations through the rules-trajectory
-    form: every step's outputs in its slice, equal to one coup_step per
+    forms: every step's outputs in its slice, equal to one coup_step per
     slice."""
     seed = 17
-    many, ref = _env(monkeypatch, B, True, seed), _env(monkeypatch, B, False, seed)
+    many, ref = _env(monkeypatch, B, form, seed), _env(monkeypatch, B, False, seed)
     for env in (many, ref):
         env.rollout(30)
     bp = many.collect_trajectory(T)
@@ -132,3 +148,24 @@ def test_default_form_by_batch(monkeypatch):
     for _ in range(4):
         b.step()
     assert torch.equal(a.obs, b.obs) and torch.equal(a.export_state(), b.export_state())
+
+
+def test_overlap_capture_without_resources_falls_back(monkeypatch):
+    """COUP_PIPE=3 switched on after coup_create (coup_reload_knobs), so the
+    env's first overlapped coup_step_many is inside a graph capture, where no
+    stream or buffer can be made: the call runs on the env's stream alone,
+    same results; the next eager call makes them and overlaps."""
+    B, seed, K = 4096, 8, 6
+    many, ref = _env(monkeypatch, B, "1", seed), _env(monkeypatch, B, False, seed)
+    monkeypatch.setenv("COUP_PIPE", "3")
+    many.reload_knobs()
+    g = many.capture_steps(K)
+    g.replay()
+    torch.cuda.synchronize()
+    for _ in range(K):
+        ref.step()
+    _same(_state(many), _state(ref), "capture fallback")
+    many.step_many(5)  # eager: now with the second stream
+    for _ in range(5):
+        ref.step()
+    _same(_state(many), _state(ref), "after")

@@ -7,8 +7,9 @@ the settle), variants interleaved round-robin.
 Each positional argument is one env created with those environment settings
 (knobs read at coup_create, e.g. COUP_PIPE, COUP_TRAJ_CHUNK, COUP_PIPE_SPAN)
 and captured with BatchedCoupEnv.capture_steps(K).  Default variants: the
-fused step, the serial split step (COUP_PIPE=0), the rules-trajectory form
-(COUP_PIPE=1, the default) at chunks of 8 / 4 / 2 / 1 steps, and with the
+serial split step (COUP_PIPE=0), the rules-trajectory form (COUP_PIPE=1)
+at chunks of 8 / 4 steps, the same overlapped on two streams (COUP_PIPE=3)
+at chunks of 8 / 4 / 2, and with the
 measurement build (COUP_LIB_PATH=build/variants/libcoup_mi355x.so) the
 merged pipelined step (COUP_PIPE=2).  Prints one JSON line per variant:
 median / min us per env step.  Measurement tool only.
@@ -22,8 +23,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-DEFAULT = ["fused:COUP_OBS_SPLIT=0", "serial:COUP_PIPE=0", "traj8:COUP_PIPE=1", "traj4:COUP_TRAJ_CHUNK=4",
-           "traj2:COUP_TRAJ_CHUNK=2", "traj1:COUP_TRAJ_CHUNK=1"]
+DEFAULT = ["serial:COUP_PIPE=0", "traj8:COUP_PIPE=1", "traj4:COUP_PIPE=1,COUP_TRAJ_CHUNK=4",
+           "over8:COUP_PIPE=3", "over4:COUP_PIPE=3,COUP_TRAJ_CHUNK=4", "over2:COUP_PIPE=3,COUP_TRAJ_CHUNK=2"]
 AB_ONLY = ["pipe85:COUP_PIPE=2,COUP_PIPE_SPAN=0.85"]
 KNOBS = ("COUP_PIPE", "COUP_PIPE_SPAN", "COUP_TRAJ_CHUNK", "COUP_OBS_SPLIT", "COUP_OBS_MODE")
 
