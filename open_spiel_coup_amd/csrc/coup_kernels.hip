@@ -2322,7 +2322,8 @@ struct coup_env {
   uint4* traj_rec;            // 2 players: [kTrajChunkMax][B] records of coup_step_many's rules trajectories
                               // ([2][kTrajChunkMax][B] once the overlapped form's resources exist)
   uint4* state2;              // = traj_rec: the second record buffer of the merged pipelined step
-  hipStream_t aux;            // kManyOverlap: the rules trajectories' stream (null until needed)
+  hipStream_t aux;            // kManyOverlap (measurement builds): the rules trajectories' stream
+  hipStream_t aux_w;          // ... and with COUP_OVERLAP_CUS the writers' (both CU-masked)
   hipEvent_t ev_fork, ev_rules[2], ev_writers[2];  // kManyOverlap's fork / chunk events
   coup::Knobs knobs;          // dispatch knobs, read once at coup_create (coup_knobs.h)
 };
@@ -2650,6 +2651,7 @@ namespace {
 void release(coup_env* env) {
   (void)hipFree(env->state);
   (void)hipFree(env->traj_rec);
+  if (env->aux_w) (void)hipStreamDestroy(env->aux_w);
   if (env->aux) {
     (void)hipStreamDestroy(env->aux);
     for (hipEvent_t ev : {env->ev_fork, env->ev_rules[0], env->ev_rules[1], env->ev_writers[0], env->ev_writers[1]})
@@ -2664,30 +2666,60 @@ void release(coup_env* env) {
   delete env;
 }
 
-// coup_step_many's overlapped form (kManyOverlap): a second stream for the
-// rules trajectories, the fork / chunk events, and the record buffer grown
-// to two chunks.  Created at coup_create where the form applies, else at the
-// first call that needs them outside a graph capture.
+#ifdef COUP_AB_VARIANTS
+// CU mask of `m` of the device's CUs (m > 0; 8-CU groups spread evenly over
+// the mask, so over the XCDs whichever way the mask's bits map to them), or
+// the complement
+std::vector<uint32_t> cu_mask(int cus, int m, bool complement) {
+  std::vector<uint32_t> w((size_t)(cus + 31) / 32, 0u);
+  const int groups = std::max(1, cus / 8), take = std::max(1, std::min(groups, m / 8));
+  for (int g = 0; g < groups; ++g) {
+    const bool on = ((int64_t)g * take / groups) != ((int64_t)(g + 1) * take / groups);  // `take` of the groups
+    if (on == complement) continue;
+    for (int i = g * 8; i < g * 8 + 8 && i < cus; ++i) w[(size_t)i / 32] |= 1u << (i % 32);
+  }
+  return w;
+}
+
+// coup_step_many's overlapped form (kManyOverlap, measurement builds): a
+// second stream for the rules trajectories (with COUP_OVERLAP_CUS, CU-masked
+// streams for the rules and the writers), the fork / chunk events, and the
+// record buffer grown to two chunks.  Created at coup_create where the form
+// applies, else at the first call that needs them outside a graph capture.
 int overlap_resources(coup_env* env) {
   if (env->aux) return COUP_OK;
   const size_t lanes = (size_t)(env->batch > 0 ? env->batch : 1);
   uint4* rec = nullptr;
   hipError_t e = hipMalloc(&rec, lanes * sizeof(uint4) * 2 * coup::kTrajChunkMax);
   if (e != hipSuccess) return fail(COUP_E_HIP, std::string("coup_step_many: ") + hipGetErrorString(e));
-  hipStream_t aux = nullptr;
+  hipStream_t aux = nullptr, aux_w = nullptr;
   hipEvent_t ev[5] = {};
-  e = hipStreamCreateWithFlags(&aux, hipStreamNonBlocking);
+  if (env->knobs.overlap_cus > 0) {
+    int dev = 0, cus = 0;
+    e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e == hipSuccess) {
+      const std::vector<uint32_t> r = cu_mask(cus, env->knobs.overlap_cus, false);
+      const std::vector<uint32_t> w = cu_mask(cus, env->knobs.overlap_cus, true);
+      e = hipExtStreamCreateWithCUMask(&aux, (uint32_t)r.size(), r.data());
+      if (e == hipSuccess) e = hipExtStreamCreateWithCUMask(&aux_w, (uint32_t)w.size(), w.data());
+    }
+  } else {
+    e = hipStreamCreateWithFlags(&aux, hipStreamNonBlocking);
+  }
   for (int i = 0; i < 5 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
   if (e != hipSuccess) {
     for (hipEvent_t x : ev)
       if (x) (void)hipEventDestroy(x);
     if (aux) (void)hipStreamDestroy(aux);
+    if (aux_w) (void)hipStreamDestroy(aux_w);
     (void)hipFree(rec);
     return fail(COUP_E_HIP, std::string("coup_step_many: ") + hipGetErrorString(e));
   }
   (void)hipFree(env->traj_rec);  // synchronises: no launch in flight still reads it
   env->traj_rec = env->state2 = rec;
   env->aux = aux;
+  env->aux_w = aux_w;
   env->ev_fork = ev[0];
   env->ev_rules[0] = ev[1];
   env->ev_rules[1] = ev[2];
@@ -2695,6 +2727,7 @@ int overlap_resources(coup_env* env) {
   env->ev_writers[1] = ev[4];
   return COUP_OK;
 }
+#endif
 
 }  // namespace
 
@@ -2753,6 +2786,7 @@ int coup_create_ex(int64_t batch, uint64_t seed, uint32_t env_id_base, int flags
   env->traj_rec = nullptr;
   env->state2 = nullptr;
   env->aux = nullptr;
+  env->aux_w = nullptr;
   env->ev_fork = env->ev_rules[0] = env->ev_rules[1] = env->ev_writers[0] = env->ev_writers[1] = nullptr;
   env->knobs = coup::read_knobs();
   const size_t lanes = (size_t)(batch > 0 ? batch : 1);
@@ -2778,12 +2812,14 @@ int coup_create_ex(int64_t batch, uint64_t seed, uint32_t env_id_base, int flags
     e = hipStreamSynchronize(env->stream);
     if (e != hipSuccess) rc = fail(COUP_E_HIP, std::string("coup_create: ") + hipGetErrorString(e));
   }
+#ifdef COUP_AB_VARIANTS
   // the overlapped coup_step_many's stream, events and second record
   // buffer, where the split observation step applies (a graph capture cannot
   // create them later)
   if (rc == COUP_OK && !generic && (batch >= kObsSplitMinLanes || env->knobs.obs_split > 0) &&
       env->knobs.pipe == coup::kManyOverlap)
     rc = overlap_resources(env);
+#endif
   if (rc != COUP_OK) {
     release(env);
     return rc;
@@ -3308,22 +3344,24 @@ coup::StepArgs uniform_args(const coup_env* env, const coup_step_outputs* out) {
 // writing step s's observations from them.  Results -- outputs, records,
 // accumulators -- equal `steps` coup_step calls; `slices`: step t's outputs
 // go to slice t of [steps][B][...] buffers, else every step overwrites out's.
-// `overlap` (kManyOverlap): the rules trajectories run on env->aux, chunk
-// c + 1's beside chunk c's writers on env->stream, the records alternating
-// between two chunk buffers; events order each writer chunk after its rules
-// and each rules chunk after the writers that last read its buffer.  The
-// stream joins back (the writers wait for the last rules chunk), so the call
-// is one fork / join of env->stream, capturable into a HIP graph.
+// `overlap` (kManyOverlap, measurement builds): the rules trajectories run
+// on env->aux, chunk c + 1's beside chunk c's writers on env->stream (or
+// env->aux_w), the records alternating between two chunk buffers; events
+// order each writer chunk after its rules and each rules chunk after the
+// writers that last read its buffer.  The streams join back into
+// env->stream, so the call is one fork / join, capturable into a HIP graph.
 int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, bool slices, bool overlap) {
   const int64_t n = env->batch;
   constexpr int TB = coup::kRolloutSortLanes;
   const int64_t chunk = env->knobs.traj_chunk;
   const int64_t nf4 = n * coup::kRowF4;
   const unsigned wgrid = (unsigned)((nf4 + 1023) / 1024);  // 512 threads x 2 passes
-  const hipStream_t S = env->stream, R = overlap ? env->aux : env->stream;
+  const hipStream_t R = overlap ? env->aux : env->stream;
+  const hipStream_t S = overlap && env->aux_w ? env->aux_w : env->stream;  // the writers'
   if (overlap) {
-    COUP_HIP_TRY(hipEventRecord(env->ev_fork, S));
+    COUP_HIP_TRY(hipEventRecord(env->ev_fork, env->stream));
     COUP_HIP_TRY(hipStreamWaitEvent(R, env->ev_fork, 0));
+    if (S != env->stream) COUP_HIP_TRY(hipStreamWaitEvent(S, env->ev_fork, 0));
   }
   int64_t k = 0;  // chunk index
   for (int64_t t0 = 0; t0 < steps; t0 += chunk, ++k) {
@@ -3352,9 +3390,12 @@ int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, b
     }
     if (overlap) COUP_HIP_TRY(hipEventRecord(env->ev_writers[b], S));
   }
+  if (overlap && S != env->stream)  // join: the last writers (which waited for the last rules)
+    COUP_HIP_TRY(hipStreamWaitEvent(env->stream, env->ev_writers[(k - 1) & 1], 0));
   return COUP_OK;
 }
 
+#ifdef COUP_AB_VARIANTS
 // kManyOverlap's resources, or false where they cannot be made now (a graph
 // capture on env->stream: the call then runs as kManyTraj, same results).
 bool overlap_ready(coup_env* env) {
@@ -3363,6 +3404,7 @@ bool overlap_ready(coup_env* env) {
   if (hipStreamIsCapturing(env->stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return false;
   return overlap_resources(env) == COUP_OK;
 }
+#endif
 
 #ifdef COUP_AB_VARIANTS
 // kManyPipe (measurement builds): `steps` uniform split steps as steps + 1
@@ -3429,10 +3471,10 @@ int coup_step_many(coup_env* env, int64_t steps, const coup_step_outputs* out) {
   if (env->batch == 0 || steps == 0) return COUP_OK;
   switch (many_form(env, out)) {
     case coup::kManyTraj: COUP_TRY(launching(env)); return step_many_traj(env, steps, out, false, false);
+#ifdef COUP_AB_VARIANTS
     case coup::kManyOverlap:
       COUP_TRY(launching(env));
       return step_many_traj(env, steps, out, false, overlap_ready(env));
-#ifdef COUP_AB_VARIANTS
     case coup::kManyPipe: COUP_TRY(launching(env)); return step_many_pipelined(env, steps, out, false);
 #endif
     default: break;
@@ -3460,10 +3502,10 @@ int coup_step_trajectory(coup_env* env, int64_t steps, const coup_step_outputs* 
     if (env->batch == 0 || steps == 0) return COUP_OK;
     switch (many_form(env, out)) {
       case coup::kManyTraj: COUP_TRY(launching(env)); return step_many_traj(env, steps, out, true, false);
+#ifdef COUP_AB_VARIANTS
       case coup::kManyOverlap:
         COUP_TRY(launching(env));
         return step_many_traj(env, steps, out, true, overlap_ready(env));
-#ifdef COUP_AB_VARIANTS
       case coup::kManyPipe: COUP_TRY(launching(env)); return step_many_pipelined(env, steps, out, true);
 #endif
       default: break;

@@ -25,11 +25,11 @@ constexpr int kInfoSplitDefault = 3;
 // coup_step_many's forms of the split observation step (COUP_PIPE): each
 // step's rules then its writer (kManySerial); chunks of up to kTrajChunkMax
 // steps as ONE regrouped rules-trajectory launch writing every step's
-// records, then a writer launch per step (kManyTraj); the same with the
-// rules trajectory of chunk c + 1 on a second stream beside the writers of
-// chunk c, the records double-buffered (kManyOverlap); the rules of step
-// t + 1 beside the writer of step t in one launch (kManyPipe, measurement
-// builds: measured slower).
+// records, then a writer launch per step (kManyTraj, shipped); measurement
+// builds also: the same with the rules trajectory of chunk c + 1 on a second
+// stream beside the writers of chunk c, the records double-buffered
+// (kManyOverlap), and the rules of step t + 1 beside the writer of step t
+// in one launch (kManyPipe) -- both measured slower, DESIGN.md section 5.
 constexpr int kManySerial = 0, kManyTraj = 1, kManyPipe = 2, kManyOverlap = 3;
 constexpr int kTrajChunkMax = 8;
 // rules blocks spread over the first kPipeSpanDefault of a pipelined
@@ -56,6 +56,7 @@ struct Knobs {
   int np_traj_stage = 1;    // COUP_TRAJ_STAGE
   int np_scan = 1;          // COUP_NP_SCAN
   double pipe_span = kPipeSpanDefault;  // COUP_PIPE_SPAN in (0, 1] (kManyPipe)
+  int overlap_cus = 0;  // COUP_OVERLAP_CUS: kManyOverlap's rules on this many CUs (CU-masked streams), 0 unmasked
 };
 
 inline int knob_int(const char* name, int dflt) {
@@ -90,8 +91,10 @@ inline Knobs read_knobs() {
   k.np_reset_group = knob_int("COUP_NP_RESET_GROUP", 0);
   k.np_traj_stage = knob_int("COUP_TRAJ_STAGE", 1);
   k.np_scan = knob_int("COUP_NP_SCAN", 1) != 0;
+  k.overlap_cus = knob_int("COUP_OVERLAP_CUS", 0);
 #else
-  if (k.pipe == kManyPipe) k.pipe = kManyTraj;  // the merged launch ships in measurement builds only
+  // the merged launch and the two-stream overlap ship in measurement builds only
+  if (k.pipe == kManyPipe || k.pipe == kManyOverlap) k.pipe = kManyTraj;
 #endif
   return k;
 }

@@ -1,0 +1,60 @@
+"""Measurement build (tests/ab_variants/conftest.py): coup_step_many's
+overlapped rules-trajectory form (COUP_PIPE=3: the rules trajectory of chunk
+c + 1 on a second stream beside chunk c's writers, records double-buffered,
+fork / join events; measured slower than the one-stream form, DESIGN.md
+section 5), unmasked and with CU-masked rules / writer streams
+(COUP_OVERLAP_CUS), through tests/test_gpu_step_many.py's checks: equal to
+coup_step launched once per step, bit for bit."""
+import pytest
+import torch
+
+from tests import test_gpu_step_many as M
+
+pytestmark = pytest.mark.gpu
+
+VARIANTS = ["0", "64"]  # COUP_OVERLAP_CUS
+
+
+@pytest.mark.parametrize("cus", VARIANTS)
+@pytest.mark.parametrize("B", [1000, (1 << 18) + 5])
+def test_overlap_equals_stepping(monkeypatch, B, cus):
+    monkeypatch.setenv("COUP_OVERLAP_CUS", cus)
+    M.test_step_many_equals_stepping(monkeypatch, B, "3")
+
+
+@pytest.mark.parametrize("cus", VARIANTS)
+@pytest.mark.parametrize("chunk", [1, 3])
+def test_overlap_chunk_length_invariant(monkeypatch, chunk, cus):
+    monkeypatch.setenv("COUP_OVERLAP_CUS", cus)
+    M.test_chunk_length_invariant(monkeypatch, chunk, "3")
+
+
+@pytest.mark.parametrize("cus", VARIANTS)
+def test_overlap_graph_capture(monkeypatch, cus):
+    monkeypatch.setenv("COUP_OVERLAP_CUS", cus)
+    M.test_graph_capture_and_packed_word(monkeypatch, "3", 2)
+
+
+def test_overlap_trajectory_slices(monkeypatch):
+    M.test_trajectory_slices_every_step(monkeypatch, 1 << 20, 21, "3")
+
+
+def test_overlap_capture_without_resources_falls_back(monkeypatch):
+    """COUP_PIPE=3 switched on after coup_create (coup_reload_knobs), so the
+    env's first overlapped coup_step_many is inside a graph capture, where no
+    stream or buffer can be made: the call runs on the env's stream alone,
+    same results; the next eager call makes them and overlaps."""
+    B, seed, K = 4096, 8, 6
+    many, ref = M._env(monkeypatch, B, "1", seed), M._env(monkeypatch, B, False, seed)
+    monkeypatch.setenv("COUP_PIPE", "3")
+    many.reload_knobs()
+    g = many.capture_steps(K)
+    g.replay()
+    torch.cuda.synchronize()
+    for _ in range(K):
+        ref.step()
+    M._same(M._state(many), M._state(ref), "capture fallback")
+    many.step_many(5)  # eager: now with the second stream
+    for _ in range(5):
+        ref.step()
+    M._same(M._state(many), M._state(ref), "after")

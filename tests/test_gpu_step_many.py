@@ -1,7 +1,5 @@
 """coup_step_many / coup_step_trajectory with observations in the
-rules-trajectory forms: COUP_PIPE=1 on the env's
-stream, COUP_PIPE=3 with the rules trajectories on a second stream beside
-the previous chunk's writers (records double-buffered, events between):
+rules-trajectory form (COUP_PIPE=1, the default):
 chunks of up to COUP_TRAJ_CHUNK steps run as ONE regrouped rules-trajectory
 launch (k_trajectory_sorted<1024, true>) that also stores every step's
 post-step records, then one k_obs_sweep_rows<512, 2> launch per step reading
@@ -27,7 +25,10 @@ from open_spiel_coup_amd import BatchedCoupEnv, _native  # noqa: E402
 KEYS = ("actions", "rewards", "step_type", "legal_mask", "current_player", "obs")
 
 
-FORMS = ["1", "3"]  # COUP_PIPE: the rules trajectory on the env's stream / overlapped on a second stream
+# COUP_PIPE: the rules trajectory on the env's stream (the measurement
+# build's overlapped form, "3", runs these tests from
+# tests/ab_variants/test_ab_overlap.py)
+FORMS = ["1"]
 
 
 def _env(monkeypatch, B, traj, seed, chunk=None, word=False):
@@ -149,23 +150,3 @@ def test_default_form_by_batch(monkeypatch):
         b.step()
     assert torch.equal(a.obs, b.obs) and torch.equal(a.export_state(), b.export_state())
 
-
-def test_overlap_capture_without_resources_falls_back(monkeypatch):
-    """COUP_PIPE=3 switched on after coup_create (coup_reload_knobs), so the
-    env's first overlapped coup_step_many is inside a graph capture, where no
-    stream or buffer can be made: the call runs on the env's stream alone,
-    same results; the next eager call makes them and overlaps."""
-    B, seed, K = 4096, 8, 6
-    many, ref = _env(monkeypatch, B, "1", seed), _env(monkeypatch, B, False, seed)
-    monkeypatch.setenv("COUP_PIPE", "3")
-    many.reload_knobs()
-    g = many.capture_steps(K)
-    g.replay()
-    torch.cuda.synchronize()
-    for _ in range(K):
-        ref.step()
-    _same(_state(many), _state(ref), "capture fallback")
-    many.step_many(5)  # eager: now with the second stream
-    for _ in range(5):
-        ref.step()
-    _same(_state(many), _state(ref), "after")

@@ -8,10 +8,12 @@ Each positional argument is one env created with those environment settings
 (knobs read at coup_create, e.g. COUP_PIPE, COUP_TRAJ_CHUNK, COUP_PIPE_SPAN)
 and captured with BatchedCoupEnv.capture_steps(K).  Default variants: the
 serial split step (COUP_PIPE=0), the rules-trajectory form (COUP_PIPE=1)
-at chunks of 8 / 4 steps, the same overlapped on two streams (COUP_PIPE=3)
-at chunks of 8 / 4 / 2, and with the
-measurement build (COUP_LIB_PATH=build/variants/libcoup_mi355x.so) the
-merged pipelined step (COUP_PIPE=2).  Prints one JSON line per variant:
+at chunks of 8 / 4 steps, and with the measurement build
+(COUP_LIB_PATH=build/variants/libcoup_mi355x.so) the merged pipelined step
+(COUP_PIPE=2) and the rules trajectories on a second stream beside the
+writers (COUP_PIPE=3; unmasked, and CU-masked rules / writer streams,
+COUP_OVERLAP_CUS).  --eager: time eager coup_step_many calls instead of
+graph replays (a graph replay may not keep a stream's CU mask).  Prints one JSON line per variant:
 median / min us per env step.  Measurement tool only.
 """
 import argparse
@@ -19,14 +21,16 @@ import json
 import os
 import statistics
 import sys
+import types
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-DEFAULT = ["serial:COUP_PIPE=0", "traj8:COUP_PIPE=1", "traj4:COUP_PIPE=1,COUP_TRAJ_CHUNK=4",
-           "over8:COUP_PIPE=3", "over4:COUP_PIPE=3,COUP_TRAJ_CHUNK=4", "over2:COUP_PIPE=3,COUP_TRAJ_CHUNK=2"]
-AB_ONLY = ["pipe85:COUP_PIPE=2,COUP_PIPE_SPAN=0.85"]
-KNOBS = ("COUP_PIPE", "COUP_PIPE_SPAN", "COUP_TRAJ_CHUNK", "COUP_OBS_SPLIT", "COUP_OBS_MODE")
+DEFAULT = ["serial:COUP_PIPE=0", "traj8:COUP_PIPE=1", "traj4:COUP_PIPE=1,COUP_TRAJ_CHUNK=4"]
+AB_ONLY = ["pipe85:COUP_PIPE=2,COUP_PIPE_SPAN=0.85", "over4:COUP_PIPE=3,COUP_TRAJ_CHUNK=4",
+           "over4m64:COUP_PIPE=3,COUP_TRAJ_CHUNK=4,COUP_OVERLAP_CUS=64",
+           "over8m32:COUP_PIPE=3,COUP_OVERLAP_CUS=32", "over8m64:COUP_PIPE=3,COUP_OVERLAP_CUS=64"]
+KNOBS = ("COUP_PIPE", "COUP_PIPE_SPAN", "COUP_TRAJ_CHUNK", "COUP_OVERLAP_CUS", "COUP_OBS_SPLIT", "COUP_OBS_MODE")
 
 
 def main():
@@ -35,6 +39,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=9)
     ap.add_argument("--settle", type=int, default=256)
+    ap.add_argument("--eager", action="store_true")
     ap.add_argument("variants", nargs="*")
     a = ap.parse_args()
     import torch
@@ -58,7 +63,10 @@ def main():
         for _ in range(5):
             env.step()
         env.clear_episode_stats()
-        graphs[name] = env.capture_steps(a.steps)
+        if a.eager:
+            graphs[name] = types.SimpleNamespace(replay=lambda e=env: e.step_many(a.steps))
+        else:
+            graphs[name] = env.capture_steps(a.steps)
         envs[name] = env
     for k in KNOBS:
         os.environ.pop(k, None)
