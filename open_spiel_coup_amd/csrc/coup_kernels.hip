@@ -3396,12 +3396,16 @@ int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, b
 }
 
 #ifdef COUP_AB_VARIANTS
-// kManyOverlap's resources, or false where they cannot be made now (a graph
-// capture on env->stream: the call then runs as kManyTraj, same results).
+// kManyOverlap's resources, or false where they cannot be made or used now
+// -- a graph capture on env->stream without them, or with CU-masked streams
+// (capturing work forked onto a CU-masked stream crashed the HIP runtime,
+// call r05j): the call then runs as kManyTraj, same results.
 bool overlap_ready(coup_env* env) {
-  if (env->aux) return true;
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(env->stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone) return false;
+  const bool capturing =
+      hipStreamIsCapturing(env->stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone;
+  if (env->aux) return !(capturing && env->aux_w);
+  if (capturing) return false;
   return overlap_resources(env) == COUP_OK;
 }
 #endif
