@@ -188,7 +188,8 @@ def step_many_form(batch, players, graph):
     default: chunks of COUP_TRAJ_CHUNK steps as one regrouped rules launch
     plus a writer launch per step; needs the regrouped rules), "pipelined"
     (COUP_PIPE=2, measurement builds: rules(t + 1) beside writer(t) in one
-    launch) -- or None (per-step launches).  Mirrors coup_kernels.hip
+    launch), "fused-trajectory" (COUP_PIPE=4: one launch for the K steps
+    writing the observations itself) -- or None (per-step launches).  Mirrors coup_kernels.hip
     `many_form`."""
     if not (graph and players == 2 and obs_split_active(batch) == 11):
         return None
@@ -199,7 +200,9 @@ def step_many_form(batch, players, graph):
         from open_spiel_coup_amd import _native
         if _native.load().coup_build_flags() & _native.BUILD_AB_VARIANTS:
             return "pipelined"
-    return "rules-trajectory" if _regrouped(batch) else None
+    if not _regrouped(batch):
+        return None
+    return "fused-trajectory" if v == "4" else "rules-trajectory"
 
 
 def traj_chunk():
@@ -785,7 +788,9 @@ def main():
                 kernel = "coup::k_step_obs_pipe<512, 2>"
             elif form:
                 # one rules-trajectory launch per chunk of steps + the writer per step
-                kernel = "coup::k_trajectory_sorted<1024, true> + " + _SPLIT_WRITERS.get(split, "coup::k_obs_sweep")
+                kernel = ("coup::k_trajectory_sorted<1024, false, true, 4>" if form == "fused-trajectory" else
+                          "coup::k_trajectory_sorted<1024, true, false, 8> + " +
+                          _SPLIT_WRITERS.get(split, "coup::k_obs_sweep"))
             elif split:
                 # the rules step without tensors (regrouped from 2^18 lanes) + the writer
                 kernel = "coup::k_step_sorted<true, 512> + " + _SPLIT_WRITERS.get(split, "coup::k_obs_sweep")

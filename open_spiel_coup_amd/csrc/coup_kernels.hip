@@ -15,6 +15,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #ifdef COUP_COUNT_PHILOX
@@ -1471,20 +1472,38 @@ __global__ __launch_bounds__(T, 8) void k_rollout_sorted(RolloutArgs a) {
 // every step overwrites them, the last step's stay).  REC: also every
 // step's post-step record (after an auto-reset) to x.rec[s * B + lane] --
 // the records the observation writer of step s reads (coup_step_many's
-// rules-trajectory form).
+// rules-trajectory form).  OBS: every step's
+// ObservationTensor [B][2][98] written by the block itself, in address
+// order, at a.obs + s * x.obs_stride floats: each thread decodes its lane's
+// two rows into LDS after the step, then the block's threads store the
+// block's contiguous 1024 x 784 B as float4s (k_obs_sweep_rows' decode); a
+// finished lane is dealt its next episode in the same step (the post-reset
+// record is the observed one), not at the next.
 struct TrajOut {
-  uint4* rec;      // REC: [steps][B] post-step records
-  int64_t stride;  // output offset per step: B or 0
+  uint4* rec;          // REC: [steps][B] post-step records
+  int64_t stride;      // output offset per step: B or 0
+  int64_t obs_stride;  // OBS: floats per step (B * 196) or 0
 };
 
-template <int T, bool REC = false>
-__global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t steps, TrajOut x) {
+template <int T>
+struct TrajObsLds {
+  alignas(16) uint32_t rows[T * 8];  // lane, row: lo.x lo.y hi.x hi.y
+  uint32_t coins[T];
+};
+template <int T>
+struct TrajNoLds {};
+
+// W: the minimum waves per SIMD the register budget is sized for (8: 64
+// VGPRs; the OBS form spills at 64, W = 4 gives it 128).
+template <int T, bool REC = false, bool OBS = false, int W = 8>
+__global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t steps, TrajOut x) {
   static_assert((T & (T - 1)) == 0 && T >= 64 && T <= 1024, "power-of-two block of whole waves");
   constexpr uint32_t kO = T <= 256 ? 8u : 10u;  // lane bits of s_meta
   __shared__ uint4 s_rec[T];
   __shared__ uint32_t s_meta[T];          // slot -> lane | key << kO
   __shared__ int32_t s_eps[T], s_ret[T];  // by lane
   __shared__ __attribute__((aligned(16))) uint32_t s_bin[2][32];
+  __shared__ typename std::conditional<OBS, TrajObsLds<T>, TrajNoLds<T>>::type s_obs;
   const uint32_t t = threadIdx.x;
   const int64_t base = (int64_t)blockIdx.x * T;
   const bool ar = a.auto_reset != 0;
@@ -1519,6 +1538,9 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
     lane = m & (T - 1u);
     key = (m >> kO) & 31u;
     L = unpack(s_rec[t]);
+    // the step's rules: `continue` ends the lane's step (the do-while), and
+    // with OBS every thread then meets the block's observation write below
+    do {
     const int64_t li = base + lane;
     if (li >= a.n) continue;  // past the batch
     const int64_t o = s * x.stride + li;
@@ -1570,6 +1592,15 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
     if (term) {
       s_eps[lane] += 1;
       s_ret[lane] += return0(L);
+      if (ar && OBS) {  // the next episode now: the observed record is the post-reset one
+        L = new_episode(L.episode + 1u, rng, none);
+        const uint32_t legal = decision_mask(L);
+        if (a.legal) a.legal[o] = legal;
+        if (a.cur_player) a.cur_player[o] = (int8_t)L.M;
+        if (REC) *rec_s = pack(L);
+        key = s + 1 < steps ? regroup_key(L, sample_action(legal, rng.draw(L.episode, L.move))) : kKeyDead;
+        continue;
+      }
       if (ar) {
         key = kKeyReset;  // legal mask and player once the next episode is dealt
         continue;
@@ -1585,6 +1616,45 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
     if (a.cur_player) a.cur_player[o] = (int8_t)L.M;
     if (REC) *rec_s = pack(L);
     if (s + 1 < steps) key = regroup_key(L, sample_action(legal, rng.draw(L.episode, L.move)));
+    } while (false);
+    if constexpr (OBS) {
+      // the block's lanes' observation rows, by lane, then the block's
+      // [lanes][2][98] floats in address order
+      const int64_t nl = a.n - base < (int64_t)T ? a.n - base : (int64_t)T;
+      if ((int64_t)lane < nl) {
+        uint64_t lo, hi;
+        const bool term = is_terminal(L);
+        obs_row_bits_rt(L, term, 0u, lo, hi);
+        reinterpret_cast<uint4*>(s_obs.rows)[2u * lane] =
+            make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+        obs_row_bits_rt(L, term, 1u, lo, hi);
+        reinterpret_cast<uint4*>(s_obs.rows)[2u * lane + 1u] =
+            make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+        s_obs.coins[lane] = L.c0 | (L.c1 << 8);
+      }
+      __syncthreads();
+      typedef float v4f __attribute__((ext_vector_type(4)));
+      v4f* const dst = reinterpret_cast<v4f*>(a.obs + s * x.obs_stride + base * (2 * kObsSize));
+      const uint32_t nf4 = (uint32_t)nl * (uint32_t)kRowF4;
+      for (uint32_t j = t; j < nf4; j += (uint32_t)T) {
+        const uint32_t ol = j / (uint32_t)kRowF4, c = j - ol * (uint32_t)kRowF4;
+        const uint32_t cn = s_obs.coins[ol];
+        float f[4];
+#pragma unroll
+        for (uint32_t e = 0; e < 4; ++e) {
+          const uint32_t k = 4u * c + e, p = k >= (uint32_t)kObsSize ? 1u : 0u, b = k - p * (uint32_t)kObsSize;
+          const uint32_t w = s_obs.rows[8u * ol + 4u * p + (b >> 5)];
+          const float bit = (float)((w >> (b & 31u)) & 1u);
+          f[e] = b == 60u ? (float)(cn & 0xFFu) : (b == 61u ? (float)(cn >> 8) : bit);
+        }
+        v4f v;
+        v.x = f[0];
+        v.y = f[1];
+        v.z = f[2];
+        v.w = f[3];
+        __builtin_nontemporal_store(v, dst + j);
+      }
+    }
   }
   if (key == kKeyReset && base + lane < a.n) {  // finished on the last step
     L = new_episode(L.episode + 1u, rng, none);
@@ -3301,7 +3371,8 @@ namespace {
 int many_form(const coup_env* env, const coup_step_outputs* out) {
   if (env->generic || env->hist || !env->traj_rec || !out || !out->obs || out->info_state) return coup::kManySerial;
   if (obs_split(env->knobs, env->batch) != coup::kObsSplitDefault) return coup::kManySerial;
-  if ((env->knobs.pipe == coup::kManyTraj || env->knobs.pipe == coup::kManyOverlap) &&
+  if ((env->knobs.pipe == coup::kManyTraj || env->knobs.pipe == coup::kManyOverlap ||
+       env->knobs.pipe == coup::kManyFused) &&
       !coup::regroup_lanes(env->knobs, env->batch))
     return coup::kManySerial;
   return env->knobs.pipe;
@@ -3350,6 +3421,42 @@ coup::StepArgs uniform_args(const coup_env* env, const coup_step_outputs* out) {
 // order each writer chunk after its rules and each rules chunk after the
 // writers that last read its buffer.  The streams join back into
 // env->stream, so the call is one fork / join, capturable into a HIP graph.
+int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, bool slices, bool overlap);
+
+// kManyFused: the `steps` uniform split steps as ONE launch of the regrouped
+// rules trajectory that also writes every step's observations itself, in
+// address order per block (k_trajectory_sorted<1024, false, true>): no
+// record round trip through HBM, and a CU's blocks overlap one block's
+// rules with another's stores.  Results equal `steps` coup_step calls.
+int step_many_fused(coup_env* env, int64_t steps, const coup_step_outputs* out, bool slices) {
+  const int64_t n = env->batch;
+  constexpr int TB = coup::kRolloutSortLanes;
+  coup::StepArgs a = uniform_args(env, out);
+  a.actions = out->actions;
+  a.rewards = out->rewards;
+  a.step_type = out->step_type;
+  a.legal = out->legal_mask;
+  a.cur_player = out->cur_player;
+  a.obs = out->obs;
+  const coup::TrajOut x{nullptr, slices ? n : 0, slices ? n * 2 * COUP_OBS_SIZE : 0};
+  auto go = [&](auto tt, auto ww) {
+    constexpr int T = decltype(tt)::value, W = decltype(ww)::value;
+    coup::k_trajectory_sorted<T, false, true, W><<<(unsigned)((n + T - 1) / T), T, 0, env->stream>>>(a, steps, x);
+  };
+#ifdef COUP_AB_VARIANTS
+  switch (env->knobs.fused_shape) {  // COUP_FUSED_SHAPE
+    case 1: go(std::integral_constant<int, 512>(), std::integral_constant<int, 4>()); break;
+    case 2: go(std::integral_constant<int, 1024>(), std::integral_constant<int, 8>()); break;
+    case 3: go(std::integral_constant<int, 512>(), std::integral_constant<int, 8>()); break;
+    default: go(std::integral_constant<int, TB>(), std::integral_constant<int, 4>()); break;
+  }
+#else
+  go(std::integral_constant<int, TB>(), std::integral_constant<int, 4>());
+#endif
+  COUP_HIP_TRY(hipGetLastError());
+  return COUP_OK;
+}
+
 int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, bool slices, bool overlap) {
   const int64_t n = env->batch;
   constexpr int TB = coup::kRolloutSortLanes;
@@ -3377,7 +3484,7 @@ int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, b
     a.cur_player = o.cur_player;
     if (overlap && k >= 2) COUP_HIP_TRY(hipStreamWaitEvent(R, env->ev_writers[b], 0));
     coup::k_trajectory_sorted<TB, true><<<(unsigned)((n + TB - 1) / TB), TB, 0, R>>>(
-        a, c, coup::TrajOut{rec, slices ? n : 0});
+        a, c, coup::TrajOut{rec, slices ? n : 0, 0});
     COUP_HIP_TRY(hipGetLastError());
     if (overlap) {
       COUP_HIP_TRY(hipEventRecord(env->ev_rules[b], R));
@@ -3475,6 +3582,7 @@ int coup_step_many(coup_env* env, int64_t steps, const coup_step_outputs* out) {
   if (env->batch == 0 || steps == 0) return COUP_OK;
   switch (many_form(env, out)) {
     case coup::kManyTraj: COUP_TRY(launching(env)); return step_many_traj(env, steps, out, false, false);
+    case coup::kManyFused: COUP_TRY(launching(env)); return step_many_fused(env, steps, out, false);
 #ifdef COUP_AB_VARIANTS
     case coup::kManyOverlap:
       COUP_TRY(launching(env));
@@ -3506,6 +3614,7 @@ int coup_step_trajectory(coup_env* env, int64_t steps, const coup_step_outputs* 
     if (env->batch == 0 || steps == 0) return COUP_OK;
     switch (many_form(env, out)) {
       case coup::kManyTraj: COUP_TRY(launching(env)); return step_many_traj(env, steps, out, true, false);
+      case coup::kManyFused: COUP_TRY(launching(env)); return step_many_fused(env, steps, out, true);
 #ifdef COUP_AB_VARIANTS
       case coup::kManyOverlap:
         COUP_TRY(launching(env));

@@ -30,7 +30,9 @@ constexpr int kInfoSplitDefault = 3;
 // stream beside the writers of chunk c, the records double-buffered
 // (kManyOverlap), and the rules of step t + 1 beside the writer of step t
 // in one launch (kManyPipe) -- both measured slower, DESIGN.md section 5.
-constexpr int kManySerial = 0, kManyTraj = 1, kManyPipe = 2, kManyOverlap = 3;
+// kManyFused: ONE regrouped rules-trajectory launch for all the steps that
+// writes every step's observations itself, block by block in address order.
+constexpr int kManySerial = 0, kManyTraj = 1, kManyPipe = 2, kManyOverlap = 3, kManyFused = 4;
 constexpr int kTrajChunkMax = 8;
 // rules blocks spread over the first kPipeSpanDefault of a pipelined
 // launch's block positions (COUP_PIPE_SPAN)
@@ -57,6 +59,7 @@ struct Knobs {
   int np_scan = 1;          // COUP_NP_SCAN
   double pipe_span = kPipeSpanDefault;  // COUP_PIPE_SPAN in (0, 1] (kManyPipe)
   int overlap_cus = 0;  // COUP_OVERLAP_CUS: kManyOverlap's rules on this many CUs (CU-masked streams), 0 unmasked
+  int fused_shape = 0;  // COUP_FUSED_SHAPE: kManyFused's block / register budget (0: 1024 lanes, 4 waves per SIMD)
 };
 
 inline int knob_int(const char* name, int dflt) {
@@ -70,7 +73,8 @@ inline Knobs read_knobs() {
   k.info_split = knob_int("COUP_INFO_SPLIT", -1);
   k.regroup = knob_int("COUP_REGROUP", -1);
   k.pipe = knob_int("COUP_PIPE", kManyTraj);
-  if (k.pipe != kManySerial && k.pipe != kManyPipe && k.pipe != kManyOverlap) k.pipe = kManyTraj;
+  if (k.pipe != kManySerial && k.pipe != kManyPipe && k.pipe != kManyOverlap && k.pipe != kManyFused)
+    k.pipe = kManyTraj;
   k.traj_chunk = knob_int("COUP_TRAJ_CHUNK", kTrajChunkMax);
   if (k.traj_chunk < 1 || k.traj_chunk > kTrajChunkMax) k.traj_chunk = kTrajChunkMax;
 #ifdef COUP_AB_VARIANTS
@@ -92,6 +96,7 @@ inline Knobs read_knobs() {
   k.np_traj_stage = knob_int("COUP_TRAJ_STAGE", 1);
   k.np_scan = knob_int("COUP_NP_SCAN", 1) != 0;
   k.overlap_cus = knob_int("COUP_OVERLAP_CUS", 0);
+  k.fused_shape = knob_int("COUP_FUSED_SHAPE", 0);
 #else
   // the merged launch and the two-stream overlap ship in measurement builds only
   if (k.pipe == kManyPipe || k.pipe == kManyOverlap) k.pipe = kManyTraj;

@@ -58,3 +58,13 @@ def test_overlap_capture_without_resources_falls_back(monkeypatch):
     for _ in range(5):
         ref.step()
     M._same(M._state(many), M._state(ref), "after")
+
+
+@pytest.mark.parametrize("shape", ["1", "2", "3"])
+def test_fused_trajectory_shapes(monkeypatch, shape):
+    """kManyFused's block / register-budget variants (COUP_FUSED_SHAPE: 512
+    lanes x 4 waves per SIMD, 1024 x 8, 512 x 8) equal stepping, and their
+    trajectory slices equal one coup_step per slice."""
+    monkeypatch.setenv("COUP_FUSED_SHAPE", shape)
+    M.test_step_many_equals_stepping(monkeypatch, 65536 + 77, "4")
+    M.test_chunk_length_invariant(monkeypatch, 8, "4")

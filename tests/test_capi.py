@@ -187,7 +187,8 @@ void coup::k_step<true, 0, 256, 2, false> | void coup::k_step<true, 4, 256, 1, f
 void coup::k_step<true, 4, 256, 2, false> | void coup::k_step<true, 9, 256, 0, false> |
 void coup::k_step_group<1, false> | void coup::k_step_group<1, true> |
 void coup::k_step_sorted<false, 512> | void coup::k_step_sorted<true, 512> |
-void coup::k_trajectory_sorted<1024, false> | void coup::k_trajectory_sorted<1024, true> |
+void coup::k_trajectory_sorted<1024, false, false, 8> | void coup::k_trajectory_sorted<1024, true, false, 8> |
+void coup::k_trajectory_sorted<1024, false, true, 4> |
 void coup::k_store_sweep<512, 2> | void coup::k_store_sweep<1024, 2>
 """
 

@@ -26,11 +26,12 @@ import types
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-DEFAULT = ["serial:COUP_PIPE=0", "traj8:COUP_PIPE=1", "traj4:COUP_PIPE=1,COUP_TRAJ_CHUNK=4"]
-AB_ONLY = ["pipe85:COUP_PIPE=2,COUP_PIPE_SPAN=0.85", "over4:COUP_PIPE=3,COUP_TRAJ_CHUNK=4",
-           "over4m64:COUP_PIPE=3,COUP_TRAJ_CHUNK=4,COUP_OVERLAP_CUS=64",
-           "over8m32:COUP_PIPE=3,COUP_OVERLAP_CUS=32", "over8m64:COUP_PIPE=3,COUP_OVERLAP_CUS=64"]
-KNOBS = ("COUP_PIPE", "COUP_PIPE_SPAN", "COUP_TRAJ_CHUNK", "COUP_OVERLAP_CUS", "COUP_OBS_SPLIT", "COUP_OBS_MODE")
+DEFAULT = ["serial:COUP_PIPE=0", "traj8:COUP_PIPE=1", "fused:COUP_PIPE=4"]
+AB_ONLY = ["fused512w4:COUP_PIPE=4,COUP_FUSED_SHAPE=1", "fused1024w8:COUP_PIPE=4,COUP_FUSED_SHAPE=2",
+           "fused512w8:COUP_PIPE=4,COUP_FUSED_SHAPE=3", "pipe85:COUP_PIPE=2,COUP_PIPE_SPAN=0.85",
+           "over4:COUP_PIPE=3,COUP_TRAJ_CHUNK=4"]
+KNOBS = ("COUP_PIPE", "COUP_PIPE_SPAN", "COUP_TRAJ_CHUNK", "COUP_OVERLAP_CUS", "COUP_FUSED_SHAPE", "COUP_OBS_SPLIT",
+         "COUP_OBS_MODE")
 
 
 def main():

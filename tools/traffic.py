@@ -67,8 +67,9 @@ def main():
     # step K alone.  The rules-trajectory step: ceil(K / chunk) rules
     # launches of up to `chunk` steps each and K writer launches.
     pipe = many == "pipelined"
-    chunks = -(-steps // traj_chunk()) if many == "rules-trajectory" else None
-    dispatches_per_window = steps + 1 if pipe else steps + chunks if chunks else None
+    chunks = -(-steps // traj_chunk()) if many == "rules-trajectory" else 1 if many == "fused-trajectory" else None
+    dispatches_per_window = (steps + 1 if pipe else 1 if many == "fused-trajectory" else steps + chunks if chunks
+                             else None)
 
     dst = os.path.join(ROOT, "profiles", tag, cfg)
     os.makedirs(dst, exist_ok=True)
@@ -99,8 +100,11 @@ def main():
             return bool("k_info_sweep" in kn or m)
         if pipe:
             return "k_step_obs_pipe" in kn or "15k_step_obs_pipe" in kn
+        if many == "fused-trajectory":
+            return bool(re.search(r"k_trajectory_sorted<\d+, false, true", kn) or
+                        re.search(r"19k_trajectory_sortedILi\d+ELb0ELb1E", kn))
         if chunks:
-            return bool("k_obs_sweep" in kn or re.search(r"k_trajectory_sorted<\d+, true>", kn) or
+            return bool("k_obs_sweep" in kn or re.search(r"k_trajectory_sorted<\d+, true", kn) or
                         re.search(r"19k_trajectory_sortedILi\d+ELb1E", kn))
         if want_obs and not want_info and split:
             # the split observation step: the rules step without tensors and
@@ -120,6 +124,8 @@ def main():
         total = CONFIGS[cfg][4]
         if pipe:
             return {"rules": 40, "writer": total - 40}.get(role, total)
+        if many == "fused-trajectory":
+            return total * steps  # every step's rules and observations in one launch
         if chunks and "trajectory_sorted" in kn:
             return 40 * steps / chunks  # the rules of the chunk's steps (mean steps per launch)
         if want_obs and split:
