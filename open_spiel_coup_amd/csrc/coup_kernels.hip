@@ -3423,11 +3423,14 @@ coup::StepArgs uniform_args(const coup_env* env, const coup_step_outputs* out) {
 // env->stream, so the call is one fork / join, capturable into a HIP graph.
 int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, bool slices, bool overlap);
 
-// kManyFused: the `steps` uniform split steps as ONE launch of the regrouped
-// rules trajectory that also writes every step's observations itself, in
-// address order per block (k_trajectory_sorted<1024, false, true>): no
-// record round trip through HBM, and a CU's blocks overlap one block's
-// rules with another's stores.  Results equal `steps` coup_step calls.
+#ifdef COUP_AB_VARIANTS
+// kManyFused (measurement builds): the `steps` uniform split steps as ONE
+// launch of the regrouped rules trajectory that also writes every step's
+// observations itself, in address order per block (k_trajectory_sorted<
+// 1024, false, true, 4>): no record round trip through HBM, a CU's blocks
+// overlapping one block's rules with another's stores.  Results equal
+// `steps` coup_step calls; measured slower than kManyTraj (153.4 against
+// 134.7 us per 2^20-lane step, call r05k): the store stream runs best alone.
 int step_many_fused(coup_env* env, int64_t steps, const coup_step_outputs* out, bool slices) {
   const int64_t n = env->batch;
   constexpr int TB = coup::kRolloutSortLanes;
@@ -3443,19 +3446,16 @@ int step_many_fused(coup_env* env, int64_t steps, const coup_step_outputs* out, 
     constexpr int T = decltype(tt)::value, W = decltype(ww)::value;
     coup::k_trajectory_sorted<T, false, true, W><<<(unsigned)((n + T - 1) / T), T, 0, env->stream>>>(a, steps, x);
   };
-#ifdef COUP_AB_VARIANTS
   switch (env->knobs.fused_shape) {  // COUP_FUSED_SHAPE
     case 1: go(std::integral_constant<int, 512>(), std::integral_constant<int, 4>()); break;
     case 2: go(std::integral_constant<int, 1024>(), std::integral_constant<int, 8>()); break;
     case 3: go(std::integral_constant<int, 512>(), std::integral_constant<int, 8>()); break;
     default: go(std::integral_constant<int, TB>(), std::integral_constant<int, 4>()); break;
   }
-#else
-  go(std::integral_constant<int, TB>(), std::integral_constant<int, 4>());
-#endif
   COUP_HIP_TRY(hipGetLastError());
   return COUP_OK;
 }
+#endif
 
 int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, bool slices, bool overlap) {
   const int64_t n = env->batch;
@@ -3582,8 +3582,8 @@ int coup_step_many(coup_env* env, int64_t steps, const coup_step_outputs* out) {
   if (env->batch == 0 || steps == 0) return COUP_OK;
   switch (many_form(env, out)) {
     case coup::kManyTraj: COUP_TRY(launching(env)); return step_many_traj(env, steps, out, false, false);
-    case coup::kManyFused: COUP_TRY(launching(env)); return step_many_fused(env, steps, out, false);
 #ifdef COUP_AB_VARIANTS
+    case coup::kManyFused: COUP_TRY(launching(env)); return step_many_fused(env, steps, out, false);
     case coup::kManyOverlap:
       COUP_TRY(launching(env));
       return step_many_traj(env, steps, out, false, overlap_ready(env));
@@ -3614,8 +3614,8 @@ int coup_step_trajectory(coup_env* env, int64_t steps, const coup_step_outputs* 
     if (env->batch == 0 || steps == 0) return COUP_OK;
     switch (many_form(env, out)) {
       case coup::kManyTraj: COUP_TRY(launching(env)); return step_many_traj(env, steps, out, true, false);
-      case coup::kManyFused: COUP_TRY(launching(env)); return step_many_fused(env, steps, out, true);
 #ifdef COUP_AB_VARIANTS
+      case coup::kManyFused: COUP_TRY(launching(env)); return step_many_fused(env, steps, out, true);
       case coup::kManyOverlap:
         COUP_TRY(launching(env));
         return step_many_traj(env, steps, out, true, overlap_ready(env));

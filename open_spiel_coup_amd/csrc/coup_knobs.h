@@ -29,9 +29,10 @@ constexpr int kInfoSplitDefault = 3;
 // builds also: the same with the rules trajectory of chunk c + 1 on a second
 // stream beside the writers of chunk c, the records double-buffered
 // (kManyOverlap), and the rules of step t + 1 beside the writer of step t
-// in one launch (kManyPipe) -- both measured slower, DESIGN.md section 5.
-// kManyFused: ONE regrouped rules-trajectory launch for all the steps that
-// writes every step's observations itself, block by block in address order.
+// in one launch (kManyPipe), and ONE regrouped rules-trajectory launch for
+// all the steps that writes every step's observations itself, block by
+// block in address order (kManyFused) -- all measured slower, DESIGN.md
+// section 5.
 constexpr int kManySerial = 0, kManyTraj = 1, kManyPipe = 2, kManyOverlap = 3, kManyFused = 4;
 constexpr int kTrajChunkMax = 8;
 // rules blocks spread over the first kPipeSpanDefault of a pipelined
@@ -98,8 +99,9 @@ inline Knobs read_knobs() {
   k.overlap_cus = knob_int("COUP_OVERLAP_CUS", 0);
   k.fused_shape = knob_int("COUP_FUSED_SHAPE", 0);
 #else
-  // the merged launch and the two-stream overlap ship in measurement builds only
-  if (k.pipe == kManyPipe || k.pipe == kManyOverlap) k.pipe = kManyTraj;
+  // the merged launch, the two-stream overlap and the fused trajectory ship
+  // in measurement builds only
+  if (k.pipe == kManyPipe || k.pipe == kManyOverlap || k.pipe == kManyFused) k.pipe = kManyTraj;
 #endif
   return k;
 }

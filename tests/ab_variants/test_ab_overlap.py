@@ -1,5 +1,6 @@
 """Measurement build (tests/ab_variants/conftest.py): coup_step_many's
-overlapped rules-trajectory form (COUP_PIPE=3: the rules trajectory of chunk
+rejected forms -- the fused trajectory writing the observations itself
+(COUP_PIPE=4, COUP_FUSED_SHAPE) and the overlapped rules-trajectory form (COUP_PIPE=3: the rules trajectory of chunk
 c + 1 on a second stream beside chunk c's writers, records double-buffered,
 fork / join events; measured slower than the one-stream form, DESIGN.md
 section 5), unmasked and with CU-masked rules / writer streams
@@ -68,3 +69,12 @@ def test_fused_trajectory_shapes(monkeypatch, shape):
     monkeypatch.setenv("COUP_FUSED_SHAPE", shape)
     M.test_step_many_equals_stepping(monkeypatch, 65536 + 77, "4")
     M.test_chunk_length_invariant(monkeypatch, 8, "4")
+
+
+@pytest.mark.parametrize("B,T", [(1000, 12), (1 << 20, 10)])
+def test_fused_trajectory_default_shape(monkeypatch, B, T):
+    """kManyFused's default shape (1024 lanes, 4 waves per SIMD): stepping,
+    graph capture and trajectory slices."""
+    M.test_step_many_equals_stepping(monkeypatch, 3, "4")
+    M.test_graph_capture_and_packed_word(monkeypatch, "4", 8)
+    M.test_trajectory_slices_every_step(monkeypatch, B, T, "4")

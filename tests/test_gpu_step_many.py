@@ -28,7 +28,7 @@ KEYS = ("actions", "rewards", "step_type", "legal_mask", "current_player", "obs"
 # COUP_PIPE: the rules trajectory on the env's stream (the measurement
 # build's overlapped form, "3", runs these tests from
 # tests/ab_variants/test_ab_overlap.py)
-FORMS = ["1", "4"]  # 4: ONE launch for all the steps, the observations written by the rules kernel itself
+FORMS = ["1"]
 
 
 def _env(monkeypatch, B, traj, seed, chunk=None, word=False):
