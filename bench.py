@@ -178,7 +178,7 @@ def obs_split_active(batch):
     return int(_native.load().coup_obs_split_variant(int(batch)))
 
 
-TRAJ_CHUNK_MAX = 8  # coup::kTrajChunkMax
+TRAJ_CHUNK_DEFAULT, TRAJ_CHUNK_MAX = 8, 32  # coup::kTrajChunkDefault, kTrajChunkMax
 
 
 def step_many_form(batch, players, graph):
@@ -208,10 +208,10 @@ def step_many_form(batch, players, graph):
 def traj_chunk():
     """COUP_TRAJ_CHUNK as coup::read_knobs clamps it."""
     try:
-        c = int(os.environ.get("COUP_TRAJ_CHUNK", TRAJ_CHUNK_MAX))
+        c = int(os.environ.get("COUP_TRAJ_CHUNK", TRAJ_CHUNK_DEFAULT))
     except ValueError:
-        c = TRAJ_CHUNK_MAX
-    return c if 1 <= c <= TRAJ_CHUNK_MAX else TRAJ_CHUNK_MAX
+        c = TRAJ_CHUNK_DEFAULT
+    return c if 1 <= c <= TRAJ_CHUNK_MAX else TRAJ_CHUNK_DEFAULT
 
 
 _INFO_WRITERS = {1: "coup::k_info_sweep<512, 2>", 2: "coup::k_info_sweep<256, 2>", 3: "coup::k_info_sweep<1024, 2>",
@@ -788,8 +788,9 @@ def main():
                 kernel = "coup::k_step_obs_pipe<512, 2>"
             elif form:
                 # one rules-trajectory launch per chunk of steps + the writer per step
-                kernel = ("coup::k_trajectory_sorted<1024, false, true, 4>" if form == "fused-trajectory" else
-                          "coup::k_trajectory_sorted<1024, true, false, 8> + " +
+                stage = os.environ.get("COUP_MANY_STAGE", "0").strip() not in ("0", "")
+                kernel = ("coup::k_trajectory_sorted<1024, false, true, 4, false>" if form == "fused-trajectory" else
+                          "coup::k_trajectory_sorted<1024, true, false, 8, %s> + " % ("true" if stage else "false") +
                           _SPLIT_WRITERS.get(split, "coup::k_obs_sweep"))
             elif split:
                 # the rules step without tensors (regrouped from 2^18 lanes) + the writer

@@ -1492,10 +1492,24 @@ struct TrajObsLds {
 };
 template <int T>
 struct TrajNoLds {};
+// STAGE: a step's outputs by lane, stored by each lane's home thread
+template <int T>
+struct TrajStageLds {
+  uint4 rec[T];
+  uint32_t legal[T];
+  uint16_t rew[T];
+  int8_t act[T];
+  uint8_t st[T];
+  int8_t cp[T];
+};
 
 // W: the minimum waves per SIMD the register budget is sized for (8: 64
-// VGPRs; the OBS form spills at 64, W = 4 gives it 128).
-template <int T, bool REC = false, bool OBS = false, int W = 8>
+// VGPRs; the OBS form spills at 64, W = 4 gives it 128).  STAGE: each
+// step's outputs (and REC records) staged by lane in LDS and stored by the
+// lanes' home threads, coalesced, instead of from the thread that played
+// the lane (a wave of regrouped lanes scatters its stores over the
+// block's window); finished lanes are dealt in the same step, as with OBS.
+template <int T, bool REC = false, bool OBS = false, int W = 8, bool STAGE = false>
 __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t steps, TrajOut x) {
   static_assert((T & (T - 1)) == 0 && T >= 64 && T <= 1024, "power-of-two block of whole waves");
   constexpr uint32_t kO = T <= 256 ? 8u : 10u;  // lane bits of s_meta
@@ -1504,6 +1518,8 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
   __shared__ int32_t s_eps[T], s_ret[T];  // by lane
   __shared__ __attribute__((aligned(16))) uint32_t s_bin[2][32];
   __shared__ typename std::conditional<OBS, TrajObsLds<T>, TrajNoLds<T>>::type s_obs;
+  __shared__ typename std::conditional<STAGE, TrajStageLds<T>, TrajNoLds<T>>::type s_st;
+  constexpr bool kNow = OBS || STAGE;  // a finished lane's next episode dealt in the same step
   const uint32_t t = threadIdx.x;
   const int64_t base = (int64_t)blockIdx.x * T;
   const bool ar = a.auto_reset != 0;
@@ -1545,6 +1561,31 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
     if (li >= a.n) continue;  // past the batch
     const int64_t o = s * x.stride + li;
     uint4* const rec_s = REC ? x.rec + s * a.n + li : nullptr;  // step s's record of the lane
+    // the lane's step-s outputs: to the buffers, or (STAGE) to LDS by lane
+    auto put_act = [&](int8_t v) {
+      if constexpr (STAGE) s_st.act[lane] = v;
+      else if (a.actions) a.actions[o] = v;
+    };
+    auto put_rew = [&](uint16_t v) {
+      if constexpr (STAGE) s_st.rew[lane] = v;
+      else if (a.rewards) reinterpret_cast<uint16_t*>(a.rewards)[o] = v;
+    };
+    auto put_st = [&](uint8_t v) {
+      if constexpr (STAGE) s_st.st[lane] = v;
+      else if (a.step_type) a.step_type[o] = v;
+    };
+    auto put_legal = [&](uint32_t v) {
+      if constexpr (STAGE) s_st.legal[lane] = v;
+      else if (a.legal) a.legal[o] = v;
+    };
+    auto put_cp = [&](int8_t v) {
+      if constexpr (STAGE) s_st.cp[lane] = v;
+      else if (a.cur_player) a.cur_player[o] = v;
+    };
+    auto put_rec = [&](const Lane& R) {
+      if constexpr (STAGE) s_st.rec[lane] = pack(R);
+      else if (REC) *rec_s = pack(R);
+    };
     rng.env_id = lane_stream_id(a.env_id_base, li);
     rng.blk_tag = 0u;
     // a new episode and a live lane after resolve_chance are at decision
@@ -1552,16 +1593,16 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
     if (key == kKeyFirst) {  // step() after LAST (rl_environment.py:310-311)
       L = new_episode(L.episode + 1u, rng, none);
       const uint32_t legal = decision_mask(L);
-      if (a.actions) a.actions[o] = -1;
-      if (a.rewards) reinterpret_cast<uint16_t*>(a.rewards)[o] = 0u;
-      if (a.step_type) a.step_type[o] = (uint8_t)COUP_STEP_FIRST;
-      if (a.legal) a.legal[o] = legal;
-      if (a.cur_player) a.cur_player[o] = (int8_t)L.M;
-      if (REC) *rec_s = pack(L);
+      put_act(-1);
+      put_rew(0u);
+      put_st((uint8_t)COUP_STEP_FIRST);
+      put_legal(legal);
+      put_cp((int8_t)L.M);
+      put_rec(L);
       key = regroup_key(L, sample_action(legal, rng.draw(L.episode, L.move)));
       continue;
     }
-    if (key == kKeyReset) {  // finished in step s - 1 with auto-reset (vector_env.py:62-65)
+    if (!kNow && key == kKeyReset) {  // finished in step s - 1 with auto-reset (vector_env.py:62-65)
       L = new_episode(L.episode + 1u, rng, none);
       const uint32_t legal = decision_mask(L);
       if (a.legal) a.legal[o - x.stride] = legal;
@@ -1571,12 +1612,12 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
     }
     if (key == kKeyDead) {  // no legal decision: coup_step's rejected step
       errs += 1u;
-      if (a.actions) a.actions[o] = -1;
-      if (a.rewards) reinterpret_cast<uint16_t*>(a.rewards)[o] = 0u;
-      if (a.step_type) a.step_type[o] = (uint8_t)COUP_STEP_MID;
-      if (a.legal) a.legal[o] = legal_mask(L);
-      if (a.cur_player) a.cur_player[o] = (int8_t)current_player(L);
-      if (REC) *rec_s = pack(L);
+      put_act(-1);
+      put_rew(0u);
+      put_st((uint8_t)COUP_STEP_MID);
+      put_legal(legal_mask(L));
+      put_cp((int8_t)current_player(L));
+      put_rec(L);
       continue;
     }
     const uint32_t act = key_action(key);
@@ -1586,18 +1627,18 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
     resolve_chance(L, rng);
     errs += (L.err && !err_before) ? 1u : 0u;
     const bool term = is_terminal(L);
-    if (a.actions) a.actions[o] = (int8_t)act;
-    if (a.rewards) reinterpret_cast<uint16_t*>(a.rewards)[o] = (uint16_t)((uint8_t)L.r0 | ((uint8_t)(-L.r0) << 8));
-    if (a.step_type) a.step_type[o] = (uint8_t)(term ? COUP_STEP_LAST : COUP_STEP_MID);
+    put_act((int8_t)act);
+    put_rew((uint16_t)((uint8_t)L.r0 | ((uint8_t)(-L.r0) << 8)));
+    put_st((uint8_t)(term ? COUP_STEP_LAST : COUP_STEP_MID));
     if (term) {
       s_eps[lane] += 1;
       s_ret[lane] += return0(L);
-      if (ar && OBS) {  // the next episode now: the observed record is the post-reset one
+      if (ar && kNow) {  // the next episode now: the observed / staged record is the post-reset one
         L = new_episode(L.episode + 1u, rng, none);
         const uint32_t legal = decision_mask(L);
-        if (a.legal) a.legal[o] = legal;
-        if (a.cur_player) a.cur_player[o] = (int8_t)L.M;
-        if (REC) *rec_s = pack(L);
+        put_legal(legal);
+        put_cp((int8_t)L.M);
+        put_rec(L);
         key = s + 1 < steps ? regroup_key(L, sample_action(legal, rng.draw(L.episode, L.move))) : kKeyDead;
         continue;
       }
@@ -1606,17 +1647,30 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
         continue;
       }
       key = kKeyFirst;
-      if (a.legal) a.legal[o] = 0u;  // terminal: no legal actions, kTerminalPlayerId
-      if (a.cur_player) a.cur_player[o] = (int8_t)-4;
-      if (REC) *rec_s = pack(L);
+      put_legal(0u);  // terminal: no legal actions, kTerminalPlayerId
+      put_cp((int8_t)-4);
+      put_rec(L);
       continue;
     }
     const uint32_t legal = decision_mask(L);
-    if (a.legal) a.legal[o] = legal;
-    if (a.cur_player) a.cur_player[o] = (int8_t)L.M;
-    if (REC) *rec_s = pack(L);
+    put_legal(legal);
+    put_cp((int8_t)L.M);
+    put_rec(L);
     if (s + 1 < steps) key = regroup_key(L, sample_action(legal, rng.draw(L.episode, L.move)));
     } while (false);
+    if constexpr (STAGE) {  // the staged outputs from each lane's home thread, coalesced
+      __syncthreads();
+      const int64_t i = base + t;
+      if (i < a.n) {
+        const int64_t oh = s * x.stride + i;
+        if (a.actions) a.actions[oh] = s_st.act[t];
+        if (a.rewards) reinterpret_cast<uint16_t*>(a.rewards)[oh] = s_st.rew[t];
+        if (a.step_type) a.step_type[oh] = s_st.st[t];
+        if (a.legal) a.legal[oh] = s_st.legal[t];
+        if (a.cur_player) a.cur_player[oh] = s_st.cp[t];
+        if (REC) x.rec[s * a.n + i] = s_st.rec[t];
+      }
+    }
     if constexpr (OBS) {
       // the block's lanes' observation rows, by lane, then the block's
       // [lanes][2][98] floats in address order
@@ -1656,7 +1710,7 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
       }
     }
   }
-  if (key == kKeyReset && base + lane < a.n) {  // finished on the last step
+  if (!kNow && key == kKeyReset && base + lane < a.n) {  // finished on the last step
     L = new_episode(L.episode + 1u, rng, none);
     const int64_t o = (steps - 1) * x.stride + base + lane;
     if (a.legal) a.legal[o] = decision_mask(L);
@@ -2389,8 +2443,9 @@ struct coup_env {
   coup_server* server;        // coup_attach_server: coup_slot_op goes through this resident wave
   bool dirty;                 // work enqueued on `stream` since its last synchronisation
   hipEvent_t stream_event;    // coup_set_stream: orders a new stream after the old one's pending work
-  uint4* traj_rec;            // 2 players: [kTrajChunkMax][B] records of coup_step_many's rules trajectories
-                              // ([2][kTrajChunkMax][B] once the overlapped form's resources exist)
+  uint4* traj_rec;            // 2 players: [traj_cap][B] records of coup_step_many's rules trajectories
+                              // ([2][traj_cap][B] once the overlapped form's resources exist)
+  int64_t traj_cap;           // steps per rules-trajectory launch the buffer holds (COUP_TRAJ_CHUNK at create)
   uint4* state2;              // = traj_rec: the second record buffer of the merged pipelined step
   hipStream_t aux;            // kManyOverlap (measurement builds): the rules trajectories' stream
   hipStream_t aux_w;          // ... and with COUP_OVERLAP_CUS the writers' (both CU-masked)
@@ -2760,7 +2815,7 @@ int overlap_resources(coup_env* env) {
   if (env->aux) return COUP_OK;
   const size_t lanes = (size_t)(env->batch > 0 ? env->batch : 1);
   uint4* rec = nullptr;
-  hipError_t e = hipMalloc(&rec, lanes * sizeof(uint4) * 2 * coup::kTrajChunkMax);
+  hipError_t e = hipMalloc(&rec, lanes * sizeof(uint4) * 2 * env->traj_cap);
   if (e != hipSuccess) return fail(COUP_E_HIP, std::string("coup_step_many: ") + hipGetErrorString(e));
   hipStream_t aux = nullptr, aux_w = nullptr;
   hipEvent_t ev[5] = {};
@@ -2854,6 +2909,7 @@ int coup_create_ex(int64_t batch, uint64_t seed, uint32_t env_id_base, int flags
   env->dirty = false;
   env->stream_event = nullptr;
   env->traj_rec = nullptr;
+  env->traj_cap = 0;
   env->state2 = nullptr;
   env->aux = nullptr;
   env->aux_w = nullptr;
@@ -2864,7 +2920,8 @@ int coup_create_ex(int64_t batch, uint64_t seed, uint32_t env_id_base, int flags
   // coup_step_many's per-step record buffer (allocated here: coup_step_many
   // may be captured into a HIP graph, where no allocation may happen)
   if (e == hipSuccess && !generic) {
-    e = hipMalloc(&env->traj_rec, lanes * sizeof(uint4) * coup::kTrajChunkMax);
+    env->traj_cap = env->knobs.traj_chunk;
+    e = hipMalloc(&env->traj_rec, lanes * sizeof(uint4) * env->traj_cap);
     env->state2 = env->traj_rec;
   }
   if (e == hipSuccess) e = hipMalloc(&env->err_count, sizeof(uint32_t));
@@ -3460,7 +3517,7 @@ int step_many_fused(coup_env* env, int64_t steps, const coup_step_outputs* out, 
 int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, bool slices, bool overlap) {
   const int64_t n = env->batch;
   constexpr int TB = coup::kRolloutSortLanes;
-  const int64_t chunk = env->knobs.traj_chunk;
+  const int64_t chunk = std::min<int64_t>(env->knobs.traj_chunk, env->traj_cap);
   const int64_t nf4 = n * coup::kRowF4;
   const unsigned wgrid = (unsigned)((nf4 + 1023) / 1024);  // 512 threads x 2 passes
   const hipStream_t R = overlap ? env->aux : env->stream;
@@ -3474,7 +3531,7 @@ int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, b
   for (int64_t t0 = 0; t0 < steps; t0 += chunk, ++k) {
     const int64_t c = std::min(chunk, steps - t0);
     const int b = (int)(k & 1);
-    uint4* const rec = env->traj_rec + (overlap ? b * coup::kTrajChunkMax * n : 0);
+    uint4* const rec = env->traj_rec + (overlap ? b * env->traj_cap * n : 0);
     const coup_step_outputs o = slices ? slice_outputs(*out, n, 2, t0) : *out;
     coup::StepArgs a = uniform_args(env, out);
     a.actions = o.actions;
@@ -3483,8 +3540,12 @@ int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, b
     a.legal = o.legal_mask;
     a.cur_player = o.cur_player;
     if (overlap && k >= 2) COUP_HIP_TRY(hipStreamWaitEvent(R, env->ev_writers[b], 0));
-    coup::k_trajectory_sorted<TB, true><<<(unsigned)((n + TB - 1) / TB), TB, 0, R>>>(
-        a, c, coup::TrajOut{rec, slices ? n : 0, 0});
+    const coup::TrajOut x{rec, slices ? n : 0, 0};
+    const unsigned grid = (unsigned)((n + TB - 1) / TB);
+    if (env->knobs.many_stage)
+      coup::k_trajectory_sorted<TB, true, false, 8, true><<<grid, TB, 0, R>>>(a, c, x);
+    else
+      coup::k_trajectory_sorted<TB, true, false, 8, false><<<grid, TB, 0, R>>>(a, c, x);
     COUP_HIP_TRY(hipGetLastError());
     if (overlap) {
       COUP_HIP_TRY(hipEventRecord(env->ev_rules[b], R));

@@ -34,7 +34,7 @@ constexpr int kInfoSplitDefault = 3;
 // block in address order (kManyFused) -- all measured slower, DESIGN.md
 // section 5.
 constexpr int kManySerial = 0, kManyTraj = 1, kManyPipe = 2, kManyOverlap = 3, kManyFused = 4;
-constexpr int kTrajChunkMax = 8;
+constexpr int kTrajChunkDefault = 8, kTrajChunkMax = 32;
 // rules blocks spread over the first kPipeSpanDefault of a pipelined
 // launch's block positions (COUP_PIPE_SPAN)
 constexpr double kPipeSpanDefault = 0.85;
@@ -45,7 +45,9 @@ struct Knobs {
   int info_split = -1;  // COUP_INFO_SPLIT: -1 by batch (from 2^18 lanes), 0 fused, 3 the shipped writer
   int regroup = -1;     // COUP_REGROUP: -1 by batch (from 2^18 lanes), 0 / 1 forced
   int pipe = kManyTraj;  // COUP_PIPE: coup_step_many's form of the split step (kMany*)
-  int traj_chunk = kTrajChunkMax;  // COUP_TRAJ_CHUNK 1..kTrajChunkMax: steps per rules-trajectory launch
+  int traj_chunk = kTrajChunkDefault;  // COUP_TRAJ_CHUNK 1..kTrajChunkMax: steps per rules-trajectory launch
+                                       // (the record buffer is sized by its value at coup_create)
+  int many_stage = 0;  // COUP_MANY_STAGE: the rules trajectory's outputs staged by lane (coalesced stores)
   // -- measurement builds (-DCOUP_AB_VARIANTS); the product ignores them
   int obs_mode = 9;       // COUP_OBS_MODE 1..9: the fused step's observation writer
   int xcd_remap = 1;      // COUP_XCD_REMAP: XCD-aware block -> lane-group mapping of the fused step
@@ -76,8 +78,9 @@ inline Knobs read_knobs() {
   k.pipe = knob_int("COUP_PIPE", kManyTraj);
   if (k.pipe != kManySerial && k.pipe != kManyPipe && k.pipe != kManyOverlap && k.pipe != kManyFused)
     k.pipe = kManyTraj;
-  k.traj_chunk = knob_int("COUP_TRAJ_CHUNK", kTrajChunkMax);
-  if (k.traj_chunk < 1 || k.traj_chunk > kTrajChunkMax) k.traj_chunk = kTrajChunkMax;
+  k.traj_chunk = knob_int("COUP_TRAJ_CHUNK", kTrajChunkDefault);
+  if (k.traj_chunk < 1 || k.traj_chunk > kTrajChunkMax) k.traj_chunk = kTrajChunkDefault;
+  k.many_stage = knob_int("COUP_MANY_STAGE", 0) != 0;
 #ifdef COUP_AB_VARIANTS
   if (const char* f = std::getenv("COUP_PIPE_SPAN")) {
     const double v = std::atof(f);

@@ -27,7 +27,7 @@ def test_overlap_equals_stepping(monkeypatch, B, cus):
 @pytest.mark.parametrize("chunk", [1, 3])
 def test_overlap_chunk_length_invariant(monkeypatch, chunk, cus):
     monkeypatch.setenv("COUP_OVERLAP_CUS", cus)
-    M.test_chunk_length_invariant(monkeypatch, chunk, "3")
+    M.test_chunk_length_invariant(monkeypatch, chunk, "3", None)
 
 
 @pytest.mark.parametrize("cus", VARIANTS)
@@ -37,7 +37,7 @@ def test_overlap_graph_capture(monkeypatch, cus):
 
 
 def test_overlap_trajectory_slices(monkeypatch):
-    M.test_trajectory_slices_every_step(monkeypatch, 1 << 20, 21, "3")
+    M.test_trajectory_slices_every_step(monkeypatch, 1 << 20, 21, "3", None)
 
 
 def test_overlap_capture_without_resources_falls_back(monkeypatch):
@@ -68,7 +68,7 @@ def test_fused_trajectory_shapes(monkeypatch, shape):
     trajectory slices equal one coup_step per slice."""
     monkeypatch.setenv("COUP_FUSED_SHAPE", shape)
     M.test_step_many_equals_stepping(monkeypatch, 65536 + 77, "4")
-    M.test_chunk_length_invariant(monkeypatch, 8, "4")
+    M.test_chunk_length_invariant(monkeypatch, 8, "4", None)
 
 
 @pytest.mark.parametrize("B,T", [(1000, 12), (1 << 20, 10)])
@@ -77,4 +77,4 @@ def test_fused_trajectory_default_shape(monkeypatch, B, T):
     graph capture and trajectory slices."""
     M.test_step_many_equals_stepping(monkeypatch, 3, "4")
     M.test_graph_capture_and_packed_word(monkeypatch, "4", 8)
-    M.test_trajectory_slices_every_step(monkeypatch, B, T, "4")
+    M.test_trajectory_slices_every_step(monkeypatch, B, T, "4", None)

@@ -31,8 +31,13 @@ KEYS = ("actions", "rewards", "step_type", "legal_mask", "current_player", "obs"
 FORMS = ["1"]
 
 
-def _env(monkeypatch, B, traj, seed, chunk=None, word=False):
-    """traj: a COUP_PIPE form ("1" / "3"), or False for per-step coup_step."""
+def _env(monkeypatch, B, traj, seed, chunk=None, word=False, stage=None):
+    """traj: a COUP_PIPE form ("1" / "3"), or False for per-step coup_step;
+    stage: COUP_MANY_STAGE."""
+    if stage is None:
+        monkeypatch.delenv("COUP_MANY_STAGE", raising=False)
+    else:
+        monkeypatch.setenv("COUP_MANY_STAGE", stage)
     monkeypatch.setenv("COUP_OBS_SPLIT", "11")  # the shipped writer at every size (the default from 2^20)
     monkeypatch.setenv("COUP_REGROUP", "1")     # the regrouped rules at every size (the default from 2^18)
     monkeypatch.setenv("COUP_PIPE", traj if traj else "0")
@@ -72,13 +77,16 @@ def test_step_many_equals_stepping(monkeypatch, B, form):
     assert many.error_count() == ref.error_count() == 0
 
 
+@pytest.mark.parametrize("stage", [None, "1"])
 @pytest.mark.parametrize("form", FORMS)
-@pytest.mark.parametrize("chunk", [1, 3, 8])
-def test_chunk_length_invariant(monkeypatch, chunk, form):
+@pytest.mark.parametrize("chunk", [1, 3, 8, 32])
+def test_chunk_length_invariant(monkeypatch, chunk, form, stage):
     """How the steps split into rules-trajectory launches changes no result
-    (episodes that end on a chunk's last step reset in the next launch)."""
+    (episodes that end on a chunk's last step reset in the next launch), nor
+    whether the outputs are staged by lane (COUP_MANY_STAGE)."""
     B, seed = 70001, 3
-    many, ref = _env(monkeypatch, B, form, seed, chunk=chunk), _env(monkeypatch, B, False, seed)
+    many = _env(monkeypatch, B, form, seed, chunk=chunk, stage=stage)
+    ref = _env(monkeypatch, B, False, seed)
     many.step_many(23)
     for _ in range(23):
         ref.step()
@@ -112,14 +120,15 @@ def test_graph_capture_and_packed_word(monkeypatch, form, chunk):
     _same(_state(many), _state(ref), "graph")
 
 
+@pytest.mark.parametrize("stage", [None, "1"])
 @pytest.mark.parametrize("form", FORMS)
 @pytest.mark.parametrize("B,T", [(1000, 12), (1 << 20, 10), (1 << 20, 21)])
-def test_trajectory_slices_every_step(monkeypatch, B, T, form):
+def test_trajectory_slices_every_step(monkeypatch, B, T, form, stage):
     """coup_step_trajectory with observations through the rules-trajectory
     forms: every step's outputs in its slice, equal to one coup_step per
-    slice."""
+    slice (outputs stored from the playing threads, or staged by lane)."""
     seed = 17
-    many, ref = _env(monkeypatch, B, form, seed), _env(monkeypatch, B, False, seed)
+    many, ref = _env(monkeypatch, B, form, seed, stage=stage), _env(monkeypatch, B, False, seed)
     for env in (many, ref):
         env.rollout(30)
     bp = many.collect_trajectory(T)
