@@ -47,7 +47,6 @@ struct Knobs {
   int pipe = kManyTraj;  // COUP_PIPE: coup_step_many's form of the split step (kMany*)
   int traj_chunk = kTrajChunkDefault;  // COUP_TRAJ_CHUNK 1..kTrajChunkMax: steps per rules-trajectory launch
                                        // (the record buffer is sized by its value at coup_create)
-  int many_stage = 0;  // COUP_MANY_STAGE: the rules trajectory's outputs staged by lane (coalesced stores)
   // -- measurement builds (-DCOUP_AB_VARIANTS); the product ignores them
   int obs_mode = 9;       // COUP_OBS_MODE 1..9: the fused step's observation writer
   int xcd_remap = 1;      // COUP_XCD_REMAP: XCD-aware block -> lane-group mapping of the fused step
@@ -62,6 +61,7 @@ struct Knobs {
   int np_scan = 1;          // COUP_NP_SCAN
   double pipe_span = kPipeSpanDefault;  // COUP_PIPE_SPAN in (0, 1] (kManyPipe)
   int overlap_cus = 0;  // COUP_OVERLAP_CUS: kManyOverlap's rules on this many CUs (CU-masked streams), 0 unmasked
+  int many_stage = 0;   // COUP_MANY_STAGE: the rules trajectory's outputs staged by lane (coalesced stores)
   int fused_shape = 0;  // COUP_FUSED_SHAPE: kManyFused's block / register budget (0: 1024 lanes, 4 waves per SIMD)
 };
 
@@ -80,7 +80,6 @@ inline Knobs read_knobs() {
     k.pipe = kManyTraj;
   k.traj_chunk = knob_int("COUP_TRAJ_CHUNK", kTrajChunkDefault);
   if (k.traj_chunk < 1 || k.traj_chunk > kTrajChunkMax) k.traj_chunk = kTrajChunkDefault;
-  k.many_stage = knob_int("COUP_MANY_STAGE", 0) != 0;
 #ifdef COUP_AB_VARIANTS
   if (const char* f = std::getenv("COUP_PIPE_SPAN")) {
     const double v = std::atof(f);
@@ -101,6 +100,7 @@ inline Knobs read_knobs() {
   k.np_scan = knob_int("COUP_NP_SCAN", 1) != 0;
   k.overlap_cus = knob_int("COUP_OVERLAP_CUS", 0);
   k.fused_shape = knob_int("COUP_FUSED_SHAPE", 0);
+  k.many_stage = knob_int("COUP_MANY_STAGE", 0) != 0;
 #else
   // the merged launch, the two-stream overlap and the fused trajectory ship
   // in measurement builds only

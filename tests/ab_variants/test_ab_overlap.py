@@ -78,3 +78,13 @@ def test_fused_trajectory_default_shape(monkeypatch, B, T):
     M.test_step_many_equals_stepping(monkeypatch, 3, "4")
     M.test_graph_capture_and_packed_word(monkeypatch, "4", 8)
     M.test_trajectory_slices_every_step(monkeypatch, B, T, "4", None)
+
+
+@pytest.mark.parametrize("chunk", [1, 8, 32])
+def test_staged_rules_trajectory(monkeypatch, chunk):
+    """The rules trajectory with its outputs staged by lane in LDS
+    (COUP_MANY_STAGE; measured slower): stepping at every chunk length, and
+    trajectory slices at the bench size."""
+    M.test_chunk_length_invariant(monkeypatch, chunk, "1", "1")
+    if chunk == 8:
+        M.test_trajectory_slices_every_step(monkeypatch, 1 << 20, 21, "1", "1")

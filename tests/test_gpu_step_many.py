@@ -77,7 +77,7 @@ def test_step_many_equals_stepping(monkeypatch, B, form):
     assert many.error_count() == ref.error_count() == 0
 
 
-@pytest.mark.parametrize("stage", [None, "1"])
+@pytest.mark.parametrize("stage", [None])  # "1" (COUP_MANY_STAGE): tests/ab_variants/test_ab_overlap.py
 @pytest.mark.parametrize("form", FORMS)
 @pytest.mark.parametrize("chunk", [1, 3, 8, 32])
 def test_chunk_length_invariant(monkeypatch, chunk, form, stage):
@@ -120,7 +120,7 @@ def test_graph_capture_and_packed_word(monkeypatch, form, chunk):
     _same(_state(many), _state(ref), "graph")
 
 
-@pytest.mark.parametrize("stage", [None, "1"])
+@pytest.mark.parametrize("stage", [None])  # "1" (COUP_MANY_STAGE): tests/ab_variants/test_ab_overlap.py
 @pytest.mark.parametrize("form", FORMS)
 @pytest.mark.parametrize("B,T", [(1000, 12), (1 << 20, 10), (1 << 20, 21)])
 def test_trajectory_slices_every_step(monkeypatch, B, T, form, stage):
