@@ -23,11 +23,19 @@
 // 4. k_sweep_rows<T, S>: the shipped form (one observer row per thread,
 //    32-bit stores).
 // Prints one JSON line per kernel: lanes whose tensor differs from k_ref.
+//
+//   build/info_prefix_repro [lanes] [module.co ...]
+//
+// With code objects (tools/info_modules.sh: this file's device IR through
+// llc at chosen settings), each module's k_sweep_uint2<512, 2> and
+// k_sweep_rows<512, 2> are loaded (hipModuleLoad) and checked against k_ref
+// the same way, one JSON line per module and kernel.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "coup_lane.h"
@@ -227,6 +235,27 @@ int main(int argc, char** argv) {
     CHECK(hipDeviceSynchronize());
     compare(name);
   };
+  if (argc > 2) {  // code objects: the modules' kernels instead of this binary's
+    for (int m = 2; m < argc; ++m) {
+      hipModule_t mod;
+      CHECK(hipModuleLoad(&mod, argv[m]));
+      const char* names[2] = {"_Z13k_sweep_uint2ILi512ELi2EEvPK15HIP_vector_typeIjLj4EEPKhPfl",
+                              "_Z12k_sweep_rowsILi512ELi2EEvPK15HIP_vector_typeIjLj4EEPKhPfl"};
+      for (const char* kn : names) {
+        hipFunction_t fn;
+        if (hipModuleGetFunction(&fn, mod, kn) != hipSuccess) continue;
+        CHECK(hipMemset(out, 0xFF, fl * sizeof(float)));
+        int64_t n64 = n;
+        void* args[] = {&recs, &hist, &out, &n64};
+        CHECK(hipModuleLaunchKernel(fn, (unsigned)((nf4 + 1023) / 1024), 1, 1, 512, 1, 1, 0, nullptr, args, nullptr));
+        CHECK(hipDeviceSynchronize());
+        std::string label = std::string(argv[m]) + " " + (kn[3] == '1' && kn[4] == '3' ? "uint2" : "rows");
+        compare(label.c_str());
+      }
+      CHECK(hipModuleUnload(mod));
+    }
+    return 0;
+  }
   run(k_sweep_rows<1024, 2>, 1024, 2, "k_sweep_rows<1024, 2> (shipped form)");
   run(k_sweep_rows<512, 2>, 512, 2, "k_sweep_rows<512, 2>");
   run(k_sweep_uint2<512, 2>, 512, 2, "k_sweep_uint2<512, 2> (round 4's first form)");
