@@ -7,7 +7,8 @@
 # globaldce), then llc at -O0 and -O3, -O3 through GlobalISel, and -O3 with
 # -opt-bisect-limit at every limit over llc's optional passes (the machine
 # passes an opt-bisect may skip) -- which names the pass if one of them
-# brings the defect.  Outputs under build/infomod/ (the .co files travel).
+# brings the defect -- and -O3 / -O0 with an s_nop before every instruction
+# or every s_waitcnt forced to zero.  Outputs under build/infomod/ (the .co files travel).
 set -euo pipefail
 R=$(cd "$(dirname "$0")/.." && pwd)
 B=/opt/rocm/llvm/bin
@@ -31,6 +32,12 @@ co() {  # co <name> <llc flags...>
 co O0 -O0
 co O3 -O3
 co O3gisel -O3 -global-isel
+# the hazard / wait hypotheses: an s_nop before every instruction (covers any
+# missing wait states of the hazard recognizer), and every s_waitcnt forced
+# to zero (covers a missing memory-counter wait)
+co O3snop4 -O3 -amdgpu-snop-padding=4
+co O3waitzero -O3 -amdgpu-waitcnt-forcezero
+co O0snop4 -O0 -amdgpu-snop-padding=4
 # the optional passes of an -O3 llc run, in order (opt-bisect's numbering)
 $B/llc $T -O3 -opt-bisect-limit=-1 -filetype=null "$O/sweep.ll" 2> "$O/passes.txt" || true
 N=$(grep -c "BISECT: running pass" "$O/passes.txt" || true)
