@@ -38,6 +38,8 @@ co O3gisel -O3 -global-isel
 co O3snop4 -O3 -amdgpu-snop-padding=4
 co O3waitzero -O3 -amdgpu-waitcnt-forcezero
 co O0snop4 -O0 -amdgpu-snop-padding=4
+co O3snop15 -O3 -amdgpu-snop-padding=15
+co O3snop15waitzero -O3 -amdgpu-snop-padding=15 -amdgpu-waitcnt-forcezero
 # the optional passes of an -O3 llc run, in order (opt-bisect's numbering)
 $B/llc $T -O3 -opt-bisect-limit=-1 -filetype=null "$O/sweep.ll" 2> "$O/passes.txt" || true
 N=$(grep -c "BISECT: running pass" "$O/passes.txt" || true)

@@ -249,7 +249,7 @@ int main(int argc, char** argv) {
         void* args[] = {&recs, &hist, &out, &n64};
         CHECK(hipModuleLaunchKernel(fn, (unsigned)((nf4 + 1023) / 1024), 1, 1, 512, 1, 1, 0, nullptr, args, nullptr));
         CHECK(hipDeviceSynchronize());
-        std::string label = std::string(argv[m]) + " " + (kn[3] == '1' && kn[4] == '3' ? "uint2" : "rows");
+        std::string label = std::string(argv[m]) + " " + (std::strstr(kn, "uint2") ? "uint2" : "rows");
         compare(label.c_str());
       }
       CHECK(hipModuleUnload(mod));
