@@ -75,7 +75,18 @@ sys.path.insert(0, ROOT)
 # step kernels (9 us, 60 us) are shorter than the host's per-step launch
 # cost, and c3, where the graph removes the ~6 us gap per step that eager
 # launches leave between kernels
-GRAPH_AUTO = ("c2", "c3")  # c4: K eager launches measured 38.1 vs 39.2 us per step (profiles/r02/ab/graph_vs_eager.log)
+# configs whose K timed steps are one HIP graph of coup_step_many (c4 since
+# round 5: coup_step_many runs tensor-free steps as one trajectory launch)
+GRAPH_AUTO = ("c2", "c3", "c4")
+
+
+def bare_many_active(with_obs, with_info, fused, graph):
+    """Whether the timed steps are coup_step_many's tensor-free form: ONE
+    trajectory launch for the K steps (every step's outputs over the [B]
+    buffers; mirrors coup_kernels.hip `many_bare`, COUP_PIPE=0 turns it
+    off)."""
+    return (graph and not fused and not with_obs and not with_info and
+            os.environ.get("COUP_PIPE", "1").strip() != "0")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
 
@@ -747,33 +758,36 @@ def main():
         elif with_info and info_split_active(B):
             ceiling_ms = _time_sweep_ceiling(env.info_state, B * 1246, 1024, 2, args.steps, stream)
             ceiling_form = "sweep: [B][2][2492] fp32 stores in address order, 1024 x 2 grid, no decode, tensor-like data"
-        elif not with_info:
+        elif not with_info and not bare_many_active(with_obs, with_info, fused, graph is not None):
             ceiling_ms = _time_traffic_ceiling(env, args.steps, stream)
             ceiling_form = "fused: the fused step's loads and stores, no rules"
 
     if rank == 0:
-        bytes_per_launch = bytes_per_lane * B * (args.steps if fused else 1)
-        launch_ms = kern_ms * (args.steps if fused else 1)
+        bare = bare_many_active(with_obs, with_info, fused, graph is not None)
+        per_launch = args.steps if (fused or bare) else 1  # env steps per launch of the timed kernel
+        bytes_per_launch = bytes_per_lane * B * per_launch
+        launch_ms = kern_ms * per_launch
         achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
         traffic = None
         if os.path.exists(TRAFFIC_FILE):
             with open(TRAFFIC_FILE) as f:
                 tr = json.load(f)
             ent = tr.get(cfg)
-            if ent and ent.get("batch") == B:
+            # the profile of the same form: batch and env steps per launch
+            if ent and ent.get("batch") == B and ent.get("steps_per_launch", 1) == per_launch:
                 traffic = ent.get("hbm_bytes_per_launch")
         sorted_ = "_sorted" if _regrouped(B) else ""
         if players != 2:
             ahead = os.environ.get("COUP_AHEAD", "1") != "0"
             kernel = (("coup::np::k_trajectory_sorted<%d, 1024>" if sorted_ else "coup::np::k_step_trajectory<%d>") % players
-                      if fused == "traj" else
+                      if fused == "traj" or bare else
                       ("coup::np::k_rollout_sorted<%d, 1024>" % players if sorted_ else
                        "coup::np::k_rollout<%d>" % players) if fused else
                       "coup::np::k_step_sorted<%d, true, %s, %d>" % (players, "true" if ahead else "false",
                                                                     _np_step_lanes(players)) if sorted_ else
                       "coup::np::k_step<%d, true>" % players)
-        elif fused == "traj":
-            kernel = "coup::k_trajectory_sorted" if sorted_ else "coup::k_step_trajectory"
+        elif fused == "traj" or bare:
+            kernel = "coup::k_trajectory_sorted<1024, false, false, 8, false>" if sorted_ else "coup::k_step_trajectory"
         elif fused:
             kernel = "coup::k_rollout" + sorted_
         elif with_info:
@@ -822,7 +836,7 @@ def main():
             "dtype": "int32",
             "data": "synthetic (uniform-random self-play games)",
             "config": {"workload": workload, "batch_per_gpu": B, "global_batch": world * B, "players": players,
-                       "outputs": outputs, "auto_reset": True, "fused_steps_per_launch": args.steps if fused else 1,
+                       "outputs": outputs, "auto_reset": True, "fused_steps_per_launch": per_launch,
                        "hip_graph": graph is not None,
                        "gate_steps": 0 if graph is not None else gate.steps,
                        "parallelism": f"dp{world} (env-id sharding)" + ("" if args.dist_backend == "nccl" else
@@ -833,7 +847,8 @@ def main():
                          "store_ceiling_ms": ceiling_ms,
                          "frac_of_store_ceiling": (ceiling_ms / launch_ms) if ceiling_ms else None,
                          "store_ceiling_form": ceiling_form,
-                         "step_form": ((with_obs and step_many_form(B, players, graph is not None))
+                         "step_form": ("trajectory (coup_step_many)" if bare else
+                                       (with_obs and step_many_form(B, players, graph is not None))
                                        or "split" if (with_obs and players == 2 and obs_split_active(B)) or
                                        (with_info and info_split_active(B)) else "fused")},
             "episodes": {"finished": ep_total, "mean_return_p0": ret_total / max(ep_total, 1),

@@ -1130,11 +1130,12 @@ __global__ __launch_bounds__(kThreads) void k_rollout(RolloutArgs a) {
 
 // coup_step_trajectory: `steps` uniform-policy env steps per lane in ONE
 // launch, the state held in registers, step t's outputs stored to slice t
-// of the caller's [steps][B] buffers.  The step is k_step's own step_lane
+// of the caller's [steps][B] buffers (stride B; coup_step_many: stride 0,
+// every step overwriting the [B] outputs).  The step is k_step's own step_lane
 // (effect form, no history), so the outputs, records and accumulators equal
 // those of `steps` coup_step launches; what goes is the per-step record
 // round trip and launch.
-__global__ __launch_bounds__(kThreads) void k_step_trajectory(StepArgs a, int64_t steps) {
+__global__ __launch_bounds__(kThreads) void k_step_trajectory(StepArgs a, int64_t steps, int64_t stride) {
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= a.n) return;
   Lane L = unpack(a.state[i]);
@@ -1145,7 +1146,7 @@ __global__ __launch_bounds__(kThreads) void k_step_trajectory(StepArgs a, int64_
     uint32_t st;
     int32_t rew, ret = 0;
     step_lane<true, false, false>(a, i, L, act, st, rew, ret, none);
-    const int64_t o = t * a.n + i;
+    const int64_t o = t * stride + i;
     if (a.actions) a.actions[o] = (int8_t)act;
     if (a.rewards) {
       a.rewards[2 * o] = (int8_t)rew;
@@ -3633,6 +3634,41 @@ int step_many_pipelined(coup_env* env, int64_t steps, const coup_step_outputs* o
 
 extern "C" {
 
+namespace {
+// coup_step_many without tensors (no observations, information state or
+// history): the `steps` steps as ONE trajectory launch -- the records in
+// registers, every step's outputs stored over the [B] buffers (stride 0),
+// so they end as the last step's -- the kernels of coup_step_trajectory
+// (2 players: k_step_trajectory in place, k_trajectory_sorted from 2^18
+// lanes; N players: np::k_step_trajectory / np::k_trajectory_sorted).
+// Results equal `steps` coup_step calls.  COUP_PIPE=0 keeps one coup_step
+// per step.
+bool many_bare(const coup_env* env, const coup_step_outputs* out) {
+  return env->knobs.pipe != coup::kManySerial && !env->hist && !(out && (out->obs || out->info_state));
+}
+
+int step_many_bare(coup_env* env, int64_t steps, const coup_step_outputs* out) {
+  if (env->generic) return np_result(coup::np::launch_trajectory(np_env(env), steps, out, false), "coup_step_many");
+  const int64_t n = env->batch;
+  coup::StepArgs a = uniform_args(env, out);
+  if (out) {
+    a.actions = out->actions;
+    a.rewards = out->rewards;
+    a.step_type = out->step_type;
+    a.legal = out->legal_mask;
+    a.cur_player = out->cur_player;
+  }
+  if (coup::regroup_lanes(env->knobs, n)) {
+    constexpr int TB = coup::kRolloutSortLanes;
+    coup::k_trajectory_sorted<TB><<<(unsigned)((n + TB - 1) / TB), TB, 0, env->stream>>>(a, steps, {nullptr, 0});
+  } else {
+    coup::k_step_trajectory<<<grid_for(n), coup::kThreads, 0, env->stream>>>(a, steps, 0);
+  }
+  COUP_HIP_TRY(hipGetLastError());
+  return COUP_OK;
+}
+}  // namespace
+
 int coup_step_many(coup_env* env, int64_t steps, const coup_step_outputs* out) {
   COUP_CHECK_ENV(env);
   if (steps < 0) return fail(COUP_E_INVALID, "coup_step_many: negative steps");
@@ -3643,6 +3679,10 @@ int coup_step_many(coup_env* env, int64_t steps, const coup_step_outputs* out) {
     if (const char* why = coup::ep_acc_of(out, ep)) return fail(COUP_E_INVALID, std::string("coup_step_many: ") + why);
   }
   if (env->batch == 0 || steps == 0) return COUP_OK;
+  if (many_bare(env, out)) {
+    COUP_TRY(launching(env));
+    return step_many_bare(env, steps, out);
+  }
   switch (many_form(env, out)) {
     case coup::kManyTraj: COUP_TRY(launching(env)); return step_many_traj(env, steps, out, false, false);
 #ifdef COUP_AB_VARIANTS
@@ -3735,7 +3775,7 @@ int coup_step_trajectory(coup_env* env, int64_t steps, const coup_step_outputs* 
     coup::k_trajectory_sorted<TB><<<(unsigned)((n + TB - 1) / TB), TB, 0, env->stream>>>(a, steps, {nullptr, n});
 #endif
   } else {
-    coup::k_step_trajectory<<<grid_for(n), coup::kThreads, 0, env->stream>>>(a, steps);
+    coup::k_step_trajectory<<<grid_for(n), coup::kThreads, 0, env->stream>>>(a, steps, n);
   }
   COUP_HIP_TRY(hipGetLastError());
   return COUP_OK;

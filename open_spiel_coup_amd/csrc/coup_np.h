@@ -30,7 +30,9 @@ struct Env {
 hipError_t launch_reset(const Env& e, const uint8_t* mask, int mode, int deal);
 hipError_t launch_step(const Env& e, const int8_t* actions, const coup_step_outputs* out);
 hipError_t launch_rollout(const Env& e, int64_t steps, const coup_rollout_stats* stats);
-hipError_t launch_trajectory(const Env& e, int64_t steps, const coup_step_outputs* out);
+// slices: step t's outputs to slice t of [steps][B] buffers; else every step
+// overwrites the [B] outputs (coup_step_many)
+hipError_t launch_trajectory(const Env& e, int64_t steps, const coup_step_outputs* out, bool slices = true);
 hipError_t launch_apply(const Env& e, const int8_t* actions);
 hipError_t launch_query(const Env& e, const coup_query_outputs* out);
 // [B][8] u32 records <-> the two planes

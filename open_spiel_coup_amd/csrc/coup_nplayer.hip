@@ -62,6 +62,7 @@ struct StepArgs {
   int8_t* cur_player;
   EpAcc ep;            // per-episode accumulators (coup_step_outputs.episodes / return_sum or episode_word)
   uint32_t* err_count;
+  int64_t ostride;     // trajectories: output offset per step (B: [steps][B] slices; 0: every step overwrites)
 #ifdef COUP_WAVE_TRACE
   // measurement builds only (tools/np_wave_trace.py): per wave of
   // k_step_sorted, 10 s_memrealtime (100 MHz) stamps at the phase edges
@@ -455,7 +456,7 @@ __global__ __launch_bounds__(kThreads) void k_step_trajectory(StepArgs a, int64_
     bool error;
     step_lane<N, true>(L, rng, 0u, a.auto_reset != 0, act, st, rl, rc, ret0, error);
     errs += error ? 1u : 0u;
-    store_step_outputs<N>(a, t * a.n + i, act, st, rl, rc, legal_mask(L), current_player(L));
+    store_step_outputs<N>(a, t * a.ostride + i, act, st, rl, rc, legal_mask(L), current_player(L));
     if (st == 2u) {
       eps += 1;
       ret_sum += ret0;
@@ -720,7 +721,7 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
   for (int64_t s = 0; s < steps; ++s) {
     uint32_t* bin = s_bin[s & 1];
     __syncthreads();  // this step's bins are zero; last step's slots and outputs are complete
-    if (STAGE == 1 && s > 0 && t < nvalid) store_staged<N>(a, (s - 1) * a.n + base + t, s_out[t], s_olegal[t]);
+    if (STAGE == 1 && s > 0 && t < nvalid) store_staged<N>(a, (s - 1) * a.ostride + base + t, s_out[t], s_olegal[t]);
     const uint32_t rank = atomicAdd(&bin[key], 1u);
     __syncthreads();
     // (wave_bins_below here spills 38 VGPRs instead of 22 and measured 26.07
@@ -739,7 +740,7 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
     L = unpack<N>(s_a[t], s_b[t]);
     const int64_t li = base + lane;
     if (li >= a.n) continue;  // past the batch
-    const int64_t o = s * a.n + li;
+    const int64_t o = s * a.ostride + li;
     rng.env_id = lane_stream_id(a.env_id_base, li);
     rng.blk_tag = 0u;
     // every output of step s goes through out(): staged by lane (STAGE > 0)
@@ -766,7 +767,7 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
       // head is already stored (above), so these two go out directly
       L = new_episode<N>(L.episode + 1u, rng);
       const uint32_t legal = decision_mask(L);
-      store_legal_player(a, o - a.n, legal, (int)L.M);
+      store_legal_player(a, o - a.ostride, legal, (int)L.M);
       key = ahead_key(L, sample_action(legal, rng.draw(L.episode, L.move)));
     }
     if (key == kKeyDead) {  // no legal decision: coup_step's rejected step
@@ -799,10 +800,11 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
     if (s + 1 < steps) key = ahead_key(L, sample_action(legal, rng.draw(L.episode, L.move)));
   }
   __syncthreads();  // the last step's staged outputs are complete
-  if (STAGE == 1 && steps > 0 && t < nvalid) store_staged<N>(a, (steps - 1) * a.n + base + t, s_out[t], s_olegal[t]);
+  if (STAGE == 1 && steps > 0 && t < nvalid)
+    store_staged<N>(a, (steps - 1) * a.ostride + base + t, s_out[t], s_olegal[t]);
   if (steps > 0 && key == kKeyReset && base + lane < a.n) {  // finished on the last step
     L = new_episode<N>(L.episode + 1u, rng);
-    store_legal_player(a, (steps - 1) * a.n + base + lane, decision_mask(L), (int)L.M);
+    store_legal_player(a, (steps - 1) * a.ostride + base + lane, decision_mask(L), (int)L.M);
   }
   __syncthreads();
   uint4 wa, wb;
@@ -1081,8 +1083,9 @@ hipError_t launch_step(const Env& e, const int8_t* actions, const coup_step_outp
   });
 }
 
-hipError_t launch_trajectory(const Env& e, int64_t steps, const coup_step_outputs* out) {
+hipError_t launch_trajectory(const Env& e, int64_t steps, const coup_step_outputs* out, bool slices) {
   StepArgs a{};
+  a.ostride = slices ? e.n : 0;
   a.sa = e.sa;
   a.sb = e.sb;
   a.n = e.n;

@@ -159,3 +159,46 @@ def test_default_form_by_batch(monkeypatch):
         b.step()
     assert torch.equal(a.obs, b.obs) and torch.equal(a.export_state(), b.export_state())
 
+
+
+def _bare_state(env):
+    out = {k: v.cpu().numpy().copy() for k, v in
+           (("actions", env.actions), ("rewards", env.rewards), ("step_type", env.step_type),
+            ("legal_mask", env.legal_mask), ("current_player", env.cur_player))}
+    eps, ret = env.episode_stats()
+    return out, env.export_state().cpu().numpy(), eps.cpu().numpy(), ret.cpu().numpy()
+
+
+@pytest.mark.parametrize("players", [2, 3, 6])
+@pytest.mark.parametrize("B", [1000, (1 << 18) + 5])
+def test_bare_step_many_equals_stepping(monkeypatch, players, B):
+    """coup_step_many without tensors: ONE trajectory launch (in place below
+    2^18 lanes, regrouped from it; 2 and N players) whose every step's
+    outputs overwrite the [B] buffers -- equal to coup_step launched once
+    per step (COUP_PIPE=0): the last step's outputs, the records, the
+    accumulators and the error count, eager and captured in a graph."""
+    seed = 5 + players
+    monkeypatch.delenv("COUP_OBS_SPLIT", raising=False)
+    monkeypatch.delenv("COUP_REGROUP", raising=False)
+    kw = dict(seed=seed, auto_reset=True, obs=False, num_players=players, episode_stats=True)
+    monkeypatch.setenv("COUP_PIPE", "1")
+    many = BatchedCoupEnv(B, **kw)
+    monkeypatch.setenv("COUP_PIPE", "0")
+    ref = BatchedCoupEnv(B, **kw)
+    for K in (1, 7, 20):
+        many.step_many(K)
+        for _ in range(K):
+            ref.step()
+        a, b = _bare_state(many), _bare_state(ref)
+        for k in a[0]:
+            np.testing.assert_array_equal(a[0][k], b[0][k], err_msg=f"{players}p B {B} K {K}: {k}")
+        for x, y, what in zip(a[1:], b[1:], ("records", "episodes", "return sums")):
+            np.testing.assert_array_equal(x, y, err_msg=f"{players}p B {B} K {K}: {what}")
+    g = many.capture_steps(9)
+    g.replay()
+    torch.cuda.synchronize()
+    for _ in range(9):
+        ref.step()
+    np.testing.assert_array_equal(many.export_state().cpu().numpy(), ref.export_state().cpu().numpy())
+    assert torch.equal(many.legal_mask, ref.legal_mask) and torch.equal(many.actions, ref.actions)
+    assert many.error_count() == ref.error_count() == 0

@@ -59,8 +59,13 @@ def main():
     from bench import info_split_active, obs_split_active, step_many_form, traj_chunk
     split = obs_split_active(batch)
     isplit = info_split_active(batch)
-    many = (step_many_form(batch, players, "--graph" not in args or "off" not in args)
+    graph_on = "--graph" not in args or "off" not in args
+    many = (step_many_form(batch, players, graph_on)
             if want_obs and not want_info and not fused and players == 2 else None)
+    from bench import GRAPH_AUTO, bare_many_active
+    # coup_step_many's tensor-free form: ONE trajectory launch per K steps,
+    # profiled like the fused trajectory configs (the timed launch is the last)
+    bare = bool(bare_many_active(want_obs, want_info, fused, graph_on and cfg in GRAPH_AUTO))
     # coup_step_many recorded in the bench's graph.  The merged pipelined
     # step: K + 1 dispatches of ONE kernel per K steps -- the rules of step 1
     # alone, K - 1 launches of rules(t + 1) beside writer(t), the writer of
@@ -77,7 +82,7 @@ def main():
 
     def timed_kernel(kn):
         """Is `kn` the kernel bench.py times for this config?"""
-        if fused == "traj":
+        if fused == "traj" or bare:
             if players != 2:
                 return bool(re.search(r"np::k_(step_trajectory|trajectory_sorted)<%d(, \w+)*>|"
                                       r"2np(17k_step_trajectory|19k_trajectory_sorted)ILi%dE" % (players, players), kn))
@@ -166,7 +171,7 @@ def main():
                         "frac_of_store_ceiling": bench["roofline"].get("frac_of_store_ceiling"),
                         "box": bench.get("box")}
                     tk = summary.get("timed_kernel")
-                    if fused:
+                    if fused or bare:
                         # a fused config launches the same kernel for the settle,
                         # warm-up and timed rollouts (different step counts): compare
                         # the timed launch, the last dispatch in the kernel trace
@@ -265,7 +270,7 @@ def main():
             vals.setdefault(kn, []).append((int(r[col(r, "dispatch")]), float(r[col(r, "counter", "value")])))
         if not vals:
             return None
-        if fused:  # the timed launch only (see above)
+        if fused or bare:  # the timed launch only (see above)
             return sum(max(v)[1] for v in vals.values())
         # per env step: the timed steps' dispatches (the last K per kernel, or
         # the pipeline's last K + 1), summed, / K
@@ -306,7 +311,8 @@ def main():
     if os.path.exists(path):
         with open(path) as f:
             table = json.load(f)
-    table[cfg] = {"batch": batch, "hbm_bytes_per_launch": traffic, "source": f"profiles/{tag}/{cfg}/summary.json"}
+    table[cfg] = {"batch": batch, "hbm_bytes_per_launch": traffic, "source": f"profiles/{tag}/{cfg}/summary.json",
+                  "steps_per_launch": steps if (fused or bare) else 1}
     with open(path, "w") as f:
         json.dump(table, f, indent=1, sort_keys=True)
     print(json.dumps(summary, indent=1))
