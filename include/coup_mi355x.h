@@ -195,9 +195,11 @@ int coup_create_ex(int64_t batch, uint64_t seed, uint32_t env_id_base, int flags
 int coup_destroy(coup_env* env);
 /* Re-read the env's dispatch knobs from the environment variables
  * coup_create reads them from (COUP_OBS_SPLIT, COUP_INFO_SPLIT,
- * COUP_REGROUP, COUP_PIPE, COUP_PIPE_SPAN; in a measurement build also the
+ * COUP_REGROUP, COUP_PIPE, COUP_TRAJ_CHUNK; in a measurement build also the
  * A/B variant knobs): for tests and A/B runs that switch one existing env
- * between forms.  Launches never read the environment themselves. */
+ * between forms.  Launches never read the environment themselves.  (The
+ * rules-trajectory record buffer keeps the size coup_create gave it: a larger
+ * COUP_TRAJ_CHUNK is capped to it.) */
 int coup_reload_knobs(coup_env* env);
 /* Use this HIP stream (hipStream_t, may be NULL = default) for later calls. */
 int coup_set_stream(coup_env* env, void* hip_stream);
@@ -258,23 +260,27 @@ size_t coup_step_host_layout(int64_t batch, int num_players, int want, size_t* o
  * the trajectory a learner collects (rl_environment.py:282-322 per step).
  * Without tensors: ONE launch, the state kept in registers (the env must not
  * keep histories, COUP_E_INVALID), lanes regrouped by decision every step
- * from 2^18 lanes.  With obs: the pipelined split step
- * of coup_step_many where it applies (from 2^20 lanes), else one coup_step
- * per slice; info_state needs COUP_FLAG_HISTORY and takes coup_step per
- * slice. */
+ * from 2^18 lanes.  With obs: coup_step_many's
+ * rules-trajectory split step where it applies (from 2^20 lanes), else one
+ * coup_step per slice; info_state needs COUP_FLAG_HISTORY and takes
+ * coup_step per slice. */
 int coup_step_trajectory(coup_env* env, int64_t steps, const coup_step_outputs* out);
 
 /* `steps` calls of coup_step(env, NULL, out) -- uniform-random policy, every
  * step writing the same output buffers -- as one call, with the same results
- * (outputs of the last step, records, accumulators).  For the split
- * observation step (2-player lanes with obs and no history, from 2^20 lanes:
- * coup_obs_split_variant) the steps are pipelined: launch m runs the rules of
- * step m beside the observation writer of step m - 1 (k_step_obs_pipe; the
- * records alternate between two buffers), so the ~30 us rules kernel no
- * longer sits between two writers.  Every other env
- * loops over coup_step.  COUP_PIPE=0 at coup_create turns the pipeline off
- * (A/B).  May be captured into a HIP graph (no allocation, no
- * synchronisation). */
+ * (outputs of the last step, records, accumulators, error count), every
+ * step's outputs stored (over the same buffers).  Forms (DESIGN.md
+ * section 5):
+ * - without tensors or history (2 and N players): ONE trajectory launch for
+ *   the steps (coup_step_trajectory's kernels, output stride 0);
+ * - the split observation step (2-player lanes with obs and no history, from
+ *   2^20 lanes: coup_obs_split_variant): chunks of up to COUP_TRAJ_CHUNK
+ *   (default 8) steps as one regrouped rules-trajectory launch that stores
+ *   every step's records to a per-env buffer, then the address-order writer
+ *   once per step from them;
+ * - otherwise one coup_step per step.
+ * COUP_PIPE=0 at coup_create keeps one coup_step per step (A/B).  May be
+ * captured into a HIP graph (no allocation, no synchronisation). */
 int coup_step_many(coup_env* env, int64_t steps, const coup_step_outputs* out);
 
 /* `steps` uniform-random env steps per lane in one launch, state kept in
