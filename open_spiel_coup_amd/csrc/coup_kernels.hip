@@ -3544,8 +3544,20 @@ int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, b
     const coup::TrajOut x{rec, slices ? n : 0, 0};
     const unsigned grid = (unsigned)((n + TB - 1) / TB);
 #ifdef COUP_AB_VARIANTS
+    auto shape = [&](auto tt, auto ww) {  // COUP_MANY_SHAPE: lanes per block, waves per SIMD budget
+      constexpr int T = decltype(tt)::value, W = decltype(ww)::value;
+      coup::k_trajectory_sorted<T, true, false, W, false><<<(unsigned)((n + T - 1) / T), T, 0, R>>>(a, c, x);
+    };
     if (env->knobs.many_stage)  // outputs staged by lane: 148.3 against 134.5 us per step (call r05m)
       coup::k_trajectory_sorted<TB, true, false, 8, true><<<grid, TB, 0, R>>>(a, c, x);
+    else if (env->knobs.many_shape == 1)
+      shape(std::integral_constant<int, 512>(), std::integral_constant<int, 8>());
+    else if (env->knobs.many_shape == 2)
+      shape(std::integral_constant<int, 512>(), std::integral_constant<int, 6>());
+    else if (env->knobs.many_shape == 3)
+      shape(std::integral_constant<int, 256>(), std::integral_constant<int, 8>());
+    else if (env->knobs.many_shape == 4)
+      shape(std::integral_constant<int, 1024>(), std::integral_constant<int, 4>());
     else
 #endif
       coup::k_trajectory_sorted<TB, true, false, 8, false><<<grid, TB, 0, R>>>(a, c, x);

@@ -88,3 +88,11 @@ def test_staged_rules_trajectory(monkeypatch, chunk):
     M.test_chunk_length_invariant(monkeypatch, chunk, "1", "1")
     if chunk == 8:
         M.test_trajectory_slices_every_step(monkeypatch, 1 << 20, 21, "1", "1")
+
+
+@pytest.mark.parametrize("shape", ["1", "2", "3", "4"])
+def test_rules_trajectory_shapes(monkeypatch, shape):
+    """The rules trajectory's block / register-budget variants
+    (COUP_MANY_SHAPE) equal stepping."""
+    monkeypatch.setenv("COUP_MANY_SHAPE", shape)
+    M.test_chunk_length_invariant(monkeypatch, 8, "1", None)
