@@ -260,6 +260,9 @@ def parse():
                          "leaves its idle power state only under sustained load (tools/dpm_probe.py: the "
                          "c3 graph 151 us per step after idle gaps, 135.7 under sustained load; DESIGN.md "
                          "section 5); 0 turns it off")
+    ap.add_argument("--gate-steps", type=int, default=-1,
+                    help="untimed rollout steps enqueued right before the timed region (the gate; -1: "
+                         "calibrated to the host's launch latency, 0: none -- tests comparing games across runs)")
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--seed", type=int, default=1)
@@ -445,17 +448,18 @@ def _time_sweep_ceiling(buf, nf4, threads, passes, steps, stream):
     return a.elapsed_time(b) / steps
 
 
-def _calibrate_gate(env, stream):
+def _calibrate_gate(env, stream, launch=None):
     """Steps of an untimed rollout (the gate) that keep the GPU busy for
-    twice the host's enqueue latency of one fused rollout (event record +
-    ctypes launch), so the timed launch's start event fires with the rollout
-    already queued behind it and the GPU never idles between them.  Each
-    step's duration is measured behind such a gate too."""
+    three times the host's enqueue latency of the timed launch (event record
+    + `launch`: one fused rollout by default, or a HIP graph's replay), so the
+    timed launch's start event fires with it already queued behind it and the
+    GPU never idles between them.  Each step's duration is measured behind
+    such a gate too."""
     import math
     import time
     import torch
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    one = env.rollout_launcher(1)
+    one = launch or env.rollout_launcher(1)
     lat = []
     for _ in range(7):
         torch.cuda.synchronize()
@@ -617,6 +621,15 @@ def main():
         torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream(dev)
+
+    def make_gate(calibrate):
+        n = calibrate() if args.gate_steps < 0 else args.gate_steps
+        if n <= 0:
+            g = lambda: None  # noqa: E731
+            g.steps = 0
+            return g
+        return env.rollout_launcher(n)
+
     if args.settle > 0 and not with_info:
         env.rollout(args.settle)
     graph = None
@@ -631,11 +644,14 @@ def main():
         # with observations its rules-trajectory split step
         graph = env.capture_steps(args.steps)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))]
+        # the gate ahead of the replay: the replay's host submission would
+        # otherwise fall inside the start event (~20 us: a fifth of a c2
+        # K-step launch; calibrated on the replay itself, untimed steps)
+        gate = make_gate(lambda: _calibrate_gate(env, stream, graph.replay))
     elif fused:
         env.rollout(args.warmup)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))]
-        gate_steps = _calibrate_gate(env, stream)
-        gate = env.rollout_launcher(gate_steps)
+        gate = make_gate(lambda: _calibrate_gate(env, stream))
         if fused == "traj":
             timed = env.step_trajectory_launcher(args.steps, env.trajectory_buffers(args.steps))
         else:
@@ -649,7 +665,7 @@ def main():
             gate = lambda: None  # noqa: E731
             gate.steps = 0
         else:
-            gate = env.rollout_launcher(_calibrate_gate(env, stream))
+            gate = make_gate(lambda: _calibrate_gate(env, stream))
     def episode_payload():
         # the accumulators themselves (no kernel runs to build the payload)
         if stats is None:
@@ -695,13 +711,12 @@ def main():
     else:
         env.clear_episode_stats()
     barrier()
-    if graph is None:
-        # an untimed rollout ahead of the start event keeps the GPU busy
-        # while the host enqueues the timed launch(es), so the event pair
-        # brackets the kernels and not the host's launch latency and an idle
-        # GPU's wake-up (~60 us: half of a 20-step c2r launch); enqueued
-        # before t0, it overlaps that latency in the wall time too
-        gate()
+    # an untimed rollout ahead of the start event keeps the GPU busy while
+    # the host enqueues the timed launch(es) or graph replay, so the event
+    # pair brackets the kernels and not the host's launch latency and an idle
+    # GPU's wake-up (~60 us: half of a 20-step c2r launch); enqueued before
+    # t0, it overlaps that latency in the wall time too
+    gate()
     t0 = time.perf_counter()
     if graph is not None:
         ev[0][0].record(stream)
@@ -757,7 +772,8 @@ def main():
             ceiling_form = "sweep: [B][2][98] fp32 stores in address order, 512 x 2 grid, no decode, tensor-like data"
         elif with_info and info_split_active(B):
             ceiling_ms = _time_sweep_ceiling(env.info_state, B * 1246, 1024, 2, args.steps, stream)
-            ceiling_form = "sweep: [B][2][2492] fp32 stores in address order, 1024 x 2 grid, no decode, tensor-like data"
+            ceiling_form = ("sweep: [B][2][2492] fp32 stores in address order, 1024 x 2 grid, no decode, "
+                            "tensor-like data")
         elif not with_info and not bare_many_active(with_obs, with_info, fused, graph is not None):
             ceiling_ms = _time_traffic_ceiling(env, args.steps, stream)
             ceiling_form = "fused: the fused step's loads and stores, no rules"
@@ -779,7 +795,8 @@ def main():
         sorted_ = "_sorted" if _regrouped(B) else ""
         if players != 2:
             ahead = os.environ.get("COUP_AHEAD", "1") != "0"
-            kernel = (("coup::np::k_trajectory_sorted<%d, 1024>" if sorted_ else "coup::np::k_step_trajectory<%d>") % players
+            traj = "coup::np::k_trajectory_sorted<%d, 1024>" if sorted_ else "coup::np::k_step_trajectory<%d>"
+            kernel = (traj % players
                       if fused == "traj" or bare else
                       ("coup::np::k_rollout_sorted<%d, 1024>" % players if sorted_ else
                        "coup::np::k_rollout<%d>" % players) if fused else
@@ -838,7 +855,7 @@ def main():
             "config": {"workload": workload, "batch_per_gpu": B, "global_batch": world * B, "players": players,
                        "outputs": outputs, "auto_reset": True, "fused_steps_per_launch": per_launch,
                        "hip_graph": graph is not None,
-                       "gate_steps": 0 if graph is not None else gate.steps,
+                       "gate_steps": gate.steps,
                        "parallelism": f"dp{world} (env-id sharding)" + ("" if args.dist_backend == "nccl" else
                                                                    " [gloo rehearsal, ranks share GPUs]")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -106,7 +106,8 @@ def test_bench_two_ranks_gloo(config):
     GPU; the line reports the gathered episodes and no lane errors."""
     batch = 1 << 16 if config == "c3" else 1 << 14
     outs = _run_ranks(lambda r: [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config",
-                                 config, "--steps", "8", "--warmup", "2", "--power-warm-ms", "0", "--settle", "16",
+                                 config, "--steps", "8", "--warmup", "2", "--power-warm-ms", "0", "--gate-steps", "0",
+                                 "--settle", "16",
                                  "--batch", str(batch), "--dist-backend", "gloo"], 2, timeout=110)
     lines = [ln for ln in outs[0].splitlines() if ln.startswith("{")]
     assert len(lines) == 1, outs[0][-2000:]
@@ -120,7 +121,8 @@ def test_bench_two_ranks_gloo(config):
     # gate steps, and no power warm-up, whose step count is timed: the runs
     # play identical games): the gathered totals match
     one = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "1", "--config", config,
-                          "--steps", "8", "--warmup", "2", "--power-warm-ms", "0", "--settle", "16",
+                          "--steps", "8", "--warmup", "2", "--power-warm-ms", "0", "--gate-steps", "0",
+                          "--settle", "16",
                           "--batch", str(2 * batch), "--no-cpu-baseline"], capture_output=True, text=True,
                          timeout=110, cwd=ROOT)
     assert one.returncode == 0, one.stderr[-2000:]
@@ -137,7 +139,8 @@ def test_bench_two_ranks_gloo_trajectory(config):
     per-episode accumulators all-gathered."""
     batch = 1 << 14
     outs = _run_ranks(lambda r: [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--config",
-                                 config, "--steps", "16", "--warmup", "2", "--power-warm-ms", "0", "--settle", "64",
+                                 config, "--steps", "16", "--warmup", "2", "--power-warm-ms", "0", "--gate-steps", "0",
+                                 "--settle", "64",
                                  "--batch", str(batch), "--dist-backend", "gloo"], 2, timeout=110)
     lines = [ln for ln in outs[0].splitlines() if ln.startswith("{")]
     assert len(lines) == 1, outs[0][-2000:]
@@ -169,7 +172,7 @@ def test_bench_one_rank_rccl_line():
     multi-GPU line's code path over a one-rank RCCL communicator, with the
     collective tail timed (episodes.collective_ms)."""
     outs = _run_ranks(lambda r: [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--config", "c3", "--steps",
-                                 "20", "--warmup", "5", "--power-warm-ms", "0", "--settle", "64",
+                                 "20", "--warmup", "5", "--power-warm-ms", "0", "--gate-steps", "0", "--settle", "64",
                                  "--dist-backend", "nccl", "--force-collective", "--no-cpu-baseline"], 1, timeout=110)
     rec = json.loads([ln for ln in outs[0].splitlines() if ln.startswith("{")][-1])
     ep = rec["episodes"]
@@ -195,7 +198,8 @@ def test_bench_gpus_flag_starts_the_ranks(tmp_path):
     rank 0's line with n_gpus 2; the gathered per-lane episode counts and
     return sums equal one process over the same 2B env ids."""
     batch = 1 << 14
-    common = ["--config", "c2", "--steps", "8", "--warmup", "2", "--power-warm-ms", "0", "--settle", "16"]
+    common = ["--config", "c2", "--steps", "8", "--warmup", "2", "--power-warm-ms", "0", "--gate-steps", "0",
+              "--settle", "16"]
     two = _bench(["--gpus", "2", "--batch", str(batch), "--dist-backend", "gloo",
                   "--dump-episodes", str(tmp_path / "two.npz")] + common, timeout=140)
     assert two["n_gpus"] == 2 and two["config"]["global_batch"] == 2 * batch and two["lane_errors"] == 0
@@ -219,7 +223,8 @@ def test_config5_rehearsal_eight_ranks_of_2_20(tmp_path):
     r * 2^20 - 128).  collective_ms per rank is reported, not bounded: ranks
     sharing one GPU and gloo say nothing about xGMI."""
     B, K, W, settle, seed = 1 << 20, 20, 5, 256, 1
-    common = ["--config", "c2", "--steps", str(K), "--warmup", str(W), "--power-warm-ms", "0", "--settle", str(settle),
+    common = ["--config", "c2", "--steps", str(K), "--warmup", str(W), "--power-warm-ms", "0", "--gate-steps", "0",
+              "--settle", str(settle),
               "--seed", str(seed)]
     eight = _bench(["--gpus", "8", "--batch", str(B), "--dist-backend", "gloo",
                     "--dump-episodes", str(tmp_path / "eight.npz")] + common, timeout=170)
