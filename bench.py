@@ -75,17 +75,20 @@ sys.path.insert(0, ROOT)
 # step kernels (9 us, 60 us) are shorter than the host's per-step launch
 # cost, and c3, where the graph removes the ~6 us gap per step that eager
 # launches leave between kernels
-# configs whose K timed steps are one HIP graph of coup_step_many (c4 since
-# round 5: coup_step_many runs tensor-free steps as one trajectory launch)
-GRAPH_AUTO = ("c2", "c3", "c4")
+# configs whose K timed steps are one HIP graph of coup_step_many (c3: 23
+# launches per 20 steps).  c2 / c4 call coup_step_many eagerly: it runs their
+# tensor-free steps as ONE trajectory launch, which a graph replay only
+# delays (~6-13 us of graph-launch packets ahead of a 87 us c2 launch,
+# profiles/r05/c2/).
+GRAPH_AUTO = ("c3",)
 
 
-def bare_many_active(with_obs, with_info, fused, graph):
+def bare_many_active(with_obs, with_info, fused):
     """Whether the timed steps are coup_step_many's tensor-free form: ONE
     trajectory launch for the K steps (every step's outputs over the [B]
     buffers; mirrors coup_kernels.hip `many_bare`, COUP_PIPE=0 turns it
-    off)."""
-    return (graph and not fused and not with_obs and not with_info and
+    off: then K coup_step launches)."""
+    return (not fused and not with_obs and not with_info and
             os.environ.get("COUP_PIPE", "1").strip() != "0")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
@@ -448,9 +451,9 @@ def _time_sweep_ceiling(buf, nf4, threads, passes, steps, stream):
     return a.elapsed_time(b) / steps
 
 
-def _calibrate_gate(env, stream, launch=None):
+def _calibrate_gate(env, stream, launch=None, factor=3.0):
     """Steps of an untimed rollout (the gate) that keep the GPU busy for
-    three times the host's enqueue latency of the timed launch (event record
+    `factor` times the host's enqueue latency of the timed launch (event record
     + `launch`: one fused rollout by default, or a HIP graph's replay), so the
     timed launch's start event fires with it already queued behind it and the
     GPU never idles between them.  Each step's duration is measured behind
@@ -475,8 +478,9 @@ def _calibrate_gate(env, stream, launch=None):
     b.record(stream)
     b.synchronize()
     step_s = a.elapsed_time(b) * 1e-3 / probe
-    # 3x the median: a launch right after a barrier is slower than a warm one
-    return max(1, math.ceil(3.0 * sorted(lat)[len(lat) // 2] / max(step_s, 1e-9)))
+    # 3x the median by default: a launch right after a barrier is slower than
+    # a warm one
+    return max(1, math.ceil(factor * sorted(lat)[len(lat) // 2] / max(step_s, 1e-9)))
 
 
 def _free_port():
@@ -633,6 +637,7 @@ def main():
     if args.settle > 0 and not with_info:
         env.rollout(args.settle)
     graph = None
+    timed = None
     if not fused and (args.graph == "on" or (args.graph == "auto" and cfg in GRAPH_AUTO)):
         for _ in range(args.warmup):
             env.step()
@@ -646,8 +651,9 @@ def main():
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))]
         # the gate ahead of the replay: the replay's host submission would
         # otherwise fall inside the start event (~20 us: a fifth of a c2
-        # K-step launch; calibrated on the replay itself, untimed steps)
-        gate = make_gate(lambda: _calibrate_gate(env, stream, graph.replay))
+        # K-step launch; calibrated on the replay itself, untimed steps).
+        # 1.5x its latency: the gate's remainder counts in the wall time
+        gate = make_gate(lambda: _calibrate_gate(env, stream, graph.replay, factor=1.5))
     elif fused:
         env.rollout(args.warmup)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))]
@@ -661,7 +667,11 @@ def main():
             env.step()
         env.clear_episode_stats()  # as above: the warm-up never folds the timed steps' word
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))]
-        if with_info:  # no rollout on a history env; a c3i step is ~1 ms, its launch latency noise
+        if bare_many_active(with_obs, with_info, fused):
+            # the K steps as one coup_step_many call (one trajectory launch)
+            timed = lambda: env.step_many(args.steps)  # noqa: E731
+            gate = make_gate(lambda: _calibrate_gate(env, stream, timed, factor=1.5))
+        elif with_info:  # no rollout on a history env; a c3i step is ~1 ms, its launch latency noise
             gate = lambda: None  # noqa: E731
             gate.steps = 0
         else:
@@ -684,7 +694,7 @@ def main():
     def unit():  # the timed region's K steps, untimed
         if graph is not None:
             graph.replay()
-        elif fused:
+        elif timed is not None:
             timed()
         else:
             for _ in range(args.steps):
@@ -722,7 +732,7 @@ def main():
         ev[0][0].record(stream)
         graph.replay()
         ev[0][1].record(stream)
-    elif fused:
+    elif timed is not None:  # one fused launch, or coup_step_many's one trajectory launch
         ev[0][0].record(stream)
         timed()
         ev[0][1].record(stream)
@@ -774,12 +784,12 @@ def main():
             ceiling_ms = _time_sweep_ceiling(env.info_state, B * 1246, 1024, 2, args.steps, stream)
             ceiling_form = ("sweep: [B][2][2492] fp32 stores in address order, 1024 x 2 grid, no decode, "
                             "tensor-like data")
-        elif not with_info and not bare_many_active(with_obs, with_info, fused, graph is not None):
+        elif not with_info and not bare_many_active(with_obs, with_info, fused):
             ceiling_ms = _time_traffic_ceiling(env, args.steps, stream)
             ceiling_form = "fused: the fused step's loads and stores, no rules"
 
     if rank == 0:
-        bare = bare_many_active(with_obs, with_info, fused, graph is not None)
+        bare = bare_many_active(with_obs, with_info, fused)
         per_launch = args.steps if (fused or bare) else 1  # env steps per launch of the timed kernel
         bytes_per_launch = bytes_per_lane * B * per_launch
         launch_ms = kern_ms * per_launch

@@ -117,9 +117,9 @@ def test_bench_two_ranks_gloo(config):
     assert rec["episodes"]["finished"] > 0 and rec["episodes"]["collective"].startswith("all_gather")
     assert "int16" in rec["episodes"]["collective"]  # K = 8: 2 bytes per lane
     assert -2.0 <= rec["episodes"]["mean_return_p0"] <= 2.0
-    # the same 2B env ids in one process (a graph config: no timing-calibrated
-    # gate steps, and no power warm-up, whose step count is timed: the runs
-    # play identical games): the gathered totals match
+    # the same 2B env ids in one process (no gate and no power warm-up, whose
+    # step counts are timed: the runs play identical games): the gathered
+    # totals match
     one = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "1", "--config", config,
                           "--steps", "8", "--warmup", "2", "--power-warm-ms", "0", "--gate-steps", "0",
                           "--settle", "16",
@@ -127,7 +127,8 @@ def test_bench_two_ranks_gloo(config):
                          timeout=110, cwd=ROOT)
     assert one.returncode == 0, one.stderr[-2000:]
     single = json.loads([ln for ln in one.stdout.splitlines() if ln.startswith("{")][-1])
-    assert single["config"]["hip_graph"] and rec["config"]["hip_graph"]
+    assert single["config"]["hip_graph"] == rec["config"]["hip_graph"]
+    assert single["config"]["gate_steps"] == rec["config"]["gate_steps"] == 0
     assert single["episodes"]["finished"] == rec["episodes"]["finished"]
     assert single["episodes"]["mean_return_p0"] == rec["episodes"]["mean_return_p0"]
 

@@ -62,10 +62,10 @@ def main():
     graph_on = "--graph" not in args or "off" not in args
     many = (step_many_form(batch, players, graph_on)
             if want_obs and not want_info and not fused and players == 2 else None)
-    from bench import GRAPH_AUTO, bare_many_active
+    from bench import bare_many_active
     # coup_step_many's tensor-free form: ONE trajectory launch per K steps,
     # profiled like the fused trajectory configs (the timed launch is the last)
-    bare = bool(bare_many_active(want_obs, want_info, fused, graph_on and cfg in GRAPH_AUTO))
+    bare = bool(bare_many_active(want_obs, want_info, fused))
     # coup_step_many recorded in the bench's graph.  The merged pipelined
     # step: K + 1 dispatches of ONE kernel per K steps -- the rules of step 1
     # alone, K - 1 launches of rules(t + 1) beside writer(t), the writer of
