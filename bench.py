@@ -654,6 +654,7 @@ def main():
         # K-step launch; calibrated on the replay itself, untimed steps).
         # 1.5x its latency: the gate's remainder counts in the wall time
         gate = make_gate(lambda: _calibrate_gate(env, stream, graph.replay, factor=1.5))
+        env.clear_episode_stats()  # the calibration's replays out of the packed word
     elif fused:
         env.rollout(args.warmup)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))]
@@ -671,6 +672,7 @@ def main():
             # the K steps as one coup_step_many call (one trajectory launch)
             timed = lambda: env.step_many(args.steps)  # noqa: E731
             gate = make_gate(lambda: _calibrate_gate(env, stream, timed, factor=1.5))
+            env.clear_episode_stats()  # the calibration's steps out of the packed word
         elif with_info:  # no rollout on a history env; a c3i step is ~1 ms, its launch latency noise
             gate = lambda: None  # noqa: E731
             gate.steps = 0
