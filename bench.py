@@ -76,11 +76,12 @@ sys.path.insert(0, ROOT)
 # cost, and c3, where the graph removes the ~6 us gap per step that eager
 # launches leave between kernels
 # configs whose K timed steps are one HIP graph of coup_step_many (c3: 23
-# launches per 20 steps).  c2 / c4 call coup_step_many eagerly: it runs their
-# tensor-free steps as ONE trajectory launch, which a graph replay only
-# delays (~6-13 us of graph-launch packets ahead of a 87 us c2 launch,
-# profiles/r05/c2/).
-GRAPH_AUTO = ("c3",)
+# launches per 20 steps; c2 / c4: ONE trajectory launch, which the graph
+# submits with less host time than an eager Python call -- the wall clock
+# counts that host time -- at the price of ~6-13 us of graph-launch packets
+# inside the event window: c2's kernel_ms is 87 us of kernel plus that,
+# profiles/r05/c2/)
+GRAPH_AUTO = ("c2", "c3", "c4")
 
 
 def bare_many_active(with_obs, with_info, fused):
@@ -649,12 +650,10 @@ def main():
         # with observations its rules-trajectory split step
         graph = env.capture_steps(args.steps)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))]
-        # the gate ahead of the replay: the replay's host submission would
-        # otherwise fall inside the start event (~20 us: a fifth of a c2
-        # K-step launch; calibrated on the replay itself, untimed steps).
-        # 1.5x its latency: the gate's remainder counts in the wall time
-        gate = make_gate(lambda: _calibrate_gate(env, stream, graph.replay, factor=1.5))
-        env.clear_episode_stats()  # the calibration's replays out of the packed word
+        # no gate ahead of a graph replay: its host submission takes a few
+        # us, and a gate's remainder would count in the wall time (c2's
+        # value 1.4e10 without, 0.9e10 with a 1.5x gate, calls r05q / r05t)
+        gate = make_gate(lambda: 0)
     elif fused:
         env.rollout(args.warmup)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))]
