@@ -929,6 +929,37 @@ __global__ __launch_bounds__(256) void k_obs_sweep(const uint4* __restrict__ sta
 // block writing T x S float4 contiguous (S passes of T float4), every lane
 // decoded on two threads (one observer row each, obs_row_bits_rt) into LDS
 // as 4 words per row, each float then picked by row and bit.
+// The split writers' float4 stores, by policy: 0 non-temporal global stores
+// (shipped), 1 plain, 2 sc1 (write-through) buffer stores through the
+// block's own resource -- base at the block's first float4, range its float4s
+// -- 3 the same nt (measurement builds: COUP_WRITER_POL).
+struct SweepDst {
+  float* base;                  // the block's first float4
+  __amdgpu_buffer_rsrc_t rsrc;  // POL >= 2
+};
+template <int POL>
+__device__ __forceinline__ SweepDst sweep_dst(float* buf, int64_t x0, int64_t nf4, int64_t block_f4) {
+  SweepDst d;
+  d.base = buf + 4 * x0;
+  if (POL >= 2) {
+    const int64_t left = nf4 - x0 < block_f4 ? nf4 - x0 : block_f4;
+    d.rsrc = __builtin_amdgcn_make_buffer_rsrc(d.base, (short)0, (int)(16 * left), 0x00020000);
+  }
+  return d;
+}
+template <int POL, class V>
+__device__ __forceinline__ void sweep_put(const SweepDst& d, uint32_t rel_f4, const V& v) {
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  if constexpr (POL == 0) {
+    __builtin_nontemporal_store(v, reinterpret_cast<V*>(d.base) + rel_f4);
+  } else if constexpr (POL == 1) {
+    reinterpret_cast<V*>(d.base)[rel_f4] = v;
+  } else {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), d.rsrc, (int)(16u * rel_f4), 0,
+                                           POL == 2 ? 16 : 18);
+  }
+}
+
 template <int T, int S>
 struct ObsSweepLds {
   static constexpr uint32_t kLanes = ((uint32_t)(T * S) + (uint32_t)kRowF4 - 1u) / (uint32_t)kRowF4 + 1u;
@@ -938,7 +969,7 @@ struct ObsSweepLds {
 
 // Block `blk` of the writer (T threads): float4s [blk T S, (blk + 1) T S) of
 // the [n][2][98] buffer from the records `state`.
-template <int T, int S>
+template <int T, int S, int POL = 0>
 __device__ __forceinline__ void obs_sweep_rows_block(const uint4* __restrict__ state, float* __restrict__ obs,
                                                      int64_t n, uint32_t blk, ObsSweepLds<T, S>& lds) {
   typedef float v4f __attribute__((ext_vector_type(4)));
@@ -960,6 +991,8 @@ __device__ __forceinline__ void obs_sweep_rows_block(const uint4* __restrict__ s
   __syncthreads();
   const int64_t nf4 = n * kRowF4;
   const uint32_t rel0 = (uint32_t)(x0 - o0 * kRowF4);
+  SweepDst dst{};
+  if constexpr (POL != 0) dst = sweep_dst<POL>(obs, x0, nf4, T * S);
 #pragma unroll
   for (int j = 0; j < S; ++j) {
     const int64_t x = x0 + j * T + t;
@@ -980,15 +1013,18 @@ __device__ __forceinline__ void obs_sweep_rows_block(const uint4* __restrict__ s
     v.y = f[1];
     v.z = f[2];
     v.w = f[3];
-    __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(obs) + x);
+    if constexpr (POL == 0)
+      __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(obs) + x);
+    else
+      sweep_put<POL>(dst, (uint32_t)(j * T) + t, v);
   }
 }
 
-template <int T, int S>
+template <int T, int S, int POL = 0>
 __global__ __launch_bounds__(T) void k_obs_sweep_rows(const uint4* __restrict__ state, float* __restrict__ obs,
                                                       int64_t n) {
   __shared__ ObsSweepLds<T, S> lds;
-  obs_sweep_rows_block<T, S>(state, obs, n, blockIdx.x, lds);
+  obs_sweep_rows_block<T, S, POL>(state, obs, n, blockIdx.x, lds);
 }
 
 // coup_measure_step_traffic: the bytes of k_step<*, kObsWaveBitsSc1, 256,
@@ -1878,7 +1914,7 @@ __global__ __launch_bounds__(kThreads) void k_info_elems(const uint4* __restrict
 // (info_prefix_to_lds) and 96 history bytes into LDS from its first
 // threads; every thread then decodes its float4s with info_f4, the fused
 // writer's decode (coup_tensor.h), and stores them non-temporally.
-template <int T, int S>
+template <int T, int S, int POL = 0>
 __global__ __launch_bounds__(T) void k_info_sweep(const uint4* __restrict__ state, const uint8_t* __restrict__ hist,
                                                   float* __restrict__ info, int64_t n) {
   typedef float v4f __attribute__((ext_vector_type(4)));
@@ -1912,6 +1948,8 @@ __global__ __launch_bounds__(T) void k_info_sweep(const uint4* __restrict__ stat
   const int64_t nf4 = n * kInfoF4;
   const uint32_t rel0 = (uint32_t)(x0 - o0 * kInfoF4);
   const uint8_t* hb = reinterpret_cast<const uint8_t*>(h4);
+  SweepDst dst{};
+  if constexpr (POL != 0) dst = sweep_dst<POL>(info, x0, nf4, T * S);
 #pragma unroll
   for (int j = 0; j < S; ++j) {
     const int64_t x = x0 + j * T + t;
@@ -1924,7 +1962,10 @@ __global__ __launch_bounds__(T) void k_info_sweep(const uint4* __restrict__ stat
     v.y = f.y;
     v.z = f.z;
     v.w = f.w;
-    __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(info) + x);
+    if constexpr (POL == 0)
+      __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(info) + x);
+    else
+      sweep_put<POL>(dst, (uint32_t)(j * T) + t, v);
   }
 }
 
@@ -3095,7 +3136,19 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
 #ifdef COUP_AB_VARIANTS
       switch (split) {
         case 2: go(std::integral_constant<int, 256>(), std::integral_constant<int, 2>()); break;
-        case 3: go(std::integral_constant<int, 1024>(), std::integral_constant<int, 2>()); break;
+        case 3: {
+          // the shipped shape; COUP_WRITER_POL: its stores plain / sc1 / sc1 nt
+          const unsigned g = (unsigned)((nf4 + 2047) / 2048);
+          if (env->knobs.writer_pol == 1)
+            coup::k_info_sweep<1024, 2, 1><<<g, 1024, 0, s>>>(env->state, env->hist, a.info, n);
+          else if (env->knobs.writer_pol == 2)
+            coup::k_info_sweep<1024, 2, 2><<<g, 1024, 0, s>>>(env->state, env->hist, a.info, n);
+          else if (env->knobs.writer_pol == 3)
+            coup::k_info_sweep<1024, 2, 3><<<g, 1024, 0, s>>>(env->state, env->hist, a.info, n);
+          else
+            go(std::integral_constant<int, 1024>(), std::integral_constant<int, 2>());
+          break;
+        }
         case 4: go(std::integral_constant<int, 512>(), std::integral_constant<int, 4>()); break;
         case 5: go(std::integral_constant<int, 256>(), std::integral_constant<int, 4>()); break;
         default: go(std::integral_constant<int, 512>(), std::integral_constant<int, 2>()); break;
@@ -3104,6 +3157,7 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
       (void)split;
       go(std::integral_constant<int, 1024>(), std::integral_constant<int, 2>());  // variant 3
 #endif
+
       COUP_HIP_TRY(hipGetLastError());
       return COUP_OK;
     }
@@ -3568,7 +3622,16 @@ int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, b
     }
     for (int64_t s = 0; s < c; ++s) {
       float* obs = out->obs + (slices ? (t0 + s) * n * 2 * COUP_OBS_SIZE : 0);
-      coup::k_obs_sweep_rows<512, 2><<<wgrid, 512, 0, S>>>(rec + s * n, obs, n);
+#ifdef COUP_AB_VARIANTS
+      if (env->knobs.writer_pol == 1)
+        coup::k_obs_sweep_rows<512, 2, 1><<<wgrid, 512, 0, S>>>(rec + s * n, obs, n);
+      else if (env->knobs.writer_pol == 2)
+        coup::k_obs_sweep_rows<512, 2, 2><<<wgrid, 512, 0, S>>>(rec + s * n, obs, n);
+      else if (env->knobs.writer_pol == 3)
+        coup::k_obs_sweep_rows<512, 2, 3><<<wgrid, 512, 0, S>>>(rec + s * n, obs, n);
+      else
+#endif
+        coup::k_obs_sweep_rows<512, 2><<<wgrid, 512, 0, S>>>(rec + s * n, obs, n);
       COUP_HIP_TRY(hipGetLastError());
     }
     if (overlap) COUP_HIP_TRY(hipEventRecord(env->ev_writers[b], S));

@@ -96,3 +96,12 @@ def test_rules_trajectory_shapes(monkeypatch, shape):
     (COUP_MANY_SHAPE) equal stepping."""
     monkeypatch.setenv("COUP_MANY_SHAPE", shape)
     M.test_chunk_length_invariant(monkeypatch, 8, "1", None)
+
+
+@pytest.mark.parametrize("pol", ["1", "2", "3"])
+def test_obs_writer_store_policies(monkeypatch, pol):
+    """COUP_WRITER_POL: the rules-trajectory form's k_obs_sweep_rows<512, 2>
+    with plain, sc1 or sc1 nt buffer stores equals stepping (ragged batch:
+    the last block's range drops the stores past it)."""
+    monkeypatch.setenv("COUP_WRITER_POL", pol)
+    M.test_chunk_length_invariant(monkeypatch, 8, "1", None)

@@ -90,3 +90,19 @@ def test_info_split_equals_fused(monkeypatch, B):
         for i in range(1, 5):
             np.testing.assert_array_equal(got[i], ref[i], err_msg=f"info split {split} B {B}: part {i}")
         assert got[5] == ref[5]
+
+
+@pytest.mark.parametrize("pol", ["1", "2", "3"])
+@pytest.mark.parametrize("B", [1000, 4099])
+def test_info_writer_store_policies(monkeypatch, B, pol):
+    """COUP_WRITER_POL: k_info_sweep<1024, 2>'s stores plain, sc1 or sc1 nt
+    buffer stores (through the block's own resource, whose range drops the
+    stores past the batch) instead of non-temporal ones: the same tensors."""
+    steps = 12
+    ref = _run_info(monkeypatch, 0, B, steps)
+    monkeypatch.setenv("COUP_WRITER_POL", pol)
+    got = _run_info(monkeypatch, 3, B, steps)
+    monkeypatch.delenv("COUP_WRITER_POL")
+    for t, (x, y) in enumerate(zip(got[0], ref[0])):
+        for k in INFO_KEYS:
+            np.testing.assert_array_equal(x[k], y[k], err_msg=f"pol {pol} B {B}: {k} at step {t}")

@@ -31,7 +31,7 @@ sys.path.insert(0, ROOT)
 KNOBS = ("COUP_OBS_MODE", "COUP_XCD_REMAP", "COUP_STEP_DYN_LDS", "COUP_REGROUP", "COUP_AHEAD",
          "COUP_NP_SORT_THREADS", "COUP_SORT_THREADS", "COUP_NP_RESET_INLINE", "COUP_TRAJ_STAGE",
          "COUP_NP_RESET_GROUP", "COUP_STEP_TPL", "COUP_OBS_SPLIT", "COUP_INFO_SPLIT", "COUP_NP_SCAN",
-         "COUP_PIPE", "COUP_PIPE_SPAN")
+         "COUP_PIPE", "COUP_PIPE_SPAN", "COUP_WRITER_POL", "COUP_TRAJ_CHUNK", "COUP_MANY_SHAPE")
 
 
 def main():
