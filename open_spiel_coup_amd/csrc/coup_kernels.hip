@@ -3137,16 +3137,16 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
       switch (split) {
         case 2: go(std::integral_constant<int, 256>(), std::integral_constant<int, 2>()); break;
         case 3: {
-          // the shipped shape; COUP_WRITER_POL: its stores nt / plain / sc1 (the shipped sc1 nt: -1, 3)
+          // the shipped shape; COUP_WRITER_POL: its stores plain / sc1 / sc1 nt (-1, 0: the shipped nt)
           const unsigned g = (unsigned)((nf4 + 2047) / 2048);
-          if (env->knobs.writer_pol == 0)
-            coup::k_info_sweep<1024, 2, 0><<<g, 1024, 0, s>>>(env->state, env->hist, a.info, n);
-          else if (env->knobs.writer_pol == 1)
+          if (env->knobs.writer_pol == 1)
             coup::k_info_sweep<1024, 2, 1><<<g, 1024, 0, s>>>(env->state, env->hist, a.info, n);
           else if (env->knobs.writer_pol == 2)
             coup::k_info_sweep<1024, 2, 2><<<g, 1024, 0, s>>>(env->state, env->hist, a.info, n);
-          else
+          else if (env->knobs.writer_pol == 3)
             coup::k_info_sweep<1024, 2, 3><<<g, 1024, 0, s>>>(env->state, env->hist, a.info, n);
+          else
+            go(std::integral_constant<int, 1024>(), std::integral_constant<int, 2>());
           break;
         }
         case 4: go(std::integral_constant<int, 512>(), std::integral_constant<int, 4>()); break;
@@ -3154,11 +3154,10 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
         default: go(std::integral_constant<int, 512>(), std::integral_constant<int, 2>()); break;
       }
 #else
-      // variant 3 with sc1 nt buffer stores: 816.7 against 838.2 us per 2^18-lane step for the
-      // non-temporal global stores (call r05x)
+      // variant 3, non-temporal global stores (sc1 nt buffer stores measured 816.7 against
+      // 838.2 us in one call, r05x, and 865.0 against 864.4 in another, r05y: not shipped)
       (void)split;
-      (void)go;
-      coup::k_info_sweep<1024, 2, 3><<<(unsigned)((nf4 + 2047) / 2048), 1024, 0, s>>>(env->state, env->hist, a.info, n);
+      go(std::integral_constant<int, 1024>(), std::integral_constant<int, 2>());
 #endif
 
       COUP_HIP_TRY(hipGetLastError());

@@ -173,7 +173,7 @@ def test_device_builds_turn_the_slp_vectorizer_off(monkeypatch):
 _SHIPPED_2P = """
 coup::k_info_elems coup::k_measure_traffic coup::k_obs_lanes coup::k_reset coup::k_rollout coup::k_server
 coup::k_step_trajectory coup::np::k_export coup::np::k_import |
-void coup::k_apply<false> | void coup::k_apply<true> | void coup::k_info_sweep<1024, 2, 3> |
+void coup::k_apply<false> | void coup::k_apply<true> | void coup::k_info_sweep<1024, 2, 0> |
 void coup::k_obs_sweep_rows<512, 2, 0> | void coup::k_query<false, false> | void coup::k_query<false, true> |
 void coup::k_query<true, false> | void coup::k_query<true, true> | void coup::k_rollout_sorted<1024> |
 void coup::k_slot<false> | void coup::k_slot<true> | void coup::k_slot_batch<false> | void coup::k_slot_batch<true> |
