@@ -202,3 +202,29 @@ def test_bare_step_many_equals_stepping(monkeypatch, players, B):
     np.testing.assert_array_equal(many.export_state().cpu().numpy(), ref.export_state().cpu().numpy())
     assert torch.equal(many.legal_mask, ref.legal_mask) and torch.equal(many.actions, ref.actions)
     assert many.error_count() == ref.error_count() == 0
+
+
+@pytest.mark.parametrize("obs", [True, False])
+def test_step_many_without_auto_reset(monkeypatch, obs):
+    """Without auto-reset a finished lane reports LAST (terminal record, no
+    legal actions) and restarts at the next step (FIRST), in both
+    coup_step_many forms (rules trajectory + writers with observations; one
+    trajectory launch without): equal to per-step coup_step."""
+    B, seed = 5000, 31
+    monkeypatch.setenv("COUP_OBS_SPLIT", "11")
+    monkeypatch.setenv("COUP_REGROUP", "1")
+    kw = dict(seed=seed, auto_reset=False, obs=obs, episode_stats=True)
+    monkeypatch.setenv("COUP_PIPE", "1")
+    many = BatchedCoupEnv(B, **kw)
+    monkeypatch.setenv("COUP_PIPE", "0")
+    ref = BatchedCoupEnv(B, **kw)
+    for K in (9, 30, 17):
+        many.step_many(K)
+        for _ in range(K):
+            ref.step()
+        a, b = (_state(many), _state(ref)) if obs else (_bare_state(many), _bare_state(ref))
+        for k in a[0]:
+            np.testing.assert_array_equal(a[0][k], b[0][k], err_msg=f"K {K}: {k}")
+        for x, y in zip(a[1:], b[1:]):
+            np.testing.assert_array_equal(x, y)
+    assert many.error_count() == ref.error_count() == 0
