@@ -1020,9 +1020,12 @@ __device__ __forceinline__ void obs_sweep_rows_block(const uint4* __restrict__ s
   }
 }
 
-template <int T, int S, int POL = 0>
+// PRIO (measurement builds, COUP_WRITER_PRIO): the writer's waves raise
+// their issue priority (s_setprio) over the rules waves beside them
+template <int T, int S, int POL = 0, int PRIO = 0>
 __global__ __launch_bounds__(T) void k_obs_sweep_rows(const uint4* __restrict__ state, float* __restrict__ obs,
                                                       int64_t n) {
+  if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO);
   __shared__ ObsSweepLds<T, S> lds;
   obs_sweep_rows_block<T, S, POL>(state, obs, n, blockIdx.x, lds);
 }
@@ -3614,6 +3617,8 @@ int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, b
       shape(std::integral_constant<int, 256>(), std::integral_constant<int, 8>());
     else if (env->knobs.many_shape == 4)
       shape(std::integral_constant<int, 1024>(), std::integral_constant<int, 4>());
+    else if (overlap && env->knobs.overlap_lds > 0)  // COUP_OVERLAP_LDS: cap the rules' blocks per CU
+      coup::k_trajectory_sorted<TB, true, false, 8, false><<<grid, TB, (unsigned)env->knobs.overlap_lds, R>>>(a, c, x);
     else
 #endif
       coup::k_trajectory_sorted<TB, true, false, 8, false><<<grid, TB, 0, R>>>(a, c, x);
@@ -3631,6 +3636,10 @@ int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, b
         coup::k_obs_sweep_rows<512, 2, 2><<<wgrid, 512, 0, S>>>(rec + s * n, obs, n);
       else if (env->knobs.writer_pol == 3)
         coup::k_obs_sweep_rows<512, 2, 3><<<wgrid, 512, 0, S>>>(rec + s * n, obs, n);
+      else if (env->knobs.writer_prio == 1)
+        coup::k_obs_sweep_rows<512, 2, 0, 1><<<wgrid, 512, 0, S>>>(rec + s * n, obs, n);
+      else if (env->knobs.writer_prio >= 2)
+        coup::k_obs_sweep_rows<512, 2, 0, 3><<<wgrid, 512, 0, S>>>(rec + s * n, obs, n);
       else
 #endif
         coup::k_obs_sweep_rows<512, 2><<<wgrid, 512, 0, S>>>(rec + s * n, obs, n);

@@ -105,3 +105,13 @@ def test_obs_writer_store_policies(monkeypatch, pol):
     the last block's range drops the stores past it)."""
     monkeypatch.setenv("COUP_WRITER_POL", pol)
     M.test_chunk_length_invariant(monkeypatch, 8, "1", None)
+
+
+@pytest.mark.parametrize("knobs", [{"COUP_WRITER_PRIO": "2"}, {"COUP_OVERLAP_LDS": "98304", "COUP_WRITER_PRIO": "1"}])
+def test_overlap_priority_and_occupancy(monkeypatch, knobs):
+    """The overlapped form with the writer's waves at a higher issue priority
+    and the rules' blocks capped per CU by dynamic LDS equals stepping."""
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    M.test_chunk_length_invariant(monkeypatch, 3, "3", None)
+    M.test_chunk_length_invariant(monkeypatch, 8, "1", None)

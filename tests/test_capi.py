@@ -174,7 +174,7 @@ _SHIPPED_2P = """
 coup::k_info_elems coup::k_measure_traffic coup::k_obs_lanes coup::k_reset coup::k_rollout coup::k_server
 coup::k_step_trajectory coup::np::k_export coup::np::k_import |
 void coup::k_apply<false> | void coup::k_apply<true> | void coup::k_info_sweep<1024, 2, 0> |
-void coup::k_obs_sweep_rows<512, 2, 0> | void coup::k_query<false, false> | void coup::k_query<false, true> |
+void coup::k_obs_sweep_rows<512, 2, 0, 0> | void coup::k_query<false, false> | void coup::k_query<false, true> |
 void coup::k_query<true, false> | void coup::k_query<true, true> | void coup::k_rollout_sorted<1024> |
 void coup::k_slot<false> | void coup::k_slot<true> | void coup::k_slot_batch<false> | void coup::k_slot_batch<true> |
 void coup::k_step<false, 0, 256, 0, true> | void coup::k_step<false, 0, 256, 1, false> |
@@ -241,7 +241,7 @@ def test_measurement_build_holds_the_variants():
     build.build()
     got = _kernel_handles(build.VARIANTS_OUT)
     assert _shipped_kernels() <= got
-    for k in ("void coup::k_obs_sweep<1>", "void coup::k_obs_sweep_rows<256, 2, 0>", "void coup::k_step_group<4, true>",
+    for k in ("void coup::k_obs_sweep<1>", "void coup::k_obs_sweep_rows<256, 2, 0, 0>", "void coup::k_step_group<4, true>",
               "void coup::k_step<true, 1, 256, 0, false>", "void coup::k_step_sorted<true, 1024>",
               "void coup::k_info_sweep<512, 2, 0>", "void coup::k_step_obs_pipe<512, 2>",
               "void coup::k_trajectory_sorted<1024, false, true, 4, false>",
