@@ -29,7 +29,8 @@
 // With code objects (tools/info_modules.sh: this file's device IR through
 // llc at chosen settings), each module's k_sweep_uint2<512, 2> and
 // k_sweep_rows<512, 2> are loaded (hipModuleLoad) and checked against k_ref
-// the same way, one JSON line per module and kernel.
+// the same way, one JSON line per module and kernel (INFO_REPRO_DYN_LDS:
+// launched with that much extra dynamic LDS per block).
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -247,7 +248,10 @@ int main(int argc, char** argv) {
         CHECK(hipMemset(out, 0xFF, fl * sizeof(float)));
         int64_t n64 = n;
         void* args[] = {&recs, &hist, &out, &n64};
-        CHECK(hipModuleLaunchKernel(fn, (unsigned)((nf4 + 1023) / 1024), 1, 1, 512, 1, 1, 0, nullptr, args, nullptr));
+        // INFO_REPRO_DYN_LDS: extra dynamic LDS per block (fewer blocks per CU)
+        const char* dl = std::getenv("INFO_REPRO_DYN_LDS");
+        const unsigned dyn = dl ? (unsigned)std::atoi(dl) : 0u;
+        CHECK(hipModuleLaunchKernel(fn, (unsigned)((nf4 + 1023) / 1024), 1, 1, 512, 1, 1, dyn, nullptr, args, nullptr));
         CHECK(hipDeviceSynchronize());
         std::string label = std::string(argv[m]) + " " + (std::strstr(kn, "uint2") ? "uint2" : "rows");
         compare(label.c_str());
