@@ -1103,6 +1103,24 @@ __global__ __launch_bounds__(T) void k_store_sweep(float* __restrict__ dst, int6
 }
 
 #ifdef COUP_AB_VARIANTS
+// measurement builds: the same stores, each float4's value the end of a
+// dependent chain of `pad` integer operations (the writers' decode work
+// stands between their stores; is the sweep's store rate a pacing effect?)
+template <int T, int S>
+__global__ __launch_bounds__(T) void k_store_sweep_paced(float* __restrict__ dst, int64_t nf4, int pad) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  const int64_t x0 = (int64_t)blockIdx.x * (T * S) + threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    const int64_t x = x0 + j * T;
+    if (x >= nf4) break;
+    uint32_t h = (uint32_t)x;
+    for (int k = 0; k < pad; ++k) h = (h ^ (h >> 7)) * 0x9E3779B1u + (uint32_t)k;
+    v4f v = v4f{(h & 31u) == 0u ? 1.0f : 0.0f, 0.0f, 0.0f, 0.0f};
+    __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(dst) + x);
+  }
+}
+
 // measurement builds: the same stores from a resident grid, each block
 // looping over chunks of T S float4 (grid-stride), without a wave launch
 // per chunk
@@ -4362,6 +4380,12 @@ int coup_measure_step_traffic(int64_t batch, uint32_t* records, const coup_step_
 
 int coup_measure_store_sweep(float* dst, int64_t n_float4, int threads, int passes, int mode, void* hip_stream) {
   if (!dst || n_float4 < 0) return fail(COUP_E_INVALID, "coup_measure_store_sweep: bad buffer");
+#ifdef COUP_AB_VARIANTS
+  const int pad = (mode >> 8) & 0xFF;  // measurement builds: bits 8-15, a paced sweep (k_store_sweep_paced)
+  mode &= ~0xFF00;
+#else
+  const int pad = 0;
+#endif
   if (mode & ~(COUP_SWEEP_RESIDENT | COUP_SWEEP_INDEX_BITS))
     return fail(COUP_E_INVALID, "coup_measure_store_sweep: unknown mode bits");
   if (n_float4 == 0) return COUP_OK;
@@ -4380,6 +4404,10 @@ int coup_measure_store_sweep(float* dst, int64_t n_float4, int threads, int pass
       coup::k_store_sweep_resident<T, S><<<(unsigned)grid, T, 0, s>>>(dst, n_float4, bits);
 #else
       return fail(COUP_E_INVALID, "coup_measure_store_sweep: the resident form is a measurement build's");
+#endif
+    } else if (pad > 0) {
+#ifdef COUP_AB_VARIANTS
+      coup::k_store_sweep_paced<T, S><<<(unsigned)blocks, T, 0, s>>>(dst, n_float4, pad);
 #endif
     } else {
       coup::k_store_sweep<T, S><<<(unsigned)blocks, T, 0, s>>>(dst, n_float4, bits);

@@ -23,8 +23,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 R, BITS = 1, 2  # _native.SWEEP_RESIDENT, _native.SWEEP_INDEX_BITS
+
+
+def PACE(n):  # measurement builds: a dependent chain of n integer ops ahead of each store
+    return n << 8
+
+
 SHAPES = [(512, 2, 0), (1024, 2, 0), (512, 2, BITS), (1024, 2, BITS), (256, 2, 0), (512, 4, 0), (1024, 4, 0),
-          (1024, 8, 0), (512, 2, R), (1024, 2, R), (1024, 8, R)]
+          (1024, 8, 0), (512, 2, R), (1024, 2, R), (1024, 8, R), (512, 2, PACE(8)), (512, 2, PACE(24)),
+          (512, 2, PACE(64)), (1024, 2, PACE(24)), (1024, 2, PACE(64))]
 
 
 def main():
@@ -36,7 +43,7 @@ def main():
     from open_spiel_coup_amd import _native
     lib = _native.load()
     ab = bool(lib.coup_build_flags() & _native.BUILD_AB_VARIANTS)
-    shapes = SHAPES if ab else [s for s in SHAPES if not s[2] & R and s[:2] in ((512, 2), (1024, 2))]
+    shapes = SHAPES if ab else [s for s in SHAPES if not s[2] & (R | 0xFF00) and s[:2] in ((512, 2), (1024, 2))]
     bufs = {"c3_obs": (1 << 20) * 2 * 98, "c3i_info": (1 << 18) * 2 * 2492}
     stream = torch.cuda.current_stream()
     graphs = {}
@@ -69,7 +76,7 @@ def main():
         med = statistics.median(ts)
         nbytes = bufs[name] * 4
         print(json.dumps({"buffer": name, "bytes": nbytes, "threads": t, "passes": s, "resident": bool(r & R),
-                          "data": "index bits" if r & BITS else "tensor-like",
+                          "data": "index bits" if r & BITS else "tensor-like", "pace_ops": r >> 8,
                           "median_us": round(med, 2), "min_us": round(min(ts), 2),
                           "tb_per_s": round(nbytes / (med * 1e-6) / 1e12, 3)}), flush=True)
 
