@@ -1121,6 +1121,36 @@ __global__ __launch_bounds__(T) void k_store_sweep_paced(float* __restrict__ dst
   }
 }
 
+// measurement builds: the writer's structure without its decode -- the
+// block's first threads load one record-sized uint4 per lane it touches (from
+// `src`, 16 B per 49 float4 stored, as the observation writer reads its
+// records), park them in LDS, a barrier, then the stores, each float4's value
+// taken from its lane's parked word (is the writer's store rate its
+// load -> LDS -> barrier -> store shape?)
+template <int T, int S>
+__global__ __launch_bounds__(T) void k_store_sweep_writerlike(float* __restrict__ dst, const uint4* __restrict__ src,
+                                                              int64_t nf4) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  constexpr uint32_t kLanes = ((uint32_t)(T * S) + (uint32_t)kRowF4 - 1u) / (uint32_t)kRowF4 + 1u;
+  __shared__ uint32_t w[kLanes];
+  const uint32_t t = threadIdx.x;
+  const int64_t x0 = (int64_t)blockIdx.x * (T * S);
+  const int64_t o0 = x0 / kRowF4;
+  if (t < kLanes && (o0 + t) * kRowF4 < nf4) w[t] = src[o0 + t].x;
+  __syncthreads();
+  const uint32_t rel0 = (uint32_t)(x0 - o0 * kRowF4);
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    const int64_t x = x0 + j * T + t;
+    if (x >= nf4) break;
+    const uint32_t rel = rel0 + (uint32_t)(j * T) + t;
+    const uint32_t o = rel / (uint32_t)kRowF4, c = rel - o * (uint32_t)kRowF4;
+    const uint32_t b = (w[o] >> (c & 31u)) & 1u;
+    v4f v = v4f{(float)b, 0.0f, 0.0f, 0.0f};
+    __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(dst) + x);
+  }
+}
+
 // measurement builds: the same stores from a resident grid, each block
 // looping over chunks of T S float4 (grid-stride), without a wave launch
 // per chunk
@@ -4382,8 +4412,10 @@ int coup_measure_store_sweep(float* dst, int64_t n_float4, int threads, int pass
   if (!dst || n_float4 < 0) return fail(COUP_E_INVALID, "coup_measure_store_sweep: bad buffer");
 #ifdef COUP_AB_VARIANTS
   const int pad = (mode >> 8) & 0xFF;  // measurement builds: bits 8-15, a paced sweep (k_store_sweep_paced)
-  mode &= ~0xFF00;
+  const bool writerlike = (mode & 0x10000) != 0;  // bit 16: k_store_sweep_writerlike (reads dst's first words)
+  mode &= ~0x1FF00;
 #else
+  const bool writerlike = false;
   const int pad = 0;
 #endif
   if (mode & ~(COUP_SWEEP_RESIDENT | COUP_SWEEP_INDEX_BITS))
@@ -4405,9 +4437,13 @@ int coup_measure_store_sweep(float* dst, int64_t n_float4, int threads, int pass
 #else
       return fail(COUP_E_INVALID, "coup_measure_store_sweep: the resident form is a measurement build's");
 #endif
-    } else if (pad > 0) {
+    } else if (pad > 0 || writerlike) {
 #ifdef COUP_AB_VARIANTS
-      coup::k_store_sweep_paced<T, S><<<(unsigned)blocks, T, 0, s>>>(dst, n_float4, pad);
+      if (writerlike)  // the "records": the buffer's own first n_float4 / 49 uint4 (read, then overwritten)
+        coup::k_store_sweep_writerlike<T, S><<<(unsigned)blocks, T, 0, s>>>(dst, reinterpret_cast<const uint4*>(dst),
+                                                                           n_float4);
+      else
+        coup::k_store_sweep_paced<T, S><<<(unsigned)blocks, T, 0, s>>>(dst, n_float4, pad);
 #endif
     } else {
       coup::k_store_sweep<T, S><<<(unsigned)blocks, T, 0, s>>>(dst, n_float4, bits);

@@ -29,9 +29,12 @@ def PACE(n):  # measurement builds: a dependent chain of n integer ops ahead of 
     return n << 8
 
 
+WRITERLIKE = 1 << 16  # measurement builds: load -> LDS -> barrier -> stores, no decode
+
+
 SHAPES = [(512, 2, 0), (1024, 2, 0), (512, 2, BITS), (1024, 2, BITS), (256, 2, 0), (512, 4, 0), (1024, 4, 0),
           (1024, 8, 0), (512, 2, R), (1024, 2, R), (1024, 8, R), (512, 2, PACE(8)), (512, 2, PACE(24)),
-          (512, 2, PACE(64)), (1024, 2, PACE(24)), (1024, 2, PACE(64))]
+          (512, 2, PACE(64)), (1024, 2, PACE(24)), (1024, 2, PACE(64)), (512, 2, WRITERLIKE), (1024, 2, WRITERLIKE)]
 
 
 def main():
@@ -43,7 +46,7 @@ def main():
     from open_spiel_coup_amd import _native
     lib = _native.load()
     ab = bool(lib.coup_build_flags() & _native.BUILD_AB_VARIANTS)
-    shapes = SHAPES if ab else [s for s in SHAPES if not s[2] & (R | 0xFF00) and s[:2] in ((512, 2), (1024, 2))]
+    shapes = SHAPES if ab else [s for s in SHAPES if not s[2] & (R | 0x1FF00) and s[:2] in ((512, 2), (1024, 2))]
     bufs = {"c3_obs": (1 << 20) * 2 * 98, "c3i_info": (1 << 18) * 2 * 2492}
     stream = torch.cuda.current_stream()
     graphs = {}
@@ -76,7 +79,7 @@ def main():
         med = statistics.median(ts)
         nbytes = bufs[name] * 4
         print(json.dumps({"buffer": name, "bytes": nbytes, "threads": t, "passes": s, "resident": bool(r & R),
-                          "data": "index bits" if r & BITS else "tensor-like", "pace_ops": r >> 8,
+                          "data": "index bits" if r & BITS else "tensor-like", "pace_ops": (r >> 8) & 0xFF, "writerlike": bool(r & WRITERLIKE),
                           "median_us": round(med, 2), "min_us": round(min(ts), 2),
                           "tb_per_s": round(nbytes / (med * 1e-6) / 1e12, 3)}), flush=True)
 
