@@ -10,7 +10,9 @@ Buffers: c3's [2^20][2][98] fp32 (822 MB) and c3i's [2^18][2][2492] fp32
 of 32) and with index bits in every float (COUP_SWEEP_INDEX_BITS): K
 launches of coup_measure_store_sweep replayed from one HIP graph, the mean
 per launch; one JSON line per (buffer, shape, data) with the median over
-rounds and the rate.  Measurement tool only.
+rounds and the rate.  With --gap-sleep an idle kernel separates the sweeps,
+so the rate printed here includes it; read the sweep's own duration from a
+rocprofv3 --kernel-trace --stats run of the same command.  Measurement tool only.
 """
 import argparse
 import ctypes
@@ -41,12 +43,17 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--gap-sleep", type=int, default=0,
+                    help="cycles of an idle kernel between sweeps (per-kernel durations then from rocprofv3)")
+    ap.add_argument("--only", default=None, help="comma list of shape indices into SHAPES")
     a = ap.parse_args()
     import torch
     from open_spiel_coup_amd import _native
     lib = _native.load()
     ab = bool(lib.coup_build_flags() & _native.BUILD_AB_VARIANTS)
     shapes = SHAPES if ab else [s for s in SHAPES if not s[2] & (R | 0x1FF00) and s[:2] in ((512, 2), (1024, 2))]
+    if a.only:
+        shapes = [shapes[int(i)] for i in a.only.split(",")]
     bufs = {"c3_obs": (1 << 20) * 2 * 98, "c3i_info": (1 << 18) * 2 * 2492}
     stream = torch.cuda.current_stream()
     graphs = {}
@@ -64,6 +71,8 @@ def main():
             with torch.cuda.graph(g, stream=side):
                 for _ in range(a.steps):
                     launch(side.cuda_stream)
+                    if a.gap_sleep:
+                        torch.cuda._sleep(a.gap_sleep)
             stream.wait_stream(side)
             graphs[(name, t, s, r)] = (g, buf)
     times = {k: [] for k in graphs}
