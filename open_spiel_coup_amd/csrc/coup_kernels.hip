@@ -1151,6 +1151,25 @@ __global__ __launch_bounds__(T) void k_store_sweep_writerlike(float* __restrict_
   }
 }
 
+// measurement builds: the same stores with a chosen share of all-zero lines:
+// a 1.0 in the float4s x with x % 2^(dens - 1) == 0 (dens 1: every float4;
+// 4: the tensor-like data; 6: one per 512 B), none at dens 31 (all zeros).
+// The observation rows are mostly zero lines; is the HBM store rate a
+// function of the share of zero lines?
+template <int T, int S>
+__global__ __launch_bounds__(T) void k_store_sweep_density(float* __restrict__ dst, int64_t nf4, int dens) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  const int64_t x0 = (int64_t)blockIdx.x * (T * S) + threadIdx.x;
+  const int64_t mask = dens >= 31 ? -1 : ((int64_t)1 << (dens - 1)) - 1;
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    const int64_t x = x0 + j * T;
+    if (x >= nf4) break;
+    v4f v = v4f{dens < 31 && (x & mask) == 0 ? 1.0f : 0.0f, 0.0f, 0.0f, 0.0f};
+    __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(dst) + x);
+  }
+}
+
 // measurement builds: the same stores from a resident grid, each block
 // looping over chunks of T S float4 (grid-stride), without a wave launch
 // per chunk
@@ -4413,10 +4432,11 @@ int coup_measure_store_sweep(float* dst, int64_t n_float4, int threads, int pass
 #ifdef COUP_AB_VARIANTS
   const int pad = (mode >> 8) & 0xFF;  // measurement builds: bits 8-15, a paced sweep (k_store_sweep_paced)
   const bool writerlike = (mode & 0x10000) != 0;  // bit 16: k_store_sweep_writerlike (reads dst's first words)
-  mode &= ~0x1FF00;
+  const int dens = (mode >> 17) & 0x1F;           // bits 17-21: k_store_sweep_density's dens
+  mode &= ~0x3FFF00;
 #else
   const bool writerlike = false;
-  const int pad = 0;
+  const int pad = 0, dens = 0;
 #endif
   if (mode & ~(COUP_SWEEP_RESIDENT | COUP_SWEEP_INDEX_BITS))
     return fail(COUP_E_INVALID, "coup_measure_store_sweep: unknown mode bits");
@@ -4437,9 +4457,11 @@ int coup_measure_store_sweep(float* dst, int64_t n_float4, int threads, int pass
 #else
       return fail(COUP_E_INVALID, "coup_measure_store_sweep: the resident form is a measurement build's");
 #endif
-    } else if (pad > 0 || writerlike) {
+    } else if (pad > 0 || writerlike || dens > 0) {
 #ifdef COUP_AB_VARIANTS
-      if (writerlike)  // the "records": the buffer's own first n_float4 / 49 uint4 (read, then overwritten)
+      if (dens > 0)
+        coup::k_store_sweep_density<T, S><<<(unsigned)blocks, T, 0, s>>>(dst, n_float4, dens);
+      else if (writerlike)  // the "records": the buffer's own first n_float4 / 49 uint4 (read, then overwritten)
         coup::k_store_sweep_writerlike<T, S><<<(unsigned)blocks, T, 0, s>>>(dst, reinterpret_cast<const uint4*>(dst),
                                                                            n_float4);
       else

@@ -34,9 +34,15 @@ def PACE(n):  # measurement builds: a dependent chain of n integer ops ahead of 
 WRITERLIKE = 1 << 16  # measurement builds: load -> LDS -> barrier -> stores, no decode
 
 
+def DENS(d):  # measurement builds: a 1.0 per 2^(d-1) float4s, all zeros at 31 (share of all-zero lines)
+    return d << 17
+
+
 SHAPES = [(512, 2, 0), (1024, 2, 0), (512, 2, BITS), (1024, 2, BITS), (256, 2, 0), (512, 4, 0), (1024, 4, 0),
           (1024, 8, 0), (512, 2, R), (1024, 2, R), (1024, 8, R), (512, 2, PACE(8)), (512, 2, PACE(24)),
-          (512, 2, PACE(64)), (1024, 2, PACE(24)), (1024, 2, PACE(64)), (512, 2, WRITERLIKE), (1024, 2, WRITERLIKE)]
+          (512, 2, PACE(64)), (1024, 2, PACE(24)), (1024, 2, PACE(64)), (512, 2, WRITERLIKE), (1024, 2, WRITERLIKE),
+          (512, 2, DENS(1)), (512, 2, DENS(4)), (512, 2, DENS(5)), (512, 2, DENS(6)), (512, 2, DENS(8)),
+          (512, 2, DENS(31)), (1024, 2, DENS(1)), (1024, 2, DENS(6)), (1024, 2, DENS(31))]
 
 
 def main():
@@ -51,7 +57,7 @@ def main():
     from open_spiel_coup_amd import _native
     lib = _native.load()
     ab = bool(lib.coup_build_flags() & _native.BUILD_AB_VARIANTS)
-    shapes = SHAPES if ab else [s for s in SHAPES if not s[2] & (R | 0x1FF00) and s[:2] in ((512, 2), (1024, 2))]
+    shapes = SHAPES if ab else [s for s in SHAPES if not s[2] & (R | 0x3FFF00) and s[:2] in ((512, 2), (1024, 2))]
     if a.only:
         shapes = [shapes[int(i)] for i in a.only.split(",")]
     bufs = {"c3_obs": (1 << 20) * 2 * 98, "c3i_info": (1 << 18) * 2 * 2492}
@@ -89,6 +95,7 @@ def main():
         nbytes = bufs[name] * 4
         print(json.dumps({"buffer": name, "bytes": nbytes, "threads": t, "passes": s, "resident": bool(r & R),
                           "data": "index bits" if r & BITS else "tensor-like", "pace_ops": (r >> 8) & 0xFF, "writerlike": bool(r & WRITERLIKE),
+                          "dens": (r >> 17) & 0x1F,
                           "median_us": round(med, 2), "min_us": round(min(ts), 2),
                           "tb_per_s": round(nbytes / (med * 1e-6) / 1e12, 3)}), flush=True)
 
