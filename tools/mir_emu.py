@@ -56,6 +56,8 @@ class Function:
                 continue
             if ln.startswith("End machine code") or ln.startswith("..."):
                 break
+            if ln == "}" or (ln.startswith("BUNDLE") and ln.endswith("{")):
+                continue  # a bundle's members run in order
             self.blocks[cur].append(ln.split(" :: ")[0].split(", debug-location")[0])
 
 
@@ -66,7 +68,7 @@ class Machine:
     # -- operands --------------------------------------------------------------------------------
     @staticmethod
     def _strip(op):
-        op = re.sub(r"\((?:s|p)\d+\)$", "", op.strip())
+        op = re.sub(r"\((?:s|p)\d+\)$|\(tied-def \d+\)$", "", op.strip())
         while True:
             m = re.match(r"^(killed|undef|dead|implicit-def|implicit|renamable|internal|early-clobber|debug-use)\s+(.*)$",
                          op)
@@ -267,6 +269,13 @@ class Machine:
                 x = [None] * n if x[0] is None else [M32 if x[0] else 0] * n
             W(defs[0], x)
             return None
+        if op == "S_BITSET1_B32":  # $d = S_BITSET1_B32 bit, $d(tied)
+            b, d = w1(R(expl[0])), w1(R(expl[1]))
+            W(defs[0], [None if b is None or d is None else d | (1 << (b & 31))])
+            return None
+        if op == "S_MOVK_I32":
+            W(defs[0], [((R(expl[0]) & 0xFFFF) ^ 0x8000) - 0x8000 & M32])
+            return None
         if op == "IMPLICIT_DEF":
             W(defs[0], [None] * 4)
             return None
@@ -326,8 +335,10 @@ class Machine:
         if op == "SI_END_CF":
             self.pr[("exec", 0)], self.pr[("exec", 1)] = M32, M32
             return None
-        m = re.match(r"^V_CMP_(EQ|NE|LG|GT|GE|LT|LE)_(U32|I32)_e64$", op)
+        m = re.match(r"^V_CMP_(EQ|NE|LG|GT|GE|LT|LE)_(U32|I32)_(e64|e32)$", op)
         if m:
+            if m.group(3) == "e32":
+                defs = ["$vcc"]
             a, b = w1(R(expl[0])), w1(R(expl[1]))
             if a is None or b is None:
                 W(defs[0], [None, None])

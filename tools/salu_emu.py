@@ -331,6 +331,12 @@ class Program:
             s(a[0], r)
             st["scc"] = int(r > M32)
             return None
+        m = re.match(r"^s_lshl([1-4])_add_u32$", op)
+        if m:
+            r = ((g(a[1]) << int(m.group(1))) & M32) + g(a[2])
+            s(a[0], r)
+            st["scc"] = int(r > M32)
+            return None
         if op == "s_addk_i32":  # d += simm16
             x, y = _s32(g(a[0])), ((self._imm(a[1]) & 0xFFFF) ^ 0x8000) - 0x8000
             r = x + y
