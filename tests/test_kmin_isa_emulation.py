@@ -78,3 +78,29 @@ def test_kmin_isa_emulation(programs):
     print("mismatches of", len(cs), bad, "slp words", words)
     assert bad["slpscal"] == 0
     assert bad["slp"] > 0  # the defect, reproduced from the instructions alone
+
+
+LLC = "/opt/rocm/llvm/bin/llc"
+
+
+@pytest.mark.skipif(not os.path.exists(LLC), reason="needs the ROCm llc")
+def test_structurizecfg_routes_poison_to_the_store(tmp_path):
+    """tools/kmin_ir_bisect.py in small: the SLP IR's <2 x i32> values carried
+    through llc's IR passes up to unify-loop-exits and scalarized there give
+    machine code (right after amdgpu-isel) that stores no undefined word;
+    carried one pass further, through structurizecfg, it stores undefined
+    words 2 and 3 on the failing cases."""
+    import kmin_ir_bisect as kb
+    kb.OUT = str(tmp_path)
+    cs = cases(120)
+    got = {}
+    for p in ("unify-loop-exits", "structurizecfg"):
+        mir, ll, sc = (str(tmp_path / (x % p)) for x in ("after_%s.mir", "after_%s.ll", "after_%s_scal.ll"))
+        import subprocess
+        subprocess.run([LLC] + kb.T + ["-stop-after=" + p, kb.SRC, "-o", mir], check=True)
+        kb.unwrap(mir, ll)
+        subprocess.run([kb.B + "/opt", "-passes=scalarizer<load-store>", ll, "-S", "-o", sc], check=True)
+        got[p] = kb.undefined_stores(kb.isel_mir(sc, p), cs)
+    print(got)
+    assert got["unify-loop-exits"] == 0
+    assert got["structurizecfg"] > 0
