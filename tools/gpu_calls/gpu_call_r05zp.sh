@@ -14,5 +14,5 @@ for i in 1 2; do
 import json
 for l in open('$D/mods_$i.jsonl'):
     if l.startswith('{'):
-        d = json.loads(l); print($i, d.get('module', '').split('/')[-1], d.get('kernel'), d.get('bad_lanes', d.get('mismatch')))"
+        d = json.loads(l); print($i, d['kernel'].split('/')[-1], d['mismatching_lanes'])"
 done
