@@ -48,12 +48,18 @@ address-order observation writer) and its K timed steps run as coup_step_many's
 rules-trajectory form (chunks of up to 8 steps as one regrouped rules launch
 that keeps the records in registers and stores every step's records, then
 the writer once per step); c3i's InformationStateTensor step is split from
-2^18 lanes.  The same process then times the writer's store ceiling on this
-box: for the split steps coup_measure_store_sweep -- the same
-address-order grid over the same tensor buffer, stores only -- and for the
-fused step coup_measure_step_traffic (its loads and stores with no rules);
-roofline.store_ceiling_ms is that ceiling, frac_of_store_ceiling = ceiling /
-kernel time, store_ceiling_form says which.
+2^18 lanes.  The same process then times a store-only sweep on this box: for
+the split steps coup_measure_store_sweep -- the same address-order grid over
+the same tensor buffer, stores only -- and for the fused step
+coup_measure_step_traffic (its loads and stores with no rules);
+roofline.store_sweep_ms is that time and sweep_over_kernel = sweep / kernel
+time, store_sweep_form says which.  It is NOT a bound: the sweep runs slower
+than the split writers themselves; the bound is the
+spec figure in `peak`.  roofline.valu_issue_frac: VALU instructions per
+launch (profiles/traffic.json, from the SQ_INSTS_VALU pass of the same form)
+x 4 cycles / (1024 SIMDs x the box's gfx clock x the launch's time) -- the
+share of the chip's VALU issue slots the timed launch used; `bound` names
+whichever of the two fractions is higher.
 `box` names the GPU box (boxes differ in HBM store rate).
 cpu_baseline: the C oracle (a scalar port of the reference rules, ~14x
 faster than the reference's own C++ on the survey host) on one
@@ -245,6 +251,59 @@ def _writer(mode_env):
     m = int(mode_env) if mode_env and mode_env.isdigit() and 1 <= int(mode_env) <= 9 else 9
     return {1: (1, 256), 2: (2, 256), 3: (3, 256), 4: (4, 256), 5: (5, 256), 6: (5, 1024), 7: (7, 1024),
             8: (8, 256), 9: (9, 256)}[m]
+
+
+def expected_kernel(cfg, batch, graph):
+    """The kernels the timed steps of config `cfg` at `batch` lanes launch
+    (graph: recorded through capture_steps), spelled as the library's launch
+    log spells them (coup_launch_log; rocprofv3 writes defaulted template
+    arguments out): the mirror of coup_kernels.hip / coup_nplayer.hip's
+    dispatch that the bench line's roofline.kernel reports.  The bench-size
+    parity tests (tests/test_gpu_every_lane.py) assert that the library's log
+    of their own calls equals it."""
+    B = batch
+    _, with_obs, with_info, fused, _, _, players = CONFIGS[cfg]
+    bare = bare_many_active(with_obs, with_info, fused)
+    sorted_ = _regrouped(B)
+    if players != 2:
+        ahead = os.environ.get("COUP_AHEAD", "1") != "0"
+        if fused == "traj" or bare:
+            return ("coup::np::k_trajectory_sorted<%d, 1024>" % players if sorted_ else
+                    "coup::np::k_step_trajectory<%d>" % players)
+        if fused:
+            return ("coup::np::k_rollout_sorted<%d, 1024>" % players if sorted_ else "coup::np::k_rollout<%d>" % players)
+        if sorted_:
+            return "coup::np::k_step_sorted<%d, true, %s, %d>" % (players, "true" if ahead else "false",
+                                                                 _np_step_lanes(players))
+        return "coup::np::k_step<%d, true>" % players
+    if fused == "traj" or bare:
+        return "coup::k_trajectory_sorted<1024, false, false, 8, false>" if sorted_ else "coup::k_step_trajectory"
+    if fused:
+        return "coup::k_rollout_sorted<1024>" if sorted_ else "coup::k_rollout"
+    if with_info:
+        isplit = info_split_active(B)
+        return ("coup::k_step<true, 0, 256, 1, false> + " + _INFO_WRITERS.get(isplit, "coup::k_info_sweep")
+                if isplit else "coup::k_step<true, 0, 256, 2, false>")
+    if with_obs:
+        split = obs_split_active(B)
+        form = step_many_form(B, players, graph)
+        if form == "pipelined":
+            # one launch per step: the rules of step t + 1 beside the writer of step t
+            return "coup::k_step_obs_pipe<512, 2>"
+        if form:
+            # one rules-trajectory launch per chunk of steps + the writer per step
+            stage = os.environ.get("COUP_MANY_STAGE", "0").strip() not in ("0", "")
+            return ("coup::k_trajectory_sorted<1024, false, true, 4, false>" if form == "fused-trajectory" else
+                    "coup::k_trajectory_sorted<1024, true, false, 8, %s> + " % ("true" if stage else "false") +
+                    _SPLIT_WRITERS.get(split, "coup::k_obs_sweep"))
+        if split:
+            # the rules step without tensors (regrouped from 2^18 lanes) + the writer
+            return "coup::k_step_sorted<true, 512> + " + _SPLIT_WRITERS.get(split, "coup::k_obs_sweep")
+        return "coup::k_step<true, %d, %d, 0, false>" % _writer(os.environ.get("COUP_OBS_MODE"))
+    tpl = os.environ.get("COUP_STEP_TPL", "1")
+    if sorted_:
+        return "coup::k_step_sorted<true, 512>"
+    return "coup::k_step_group<%s, true>" % tpl if tpl in ("1", "2", "4") else "coup::k_step<true, 0, 256, 0, false>"
 
 
 def parse():
@@ -452,6 +511,47 @@ def _time_sweep_ceiling(buf, nf4, threads, passes, steps, stream):
     return a.elapsed_time(b) / steps
 
 
+VALU_CLOCK_GHZ = 2.4  # MI355X peak gfx clock (MI355X_MICROARCH.md), when the box's is unreadable
+SIMDS = 1024          # 256 CUs x 4 SIMDs
+
+
+def valu_issue_frac(valu_insts, launch_ms, box):
+    """Share of the chip's VALU issue slots a launch used: VALU instructions
+    (summed over its waves; one wave64 VALU instruction takes 4 SIMD cycles)
+    x 4 / (1024 SIMDs x gfx clock x the launch's time).  None without a
+    profile of the same form."""
+    if not valu_insts or not launch_ms:
+        return None
+    ghz = VALU_CLOCK_GHZ
+    sclk = (box or {}).get("sclk") or ""
+    digits = "".join(c for c in sclk.split(":")[-1] if c.isdigit())
+    if digits and 500 <= int(digits) <= 4000:  # "1: 2376Mhz"
+        ghz = int(digits) / 1000.0
+    return valu_insts * 4.0 / (SIMDS * ghz * 1e9 * launch_ms * 1e-3)
+
+
+def roofline_fields(kernel, launched, achieved, traffic, valu_insts, launch_ms, bytes_per_launch, box, sweep_ms,
+                    sweep_form, step_form):
+    """The line's roofline object.  frac: algorithmic bytes / time against the
+    HBM spec peak (the contract's roofline); valu_issue_frac: the VALU issue
+    slots used (valu_issue_frac()); bound: whichever is higher (VERDICT r5
+    item 4: the tensor-free trajectory forms keep their state in registers
+    and move far fewer bytes than their algorithmic count, so their HBM
+    fraction bounds nothing).  store_sweep_ms is a measurement, not a bound,
+    and no field is called a ceiling."""
+    hbm_frac = achieved / HBM_PEAK_GBS
+    valu_frac = valu_issue_frac(valu_insts, launch_ms, box)
+    return {"bound": "valu" if valu_frac is not None and valu_frac > hbm_frac else "hbm",
+            "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_frac, "traffic": traffic,
+            "kernel": kernel, "kernel_launched": launched, "kernel_ms": launch_ms,
+            "bytes_per_launch": bytes_per_launch,
+            "valu_issue_frac": valu_frac, "valu_insts_per_launch": valu_insts,
+            "store_sweep_ms": sweep_ms, "sweep_over_kernel": (sweep_ms / launch_ms) if sweep_ms else None,
+            "store_sweep_form": sweep_form,
+            "store_sweep_note": "a store-only sweep timed beside the step, not a bound" if sweep_ms else None,
+            "step_form": step_form}
+
+
 def _calibrate_gate(env, stream, launch=None, factor=3.0):
     """Steps of an untimed rollout (the gate) that keep the GPU busy for
     `factor` times the host's enqueue latency of the timed launch (event record
@@ -598,6 +698,7 @@ def main():
     import torch.distributed as dist
 
     from open_spiel_coup_amd import BatchedCoupEnv
+    from open_spiel_coup_amd import _native
     from open_spiel_coup_amd import distributed as D
 
     rank, world, _ = D.world_info()
@@ -639,6 +740,7 @@ def main():
         env.rollout(args.settle)
     graph = None
     timed = None
+    launched = None  # the library's launch log of the timed steps (coup_launch_log)
     if not fused and (args.graph == "on" or (args.graph == "auto" and cfg in GRAPH_AUTO)):
         for _ in range(args.warmup):
             env.step()
@@ -648,7 +750,9 @@ def main():
         env.clear_episode_stats()
         # uniform steps are recorded through coup_step_many: from 2^20 lanes
         # with observations its rules-trajectory split step
+        _native.launch_log()  # clear: the log of the capture is the timed region's kernels
         graph = env.capture_steps(args.steps)
+        launched = _native.launch_log()
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))]
         # no gate ahead of a graph replay: its host submission takes a few
         # us, and a gate's remainder would count in the wall time (c2's
@@ -707,7 +811,11 @@ def main():
     power_warm_steps, power_warm_ms = 0, 0.0
     if args.power_warm_ms > 0:
         tw = time.perf_counter()
+        if graph is None:
+            _native.launch_log()  # clear; the first repeat's launches are the timed region's
         unit()
+        if graph is None:
+            launched = _native.launch_log()
         torch.cuda.synchronize()
         one_ms = (time.perf_counter() - tw) * 1e3
         reps = min(int(args.power_warm_ms / max(one_ms, 1e-3)), 1000)
@@ -776,7 +884,7 @@ def main():
     # box: the split / pipelined steps' address-order writers against a
     # store-only sweep of their tensor buffer with the same grid; the fused
     # step against its own loads and stores with no rules
-    ceiling_ms, ceiling_form = None, None
+    ceiling_ms, ceiling_form = None, None  # the store-only sweep (not a bound, see the docstring)
     if players == 2 and not fused:
         if with_obs and obs_split_active(B):
             ceiling_ms = _time_sweep_ceiling(env.obs, B * 49, 512, 2, args.steps, stream)
@@ -795,7 +903,7 @@ def main():
         bytes_per_launch = bytes_per_lane * B * per_launch
         launch_ms = kern_ms * per_launch
         achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
-        traffic = None
+        traffic, valu_insts = None, None
         if os.path.exists(TRAFFIC_FILE):
             with open(TRAFFIC_FILE) as f:
                 tr = json.load(f)
@@ -803,51 +911,19 @@ def main():
             # the profile of the same form: batch and env steps per launch
             if ent and ent.get("batch") == B and ent.get("steps_per_launch", 1) == per_launch:
                 traffic = ent.get("hbm_bytes_per_launch")
-        sorted_ = "_sorted" if _regrouped(B) else ""
-        if players != 2:
-            ahead = os.environ.get("COUP_AHEAD", "1") != "0"
-            traj = "coup::np::k_trajectory_sorted<%d, 1024>" if sorted_ else "coup::np::k_step_trajectory<%d>"
-            kernel = (traj % players
-                      if fused == "traj" or bare else
-                      ("coup::np::k_rollout_sorted<%d, 1024>" % players if sorted_ else
-                       "coup::np::k_rollout<%d>" % players) if fused else
-                      "coup::np::k_step_sorted<%d, true, %s, %d>" % (players, "true" if ahead else "false",
-                                                                    _np_step_lanes(players)) if sorted_ else
-                      "coup::np::k_step<%d, true>" % players)
-        elif fused == "traj" or bare:
-            kernel = "coup::k_trajectory_sorted<1024, false, false, 8, false>" if sorted_ else "coup::k_step_trajectory"
-        elif fused:
-            kernel = "coup::k_rollout" + sorted_
-        elif with_info:
-            isplit = info_split_active(B)
-            kernel = ("coup::k_step<true, 0, 256, 1, false> + " + _INFO_WRITERS.get(isplit, "coup::k_info_sweep")
-                      if isplit else "coup::k_step<true, 0, 256, 2, false>")
-        elif with_obs:
-            split = obs_split_active(B) if players == 2 else 0
-            form = step_many_form(B, players, graph is not None)
-            if form == "pipelined":
-                # one launch per step: the rules of step t + 1 beside the writer of step t
-                kernel = "coup::k_step_obs_pipe<512, 2>"
-            elif form:
-                # one rules-trajectory launch per chunk of steps + the writer per step
-                stage = os.environ.get("COUP_MANY_STAGE", "0").strip() not in ("0", "")
-                kernel = ("coup::k_trajectory_sorted<1024, false, true, 4, false>" if form == "fused-trajectory" else
-                          "coup::k_trajectory_sorted<1024, true, false, 8, %s> + " % ("true" if stage else "false") +
-                          _SPLIT_WRITERS.get(split, "coup::k_obs_sweep"))
-            elif split:
-                # the rules step without tensors (regrouped from 2^18 lanes) + the writer
-                kernel = "coup::k_step_sorted<true, 512> + " + _SPLIT_WRITERS.get(split, "coup::k_obs_sweep")
-            else:
-                kernel = "coup::k_step<true, %d, %d, 0, false>" % _writer(os.environ.get("COUP_OBS_MODE"))
-        else:
-            tpl = os.environ.get("COUP_STEP_TPL", "1")
-            kernel = ("coup::k_step_group<%s, true>" % tpl if tpl in ("1", "2", "4") else
-                      "coup::k_step<true, 0, 256, 0, false>")
+                valu_insts = ent.get("valu_insts_per_launch")
+        box = _box_identity(dev)
+        kernel = expected_kernel(cfg, B, graph is not None)
+        if launched is not None and launched != kernel:
+            print(f"bench.py: the library launched {launched!r}, not the expected {kernel!r}", file=sys.stderr)
         outputs = ("ObservationTensor fp32 [B][2][98] per step" if with_obs else
                    "InformationStateTensor fp32 [B][2][2492] per step" if with_info else
                    "per-episode statistics only" if fused == "rollout" else
                    "actions, rewards, step types, legal masks, players: [K][B] trajectory buffers" if fused else
-                   "actions, rewards, step types, legal masks, players per step")
+                   "actions, rewards, step types, legal masks, players per step, as ONE coup_step_many trajectory "
+                   "launch for the K steps (state in registers, each step's outputs over the [B] buffers; not "
+                   "comparable with per-step launches: COUP_PIPE=0)" if bare_many_active(with_obs, with_info, fused)
+                   else "actions, rewards, step types, legal masks, players per step")
         line = {
             "metric": "Coup env-steps/sec at batch 2^20, 1/2/4/8 MI355X; HBM GB/s vs peak",
             "value": world * B * args.steps / elapsed,
@@ -869,16 +945,14 @@ def main():
                        "gate_steps": gate.steps,
                        "parallelism": f"dp{world} (env-id sharding)" + ("" if args.dist_backend == "nccl" else
                                                                    " [gloo rehearsal, ranks share GPUs]")},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kernel,
-                         "kernel_ms": launch_ms, "bytes_per_launch": bytes_per_launch,
-                         "store_ceiling_ms": ceiling_ms,
-                         "frac_of_store_ceiling": (ceiling_ms / launch_ms) if ceiling_ms else None,
-                         "store_ceiling_form": ceiling_form,
-                         "step_form": ("trajectory (coup_step_many)" if bare else
-                                       (with_obs and step_many_form(B, players, graph is not None))
-                                       or "split" if (with_obs and players == 2 and obs_split_active(B)) or
-                                       (with_info and info_split_active(B)) else "fused")},
+            "roofline": roofline_fields(
+                kernel=kernel, launched=launched, achieved=achieved, traffic=traffic, valu_insts=valu_insts,
+                launch_ms=launch_ms, bytes_per_launch=bytes_per_launch, box=box, sweep_ms=ceiling_ms,
+                sweep_form=ceiling_form,
+                step_form=("trajectory (coup_step_many)" if bare else
+                           (with_obs and step_many_form(B, players, graph is not None))
+                           or "split" if (with_obs and players == 2 and obs_split_active(B)) or
+                           (with_info and info_split_active(B)) else "fused")),
             "episodes": {"finished": ep_total, "mean_return_p0": ret_total / max(ep_total, 1),
                          "collective": ("all_gather [world*B] int16 (return sum << 8 | episodes per lane)"
                                         if width == 2 else
@@ -891,7 +965,7 @@ def main():
                          "collective_backend": (args.dist_backend + (" (one-rank communicator)" if world == 1 else ""))
                          if grouped else None},
             "lane_errors": errors,
-            "box": _box_identity(dev),
+            "box": box,
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds, with_obs, with_info, players)

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define COUP_ABI_VERSION 13
+#define COUP_ABI_VERSION 14
 
 #define COUP_NUM_PLAYERS 2          /* coup.h:42 */
 #define COUP_MAX_PLAYERS 6          /* N-player extension */
@@ -464,6 +464,18 @@ int coup_info_split_variant(int64_t batch);
  * build/ab/libcoup_mi355x.so for A/B runs and their equality tests). */
 #define COUP_BUILD_AB_VARIANTS 1
 int coup_build_flags(void);
+
+/* The kernels this thread's library calls have launched -- enqueued, or
+ * recorded into a HIP graph being captured -- since the log was last reset:
+ * in first-launch order, repeats collapsed, joined by " + ", spelled as
+ * bench.py's roofline.kernel spells them (rocprofv3 prints the same kernels
+ * with their defaulted template arguments written out).  The step, step_many,
+ * trajectory and rollout paths of both engines note their launches.  Writes
+ * up to cap - 1 bytes and a NUL to buf (may be null), returns the full
+ * length; reset != 0 clears the log after reading it.  Host bookkeeping only
+ * (ABI 14: the every-lane parity tests assert with it that they ran the
+ * kernels the bench line names). */
+int coup_launch_log(char* buf, int cap, int reset);
 
 #ifdef __cplusplus
 }

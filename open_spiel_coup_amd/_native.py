@@ -11,7 +11,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # COUP_LIB_PATH: load another build of the same library (A/B timing of two
 # builds, tools/ab_builds.sh); there is still no fallback
 LIB_PATH = os.environ.get("COUP_LIB_PATH") or os.path.join(HERE, "libcoup_mi355x.so")
-ABI_VERSION = 13
+ABI_VERSION = 14
 FLAG_AUTO_RESET, FLAG_HISTORY, FLAG_GENERIC, FLAG_UNCHECKED = 1, 2, 4, 8
 MAX_PLAYERS = 6
 HISTORY_BYTES = 96
@@ -28,7 +28,7 @@ SYMBOLS = (
     "coup_new_initial_state", "coup_apply_action", "coup_query",
     "coup_export_state", "coup_import_state", "coup_export_history",
     "coup_import_history", "coup_error_count", "coup_slot_op", "coup_slot_ops", "coup_measure_step_traffic", "coup_measure_store_sweep", "coup_obs_split_variant",
-    "coup_info_split_variant", "coup_build_flags",
+    "coup_info_split_variant", "coup_build_flags", "coup_launch_log",
     "coup_server_create", "coup_server_destroy", "coup_attach_server", "coup_server_stats",
     "coup_host_state_init", "coup_host_state_apply", "coup_host_state_tensors", "coup_host_state_string",
     "coup_host_state_step",
@@ -120,6 +120,7 @@ def load():
         "coup_obs_split_variant": ([i64], i32),
         "coup_info_split_variant": ([i64], i32),
         "coup_build_flags": ([], i32),
+        "coup_launch_log": ([ctypes.c_char_p, i32, i32], i32),
         "coup_server_create": ([i64, ctypes.POINTER(vp)], i32),
         "coup_server_destroy": ([vp], i32),
         "coup_attach_server": ([vp, vp], i32),
@@ -139,6 +140,16 @@ def load():
         raise ImportError(f"libcoup_mi355x ABI {L.coup_abi_version()} != {ABI_VERSION}")
     _lib = L
     return L
+
+
+def launch_log(reset=True):
+    """The kernels this thread's library calls launched since the last reset
+    (coup_launch_log): "coup::k_a<...> + coup::k_b<...>"; clears it."""
+    L = load()
+    n = L.coup_launch_log(None, 0, 0)
+    buf = ctypes.create_string_buffer(n + 1)
+    L.coup_launch_log(buf, n + 1, 1 if reset else 0)
+    return buf.value.decode()
 
 
 def check(rc):

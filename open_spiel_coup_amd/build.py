@@ -30,7 +30,7 @@ SOURCES = [os.path.join(CSRC, "coup_kernels.hip"), os.path.join(CSRC, "coup_npla
 HOST_SRC = os.path.join(CSRC, "coup_host.cpp")
 HOST_INC = os.path.join(CSRC, "host")
 DEPS = SOURCES + [os.path.join(CSRC, h) for h in ("coup_lane.h", "coup_nlane.h", "coup_np.h", "coup_regroup.h", "coup_episodes.h",
-                                                 "coup_tensor.h", "coup_knobs.h")] + [
+                                                 "coup_tensor.h", "coup_knobs.h", "coup_launch_log.h")] + [
     os.path.join(ROOT, "include", "coup_mi355x.h"), HOST_SRC, os.path.join(HOST_INC, "hip", "hip_runtime.h")]
 OUT = os.path.join(HERE, "libcoup_mi355x.so")
 OBJ_DIR = os.path.join(ROOT, "build", "obj")  # git-ignored (build/)

@@ -71,10 +71,13 @@ int coup_host_state_init(coup_slot_result* out) {
 // rejected action leaves the record and history unchanged with ok = 0 (and
 // unrepresentable = 1 where the reference accepts it but the result leaves
 // the packed record's fields); an accepted one records its history entry at
-// index move_number_.
+// index move_number_.  Ids 18..127 are rejected actions (ok = 0), as
+// coup_host_state_step and the device lane op report them (DoApplyAction
+// raises: coup.cc:493, :806); negative ids and ids past int8 are invalid
+// arguments (the two host entry points disagreed).
 int coup_host_state_apply(const coup_slot_result* in, int action, int flags, coup_slot_result* out) {
   if (!in || !out) return COUP_E_INVALID;
-  if (action < 0 || action >= COUP_NUM_ACTIONS) return COUP_E_INVALID;
+  if (action < 0 || action > 127) return COUP_E_INVALID;
   const uint32_t x = (uint32_t)action;
   uint8_t hist[kHistoryBytes];
   std::memcpy(hist, in->history, sizeof(hist));

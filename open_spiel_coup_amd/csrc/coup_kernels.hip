@@ -32,6 +32,7 @@ __device__ __forceinline__ void count_philox_eval() {
 #define COUP_PHILOX_HOOK() count_philox_eval()
 #endif
 #include "coup_lane.h"
+#include "coup_launch_log.h"
 #include "coup_mi355x.h"
 #include "coup_np.h"
 #include "coup_regroup.h"
@@ -44,6 +45,53 @@ constexpr int kThreads = 256;
 // (profiles/r02/ab/sort_block_size_2p.log)
 constexpr int kStepSortLanes = 512;
 constexpr int kRolloutSortLanes = 1024;
+
+// The per-thread launch log (coup_launch_log.h): distinct (format, values)
+// entries in first-launch order.
+namespace {
+struct LaunchNote {
+  const char* fmt;
+  int v[5];
+};
+constexpr int kLaunchNotes = 32;
+thread_local LaunchNote g_launch_notes[kLaunchNotes];
+thread_local int g_launch_count = 0;
+}  // namespace
+
+void note_launch(const char* fmt, int v0, int v1, int v2, int v3, int v4) {
+  const int v[5] = {v0, v1, v2, v3, v4};
+  for (int i = 0; i < g_launch_count; ++i)
+    if (g_launch_notes[i].fmt == fmt && std::memcmp(g_launch_notes[i].v, v, sizeof(v)) == 0) return;
+  if (g_launch_count == kLaunchNotes) return;
+  LaunchNote& e = g_launch_notes[g_launch_count++];
+  e.fmt = fmt;
+  std::memcpy(e.v, v, sizeof(v));
+}
+
+std::string launch_log_text() {
+  std::string out;
+  for (int i = 0; i < g_launch_count; ++i) {
+    if (i) out += " + ";
+    const LaunchNote& e = g_launch_notes[i];
+    int k = 0;
+    for (const char* c = e.fmt; *c; ++c) {
+      if (c[0] == '{' && c[1] == '}') {
+        out += std::to_string(k < 5 ? e.v[k] : 0);
+        ++k;
+        ++c;
+      } else if (c[0] == '{' && c[1] == 'b' && c[2] == '}') {
+        out += (k < 5 && e.v[k]) ? "true" : "false";
+        ++k;
+        c += 2;
+      } else {
+        out += *c;
+      }
+    }
+  }
+  return out;
+}
+
+void clear_launch_log() { g_launch_count = 0; }
 
 // The RNG key of lane i (global env id).  A measurement
 // build with -DCOUP_ABLATE_SAME_STREAM gives every lane the same stream, so
@@ -2560,7 +2608,6 @@ struct coup_env {
   int64_t traj_cap;           // steps per rules-trajectory launch the buffer holds (COUP_TRAJ_CHUNK at create)
   uint4* state2;              // = traj_rec: the second record buffer of the merged pipelined step
   hipStream_t aux;            // kManyOverlap (measurement builds): the rules trajectories' stream
-  hipStream_t aux_w;          // ... and with COUP_OVERLAP_CUS the writers' (both CU-masked)
   hipEvent_t ev_fork, ev_rules[2], ev_writers[2];  // kManyOverlap's fork / chunk events
   coup::Knobs knobs;          // dispatch knobs, read once at coup_create (coup_knobs.h)
 };
@@ -2706,6 +2753,7 @@ unsigned step_grid(int64_t groups, int) { return (unsigned)(groups > 0 ? groups 
 template <bool U, int M, int T, int I, bool UC = false>
 void launch_step(const coup_env*, const coup::StepArgs& a, int64_t n, unsigned dyn_lds, hipStream_t s) {
   const int64_t groups = (n + T - 1) / T;
+  coup::note_launch("coup::k_step<{b}, {}, {}, {}, {b}>", U, M, T, I, UC);
   coup::k_step<U, M, T, I, UC><<<step_grid(groups, T), T, dyn_lds, s>>>(a);
 }
 unsigned grid_for(int64_t n) { return (unsigned)((n + coup::kThreads - 1) / coup::kThreads); }
@@ -2888,7 +2936,6 @@ namespace {
 void release(coup_env* env) {
   (void)hipFree(env->state);
   (void)hipFree(env->traj_rec);
-  if (env->aux_w) (void)hipStreamDestroy(env->aux_w);
   if (env->aux) {
     (void)hipStreamDestroy(env->aux);
     for (hipEvent_t ev : {env->ev_fork, env->ev_rules[0], env->ev_rules[1], env->ev_writers[0], env->ev_writers[1]})
@@ -2904,23 +2951,8 @@ void release(coup_env* env) {
 }
 
 #ifdef COUP_AB_VARIANTS
-// CU mask of `m` of the device's CUs (m > 0; 8-CU groups spread evenly over
-// the mask, so over the XCDs whichever way the mask's bits map to them), or
-// the complement
-std::vector<uint32_t> cu_mask(int cus, int m, bool complement) {
-  std::vector<uint32_t> w((size_t)(cus + 31) / 32, 0u);
-  const int groups = std::max(1, cus / 8), take = std::max(1, std::min(groups, m / 8));
-  for (int g = 0; g < groups; ++g) {
-    const bool on = ((int64_t)g * take / groups) != ((int64_t)(g + 1) * take / groups);  // `take` of the groups
-    if (on == complement) continue;
-    for (int i = g * 8; i < g * 8 + 8 && i < cus; ++i) w[(size_t)i / 32] |= 1u << (i % 32);
-  }
-  return w;
-}
-
 // coup_step_many's overlapped form (kManyOverlap, measurement builds): a
-// second stream for the rules trajectories (with COUP_OVERLAP_CUS, CU-masked
-// streams for the rules and the writers), the fork / chunk events, and the
+// second stream for the rules trajectories, the fork / chunk events, and the
 // record buffer grown to two chunks.  Created at coup_create where the form
 // applies, else at the first call that needs them outside a graph capture.
 int overlap_resources(coup_env* env) {
@@ -2929,34 +2961,20 @@ int overlap_resources(coup_env* env) {
   uint4* rec = nullptr;
   hipError_t e = hipMalloc(&rec, lanes * sizeof(uint4) * 2 * env->traj_cap);
   if (e != hipSuccess) return fail(COUP_E_HIP, std::string("coup_step_many: ") + hipGetErrorString(e));
-  hipStream_t aux = nullptr, aux_w = nullptr;
+  hipStream_t aux = nullptr;
   hipEvent_t ev[5] = {};
-  if (env->knobs.overlap_cus > 0) {
-    int dev = 0, cus = 0;
-    e = hipGetDevice(&dev);
-    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (e == hipSuccess) {
-      const std::vector<uint32_t> r = cu_mask(cus, env->knobs.overlap_cus, false);
-      const std::vector<uint32_t> w = cu_mask(cus, env->knobs.overlap_cus, true);
-      e = hipExtStreamCreateWithCUMask(&aux, (uint32_t)r.size(), r.data());
-      if (e == hipSuccess) e = hipExtStreamCreateWithCUMask(&aux_w, (uint32_t)w.size(), w.data());
-    }
-  } else {
-    e = hipStreamCreateWithFlags(&aux, hipStreamNonBlocking);
-  }
+  e = hipStreamCreateWithFlags(&aux, hipStreamNonBlocking);
   for (int i = 0; i < 5 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&ev[i], hipEventDisableTiming);
   if (e != hipSuccess) {
     for (hipEvent_t x : ev)
       if (x) (void)hipEventDestroy(x);
     if (aux) (void)hipStreamDestroy(aux);
-    if (aux_w) (void)hipStreamDestroy(aux_w);
     (void)hipFree(rec);
     return fail(COUP_E_HIP, std::string("coup_step_many: ") + hipGetErrorString(e));
   }
   (void)hipFree(env->traj_rec);  // synchronises: no launch in flight still reads it
   env->traj_rec = env->state2 = rec;
   env->aux = aux;
-  env->aux_w = aux_w;
   env->ev_fork = ev[0];
   env->ev_rules[0] = ev[1];
   env->ev_rules[1] = ev[2];
@@ -3024,14 +3042,18 @@ int coup_create_ex(int64_t batch, uint64_t seed, uint32_t env_id_base, int flags
   env->traj_cap = 0;
   env->state2 = nullptr;
   env->aux = nullptr;
-  env->aux_w = nullptr;
   env->ev_fork = env->ev_rules[0] = env->ev_rules[1] = env->ev_writers[0] = env->ev_writers[1] = nullptr;
   env->knobs = coup::read_knobs();
   const size_t lanes = (size_t)(batch > 0 ? batch : 1);
   hipError_t e = hipMalloc(&env->state, lanes * sizeof(uint4) * (generic ? 2 : 1));
   // coup_step_many's per-step record buffer (allocated here: coup_step_many
-  // may be captured into a HIP graph, where no allocation may happen)
-  if (e == hipSuccess && !generic) {
+  // may be captured into a HIP graph, where no allocation may happen), only
+  // where its rules-trajectory split step can apply -- the split observation
+  // step's batch (or COUP_OBS_SPLIT forced), no history, COUP_PIPE not 0
+  // (every 2-player env paid traj_chunk x 16 B per lane for it);
+  // many_form runs one coup_step per step where it is missing
+  if (e == hipSuccess && !generic && !(flags & COUP_FLAG_HISTORY) && env->knobs.pipe != coup::kManySerial &&
+      obs_split(env->knobs, batch) != 0) {
     env->traj_cap = env->knobs.traj_chunk;
     e = hipMalloc(&env->traj_rec, lanes * sizeof(uint4) * env->traj_cap);
     env->state2 = env->traj_rec;
@@ -3200,6 +3222,7 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
       const int64_t nf4 = n * coup::kInfoF4;
       auto go = [&](auto tt, auto ss) {
         constexpr int T = decltype(tt)::value, S = decltype(ss)::value;
+        coup::note_launch("coup::k_info_sweep<{}, {}>", T, S);
         coup::k_info_sweep<T, S><<<(unsigned)((nf4 + T * S - 1) / (T * S)), T, 0, s>>>(env->state, env->hist, a.info,
                                                                                         n);
       };
@@ -3210,11 +3233,11 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
           // the shipped shape; COUP_WRITER_POL: its stores plain / sc1 / sc1 nt (-1, 0: the shipped nt)
           const unsigned g = (unsigned)((nf4 + 2047) / 2048);
           if (env->knobs.writer_pol == 1)
-            coup::k_info_sweep<1024, 2, 1><<<g, 1024, 0, s>>>(env->state, env->hist, a.info, n);
+            coup::note_launch("coup::k_info_sweep<1024, 2, 1>"), coup::k_info_sweep<1024, 2, 1><<<g, 1024, 0, s>>>(env->state, env->hist, a.info, n);
           else if (env->knobs.writer_pol == 2)
-            coup::k_info_sweep<1024, 2, 2><<<g, 1024, 0, s>>>(env->state, env->hist, a.info, n);
+            coup::note_launch("coup::k_info_sweep<1024, 2, 2>"), coup::k_info_sweep<1024, 2, 2><<<g, 1024, 0, s>>>(env->state, env->hist, a.info, n);
           else if (env->knobs.writer_pol == 3)
-            coup::k_info_sweep<1024, 2, 3><<<g, 1024, 0, s>>>(env->state, env->hist, a.info, n);
+            coup::note_launch("coup::k_info_sweep<1024, 2, 3>"), coup::k_info_sweep<1024, 2, 3><<<g, 1024, 0, s>>>(env->state, env->hist, a.info, n);
           else
             go(std::integral_constant<int, 1024>(), std::integral_constant<int, 2>());
           break;
@@ -3245,12 +3268,13 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
       const int64_t nf4 = n * coup::kRowF4;
       auto rows = [&](auto tt, auto ss) {
         constexpr int T = decltype(tt)::value, S = decltype(ss)::value;
+        coup::note_launch("coup::k_obs_sweep_rows<{}, {}>", T, S);
         coup::k_obs_sweep_rows<T, S><<<(unsigned)((nf4 + T * S - 1) / (T * S)), T, 0, s>>>(env->state, a.obs, n);
       };
 #ifdef COUP_AB_VARIANTS
       const unsigned g = (unsigned)((nf4 + 255) / 256);
       switch (split) {
-        case 2: coup::k_obs_sweep<0><<<g, 256, 0, s>>>(env->state, a.obs, n); break;
+        case 2: coup::note_launch("coup::k_obs_sweep<0>"), coup::k_obs_sweep<0><<<g, 256, 0, s>>>(env->state, a.obs, n); break;
         case 3: rows(std::integral_constant<int, 256>(), std::integral_constant<int, 1>()); break;
         case 4: rows(std::integral_constant<int, 256>(), std::integral_constant<int, 2>()); break;
         case 5: rows(std::integral_constant<int, 128>(), std::integral_constant<int, 1>()); break;
@@ -3265,7 +3289,7 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
         case 15: rows(std::integral_constant<int, 1024>(), std::integral_constant<int, 1>()); break;
         case 16: rows(std::integral_constant<int, 512>(), std::integral_constant<int, 3>()); break;
         case 17: rows(std::integral_constant<int, 512>(), std::integral_constant<int, 4>()); break;
-        default: coup::k_obs_sweep<1><<<g, 256, 0, s>>>(env->state, a.obs, n); break;
+        default: coup::note_launch("coup::k_obs_sweep<1>"), coup::k_obs_sweep<1><<<g, 256, 0, s>>>(env->state, a.obs, n); break;
       }
 #else
       (void)split;
@@ -3279,6 +3303,7 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
     auto go = [&](auto tb) {
       constexpr int TB = decltype(tb)::value;
       const unsigned g = (unsigned)((n + TB - 1) / TB);
+      coup::note_launch("coup::k_step_sorted<{b}, {}>", uniform, TB);
       if (uniform)
         coup::k_step_sorted<true, TB><<<g, TB, 0, s>>>(a);
       else
@@ -3306,6 +3331,7 @@ int coup_step(coup_env* env, const int8_t* actions, const coup_step_outputs* out
       auto go = [&](auto tp) {
         constexpr int TP = decltype(tp)::value;
         const unsigned g = (unsigned)((n + 256 / TP - 1) / (256 / TP));
+        coup::note_launch("coup::k_step_group<{}, {b}>", TP, uniform);
         if (uniform)
           coup::k_step_group<TP, true><<<g, 256, 0, s>>>(a);
         else
@@ -3412,16 +3438,19 @@ int coup_rollout(coup_env* env, int64_t steps, const coup_rollout_stats* stats) 
     const int64_t n = env->batch;
 #ifdef COUP_AB_VARIANTS
     switch (coup::sort_lanes(env->knobs.sort_lanes, coup::kRolloutSortLanes)) {
-      case 256: coup::k_rollout_sorted<256><<<grid_for(n), 256, 0, env->stream>>>(a); break;
-      case 512: coup::k_rollout_sorted<512><<<(unsigned)((n + 511) / 512), 512, 0, env->stream>>>(a); break;
-      default: coup::k_rollout_sorted<1024><<<(unsigned)((n + 1023) / 1024), 1024, 0, env->stream>>>(a); break;
+      case 256: coup::note_launch("coup::k_rollout_sorted<256>"), coup::k_rollout_sorted<256><<<grid_for(n), 256, 0, env->stream>>>(a); break;
+      case 512: coup::note_launch("coup::k_rollout_sorted<512>"), coup::k_rollout_sorted<512><<<(unsigned)((n + 511) / 512), 512, 0, env->stream>>>(a); break;
+      default: coup::note_launch("coup::k_rollout_sorted<1024>"), coup::k_rollout_sorted<1024><<<(unsigned)((n + 1023) / 1024), 1024, 0, env->stream>>>(a); break;
     }
 #else
     constexpr int TB = coup::kRolloutSortLanes;
+    coup::note_launch("coup::k_rollout_sorted<{}>", TB);
     coup::k_rollout_sorted<TB><<<(unsigned)((n + TB - 1) / TB), TB, 0, env->stream>>>(a);
 #endif
-  } else
+  } else {
+    coup::note_launch("coup::k_rollout");
     coup::k_rollout<<<grid_for(env->batch), coup::kThreads, 0, env->stream>>>(a);
+  }
   COUP_HIP_TRY(hipGetLastError());
   return COUP_OK;
 }
@@ -3600,8 +3629,7 @@ coup::StepArgs uniform_args(const coup_env* env, const coup_step_outputs* out) {
 // accumulators -- equal `steps` coup_step calls; `slices`: step t's outputs
 // go to slice t of [steps][B][...] buffers, else every step overwrites out's.
 // `overlap` (kManyOverlap, measurement builds): the rules trajectories run
-// on env->aux, chunk c + 1's beside chunk c's writers on env->stream (or
-// env->aux_w), the records alternating between two chunk buffers; events
+// on env->aux, chunk c + 1's beside chunk c's writers on env->stream, the records alternating between two chunk buffers; events
 // order each writer chunk after its rules and each rules chunk after the
 // writers that last read its buffer.  The streams join back into
 // env->stream, so the call is one fork / join, capturable into a HIP graph.
@@ -3628,6 +3656,7 @@ int step_many_fused(coup_env* env, int64_t steps, const coup_step_outputs* out, 
   const coup::TrajOut x{nullptr, slices ? n : 0, slices ? n * 2 * COUP_OBS_SIZE : 0};
   auto go = [&](auto tt, auto ww) {
     constexpr int T = decltype(tt)::value, W = decltype(ww)::value;
+    coup::note_launch("coup::k_trajectory_sorted<{}, false, true, {}, false>", T, W);
     coup::k_trajectory_sorted<T, false, true, W><<<(unsigned)((n + T - 1) / T), T, 0, env->stream>>>(a, steps, x);
   };
   switch (env->knobs.fused_shape) {  // COUP_FUSED_SHAPE
@@ -3648,7 +3677,7 @@ int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, b
   const int64_t nf4 = n * coup::kRowF4;
   const unsigned wgrid = (unsigned)((nf4 + 1023) / 1024);  // 512 threads x 2 passes
   const hipStream_t R = overlap ? env->aux : env->stream;
-  const hipStream_t S = overlap && env->aux_w ? env->aux_w : env->stream;  // the writers'
+  const hipStream_t S = env->stream;  // the writers'
   if (overlap) {
     COUP_HIP_TRY(hipEventRecord(env->ev_fork, env->stream));
     COUP_HIP_TRY(hipStreamWaitEvent(R, env->ev_fork, 0));
@@ -3672,10 +3701,12 @@ int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, b
 #ifdef COUP_AB_VARIANTS
     auto shape = [&](auto tt, auto ww) {  // COUP_MANY_SHAPE: lanes per block, waves per SIMD budget
       constexpr int T = decltype(tt)::value, W = decltype(ww)::value;
+      coup::note_launch("coup::k_trajectory_sorted<{}, true, false, {}, false>", T, W);
       coup::k_trajectory_sorted<T, true, false, W, false><<<(unsigned)((n + T - 1) / T), T, 0, R>>>(a, c, x);
     };
     if (env->knobs.many_stage)  // outputs staged by lane: 148.3 against 134.5 us per step (call r05m)
-      coup::k_trajectory_sorted<TB, true, false, 8, true><<<grid, TB, 0, R>>>(a, c, x);
+      coup::note_launch("coup::k_trajectory_sorted<{}, true, false, 8, true>", TB),
+          coup::k_trajectory_sorted<TB, true, false, 8, true><<<grid, TB, 0, R>>>(a, c, x);
     else if (env->knobs.many_shape == 1)
       shape(std::integral_constant<int, 512>(), std::integral_constant<int, 8>());
     else if (env->knobs.many_shape == 2)
@@ -3685,10 +3716,12 @@ int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, b
     else if (env->knobs.many_shape == 4)
       shape(std::integral_constant<int, 1024>(), std::integral_constant<int, 4>());
     else if (overlap && env->knobs.overlap_lds > 0)  // COUP_OVERLAP_LDS: cap the rules' blocks per CU
-      coup::k_trajectory_sorted<TB, true, false, 8, false><<<grid, TB, (unsigned)env->knobs.overlap_lds, R>>>(a, c, x);
+      coup::note_launch("coup::k_trajectory_sorted<{}, true, false, 8, false>", TB),
+          coup::k_trajectory_sorted<TB, true, false, 8, false><<<grid, TB, (unsigned)env->knobs.overlap_lds, R>>>(a, c, x);
     else
 #endif
-      coup::k_trajectory_sorted<TB, true, false, 8, false><<<grid, TB, 0, R>>>(a, c, x);
+      coup::note_launch("coup::k_trajectory_sorted<{}, true, false, 8, false>", TB),
+          coup::k_trajectory_sorted<TB, true, false, 8, false><<<grid, TB, 0, R>>>(a, c, x);
     COUP_HIP_TRY(hipGetLastError());
     if (overlap) {
       COUP_HIP_TRY(hipEventRecord(env->ev_rules[b], R));
@@ -3698,18 +3731,18 @@ int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, b
       float* obs = out->obs + (slices ? (t0 + s) * n * 2 * COUP_OBS_SIZE : 0);
 #ifdef COUP_AB_VARIANTS
       if (env->knobs.writer_pol == 1)  // (-1 / 0: the shipped non-temporal stores)
-        coup::k_obs_sweep_rows<512, 2, 1><<<wgrid, 512, 0, S>>>(rec + s * n, obs, n);
+        coup::note_launch("coup::k_obs_sweep_rows<512, 2, 1>"), coup::k_obs_sweep_rows<512, 2, 1><<<wgrid, 512, 0, S>>>(rec + s * n, obs, n);
       else if (env->knobs.writer_pol == 2)
-        coup::k_obs_sweep_rows<512, 2, 2><<<wgrid, 512, 0, S>>>(rec + s * n, obs, n);
+        coup::note_launch("coup::k_obs_sweep_rows<512, 2, 2>"), coup::k_obs_sweep_rows<512, 2, 2><<<wgrid, 512, 0, S>>>(rec + s * n, obs, n);
       else if (env->knobs.writer_pol == 3)
-        coup::k_obs_sweep_rows<512, 2, 3><<<wgrid, 512, 0, S>>>(rec + s * n, obs, n);
+        coup::note_launch("coup::k_obs_sweep_rows<512, 2, 3>"), coup::k_obs_sweep_rows<512, 2, 3><<<wgrid, 512, 0, S>>>(rec + s * n, obs, n);
       else if (env->knobs.writer_prio == 1)
-        coup::k_obs_sweep_rows<512, 2, 0, 1><<<wgrid, 512, 0, S>>>(rec + s * n, obs, n);
+        coup::note_launch("coup::k_obs_sweep_rows<512, 2, 0, 1>"), coup::k_obs_sweep_rows<512, 2, 0, 1><<<wgrid, 512, 0, S>>>(rec + s * n, obs, n);
       else if (env->knobs.writer_prio >= 2)
-        coup::k_obs_sweep_rows<512, 2, 0, 3><<<wgrid, 512, 0, S>>>(rec + s * n, obs, n);
+        coup::note_launch("coup::k_obs_sweep_rows<512, 2, 0, 3>"), coup::k_obs_sweep_rows<512, 2, 0, 3><<<wgrid, 512, 0, S>>>(rec + s * n, obs, n);
       else
 #endif
-        coup::k_obs_sweep_rows<512, 2><<<wgrid, 512, 0, S>>>(rec + s * n, obs, n);
+        coup::note_launch("coup::k_obs_sweep_rows<512, 2>"), coup::k_obs_sweep_rows<512, 2><<<wgrid, 512, 0, S>>>(rec + s * n, obs, n);
       COUP_HIP_TRY(hipGetLastError());
     }
     if (overlap) COUP_HIP_TRY(hipEventRecord(env->ev_writers[b], S));
@@ -3720,15 +3753,14 @@ int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, b
 }
 
 #ifdef COUP_AB_VARIANTS
-// kManyOverlap's resources, or false where they cannot be made or used now
-// -- a graph capture on env->stream without them, or with CU-masked streams
-// (capturing work forked onto a CU-masked stream crashed the HIP runtime,
-// call r05j): the call then runs as kManyTraj, same results.
+// kManyOverlap's resources, or false where they cannot be made now -- a graph
+// capture on env->stream without them: the call then runs as kManyTraj, same
+// results.
 bool overlap_ready(coup_env* env) {
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
   const bool capturing =
       hipStreamIsCapturing(env->stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone;
-  if (env->aux) return !(capturing && env->aux_w);
+  if (env->aux) return true;
   if (capturing) return false;
   return overlap_resources(env) == COUP_OK;
 }
@@ -3774,6 +3806,7 @@ int step_many_pipelined(coup_env* env, int64_t steps, const coup_step_outputs* o
     p.obs = writer ? out->obs + (slices ? (m - 1) * n * 2 * COUP_OBS_SIZE : 0) : nullptr;
     const uint32_t total = p.rules_blocks + p.writer_blocks;
     p.stride = (rules && writer) ? std::max<uint32_t>(1u, (uint32_t)(env->knobs.pipe_span * total / R)) : 1u;
+    coup::note_launch("coup::k_step_obs_pipe<{}, {}>", kPipeT, kPipeS);
     coup::k_step_obs_pipe<kPipeT, kPipeS><<<total, kPipeT, 0, env->stream>>>(p);
     COUP_HIP_TRY(hipGetLastError());
     cur = next;
@@ -3813,8 +3846,10 @@ int step_many_bare(coup_env* env, int64_t steps, const coup_step_outputs* out) {
   }
   if (coup::regroup_lanes(env->knobs, n)) {
     constexpr int TB = coup::kRolloutSortLanes;
+    coup::note_launch("coup::k_trajectory_sorted<{}, false, false, 8, false>", TB);
     coup::k_trajectory_sorted<TB><<<(unsigned)((n + TB - 1) / TB), TB, 0, env->stream>>>(a, steps, {nullptr, 0});
   } else {
+    coup::note_launch("coup::k_step_trajectory");
     coup::k_step_trajectory<<<grid_for(n), coup::kThreads, 0, env->stream>>>(a, steps, 0);
   }
   COUP_HIP_TRY(hipGetLastError());
@@ -3915,19 +3950,26 @@ int coup_step_trajectory(coup_env* env, int64_t steps, const coup_step_outputs* 
   if (coup::regroup_lanes(env->knobs, n)) {
 #ifdef COUP_AB_VARIANTS
     switch (coup::sort_lanes(env->knobs.sort_lanes, coup::kRolloutSortLanes)) {
-      case 256: coup::k_trajectory_sorted<256><<<grid_for(n), 256, 0, env->stream>>>(a, steps, {nullptr, n}); break;
+      case 256:
+        coup::note_launch("coup::k_trajectory_sorted<256, false, false, 8, false>");
+        coup::k_trajectory_sorted<256><<<grid_for(n), 256, 0, env->stream>>>(a, steps, {nullptr, n});
+        break;
       case 512:
+        coup::note_launch("coup::k_trajectory_sorted<512, false, false, 8, false>");
         coup::k_trajectory_sorted<512><<<(unsigned)((n + 511) / 512), 512, 0, env->stream>>>(a, steps, {nullptr, n});
         break;
       default:
+        coup::note_launch("coup::k_trajectory_sorted<1024, false, false, 8, false>");
         coup::k_trajectory_sorted<1024><<<(unsigned)((n + 1023) / 1024), 1024, 0, env->stream>>>(a, steps, {nullptr, n});
         break;
     }
 #else
     constexpr int TB = coup::kRolloutSortLanes;
+    coup::note_launch("coup::k_trajectory_sorted<{}, false, false, 8, false>", TB);
     coup::k_trajectory_sorted<TB><<<(unsigned)((n + TB - 1) / TB), TB, 0, env->stream>>>(a, steps, {nullptr, n});
 #endif
   } else {
+    coup::note_launch("coup::k_step_trajectory");
     coup::k_step_trajectory<<<grid_for(n), coup::kThreads, 0, env->stream>>>(a, steps, n);
   }
   COUP_HIP_TRY(hipGetLastError());
@@ -4396,6 +4438,17 @@ int coup_error_count(coup_env* env, int64_t* out) {
 int coup_obs_split_variant(int64_t batch) { return batch > 0 ? obs_split(coup::read_knobs(), batch) : 0; }
 
 int coup_info_split_variant(int64_t batch) { return batch > 0 ? info_split(coup::read_knobs(), batch) : 0; }
+
+int coup_launch_log(char* buf, int cap, int reset) {
+  const std::string t = coup::launch_log_text();
+  if (buf && cap > 0) {
+    const size_t m = std::min<size_t>(t.size(), (size_t)cap - 1);
+    std::memcpy(buf, t.data(), m);
+    buf[m] = 0;
+  }
+  if (reset) coup::clear_launch_log();
+  return (int)t.size();
+}
 
 int coup_build_flags(void) {
 #ifdef COUP_AB_VARIANTS

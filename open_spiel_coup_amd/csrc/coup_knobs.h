@@ -60,7 +60,6 @@ struct Knobs {
   int np_traj_stage = 1;    // COUP_TRAJ_STAGE
   int np_scan = 1;          // COUP_NP_SCAN
   double pipe_span = kPipeSpanDefault;  // COUP_PIPE_SPAN in (0, 1] (kManyPipe)
-  int overlap_cus = 0;  // COUP_OVERLAP_CUS: kManyOverlap's rules on this many CUs (CU-masked streams), 0 unmasked
   int many_stage = 0;   // COUP_MANY_STAGE: the rules trajectory's outputs staged by lane (coalesced stores)
   int writer_pol = -1;  // COUP_WRITER_POL: the split writers' stores (-1 shipped, 0 nt, 1 plain, 2 sc1, 3 sc1 nt)
   int writer_prio = 0;  // COUP_WRITER_PRIO: the split writer's waves at s_setprio 1 (1) or 3 (2)
@@ -102,7 +101,6 @@ inline Knobs read_knobs() {
   k.np_reset_group = knob_int("COUP_NP_RESET_GROUP", 0);
   k.np_traj_stage = knob_int("COUP_TRAJ_STAGE", 1);
   k.np_scan = knob_int("COUP_NP_SCAN", 1) != 0;
-  k.overlap_cus = knob_int("COUP_OVERLAP_CUS", 0);
   k.fused_shape = knob_int("COUP_FUSED_SHAPE", 0);
   k.many_stage = knob_int("COUP_MANY_STAGE", 0) != 0;
   k.many_shape = knob_int("COUP_MANY_SHAPE", 0);

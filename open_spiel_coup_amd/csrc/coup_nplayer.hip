@@ -22,6 +22,7 @@ __device__ __forceinline__ void count_philox_eval() {
 }
 #define COUP_PHILOX_HOOK() count_philox_eval()
 #endif
+#include "coup_launch_log.h"
 #include "coup_nlane.h"
 #include "coup_np.h"
 #include "coup_regroup.h"
@@ -1049,15 +1050,20 @@ hipError_t launch_step(const Env& e, const int8_t* actions, const coup_step_outp
         constexpr int TB = decltype(lanes)::value;
         const unsigned g = grid_for(e.n, TB);
         if (actions)
-          k_step_sorted<N, false, false, TB><<<g, TB, 0, e.stream>>>(a);
+          note_launch("coup::np::k_step_sorted<{}, false, false, {}>", N, TB),
+              k_step_sorted<N, false, false, TB><<<g, TB, 0, e.stream>>>(a);
         else if (ahead && inl)
-          k_step_sorted<N, true, true, TB, true><<<g, TB, 0, e.stream>>>(a);
+          note_launch("coup::np::k_step_sorted<{}, true, true, {}, true>", N, TB),
+              k_step_sorted<N, true, true, TB, true><<<g, TB, 0, e.stream>>>(a);
         else if (ahead && single)
-          k_step_sorted<N, true, true, TB, false, 1><<<g, TB, 0, e.stream>>>(a);
+          note_launch("coup::np::k_step_sorted<{}, true, true, {}, false, 1>", N, TB),
+              k_step_sorted<N, true, true, TB, false, 1><<<g, TB, 0, e.stream>>>(a);
         else if (ahead)
-          k_step_sorted<N, true, true, TB><<<g, TB, 0, e.stream>>>(a);
+          note_launch("coup::np::k_step_sorted<{}, true, true, {}>", N, TB),
+              k_step_sorted<N, true, true, TB><<<g, TB, 0, e.stream>>>(a);
         else
-          k_step_sorted<N, true, false, TB><<<g, TB, 0, e.stream>>>(a);
+          note_launch("coup::np::k_step_sorted<{}, true, false, {}>", N, TB),
+              k_step_sorted<N, true, false, TB><<<g, TB, 0, e.stream>>>(a);
       };
       switch (sort_lanes(e.knobs.np_sort_lanes, step_sort_lanes(N))) {
         case 256: go(std::integral_constant<int, 256>()); break;
@@ -1069,17 +1075,23 @@ hipError_t launch_step(const Env& e, const int8_t* actions, const coup_step_outp
       // groups, step_sort_lanes(N) lanes per block
       constexpr int TB = step_sort_lanes(N);
       const unsigned g = grid_for(e.n, TB);
+      note_launch("coup::np::k_step_sorted<{}, {b}, {b}, {}>", N, !actions, !actions, TB);
       if (actions)
         k_step_sorted<N, false, false, TB><<<g, TB, 0, e.stream>>>(a);
       else
         k_step_sorted<N, true, true, TB><<<g, TB, 0, e.stream>>>(a);
 #endif
     } else if (actions) {
+      note_launch("coup::np::k_step<{}, false>", N);
       k_step<N, false><<<grid, kThreads, 0, e.stream>>>(a);
     } else {
+      note_launch("coup::np::k_step<{}, true>", N);
       k_step<N, true><<<grid, kThreads, 0, e.stream>>>(a);
     }
-    if (obs) k_obs<N><<<grid_for(e.n, kObsLanes), kThreads, 0, e.stream>>>(e.sa, e.sb, e.n, obs);
+    if (obs) {
+      note_launch("coup::np::k_obs<{}>", N);
+      k_obs<N><<<grid_for(e.n, kObsLanes), kThreads, 0, e.stream>>>(e.sa, e.sb, e.n, obs);
+    }
   });
 }
 
@@ -1107,21 +1119,31 @@ hipError_t launch_trajectory(const Env& e, int64_t steps, const coup_step_output
     if (regroup_lanes(e.knobs, e.n)) {
 #ifdef COUP_AB_VARIANTS
       switch (sort_lanes(e.knobs.np_sort_lanes, kRolloutSortLanes)) {
-        case 256: k_trajectory_sorted<N, 256><<<grid_for(e.n, 256), 256, 0, e.stream>>>(a, steps); break;
-        case 512: k_trajectory_sorted<N, 512><<<grid_for(e.n, 512), 512, 0, e.stream>>>(a, steps); break;
+        case 256:
+          note_launch("coup::np::k_trajectory_sorted<{}, 256>", N);
+          k_trajectory_sorted<N, 256><<<grid_for(e.n, 256), 256, 0, e.stream>>>(a, steps);
+          break;
+        case 512:
+          note_launch("coup::np::k_trajectory_sorted<{}, 512>", N);
+          k_trajectory_sorted<N, 512><<<grid_for(e.n, 512), 512, 0, e.stream>>>(a, steps);
+          break;
         default:
           // COUP_TRAJ_STAGE=0: the round-2 stores (1024-lane blocks)
           if (e.knobs.np_traj_stage == 0)
-            k_trajectory_sorted<N, 1024, 0><<<grid_for(e.n, 1024), 1024, 0, e.stream>>>(a, steps);
+            note_launch("coup::np::k_trajectory_sorted<{}, 1024, 0>", N),
+                k_trajectory_sorted<N, 1024, 0><<<grid_for(e.n, 1024), 1024, 0, e.stream>>>(a, steps);
           else
-            k_trajectory_sorted<N, 1024><<<grid_for(e.n, 1024), 1024, 0, e.stream>>>(a, steps);
+            note_launch("coup::np::k_trajectory_sorted<{}, 1024>", N),
+                k_trajectory_sorted<N, 1024><<<grid_for(e.n, 1024), 1024, 0, e.stream>>>(a, steps);
           break;
       }
 #else
+      note_launch("coup::np::k_trajectory_sorted<{}, {}>", N, kRolloutSortLanes);
       k_trajectory_sorted<N, kRolloutSortLanes><<<grid_for(e.n, kRolloutSortLanes), kRolloutSortLanes, 0, e.stream>>>(
           a, steps);
 #endif
     } else {
+      note_launch("coup::np::k_step_trajectory<{}>", N);
       k_step_trajectory<N><<<grid_for(e.n, kThreads), kThreads, 0, e.stream>>>(a, steps);
     }
   });
@@ -1148,19 +1170,29 @@ hipError_t launch_rollout(const Env& e, int64_t steps, const coup_rollout_stats*
     if (regroup_lanes(e.knobs, e.n)) {
 #ifdef COUP_AB_VARIANTS
       switch (sort_lanes(e.knobs.np_sort_lanes, kRolloutSortLanes)) {
-        case 512: k_rollout_sorted<N, 512><<<grid_for(e.n, 512), 512, 0, e.stream>>>(a); break;
-        case 256: k_rollout_sorted<N, 256><<<grid, 256, 0, e.stream>>>(a); break;
+        case 512:
+          note_launch("coup::np::k_rollout_sorted<{}, 512>", N);
+          k_rollout_sorted<N, 512><<<grid_for(e.n, 512), 512, 0, e.stream>>>(a);
+          break;
+        case 256:
+          note_launch("coup::np::k_rollout_sorted<{}, 256>", N);
+          k_rollout_sorted<N, 256><<<grid, 256, 0, e.stream>>>(a);
+          break;
         default:
           if (!e.knobs.np_scan)  // COUP_NP_SCAN=0: the per-lane bin prefix
-            k_rollout_sorted<N, 1024, false><<<grid_for(e.n, 1024), 1024, 0, e.stream>>>(a);
+            note_launch("coup::np::k_rollout_sorted<{}, 1024, false>", N),
+                k_rollout_sorted<N, 1024, false><<<grid_for(e.n, 1024), 1024, 0, e.stream>>>(a);
           else
-            k_rollout_sorted<N, 1024><<<grid_for(e.n, 1024), 1024, 0, e.stream>>>(a);
+            note_launch("coup::np::k_rollout_sorted<{}, 1024>", N),
+                k_rollout_sorted<N, 1024><<<grid_for(e.n, 1024), 1024, 0, e.stream>>>(a);
           break;
       }
 #else
+      note_launch("coup::np::k_rollout_sorted<{}, {}>", N, kRolloutSortLanes);
       k_rollout_sorted<N, kRolloutSortLanes><<<grid_for(e.n, kRolloutSortLanes), kRolloutSortLanes, 0, e.stream>>>(a);
 #endif
     } else {
+      note_launch("coup::np::k_rollout<{}>", N);
       k_rollout<N><<<grid, kThreads, 0, e.stream>>>(a);
     }
   });

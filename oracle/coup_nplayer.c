@@ -593,3 +593,74 @@ int np_rollout(const np_rollout_args* a) {
   if (a->return_sum_p0) *a->return_sum_p0 = ret_sum;
   return 0;
 }
+
+/* np_rollout's per-lane loop recording only steps [from, steps) into rows of
+ * `stride` lanes, with record / accumulator snapshots (coup_oracle.h). */
+int np_rollout_window(const oc_window_args* a) {
+  const int P = a->players;
+  if (P < 2 || P > NP_MAX_PLAYERS || a->n > a->stride || a->from < 0 || a->from > a->steps || a->obs_hash ||
+      a->info_hash)
+    return 1;
+  for (int64_t lane = 0; lane < a->n; ++lane) {
+    uint32_t env = a->env_id_base + (uint32_t)lane, ep = 0;
+    int32_t eps = 0, ret_sum = 0;
+    np_state s;
+    np_init(&s, P);
+    resolve(&s, a->seed, env, ep);
+    int pending = 0;
+    for (int64_t t = 0; t < a->steps; ++t) {
+      int act = -1, rw[NP_MAX_PLAYERS] = {0};
+      uint8_t st;
+      if (pending) {
+        ep++;
+        np_init(&s, P);
+        resolve(&s, a->seed, env, ep);
+        pending = 0;
+        st = 0;
+      } else {
+        uint32_t m = np_legal_mask(&s);
+        uint32_t u = oc_draw(a->seed, env, ep & NP_EPISODE_MASK, (uint32_t)s.move);
+        uint32_t idx = (uint32_t)(((uint64_t)u * (uint32_t)__builtin_popcount(m)) >> 32);
+        for (uint32_t k = 0; k < idx; ++k) m &= m - 1;
+        act = __builtin_ctz(m);
+        np_apply_action(&s, act);
+        resolve(&s, a->seed, env, ep);
+        for (int p = 0; p < P; ++p) rw[p] = s.rewards[p];
+        if (np_is_terminal(&s)) {
+          int ret[NP_MAX_PLAYERS];
+          np_returns(&s, ret);
+          if (t >= a->stats_from) {
+            eps += 1;
+            ret_sum += ret[0];
+          }
+          st = 2;
+          if (a->auto_reset) {
+            ep++;
+            np_init(&s, P);
+            resolve(&s, a->seed, env, ep);
+          } else {
+            pending = 1;
+          }
+        } else {
+          st = 1;
+        }
+      }
+      if (t >= a->from) {
+        int64_t o = (t - a->from) * a->stride + lane;
+        if (a->actions) a->actions[o] = (int8_t)act;
+        if (a->rewards)
+          for (int p = 0; p < P; ++p) a->rewards[o * P + p] = (int8_t)rw[p];
+        if (a->step_type) a->step_type[o] = st;
+        if (a->legal) a->legal[o] = np_legal_mask(&s);
+        if (a->cur_player) a->cur_player[o] = (int8_t)np_current_player(&s);
+      }
+      for (int k = 0; k < a->nsnap; ++k) {
+        if (a->snap_at[k] != t + 1) continue;
+        if (a->snap_state[k]) np_pack(&s, ep, a->snap_state[k] + 8 * lane);
+        if (a->snap_eps[k]) a->snap_eps[k][lane] = eps;
+        if (a->snap_ret[k]) a->snap_ret[k][lane] = ret_sum;
+      }
+    }
+  }
+  return 0;
+}

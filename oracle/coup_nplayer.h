@@ -29,6 +29,8 @@
 
 #include <stdint.h>
 
+#include "coup_oracle.h" /* oc_window_args */
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -88,6 +90,9 @@ typedef struct {
   int8_t* cur_player;       /* [steps][n] CurrentPlayer() after the step (optional) */
 } np_rollout_args;
 int np_rollout(const np_rollout_args* a);
+/* the every-lane window driver (oc_window_args, coup_oracle.h) for 3..6
+ * players (no tensor hashes: the N-player benches write no tensors) */
+int np_rollout_window(const oc_window_args* a);
 
 #ifdef __cplusplus
 }

@@ -970,3 +970,97 @@ int oc_rollout(const oc_rollout_args* a) {
   if (a->return_sum_p0) *a->return_sum_p0 = ret_sum;
   return 0;
 }
+
+/* The every-lane window driver (coup_oracle.h): oc_rollout's per-lane loop,
+ * recording only steps [from, steps) and hashing the tensors. */
+static void window_hash(const float* x, int len, const uint32_t* w, uint64_t* out2) {
+  uint64_t h0 = 0, h1 = 0;
+  for (int i = 0; i < len; ++i) {
+    uint32_t b;
+    memcpy(&b, x + i, 4);
+    h0 += (uint64_t)b * w[i];
+    h1 += (uint64_t)b * w[len + i];
+  }
+  out2[0] = h0;
+  out2[1] = h1;
+}
+
+int oc_rollout_window(const oc_window_args* a) {
+  if (a->players != 2 || a->n > a->stride || a->from < 0 || a->from > a->steps) return OC_ERR_ILLEGAL;
+  float obs[2 * OC_OBS_SIZE];
+  float info[2 * OC_INFO_SIZE]; /* 20 KB of stack */
+  for (int64_t lane = 0; lane < a->n; ++lane) {
+    uint32_t env_id = a->env_id_base + (uint32_t)lane;
+    uint32_t episode = 0;
+    int32_t eps = 0, ret_sum = 0;
+    oc_state s;
+    oc_init(&s);
+    resolve_chance(&s, a->seed, env_id, episode);
+    int pending_reset = 0;
+    for (int64_t t = 0; t < a->steps; ++t) {
+      int8_t act = -1;
+      int rw[2] = {0, 0};
+      uint8_t st;
+      if (pending_reset) {
+        episode++;
+        oc_init(&s);
+        resolve_chance(&s, a->seed, env_id, episode);
+        pending_reset = 0;
+        st = 0;
+      } else {
+        uint32_t u = oc_draw(a->seed, env_id, episode & OC_EPISODE_MASK, (uint32_t)s.move_number);
+        int action = sample_uniform(&s, u);
+        act = (int8_t)action;
+        oc_apply_action(&s, action);
+        resolve_chance(&s, a->seed, env_id, episode);
+        oc_rewards(&s, rw);
+        if (oc_is_terminal(&s)) {
+          int ret[2];
+          oc_returns(&s, ret);
+          if (t >= a->stats_from) {
+            eps += 1;
+            ret_sum += ret[0];
+          }
+          st = 2;
+          if (a->auto_reset) {
+            episode++;
+            oc_init(&s);
+            resolve_chance(&s, a->seed, env_id, episode);
+          } else {
+            pending_reset = 1;
+          }
+        } else {
+          st = 1;
+        }
+      }
+      if (t >= a->from) {
+        int64_t o = (t - a->from) * a->stride + lane;
+        if (a->actions) a->actions[o] = act;
+        if (a->rewards) {
+          a->rewards[2 * o] = (int8_t)rw[0];
+          a->rewards[2 * o + 1] = (int8_t)rw[1];
+        }
+        if (a->step_type) a->step_type[o] = st;
+        if (a->legal) a->legal[o] = oc_legal_mask(&s);
+        if (a->cur_player) a->cur_player[o] = (int8_t)oc_current_player(&s);
+        if (a->obs_hash) {
+          oc_observation_tensor(&s, 0, obs);
+          oc_observation_tensor(&s, 1, obs + OC_OBS_SIZE);
+          window_hash(obs, 2 * OC_OBS_SIZE, a->obs_w, a->obs_hash + 2 * o);
+        }
+        if (a->info_hash) {
+          oc_info_state_tensor(&s, 0, info);
+          oc_info_state_tensor(&s, 1, info + OC_INFO_SIZE);
+          window_hash(info, 2 * OC_INFO_SIZE, a->info_w, a->info_hash + 2 * o);
+        }
+      }
+      for (int k = 0; k < a->nsnap; ++k) {
+        if (a->snap_at[k] != t + 1) continue;
+        if (a->snap_state[k]) oc_pack(&s, episode, s.error ? 1u : 0u, a->snap_state[k] + 4 * lane);
+        if (a->snap_eps[k]) a->snap_eps[k][lane] = eps;
+        if (a->snap_ret[k]) a->snap_ret[k][lane] = ret_sum;
+      }
+    }
+  }
+  return 0;
+}

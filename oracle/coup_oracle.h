@@ -155,6 +155,42 @@ typedef struct {
 } oc_rollout_args;
 int oc_rollout(const oc_rollout_args* a);
 
+/* --- Every-lane window driver (the bench-size parity tests) ---------------
+ * The same uniform rollout as oc_rollout (2 players) / np_rollout (N), with
+ * only the steps [from, steps) recorded, in rows of `stride` lanes, so a
+ * caller can split the lanes of one [steps - from][B] array over threads
+ * (every pointer pre-offset to the chunk's first lane; n <= stride).
+ * Tensors are not stored but reduced per lane and step to two linear hashes
+ * of their fp32 bit patterns, h_j = sum_i bits(x_i) * w_j[i] (exact in 64
+ * bits: w < 2^18, at most 2 x 2492 terms), which the GPU side computes the
+ * same way.  Snapshots: the packed records and the per-lane episode counts /
+ * player-0 return sums (counted from step stats_from) after snap_at[k] steps.
+ */
+#define OC_WINDOW_SNAPS 4
+typedef struct {
+  uint64_t seed;
+  uint32_t env_id_base;   /* of this chunk's first lane */
+  int players;            /* 2: coup_oracle.c; 3..6: the written N-player spec */
+  int64_t n, steps, from, stride;
+  int auto_reset;
+  int8_t* actions;        /* [steps - from][stride] */
+  int8_t* rewards;        /* [steps - from][stride][players] */
+  uint8_t* step_type;     /* [steps - from][stride] */
+  uint32_t* legal;        /* [steps - from][stride] */
+  int8_t* cur_player;     /* [steps - from][stride] */
+  const uint32_t* obs_w;  /* [2][2 * 98] (2 players) */
+  uint64_t* obs_hash;     /* [steps - from][stride][2] */
+  const uint32_t* info_w; /* [2][2 * 2492] */
+  uint64_t* info_hash;    /* [steps - from][stride][2] */
+  int64_t stats_from;
+  int nsnap;
+  int64_t snap_at[OC_WINDOW_SNAPS];
+  uint32_t* snap_state[OC_WINDOW_SNAPS]; /* [stride][4] (2 players) or [stride][8] */
+  int32_t* snap_eps[OC_WINDOW_SNAPS];    /* [stride] */
+  int32_t* snap_ret[OC_WINDOW_SNAPS];    /* [stride] */
+} oc_window_args;
+int oc_rollout_window(const oc_window_args* a); /* players == 2 */
+
 #ifdef __cplusplus
 }
 #endif

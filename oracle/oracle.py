@@ -77,6 +77,19 @@ class _NpRolloutArgs(ctypes.Structure):
                 ("cur_player", ctypes.c_void_p)]
 
 
+class _WindowArgs(ctypes.Structure):
+    _fields_ = [("seed", ctypes.c_uint64), ("env_id_base", ctypes.c_uint32), ("players", ctypes.c_int),
+                ("n", ctypes.c_int64), ("steps", ctypes.c_int64), ("from_", ctypes.c_int64), ("stride", ctypes.c_int64),
+                ("auto_reset", ctypes.c_int),
+                ("actions", ctypes.c_void_p), ("rewards", ctypes.c_void_p), ("step_type", ctypes.c_void_p),
+                ("legal", ctypes.c_void_p), ("cur_player", ctypes.c_void_p),
+                ("obs_w", ctypes.c_void_p), ("obs_hash", ctypes.c_void_p),
+                ("info_w", ctypes.c_void_p), ("info_hash", ctypes.c_void_p),
+                ("stats_from", ctypes.c_int64), ("nsnap", ctypes.c_int),
+                ("snap_at", ctypes.c_int64 * 4), ("snap_state", ctypes.c_void_p * 4),
+                ("snap_eps", ctypes.c_void_p * 4), ("snap_ret", ctypes.c_void_p * 4)]
+
+
 _lib = None
 
 
@@ -126,6 +139,8 @@ def lib():
         L.np_observation_tensor.argtypes = [NP, ctypes.c_int, ctypes.POINTER(ctypes.c_float)]
         L.np_pack.argtypes = [NP, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
         L.np_rollout.argtypes = [ctypes.POINTER(_NpRolloutArgs)]
+        L.oc_rollout_window.argtypes = [ctypes.POINTER(_WindowArgs)]
+        L.np_rollout_window.argtypes = [ctypes.POINTER(_WindowArgs)]
         _lib = L
     return _lib
 
@@ -378,4 +393,80 @@ def np_rollout(n_players, seed, n, steps, env_id_base=0, auto_reset=True, want_o
     a.lane_return_sum = buf("lane_return_sum", (n,), np.int32)
     a.cur_player = buf("cur_player", (steps, n), np.int8)
     lib().np_rollout(ctypes.byref(a))
+    return out
+
+
+def hash_weights(length):
+    """The two rows of linear-hash weights (uint32 in [1, 2^18)) for tensors
+    of `length` floats per lane (oc_window_args): fixed, so the GPU side
+    (tests/lane_digest.py) hashes with the same ones."""
+    rng = np.random.default_rng(0x436F7570 + length)
+    return np.ascontiguousarray(rng.integers(1, 1 << 18, size=(2, length), dtype=np.uint32))
+
+
+def window_threads():
+    """Host threads for the window driver: the job's CPU share (OMP_NUM_THREADS
+    on the GPU box), at most the affinity set."""
+    avail = len(os.sched_getaffinity(0))
+    want = int(os.environ.get("OMP_NUM_THREADS", avail) or avail)
+    return max(1, min(avail, want))
+
+
+def window(players, seed, n, steps, from_, env_id_base=0, auto_reset=True, obs_hash=False, info_hash=False,
+           snaps=(), stats_from=0, threads=None, chunk=None):
+    """Every lane of a uniform rollout of `n` lanes, outputs of steps
+    [from_, steps) only ([steps - from_][n] step-major arrays: actions,
+    rewards, step_type, legal, cur_player, and with obs_hash / info_hash the
+    [.., n, 2] uint64 hashes of the ObservationTensor / InformationStateTensor
+    pair, hash_weights), plus per snapshot step s in `snaps` the records
+    snap_state[s] ([n, 4] / [n, 8]) and the per-lane episode counts / player-0
+    return sums counted from step stats_from (snap_eps[s], snap_ret[s]).  The
+    lanes are split over `threads` host threads (ctypes releases the GIL)."""
+    import concurrent.futures
+    assert len(snaps) <= 4 and all(0 < x <= steps for x in snaps)
+    R, P = steps - from_, players
+    W = 4 if players == 2 else 8
+    out = {"actions": np.zeros((R, n), np.int8), "rewards": np.zeros((R, n, P), np.int8),
+           "step_type": np.zeros((R, n), np.uint8), "legal": np.zeros((R, n), np.uint32),
+           "cur_player": np.zeros((R, n), np.int8),
+           "snap_state": {x: np.zeros((n, W), np.uint32) for x in snaps},
+           "snap_eps": {x: np.zeros(n, np.int32) for x in snaps},
+           "snap_ret": {x: np.zeros(n, np.int32) for x in snaps}}
+    ow = iw = None
+    if obs_hash:
+        ow = hash_weights(2 * OBS_SIZE)
+        out["obs_hash"] = np.zeros((R, n, 2), np.uint64)
+    if info_hash:
+        iw = hash_weights(2 * INFO_SIZE)
+        out["info_hash"] = np.zeros((R, n, 2), np.uint64)
+    threads = threads or window_threads()
+    chunk = chunk or max(256, -(-n // (4 * threads)))
+    fn = lib().oc_rollout_window if players == 2 else lib().np_rollout_window
+
+    def run(lo):
+        m = min(chunk, n - lo)
+        a = _WindowArgs()
+        a.seed, a.env_id_base, a.players = seed, env_id_base + lo, players
+        a.n, a.steps, a.from_, a.stride, a.auto_reset = m, steps, from_, n, int(auto_reset)
+        a.actions = out["actions"].ctypes.data + lo
+        a.rewards = out["rewards"].ctypes.data + lo * P
+        a.step_type = out["step_type"].ctypes.data + lo
+        a.legal = out["legal"].ctypes.data + 4 * lo
+        a.cur_player = out["cur_player"].ctypes.data + lo
+        if ow is not None:
+            a.obs_w, a.obs_hash = ow.ctypes.data, out["obs_hash"].ctypes.data + 16 * lo
+        if iw is not None:
+            a.info_w, a.info_hash = iw.ctypes.data, out["info_hash"].ctypes.data + 16 * lo
+        a.stats_from, a.nsnap = stats_from, len(snaps)
+        for k, x in enumerate(snaps):
+            a.snap_at[k] = x
+            a.snap_state[k] = out["snap_state"][x].ctypes.data + 4 * W * lo
+            a.snap_eps[k] = out["snap_eps"][x].ctypes.data + 4 * lo
+            a.snap_ret[k] = out["snap_ret"][x].ctypes.data + 4 * lo
+        rc = fn(ctypes.byref(a))
+        if rc:
+            raise RuntimeError(f"oracle window driver failed ({rc})")
+
+    with concurrent.futures.ThreadPoolExecutor(threads) as ex:
+        list(ex.map(run, range(0, n, chunk)))
     return out

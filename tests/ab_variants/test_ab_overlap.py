@@ -3,9 +3,9 @@ rejected forms -- the fused trajectory writing the observations itself
 (COUP_PIPE=4, COUP_FUSED_SHAPE) and the overlapped rules-trajectory form (COUP_PIPE=3: the rules trajectory of chunk
 c + 1 on a second stream beside chunk c's writers, records double-buffered,
 fork / join events; measured slower than the one-stream form, DESIGN.md
-section 5), unmasked and with CU-masked rules / writer streams
-(COUP_OVERLAP_CUS), through tests/test_gpu_step_many.py's checks: equal to
-coup_step launched once per step, bit for bit."""
+section 5), through tests/test_gpu_step_many.py's checks: equal to
+coup_step launched once per step, bit for bit.  (The CU-masked stream form,
+COUP_OVERLAP_CUS, was deleted in round 6: DESIGN.md section 5.)"""
 import pytest
 import torch
 
@@ -13,26 +13,17 @@ from tests import test_gpu_step_many as M
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = ["0", "64"]  # COUP_OVERLAP_CUS
-
-
-@pytest.mark.parametrize("cus", VARIANTS)
 @pytest.mark.parametrize("B", [1000, (1 << 18) + 5])
-def test_overlap_equals_stepping(monkeypatch, B, cus):
-    monkeypatch.setenv("COUP_OVERLAP_CUS", cus)
+def test_overlap_equals_stepping(monkeypatch, B):
     M.test_step_many_equals_stepping(monkeypatch, B, "3")
 
 
-@pytest.mark.parametrize("cus", VARIANTS)
 @pytest.mark.parametrize("chunk", [1, 3])
-def test_overlap_chunk_length_invariant(monkeypatch, chunk, cus):
-    monkeypatch.setenv("COUP_OVERLAP_CUS", cus)
+def test_overlap_chunk_length_invariant(monkeypatch, chunk):
     M.test_chunk_length_invariant(monkeypatch, chunk, "3", None)
 
 
-@pytest.mark.parametrize("cus", VARIANTS)
-def test_overlap_graph_capture(monkeypatch, cus):
-    monkeypatch.setenv("COUP_OVERLAP_CUS", cus)
+def test_overlap_graph_capture(monkeypatch):
     M.test_graph_capture_and_packed_word(monkeypatch, "3", 2)
 
 

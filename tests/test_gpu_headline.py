@@ -172,12 +172,14 @@ def test_c3i_info_state_kernel_full_batch_slices_match_oracle():
     assert env.error_count() == 0
 
 
-def test_c4_bench_kernel_full_batch_slices_match_oracle():
-    """bench.py --config c4 at its size: 6 players,
-    2^20 lanes, settle 256 through the regrouped fused rollout, 5 warm-up and
-    20 eager coup_step launches of np::k_step_sorted<6, true, true, 1024> (the
-    decision drawn ahead, resets dealt by 4-thread groups), the bench's
-    packed accumulators.  At every timed step the actions, rewards, step
+def test_c4_eager_step_full_batch_slices_match_oracle():
+    """c4's batch with EAGER per-step launches: 6
+    players, 2^20 lanes, settle 256 through the regrouped fused rollout, 5
+    warm-up and 20 eager coup_step launches of np::k_step_sorted<6, true,
+    true, 1024> (the decision drawn ahead, resets dealt by 4-thread groups)
+    -- bench.py's c4 warm-up form; its timed steps are ONE coup_step_many
+    launch of np::k_trajectory_sorted<6, 1024>, checked on every lane by
+    tests/test_gpu_every_lane.py.  At every step the actions, rewards, step
     types, legal masks and current players of three 256-lane slices against
     the written N-player spec (oracle/coup_nplayer.c, parity unpinned w.r.t.
     the 2-player reference: coup.h:42); then the full records and the

@@ -190,14 +190,17 @@ def test_history_kept_by_apply_and_step():
         assert bytes(h[i, :m]) == st.history_bytes()[:m], s["name"]
 
 
-def test_c2_bench_kernel_matches_oracle_every_step():
-    """BASELINE config 2 exactly as bench.py's c2 runs it: 65,536 lanes,
-    in-kernel uniform policy (random_agent.py:29-42), no observations, so
-    coup_step launches the in-place k_step<true, 0, 256, 0> (regrouping
-    starts at 2^18 lanes).  Every lane's action, rewards, step type and
-    post-step legal mask (LegalActions, coup.cc:824-938) equal the oracle's
-    at each of 160 steps; so do the per-lane episode accumulators and the
-    final records."""
+def test_c2_eager_step_matches_oracle_every_step():
+    """BASELINE config 2's batch with EAGER per-step launches: 65,536 lanes,
+    in-kernel uniform policy (random_agent.py:29-42), no observations, one
+    coup_step per step (the group-Philox step k_step_group<1, true>;
+    regrouping starts at 2^18 lanes) -- what a learner passing actions each
+    step runs, and bench.py's c2 warm-up.  bench.py's timed c2 steps are ONE
+    coup_step_many trajectory launch instead (k_step_trajectory, output
+    stride 0): tests/test_gpu_every_lane.py checks that form on every lane.
+    Every lane's action, rewards, step type and post-step legal mask
+    (LegalActions, coup.cc:824-938) equal the oracle's at each of 160 steps;
+    so do the per-lane episode accumulators and the final records."""
     from open_spiel_coup_amd import _native  # noqa: F401
     n, steps, seed = 65536, 160, 1
     assert n < (1 << 18)  # the in-place kernel, not k_step_sorted

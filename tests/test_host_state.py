@@ -123,7 +123,13 @@ def test_host_apply_argument_checks():
     out = ctypes.create_string_buffer(RESULT)
     lib.coup_host_state_init(out)
     raw = out.raw
-    assert lib.coup_host_state_apply(raw, 18, 0, out) == _native.COUP_E_INVALID
+    # ids 18..127: a rejected action (ok = 0, record and history unchanged), as
+    # coup_host_state_step reports it; -1 and 128 are invalid arguments
+    for a in (18, 127):
+        for flags in (0, _native.SLOT_UNCHECKED):
+            assert lib.coup_host_state_apply(raw, a, flags, out) == 0
+            assert out.raw[118] == 0 and out.raw[:112] == raw[:112], (a, flags)
+    assert lib.coup_host_state_apply(raw, 128, 0, out) == _native.COUP_E_INVALID
     assert lib.coup_host_state_apply(raw, -1, 0, out) == _native.COUP_E_INVALID
     assert lib.coup_host_state_apply(None, 0, 0, out) == _native.COUP_E_INVALID
     assert lib.coup_host_state_tensors(None, None, None) == _native.COUP_E_INVALID

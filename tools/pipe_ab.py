@@ -11,9 +11,8 @@ serial split step (COUP_PIPE=0), the rules-trajectory form (COUP_PIPE=1)
 at chunks of 8 / 4 steps, and with the measurement build
 (COUP_LIB_PATH=build/variants/libcoup_mi355x.so) the merged pipelined step
 (COUP_PIPE=2) and the rules trajectories on a second stream beside the
-writers (COUP_PIPE=3; unmasked, and CU-masked rules / writer streams,
-COUP_OVERLAP_CUS).  --eager: time eager coup_step_many calls instead of
-graph replays (a graph replay may not keep a stream's CU mask).  Prints one JSON line per variant:
+writers (COUP_PIPE=3; the CU-masked form was deleted in round 6).  --eager:
+time eager coup_step_many calls instead of graph replays.  Prints one JSON line per variant:
 median / min us per env step.  Measurement tool only.
 """
 import argparse
@@ -32,7 +31,7 @@ AB_ONLY = ["t512w8:COUP_MANY_SHAPE=1", "t512w6:COUP_MANY_SHAPE=2", "t256w8:COUP_
            "fused512w8:COUP_PIPE=4,COUP_FUSED_SHAPE=3", "pipe85:COUP_PIPE=2,COUP_PIPE_SPAN=0.85",
            "over4:COUP_PIPE=3,COUP_TRAJ_CHUNK=4"]
 KNOBS = ("COUP_PIPE", "COUP_PIPE_SPAN", "COUP_TRAJ_CHUNK", "COUP_MANY_STAGE", "COUP_MANY_SHAPE", "COUP_WRITER_POL",
-         "COUP_WRITER_PRIO", "COUP_OVERLAP_LDS", "COUP_OVERLAP_CUS", "COUP_FUSED_SHAPE", "COUP_OBS_SPLIT", "COUP_OBS_MODE")
+         "COUP_WRITER_PRIO", "COUP_OVERLAP_LDS", "COUP_FUSED_SHAPE", "COUP_OBS_SPLIT", "COUP_OBS_MODE")
 
 
 def main():

@@ -167,8 +167,8 @@ def main():
                     summary["bench_line_of_traced_command"] = {
                         "value": bench["value"], "ms_per_step": bench["ms_per_step"],
                         "kernel_ms": bench["roofline"]["kernel_ms"], "frac": bench["roofline"]["frac"],
-                        "store_ceiling_ms": bench["roofline"].get("store_ceiling_ms"),
-                        "frac_of_store_ceiling": bench["roofline"].get("frac_of_store_ceiling"),
+                        "store_sweep_ms": bench["roofline"].get("store_sweep_ms"),
+                        "sweep_over_kernel": bench["roofline"].get("sweep_over_kernel"),
                         "box": bench.get("box")}
                     tk = summary.get("timed_kernel")
                     if fused or bare:
@@ -250,8 +250,8 @@ def main():
                         b = json.loads(line)
                         summary[f"bench_line_{which}"] = {
                             "value": b["value"], "kernel_ms": b["roofline"]["kernel_ms"],
-                            "frac": b["roofline"]["frac"], "store_ceiling_ms": b["roofline"].get("store_ceiling_ms"),
-                            "frac_of_store_ceiling": b["roofline"].get("frac_of_store_ceiling")}
+                            "frac": b["roofline"]["frac"], "store_sweep_ms": b["roofline"].get("store_sweep_ms"),
+                            "sweep_over_kernel": b["roofline"].get("sweep_over_kernel")}
                         shutil.copy(path, os.path.join(dst, f"bench_{which}.json"))
     if summary.get("bench_vs_rocprof_kernel_ms"):
         a, b = summary["bench_vs_rocprof_kernel_ms"]
@@ -313,6 +313,11 @@ def main():
             table = json.load(f)
     table[cfg] = {"batch": batch, "hbm_bytes_per_launch": traffic, "source": f"profiles/{tag}/{cfg}/summary.json",
                   "steps_per_launch": steps if (fused or bare) else 1}
+    if summary.get("issue"):
+        # VALU instructions (summed over waves) per launch as bench.py counts
+        # launches: bench.py's roofline.valu_issue_frac
+        table[cfg]["valu_insts_per_launch"] = summary["issue"]["counters"]["SQ_INSTS_VALU"]
+        table[cfg]["valu_source"] = f"profiles/{tag}/{cfg}/summary.json"
     with open(path, "w") as f:
         json.dump(table, f, indent=1, sort_keys=True)
     print(json.dumps(summary, indent=1))
