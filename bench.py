@@ -511,37 +511,41 @@ def _time_sweep_ceiling(buf, nf4, threads, passes, steps, stream):
     return a.elapsed_time(b) / steps
 
 
-VALU_CLOCK_GHZ = 2.4  # MI355X peak gfx clock (MI355X_MICROARCH.md), when the box's is unreadable
+VALU_CLOCK_GHZ = 2.4  # MI355X peak gfx clock (MI355X_MICROARCH.md)
 SIMDS = 1024          # 256 CUs x 4 SIMDs
 
 
-def valu_issue_frac(valu_insts, launch_ms, box):
+def valu_issue_frac(valu_insts, launch_ms, box=None):
     """Share of the chip's VALU issue slots a launch used: VALU instructions
     (summed over its waves; one wave64 VALU instruction takes 4 SIMD cycles)
-    x 4 / (1024 SIMDs x gfx clock x the launch's time).  None without a
-    profile of the same form."""
+    x 4 / (1024 SIMDs x 2.4 GHz x the launch's time).  The peak gfx clock,
+    not the box's: sysfs shows the clock at the moment it is read (2252 MHz
+    after a run that sustained ~2370, call r06a), so the peak figure gives
+    the conservative (lower) fraction.  None without a profile of the same
+    form."""
     if not valu_insts or not launch_ms:
         return None
-    ghz = VALU_CLOCK_GHZ
-    sclk = (box or {}).get("sclk") or ""
-    digits = "".join(c for c in sclk.split(":")[-1] if c.isdigit())
-    if digits and 500 <= int(digits) <= 4000:  # "1: 2376Mhz"
-        ghz = int(digits) / 1000.0
-    return valu_insts * 4.0 / (SIMDS * ghz * 1e9 * launch_ms * 1e-3)
+    return valu_insts * 4.0 / (SIMDS * VALU_CLOCK_GHZ * 1e9 * launch_ms * 1e-3)
 
 
 def roofline_fields(kernel, launched, achieved, traffic, valu_insts, launch_ms, bytes_per_launch, box, sweep_ms,
-                    sweep_form, step_form):
+                    sweep_form, step_form, tensors=False):
     """The line's roofline object.  frac: algorithmic bytes / time against the
     HBM spec peak (the contract's roofline); valu_issue_frac: the VALU issue
-    slots used (valu_issue_frac()); bound: whichever is higher (VERDICT r5
-    item 4: the tensor-free trajectory forms keep their state in registers
-    and move far fewer bytes than their algorithmic count, so their HBM
-    fraction bounds nothing).  store_sweep_ms is a measurement, not a bound,
-    and no field is called a ceiling."""
+    slots used (valu_issue_frac()).  bound: for the tensor-free forms
+    (tensors False) whichever fraction is higher (the
+    trajectory forms keep their state in registers and move far fewer bytes
+    than their algorithmic count, so their HBM fraction bounds nothing); for
+    the tensor-writing steps "hbm": their writers issue VALU on ~90% of the
+    slots, but cutting the writer's VALU per float4 in half made the c3 step
+    SLOWER (the nibble + table writer, 154.3 against 136.5 us, call r06d;
+    DESIGN.md section 5), so VALU issue does not bound them.
+    store_sweep_ms is a measurement, not a bound, and no field is called a
+    ceiling."""
     hbm_frac = achieved / HBM_PEAK_GBS
     valu_frac = valu_issue_frac(valu_insts, launch_ms, box)
-    return {"bound": "valu" if valu_frac is not None and valu_frac > hbm_frac else "hbm",
+    valu_bound = not tensors and valu_frac is not None and valu_frac > hbm_frac
+    return {"bound": "valu" if valu_bound else "hbm",
             "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": hbm_frac, "traffic": traffic,
             "kernel": kernel, "kernel_launched": launched, "kernel_ms": launch_ms,
             "bytes_per_launch": bytes_per_launch,
@@ -948,7 +952,7 @@ def main():
             "roofline": roofline_fields(
                 kernel=kernel, launched=launched, achieved=achieved, traffic=traffic, valu_insts=valu_insts,
                 launch_ms=launch_ms, bytes_per_launch=bytes_per_launch, box=box, sweep_ms=ceiling_ms,
-                sweep_form=ceiling_form,
+                sweep_form=ceiling_form, tensors=bool(with_obs or with_info),
                 step_form=("trajectory (coup_step_many)" if bare else
                            (with_obs and step_many_form(B, players, graph is not None))
                            or "split" if (with_obs and players == 2 and obs_split_active(B)) or

@@ -1068,6 +1068,90 @@ __device__ __forceinline__ void obs_sweep_rows_block(const uint4* __restrict__ s
   }
 }
 
+// The nibble form of the split observation writer (round 6).  The profile
+// of the rows form above (profiles/r05/c3: 176 VALU instructions per wave,
+// ~88 per thread for its two float4, VALU busy ~81% over the step) says its
+// store loop is VALU-heavy: four LDS word lookups, shifts, conversions and
+// coin selects per float4.  Here a lane's two 98-float rows are ONE 196-bit
+// string in LDS (row P1 at bits 0..97, row P2 at 98..195, as
+// obs_bits_to_lds lays it out), so float4 c of the lane is nibble c of the
+// string, and a 16-entry float4 table in LDS turns the nibble into the four
+// floats with one ds_read_b128 (entry e of 16 covers banks 4e..4e+3: no
+// conflicts).  The coins (elements 60, 61 of each row: float4 15 .x .y and
+// float4 39 .z .w) are patched in from two floats per lane.  The two
+// decoding threads of a lane split the string: P1's thread words 0..2 and
+// the coins, P2's thread words 3..6 (word 3 also holds P1's bits 96, 97,
+// which are the same in both rows: the last actions are public).
+template <int T, int S>
+struct ObsNibLds {
+  static constexpr uint32_t kLanes = ((uint32_t)(T * S) + (uint32_t)kRowF4 - 1u) / (uint32_t)kRowF4 + 1u;
+  alignas(16) float lut[16 * 4];
+  alignas(16) uint32_t bits[kLanes * 8];  // words 0..6 of the lane's 196-bit string
+  alignas(8) float coins[kLanes * 2];     // P1, P2 coins as floats
+};
+
+template <int T, int S>
+__device__ __forceinline__ void obs_sweep_nib_block(const uint4* __restrict__ state, float* __restrict__ obs, int64_t n,
+                                                    uint32_t blk, ObsNibLds<T, S>& lds) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  typedef float v2f __attribute__((ext_vector_type(2)));
+  constexpr uint32_t kLanes = ObsNibLds<T, S>::kLanes;
+  static_assert(2 * kLanes + 16 <= T, "two decoding threads per lane and the table's 16 threads");
+  const uint32_t t = threadIdx.x;
+  const int64_t x0 = (int64_t)blk * (T * S);
+  const int64_t o0 = x0 / kRowF4;
+  if (t < 2u * kLanes) {
+    if (o0 + (t >> 1) < n) {
+      const Lane L = unpack(state[o0 + (t >> 1)]);
+      const uint32_t p = t & 1u;
+      uint64_t lo, hi;
+      obs_row_bits_rt(L, is_terminal(L), p, lo, hi);
+      uint32_t* w = lds.bits + 8u * (t >> 1);
+      if (p == 0u) {
+        w[0] = (uint32_t)lo;
+        w[1] = (uint32_t)(lo >> 32);
+        w[2] = (uint32_t)hi;
+        lds.coins[t] = (float)L.c0;
+        lds.coins[t + 1u] = (float)L.c1;
+      } else {
+        w[3] = ((uint32_t)(hi >> 32) & 3u) | ((uint32_t)lo << 2);
+        w[4] = (uint32_t)(lo >> 30);
+        w[5] = (uint32_t)(lo >> 62) | ((uint32_t)hi << 2);
+        w[6] = (uint32_t)(hi >> 30) & 0xFu;
+      }
+    }
+  } else if (t < 2u * kLanes + 16u) {
+    const uint32_t e = t - 2u * kLanes;
+    reinterpret_cast<v4f*>(lds.lut)[e] = v4f{(float)(e & 1u), (float)((e >> 1) & 1u), (float)((e >> 2) & 1u),
+                                             (float)(e >> 3)};
+  }
+  __syncthreads();
+  const int64_t nf4 = n * kRowF4;
+  const uint32_t rel0 = (uint32_t)(x0 - o0 * kRowF4);
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    const int64_t x = x0 + j * T + t;
+    if (x >= nf4) break;
+    const uint32_t rel = rel0 + (uint32_t)(j * T) + t;
+    const uint32_t o = rel / (uint32_t)kRowF4, c = rel - o * (uint32_t)kRowF4;
+    const uint32_t nb = (lds.bits[8u * o + (c >> 3)] >> (4u * (c & 7u))) & 0xFu;
+    v4f v = reinterpret_cast<const v4f*>(lds.lut)[nb];
+    const v2f cn = reinterpret_cast<const v2f*>(lds.coins)[o];
+    v.x = c == 15u ? cn.x : v.x;
+    v.y = c == 15u ? cn.y : v.y;
+    v.z = c == 39u ? cn.x : v.z;
+    v.w = c == 39u ? cn.y : v.w;
+    __builtin_nontemporal_store(v, reinterpret_cast<v4f*>(obs) + x);
+  }
+}
+
+template <int T, int S>
+__global__ __launch_bounds__(T) void k_obs_sweep_nib(const uint4* __restrict__ state, float* __restrict__ obs,
+                                                     int64_t n) {
+  __shared__ ObsNibLds<T, S> lds;
+  obs_sweep_nib_block<T, S>(state, obs, n, blockIdx.x, lds);
+}
+
 // PRIO (measurement builds, COUP_WRITER_PRIO): the writer's waves raise
 // their issue priority (s_setprio) over the rules waves beside them
 template <int T, int S, int POL = 0, int PRIO = 0>
@@ -3730,7 +3814,20 @@ int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, b
     for (int64_t s = 0; s < c; ++s) {
       float* obs = out->obs + (slices ? (t0 + s) * n * 2 * COUP_OBS_SIZE : 0);
 #ifdef COUP_AB_VARIANTS
-      if (env->knobs.writer_pol == 1)  // (-1 / 0: the shipped non-temporal stores)
+      auto nib = [&](auto tt, auto ss) {  // COUP_WRITER_FORM: the nibble writer's shapes
+        constexpr int TT = decltype(tt)::value, SS = decltype(ss)::value;
+        coup::note_launch("coup::k_obs_sweep_nib<{}, {}>", TT, SS);
+        coup::k_obs_sweep_nib<TT, SS><<<(unsigned)((nf4 + TT * SS - 1) / (TT * SS)), TT, 0, S>>>(rec + s * n, obs, n);
+      };
+      if (env->knobs.writer_form == 1)
+        nib(std::integral_constant<int, 512>(), std::integral_constant<int, 2>());
+      else if (env->knobs.writer_form == 2)
+        nib(std::integral_constant<int, 512>(), std::integral_constant<int, 4>());
+      else if (env->knobs.writer_form == 3)
+        nib(std::integral_constant<int, 1024>(), std::integral_constant<int, 2>());
+      else if (env->knobs.writer_form == 4)
+        nib(std::integral_constant<int, 256>(), std::integral_constant<int, 4>());
+      else if (env->knobs.writer_pol == 1)  // (-1 / 0: the shipped non-temporal stores)
         coup::note_launch("coup::k_obs_sweep_rows<512, 2, 1>"), coup::k_obs_sweep_rows<512, 2, 1><<<wgrid, 512, 0, S>>>(rec + s * n, obs, n);
       else if (env->knobs.writer_pol == 2)
         coup::note_launch("coup::k_obs_sweep_rows<512, 2, 2>"), coup::k_obs_sweep_rows<512, 2, 2><<<wgrid, 512, 0, S>>>(rec + s * n, obs, n);

@@ -106,3 +106,15 @@ def test_overlap_priority_and_occupancy(monkeypatch, knobs):
         monkeypatch.setenv(k, v)
     M.test_chunk_length_invariant(monkeypatch, 3, "3", None)
     M.test_chunk_length_invariant(monkeypatch, 8, "1", None)
+
+
+@pytest.mark.parametrize("form", ["1", "2", "3", "4"])
+def test_nibble_writer_shapes(monkeypatch, form):
+    """COUP_WRITER_FORM: the nibble + table observation writer
+    (k_obs_sweep_nib, round 6) in the rules-trajectory form equals stepping
+    at every chunk length, and (512 x 2) its trajectory slices at the bench
+    size."""
+    monkeypatch.setenv("COUP_WRITER_FORM", form)
+    M.test_chunk_length_invariant(monkeypatch, 8, "1", None)
+    if form == "1":
+        M.test_trajectory_slices_every_step(monkeypatch, 1 << 20, 21, "1", None)

@@ -23,13 +23,14 @@ def test_valu_issue_fraction_and_bound():
     r = _fields(valu_insts=272.8e6, launch_ms=0.510, achieved=4440.0)
     assert r["valu_issue_frac"] == pytest.approx(272.8e6 * 4 / (1024 * 2.4e9 * 0.510e-3))
     assert 0.85 < r["valu_issue_frac"] < 0.9 and r["bound"] == "valu"
+    # a tensor-writing step stays HBM-bound whatever its VALU share (call r06d)
+    r = _fields(valu_insts=71.08e6, launch_ms=0.1331, achieved=6490.0, tensors=True)
+    assert r["valu_issue_frac"] > r["frac"] and r["bound"] == "hbm"
     # without a profile of the same form: no VALU fraction, the HBM bound
     r = _fields(valu_insts=None, achieved=6400.0)
     assert r["valu_issue_frac"] is None and r["bound"] == "hbm" and r["frac"] == pytest.approx(0.8)
-    # the box's own clock is used when it reads as one
+    # at the peak gfx clock, whatever the box's clock read afterwards
     r = _fields(valu_insts=1e6, launch_ms=1.0, box={"sclk": "1: 2000Mhz"})
-    assert r["valu_issue_frac"] == pytest.approx(4e6 / (1024 * 2.0e9 * 1e-3))
-    r = _fields(valu_insts=1e6, launch_ms=1.0, box={})
     assert r["valu_issue_frac"] == pytest.approx(4e6 / (1024 * 2.4e9 * 1e-3))
 
 
