@@ -294,7 +294,8 @@ def expected_kernel(cfg, batch, graph):
             # one rules-trajectory launch per chunk of steps + the writer per step
             stage = os.environ.get("COUP_MANY_STAGE", "0").strip() not in ("0", "")
             return ("coup::k_trajectory_sorted<1024, false, true, 4, false>" if form == "fused-trajectory" else
-                    "coup::k_trajectory_sorted<1024, true, false, 8, %s> + " % ("true" if stage else "false") +
+                    ("coup::k_trajectory_sorted<1024, true, false, 8, true> + " if stage else
+                     "coup::k_trajectory_sorted<1024, true, false, 8, false, true> + ") +
                     _SPLIT_WRITERS.get(split, "coup::k_obs_sweep"))
         if split:
             # the rules step without tensors (regrouped from 2^18 lanes) + the writer

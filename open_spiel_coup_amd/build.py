@@ -220,10 +220,22 @@ def main():
     ap.add_argument("--no-variants", action="store_true", help="skip the A/B-variant measurement build")
     a = ap.parse_args()
     if a.out or a.define:
+        # a measurement build: objects per source under build/obj/m_<defines>/
+        # (hipcc would take the host object for a HIP source in one command)
         out = os.path.abspath(a.out or OUT)
-        os.makedirs(OBJ_DIR, exist_ok=True)
-        subprocess.check_call(host_command(HOST_OBJ))
-        subprocess.check_call(command(a.verbose, out, a.define))
+        odir = os.path.join(OBJ_DIR, "m_" + ("_".join(a.define) or "plain"))
+        os.makedirs(odir, exist_ok=True)
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        host_obj = os.path.join(odir, "coup_host.o")
+        jobs, objs = [host_command(host_obj)], []
+        for src in SOURCES:
+            obj = os.path.join(odir, os.path.basename(src) + ".o")
+            objs.append(obj)
+            jobs.append([HIPCC, f"--offload-arch={ARCH}", OPT[os.path.basename(src)], NO_SLP, "-std=c++17", "-fPIC",
+                         "-Wall", "-I", os.path.join(ROOT, "include"), "-c", src, "-o", obj] +
+                        [f"-D{d}" for d in a.define])
+        _run_all(jobs, a.verbose)
+        _run_all([[HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs + [host_obj]], a.verbose)
         print(out)
         return
     print(build(force=a.force, verbose=a.verbose, variants=not a.no_variants))

@@ -41,6 +41,15 @@ __device__ __forceinline__ void count_philox_eval() {
 namespace coup {
 
 constexpr int kThreads = 256;
+// the 2-player sorted kernels' bin prefix (coup_regroup.h): per wave in DPP
+// (bins_below_dpp; the bare rules trajectory at 2^20 lanes 18.52-18.57 ->
+// 16.59-17.24 us per step, c3 -0.7..-1.0 us per step, alternating builds,
+// call r06e) or, in -DCOUP_BINS_LANE A/B builds, per lane (bins_below)
+#ifdef COUP_BINS_LANE
+#define COUP_BINS_BELOW(bin, key) bins_below<7>(bin, key)
+#else
+#define COUP_BINS_BELOW(bin, key) bins_below_dpp(bin, key)
+#endif
 // lanes per regrouping block of the 2-player sorted step / rollout
 // (profiles/r02/ab/sort_block_size_2p.log)
 constexpr int kStepSortLanes = 512;
@@ -1489,7 +1498,7 @@ __device__ __forceinline__ void step_sorted_block(const StepArgs& a, uint32_t bl
   __syncthreads();
   const uint32_t rank = atomicAdd(&s_bin[key], 1u);
   __syncthreads();
-  const uint32_t pos = bins_below<7>(s_bin, key) + rank;  // keys up to kKeyChallengeLost = 25
+  const uint32_t pos = COUP_BINS_BELOW(s_bin, key) + rank;  // keys up to kKeyChallengeLost = 25
   s_rec[pos] = pack(L);
   s_meta[pos] = t | (key << kO) | (st << (kO + 5));
   __syncthreads();
@@ -1652,7 +1661,7 @@ __global__ __launch_bounds__(T, 8) void k_rollout_sorted(RolloutArgs a) {
     __syncthreads();  // this step's bins are zero; last step's slots are read
     const uint32_t rank = atomicAdd(&bin[key], 1u);
     __syncthreads();
-    const uint32_t pos = bins_below<7>(bin, key) + rank;  // keys up to kKeyChallengeLost = 25
+    const uint32_t pos = COUP_BINS_BELOW(bin, key) + rank;  // keys up to kKeyChallengeLost = 25
     if (t < 32u) s_bin[(s + 1) & 1][t] = 0u;  // read for the last time in step s - 1
     s_rec[pos] = pack(L);
     s_meta[pos] = lane | (key << kO) | (cur << (kO + 5));
@@ -1748,7 +1757,9 @@ struct TrajStageLds {
 // lanes' home threads, coalesced, instead of from the thread that played
 // the lane (a wave of regrouped lanes scatters its stores over the
 // block's window); finished lanes are dealt in the same step, as with OBS.
-template <int T, bool REC = false, bool OBS = false, int W = 8, bool STAGE = false>
+// FULL: every per-step output buffer (actions, rewards, step types, legal
+// masks, players) is present, so no store tests its pointer.
+template <int T, bool REC = false, bool OBS = false, int W = 8, bool STAGE = false, bool FULL = false>
 __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t steps, TrajOut x) {
   static_assert((T & (T - 1)) == 0 && T >= 64 && T <= 1024, "power-of-two block of whole waves");
   constexpr uint32_t kO = T <= 256 ? 8u : 10u;  // lane bits of s_meta
@@ -1784,7 +1795,7 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
     __syncthreads();  // this step's bins are zero; last step's slots are read
     const uint32_t rank = atomicAdd(&bin[key], 1u);
     __syncthreads();
-    const uint32_t pos = bins_below<7>(bin, key) + rank;  // keys up to kKeyFirst = 26
+    const uint32_t pos = COUP_BINS_BELOW(bin, key) + rank;  // keys up to kKeyFirst = 26
     if (t < 32u) s_bin[(s + 1) & 1][t] = 0u;  // read for the last time in step s - 1
     s_rec[pos] = pack(L);
     s_meta[pos] = lane | (key << kO);
@@ -1803,23 +1814,23 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
     // the lane's step-s outputs: to the buffers, or (STAGE) to LDS by lane
     auto put_act = [&](int8_t v) {
       if constexpr (STAGE) s_st.act[lane] = v;
-      else if (a.actions) a.actions[o] = v;
+      else if (FULL || a.actions) a.actions[o] = v;
     };
     auto put_rew = [&](uint16_t v) {
       if constexpr (STAGE) s_st.rew[lane] = v;
-      else if (a.rewards) reinterpret_cast<uint16_t*>(a.rewards)[o] = v;
+      else if (FULL || a.rewards) reinterpret_cast<uint16_t*>(a.rewards)[o] = v;
     };
     auto put_st = [&](uint8_t v) {
       if constexpr (STAGE) s_st.st[lane] = v;
-      else if (a.step_type) a.step_type[o] = v;
+      else if (FULL || a.step_type) a.step_type[o] = v;
     };
     auto put_legal = [&](uint32_t v) {
       if constexpr (STAGE) s_st.legal[lane] = v;
-      else if (a.legal) a.legal[o] = v;
+      else if (FULL || a.legal) a.legal[o] = v;
     };
     auto put_cp = [&](int8_t v) {
       if constexpr (STAGE) s_st.cp[lane] = v;
-      else if (a.cur_player) a.cur_player[o] = v;
+      else if (FULL || a.cur_player) a.cur_player[o] = v;
     };
     auto put_rec = [&](const Lane& R) {
       if constexpr (STAGE) s_st.rec[lane] = pack(R);
@@ -1844,8 +1855,8 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
     if (!kNow && key == kKeyReset) {  // finished in step s - 1 with auto-reset (vector_env.py:62-65)
       L = new_episode(L.episode + 1u, rng, none);
       const uint32_t legal = decision_mask(L);
-      if (a.legal) a.legal[o - x.stride] = legal;
-      if (a.cur_player) a.cur_player[o - x.stride] = (int8_t)L.M;
+      if (FULL || a.legal) a.legal[o - x.stride] = legal;
+      if (FULL || a.cur_player) a.cur_player[o - x.stride] = (int8_t)L.M;
       if (REC) *(rec_s - a.n) = pack(L);  // step s - 1's record, after its auto-reset
       key = regroup_key(L, sample_action(legal, rng.draw(L.episode, L.move)));
     }
@@ -1952,8 +1963,8 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
   if (!kNow && key == kKeyReset && base + lane < a.n) {  // finished on the last step
     L = new_episode(L.episode + 1u, rng, none);
     const int64_t o = (steps - 1) * x.stride + base + lane;
-    if (a.legal) a.legal[o] = decision_mask(L);
-    if (a.cur_player) a.cur_player[o] = (int8_t)L.M;
+    if (FULL || a.legal) a.legal[o] = decision_mask(L);
+    if (FULL || a.cur_player) a.cur_player[o] = (int8_t)L.M;
     if (REC) x.rec[(steps - 1) * a.n + base + lane] = pack(L);
   }
   __syncthreads();
@@ -3802,6 +3813,15 @@ int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, b
     else if (overlap && env->knobs.overlap_lds > 0)  // COUP_OVERLAP_LDS: cap the rules' blocks per CU
       coup::note_launch("coup::k_trajectory_sorted<{}, true, false, 8, false>", TB),
           coup::k_trajectory_sorted<TB, true, false, 8, false><<<grid, TB, (unsigned)env->knobs.overlap_lds, R>>>(a, c, x);
+    else
+#endif
+#ifndef COUP_TRAJ_NOFULL
+    // every output present (the env's own buffers, bench.py's c3): the FULL
+    // form, no pointer tests (c3 132.3 against 133.6-133.9 us per step, call
+    // r06f; within the process-to-process spread, and fewer instructions)
+    if (a.actions && a.rewards && a.step_type && a.legal && a.cur_player)
+      coup::note_launch("coup::k_trajectory_sorted<{}, true, false, 8, false, true>", TB),
+          coup::k_trajectory_sorted<TB, true, false, 8, false, true><<<grid, TB, 0, R>>>(a, c, x);
     else
 #endif
       coup::note_launch("coup::k_trajectory_sorted<{}, true, false, 8, false>", TB),

@@ -950,8 +950,15 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1
 #define COUP_ABLATE_PHILOX_ROUNDS 10  // measurement builds may time fewer rounds (wrong streams)
 #endif
   for (int r = 0; r < COUP_ABLATE_PHILOX_ROUNDS; ++r) {
+#ifdef COUP_ABLATE_PHILOX_FULLRATE
+    // measurement builds only (wrong streams, lanes still decorrelated): the
+    // products from full-rate 24-bit multiplies, pricing the 64-bit ones
+    const uint64_t p0 = ((uint64_t)__umulhi((c.x & 0xFFFFFFu) << 8, 0xD2511Fu << 8) << 32) | __umul24(c.x, 0x511F53u);
+    const uint64_t p1 = ((uint64_t)__umulhi((c.z & 0xFFFFFFu) << 8, 0xCD9E8Du << 8) << 32) | __umul24(c.z, 0x9E8D57u);
+#else
     const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+#endif
     const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
     const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
     c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);

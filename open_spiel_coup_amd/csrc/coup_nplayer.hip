@@ -598,7 +598,13 @@ __global__ __launch_bounds__(T, 8) void k_rollout_sorted(RolloutArgs a) {
     __syncthreads();  // this step's bins are zero; last step's slots are read
     const uint32_t rank = atomicAdd(&bin[key], 1u);
     __syncthreads();
+#ifndef COUP_NP_BINS_LANE
+    // the DPP wave scan: 6-player fused rollout 22.0-22.1 -> 20.9-21.0 us per
+    // step against the shuffle scan of wave_bins_below (call r06f)
+    const uint32_t pos = (WS ? bins_below_dpp(bin, key) : bins_below<7>(bin, key)) + rank;
+#else
     const uint32_t pos = (WS ? wave_bins_below(bin, key) : bins_below<7>(bin, key)) + rank;  // keys up to kKeyChallengeLost = 25
+#endif
     if (t < 32u) s_bin[(s + 1) & 1][t] = 0u;  // read for the last time in step s - 1
     uint4 wa, wb;
     pack(L, wa, wb);
@@ -725,9 +731,17 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
     if (STAGE == 1 && s > 0 && t < nvalid) store_staged<N>(a, (s - 1) * a.ostride + base + t, s_out[t], s_olegal[t]);
     const uint32_t rank = atomicAdd(&bin[key], 1u);
     __syncthreads();
-    // (wave_bins_below here spills 38 VGPRs instead of 22 and measured 26.07
-    // vs 24.12 us per step: profiles/r03/ab/np_scan_forms_traj_rollout.jsonl)
+    // (the shuffle form, wave_bins_below, spilled 38 VGPRs instead of 22 here
+    // and measured 26.07 vs 24.12 us per step: profiles/r03/ab/
+    // np_scan_forms_traj_rollout.jsonl; the DPP form below does not spill)
+#ifndef COUP_NP_BINS_LANE
+    // the wave scan in DPP (coup_regroup.h): 6-player trajectory 26.36-26.72 ->
+    // 25.06-25.50 us per 2^20-lane step against the per-lane prefix below,
+    // alternating builds (call r06f)
+    const uint32_t pos = bins_below_dpp(bin, key) + rank;
+#else
     const uint32_t pos = bins_below<7>(bin, key) + rank;  // keys up to kKeyFirst = 26
+#endif
     if (t < 32u) s_bin[(s + 1) & 1][t] = 0u;  // read for the last time in step s - 1
     uint4 wa, wb;
     pack(L, wa, wb);

@@ -51,6 +51,32 @@ __device__ __forceinline__ uint32_t bins_below(const uint32_t* bin, uint32_t key
   return below;
 }
 
+// The same prefix from a wave-level scan of the 32 bins in DPP row
+// operations (no LDS round trip, no per-lane selects): every lane reads bin
+// (lane & 31), an inclusive scan over each 32-lane half (row_shr 1..3, then
+// row_shr 4 / 8 on the upper banks, then row 0's total broadcast into row 1:
+// the cross-lane prefix of the GCN ISA's DPP examples), the exclusive prefix
+// of bin `key` taken from lane `key` with ds_bpermute.  6 DPP adds and one
+// permute per wave against bins_below's Q 16-byte reads and ~12 Q selects
+// and adds per lane (Q = 7: ~84 VALU per wave-step of the 2-player sorted
+// kernels).  All 32 bins must hold valid counts (unused ones zero); key < 32.
+#ifndef COUP_HOST_STANDIN
+template <int CTRL, int ROW_MASK = 0xF, int BANK_MASK = 0xF>
+__device__ __forceinline__ uint32_t dpp_src(uint32_t x) {
+  // lanes without a source in their row (bound_ctrl) or masked off read 0
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROW_MASK, BANK_MASK, true);
+}
+__device__ __forceinline__ uint32_t bins_below_dpp(const uint32_t* bin, uint32_t key) {
+  const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  const uint32_t v = bin[lane & 31u];
+  uint32_t x = v + dpp_src<0x111>(v) + dpp_src<0x112>(v) + dpp_src<0x113>(v);  // row_shr:1..3
+  x += dpp_src<0x114, 0xF, 0xE>(x);                                            // row_shr:4, banks 1..3
+  x += dpp_src<0x118, 0xF, 0xC>(x);                                            // row_shr:8, banks 2..3
+  x += dpp_src<0x142, 0xA, 0xF>(x);  // row_bcast:15 into rows 1 and 3: the 32-lane inclusive scan
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(key << 2), (int)(x - v));
+}
+#endif
+
 // The host-side choice of regrouping and block sizes is coup_knobs.h's
 // (regroup_lanes, sort_lanes), read once per env at coup_create.
 

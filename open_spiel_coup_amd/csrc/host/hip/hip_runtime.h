@@ -5,6 +5,8 @@
 #pragma once
 #include <stdint.h>
 
+#define COUP_HOST_STANDIN 1  // device-only helpers (cross-lane builtins) are left out of the host build
+
 #define __device__
 #define __host__
 #define __forceinline__ inline __attribute__((always_inline))

@@ -3,6 +3,7 @@
 // with g++ for debugging.  Test tooling only; never used by the product build.
 #pragma once
 #include <stdint.h>
+#define COUP_HOST_STANDIN 1  // device-only helpers (cross-lane builtins) are left out
 #define __device__
 #define __host__
 #define __forceinline__ inline
