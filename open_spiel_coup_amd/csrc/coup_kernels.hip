@@ -3853,6 +3853,9 @@ int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, b
         coup::note_launch("coup::k_obs_sweep_rows<512, 2, 2>"), coup::k_obs_sweep_rows<512, 2, 2><<<wgrid, 512, 0, S>>>(rec + s * n, obs, n);
       else if (env->knobs.writer_pol == 3)
         coup::note_launch("coup::k_obs_sweep_rows<512, 2, 3>"), coup::k_obs_sweep_rows<512, 2, 3><<<wgrid, 512, 0, S>>>(rec + s * n, obs, n);
+      else if (env->knobs.writer_dyn_lds > 0)  // COUP_WRITER_DYN_LDS: fewer writer blocks per CU
+        coup::note_launch("coup::k_obs_sweep_rows<512, 2>"),
+            coup::k_obs_sweep_rows<512, 2><<<wgrid, 512, (unsigned)env->knobs.writer_dyn_lds, S>>>(rec + s * n, obs, n);
       else if (env->knobs.writer_prio == 1)
         coup::note_launch("coup::k_obs_sweep_rows<512, 2, 0, 1>"), coup::k_obs_sweep_rows<512, 2, 0, 1><<<wgrid, 512, 0, S>>>(rec + s * n, obs, n);
       else if (env->knobs.writer_prio >= 2)

@@ -31,7 +31,8 @@ AB_ONLY = ["t512w8:COUP_MANY_SHAPE=1", "t512w6:COUP_MANY_SHAPE=2", "t256w8:COUP_
            "fused512w8:COUP_PIPE=4,COUP_FUSED_SHAPE=3", "pipe85:COUP_PIPE=2,COUP_PIPE_SPAN=0.85",
            "over4:COUP_PIPE=3,COUP_TRAJ_CHUNK=4"]
 KNOBS = ("COUP_PIPE", "COUP_PIPE_SPAN", "COUP_TRAJ_CHUNK", "COUP_MANY_STAGE", "COUP_MANY_SHAPE", "COUP_WRITER_POL",
-         "COUP_WRITER_PRIO", "COUP_OVERLAP_LDS", "COUP_FUSED_SHAPE", "COUP_OBS_SPLIT", "COUP_OBS_MODE")
+         "COUP_WRITER_PRIO", "COUP_OVERLAP_LDS", "COUP_FUSED_SHAPE", "COUP_OBS_SPLIT", "COUP_OBS_MODE", "COUP_WRITER_FORM",
+         "COUP_WRITER_DYN_LDS")
 
 
 def main():
