@@ -226,6 +226,13 @@ def step_many_form(batch, players, graph):
     return "fused-trajectory" if v == "4" else "rules-trajectory"
 
 
+def traj_stage():
+    """The library's rules-trajectory output staging (coup_build_flags bits
+    3:1; the STAGE template argument the launch log spells)."""
+    from open_spiel_coup_amd import _native
+    return (_native.load().coup_build_flags() >> _native.BUILD_TRAJ_STAGE_SHIFT) & _native.BUILD_TRAJ_STAGE_MASK
+
+
 def traj_chunk():
     """COUP_TRAJ_CHUNK as coup::read_knobs clamps it."""
     try:
@@ -277,7 +284,8 @@ def expected_kernel(cfg, batch, graph):
                                                                  _np_step_lanes(players))
         return "coup::np::k_step<%d, true>" % players
     if fused == "traj" or bare:
-        return "coup::k_trajectory_sorted<1024, false, false, 8, false>" if sorted_ else "coup::k_step_trajectory"
+        return ("coup::k_trajectory_sorted<1024, false, false, 8, %d>" % traj_stage() if sorted_ else
+                "coup::k_step_trajectory")
     if fused:
         return "coup::k_rollout_sorted<1024>" if sorted_ else "coup::k_rollout"
     if with_info:
@@ -293,9 +301,9 @@ def expected_kernel(cfg, batch, graph):
         if form:
             # one rules-trajectory launch per chunk of steps + the writer per step
             stage = os.environ.get("COUP_MANY_STAGE", "0").strip() not in ("0", "")
-            return ("coup::k_trajectory_sorted<1024, false, true, 4, false>" if form == "fused-trajectory" else
-                    ("coup::k_trajectory_sorted<1024, true, false, 8, true> + " if stage else
-                     "coup::k_trajectory_sorted<1024, true, false, 8, false, true> + ") +
+            return ("coup::k_trajectory_sorted<1024, false, true, 4, 0>" if form == "fused-trajectory" else
+                    ("coup::k_trajectory_sorted<1024, true, false, 8, 1> + " if stage else
+                     "coup::k_trajectory_sorted<1024, true, false, 8, %d, true> + " % traj_stage()) +
                     _SPLIT_WRITERS.get(split, "coup::k_obs_sweep"))
         if split:
             # the rules step without tensors (regrouped from 2^18 lanes) + the writer

@@ -463,6 +463,12 @@ int coup_info_split_variant(int64_t batch);
  * variables read at coup_create (build.py writes it to
  * build/ab/libcoup_mi355x.so for A/B runs and their equality tests). */
 #define COUP_BUILD_AB_VARIANTS 1
+/* Bits 3:1: how the 2-player rules trajectories store each step's outputs
+ * (their STAGE template argument): 0 from the thread
+ * that played the lane, 2 staged by lane in LDS and stored by the lane's
+ * home thread behind the next step's count barrier (the product). */
+#define COUP_BUILD_TRAJ_STAGE_SHIFT 1
+#define COUP_BUILD_TRAJ_STAGE_MASK 0x7
 int coup_build_flags(void);
 
 /* The kernels this thread's library calls have launched -- enqueued, or

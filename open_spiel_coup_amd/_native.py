@@ -18,6 +18,7 @@ HISTORY_BYTES = 96
 
 COUP_OK, COUP_E_INVALID, COUP_E_HIP, COUP_E_LANES = 0, 1, 2, 3
 BUILD_AB_VARIANTS = 1  # coup_build_flags: a measurement build with every A/B variant
+BUILD_TRAJ_STAGE_SHIFT, BUILD_TRAJ_STAGE_MASK = 1, 0x7  # coup_build_flags: the rules trajectories' output staging
 SWEEP_RESIDENT, SWEEP_INDEX_BITS = 1, 2  # coup_measure_store_sweep mode bits
 
 # Every symbol declared in include/coup_mi355x.h

@@ -31,6 +31,37 @@ __device__ __forceinline__ void count_philox_eval() {
 }
 #define COUP_PHILOX_HOOK() count_philox_eval()
 #endif
+#ifdef COUP_TRAJ_PHASES
+// Measurement builds: where k_trajectory_sorted's waves spend their steps.
+// Each wave stamps s_memtime (the shader clock) at fixed points of every
+// step and accumulates the cycles between consecutive stamps per phase
+// (coup_debug_traj_phases): [0] the count atomic and the count barrier,
+// [1] the prefix and the slot writes, [2] the slot barrier, [3] the slot
+// read, unpack and the FIRST / reset / rejected paths, [4] the decision and
+// its deals, [5] the outputs, the legal mask and the next draw; [6] wave-steps.
+// A stamp in a branch no lane of the wave takes is skipped, and its cycles
+// go to the next stamp's phase.
+constexpr int kTrajPhases = 6;
+__device__ unsigned long long g_traj_phases[kTrajPhases + 1];
+#define COUP_TRAJ_STAMP(k)                                                    \
+  do {                                                                         \
+    const uint32_t now_ = (uint32_t)__builtin_amdgcn_s_memtime();             \
+    ph_[k] += now_ - ph_last_;                                                 \
+    ph_last_ = now_;                                                           \
+  } while (0)
+#define COUP_TRAJ_STAMP_DECL uint32_t ph_[kTrajPhases] = {}, ph_last_ = (uint32_t)__builtin_amdgcn_s_memtime();
+#define COUP_TRAJ_STAMP_FLUSH(steps)                                          \
+  do {                                                                         \
+    if ((threadIdx.x & 63u) == 0u) {                                           \
+      for (int k_ = 0; k_ < kTrajPhases; ++k_) atomicAdd(&g_traj_phases[k_], (unsigned long long)ph_[k_]); \
+      atomicAdd(&g_traj_phases[kTrajPhases], (unsigned long long)(steps));    \
+    }                                                                          \
+  } while (0)
+#else
+#define COUP_TRAJ_STAMP(k)
+#define COUP_TRAJ_STAMP_DECL
+#define COUP_TRAJ_STAMP_FLUSH(steps)
+#endif
 #include "coup_lane.h"
 #include "coup_launch_log.h"
 #include "coup_mi355x.h"
@@ -1656,9 +1687,13 @@ __global__ __launch_bounds__(T, 8) void k_rollout_sorted(RolloutArgs a) {
     resolve_chance(L, rng);  // a lane left at a chance node
     key = draw_key(L, rng, errs);
   }
+  // two barriers per step, as k_trajectory_sorted (its comment)
+  __syncthreads();  // the bins and by-lane counters above are initialised
   for (int64_t s = 0; s < a.steps; ++s) {
     uint32_t* bin = s_bin[s & 1];
-    __syncthreads();  // this step's bins are zero; last step's slots are read
+#ifdef COUP_TRAJ_TOP_BARRIER
+    __syncthreads();  // measurement builds: the third barrier of rounds 2-5
+#endif
     const uint32_t rank = atomicAdd(&bin[key], 1u);
     __syncthreads();
     const uint32_t pos = COUP_BINS_BELOW(bin, key) + rank;  // keys up to kKeyChallengeLost = 25
@@ -1741,6 +1776,13 @@ struct TrajObsLds {
 template <int T>
 struct TrajNoLds {};
 // STAGE: a step's outputs by lane, stored by each lane's home thread
+// The output staging the shipped rules trajectories use (STAGE above;
+// -DCOUP_TRAJ_OUT_STAGE=0 measurement builds store from the playing thread)
+#ifndef COUP_TRAJ_OUT_STAGE
+#define COUP_TRAJ_OUT_STAGE 2
+#endif
+constexpr int kTrajStage = COUP_TRAJ_OUT_STAGE;
+constexpr int8_t kCpDeferred = -128;  // STAGE 2: legal mask, player and record stored by the reset group
 template <int T>
 struct TrajStageLds {
   uint4 rec[T];
@@ -1756,10 +1798,15 @@ struct TrajStageLds {
 // step's outputs (and REC records) staged by lane in LDS and stored by the
 // lanes' home threads, coalesced, instead of from the thread that played
 // the lane (a wave of regrouped lanes scatters its stores over the
-// block's window); finished lanes are dealt in the same step, as with OBS.
+// block's window, one cache line per lane or so): 1 (round 5) behind a
+// barrier of their own in the same step, finished lanes dealt in the same
+// step as with OBS; 2 behind the next step's count barrier (the block has
+// it anyway), finished lanes dealt in the reset group of the next step,
+// whose direct stores of the finished step's legal mask, player and record
+// follow the staged ones (the slot barrier orders them).
 // FULL: every per-step output buffer (actions, rewards, step types, legal
 // masks, players) is present, so no store tests its pointer.
-template <int T, bool REC = false, bool OBS = false, int W = 8, bool STAGE = false, bool FULL = false>
+template <int T, bool REC = false, bool OBS = false, int W = 8, int STAGE = 0, bool FULL = false>
 __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t steps, TrajOut x) {
   static_assert((T & (T - 1)) == 0 && T >= 64 && T <= 1024, "power-of-two block of whole waves");
   constexpr uint32_t kO = T <= 256 ? 8u : 10u;  // lane bits of s_meta
@@ -1768,8 +1815,8 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
   __shared__ int32_t s_eps[T], s_ret[T];  // by lane
   __shared__ __attribute__((aligned(16))) uint32_t s_bin[2][32];
   __shared__ typename std::conditional<OBS, TrajObsLds<T>, TrajNoLds<T>>::type s_obs;
-  __shared__ typename std::conditional<STAGE, TrajStageLds<T>, TrajNoLds<T>>::type s_st;
-  constexpr bool kNow = OBS || STAGE;  // a finished lane's next episode dealt in the same step
+  __shared__ typename std::conditional<STAGE != 0, TrajStageLds<T>, TrajNoLds<T>>::type s_st;
+  constexpr bool kNow = OBS || STAGE == 1;  // a finished lane's next episode dealt in the same step
   const uint32_t t = threadIdx.x;
   const int64_t base = (int64_t)blockIdx.x * T;
   const bool ar = a.auto_reset != 0;
@@ -1779,31 +1826,75 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
   Rng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, base + t), 0u, make_uint4(0, 0, 0, 0)};
   NoHistory none;
   Lane L = initial_lane(0u);
+  // rw: the lane's packed record, the one value that crosses the step loop's
+  // back edge (the regroup moves it through LDS).  Every path of the step
+  // ends by packing its Lane into rw -- the same value its record store
+  // needs -- so the unpacked Lane's ~20 fields die inside the step, and the
+  // join of the step's exits copies 4 registers instead of ~23 (and packs
+  // once, not again at the next step's top).
+  uint4 rw = make_uint4(0u, 0u, 0u, 0u);
   uint32_t lane = t, key = kKeyDead, errs = 0u;
+  // a drawn decision's sort key
+  auto draw_decision = [&](uint32_t legal) { return regroup_key(L, sample_action(legal, rng.draw(L.episode, L.move))); };
+  // STAGE 2: step sp's staged outputs of lane base + t, from its home thread
+  auto store_staged = [&](int64_t sp) {
+    if constexpr (STAGE == 2) {
+      const int64_t i = base + t;
+      if (i < a.n) {
+        const int64_t oh = sp * x.stride + i;
+        if (FULL || a.actions) a.actions[oh] = s_st.act[t];
+        if (FULL || a.rewards) reinterpret_cast<uint16_t*>(a.rewards)[oh] = s_st.rew[t];
+        if (FULL || a.step_type) a.step_type[oh] = s_st.st[t];
+        const int8_t cp = s_st.cp[t];
+        if (cp != kCpDeferred) {  // else the next step's reset group stores these three, once
+          if (FULL || a.legal) a.legal[oh] = s_st.legal[t];
+          if (FULL || a.cur_player) a.cur_player[oh] = cp;
+          if (REC) x.rec[sp * a.n + i] = s_st.rec[t];
+        }
+      }
+    }
+  };
   if (base + t < a.n) {
-    L = unpack(a.state[base + t]);
+    rw = a.state[base + t];
+    L = unpack(rw);
     if (is_terminal(L)) {
       key = kKeyFirst;
     } else {
       resolve_chance(L, rng);  // a lane left at a chance node
       const uint32_t m = decision_mask(L);
-      key = m ? regroup_key(L, sample_action(m, rng.draw(L.episode, L.move))) : kKeyDead;
+      key = m ? draw_decision(m) : kKeyDead;
+      rw = pack(L);
     }
   }
+  // Two barriers per step.  The bins, slots and by-lane LDS need no third at
+  // the step's top: this step's bins were zeroed before the last step's
+  // slot barrier, and every thread reads its slot (and finishes the last
+  // step's LDS work: OBS rows, STAGE outputs) before it reaches this step's
+  // count barrier, which any write of this step's slots follows.
+  __syncthreads();  // the bins and by-lane counters above are initialised
+  COUP_TRAJ_STAMP_DECL
   for (int64_t s = 0; s < steps; ++s) {
     uint32_t* bin = s_bin[s & 1];
-    __syncthreads();  // this step's bins are zero; last step's slots are read
+#ifdef COUP_TRAJ_TOP_BARRIER
+    __syncthreads();  // measurement builds: the third barrier of rounds 2-5
+#endif
     const uint32_t rank = atomicAdd(&bin[key], 1u);
     __syncthreads();
+    COUP_TRAJ_STAMP(0);
+    if constexpr (STAGE == 2)
+      if (s > 0) store_staged(s - 1);  // the last step's outputs, complete behind the count barrier
     const uint32_t pos = COUP_BINS_BELOW(bin, key) + rank;  // keys up to kKeyFirst = 26
     if (t < 32u) s_bin[(s + 1) & 1][t] = 0u;  // read for the last time in step s - 1
-    s_rec[pos] = pack(L);
+    s_rec[pos] = rw;
     s_meta[pos] = lane | (key << kO);
+    COUP_TRAJ_STAMP(1);
     __syncthreads();
+    COUP_TRAJ_STAMP(2);
     const uint32_t m = s_meta[t];
     lane = m & (T - 1u);
     key = (m >> kO) & 31u;
-    L = unpack(s_rec[t]);
+    rw = s_rec[t];
+    L = unpack(rw);
     // the step's rules: `continue` ends the lane's step (the do-while), and
     // with OBS every thread then meets the block's observation write below
     do {
@@ -1813,28 +1904,29 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
     uint4* const rec_s = REC ? x.rec + s * a.n + li : nullptr;  // step s's record of the lane
     // the lane's step-s outputs: to the buffers, or (STAGE) to LDS by lane
     auto put_act = [&](int8_t v) {
-      if constexpr (STAGE) s_st.act[lane] = v;
+      if constexpr (STAGE != 0) s_st.act[lane] = v;
       else if (FULL || a.actions) a.actions[o] = v;
     };
     auto put_rew = [&](uint16_t v) {
-      if constexpr (STAGE) s_st.rew[lane] = v;
+      if constexpr (STAGE != 0) s_st.rew[lane] = v;
       else if (FULL || a.rewards) reinterpret_cast<uint16_t*>(a.rewards)[o] = v;
     };
     auto put_st = [&](uint8_t v) {
-      if constexpr (STAGE) s_st.st[lane] = v;
+      if constexpr (STAGE != 0) s_st.st[lane] = v;
       else if (FULL || a.step_type) a.step_type[o] = v;
     };
     auto put_legal = [&](uint32_t v) {
-      if constexpr (STAGE) s_st.legal[lane] = v;
+      if constexpr (STAGE != 0) s_st.legal[lane] = v;
       else if (FULL || a.legal) a.legal[o] = v;
     };
     auto put_cp = [&](int8_t v) {
-      if constexpr (STAGE) s_st.cp[lane] = v;
+      if constexpr (STAGE != 0) s_st.cp[lane] = v;
       else if (FULL || a.cur_player) a.cur_player[o] = v;
     };
-    auto put_rec = [&](const Lane& R) {
-      if constexpr (STAGE) s_st.rec[lane] = pack(R);
-      else if (REC) *rec_s = pack(R);
+    auto put_rec = [&](const Lane& R) {  // also the lane's rw
+      rw = pack(R);
+      if constexpr (STAGE != 0) s_st.rec[lane] = rw;
+      else if (REC) *rec_s = rw;
     };
     rng.env_id = lane_stream_id(a.env_id_base, li);
     rng.blk_tag = 0u;
@@ -1849,7 +1941,7 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
       put_legal(legal);
       put_cp((int8_t)L.M);
       put_rec(L);
-      key = regroup_key(L, sample_action(legal, rng.draw(L.episode, L.move)));
+      key = draw_decision(legal);
       continue;
     }
     if (!kNow && key == kKeyReset) {  // finished in step s - 1 with auto-reset (vector_env.py:62-65)
@@ -1857,7 +1949,8 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
       const uint32_t legal = decision_mask(L);
       if (FULL || a.legal) a.legal[o - x.stride] = legal;
       if (FULL || a.cur_player) a.cur_player[o - x.stride] = (int8_t)L.M;
-      if (REC) *(rec_s - a.n) = pack(L);  // step s - 1's record, after its auto-reset
+      rw = pack(L);
+      if (REC) *(rec_s - a.n) = rw;  // step s - 1's record, after its auto-reset
       key = regroup_key(L, sample_action(legal, rng.draw(L.episode, L.move)));
     }
     if (key == kKeyDead) {  // no legal decision: coup_step's rejected step
@@ -1870,12 +1963,14 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
       put_rec(L);
       continue;
     }
+    COUP_TRAJ_STAMP(3);
     const uint32_t act = key_action(key);
     const uint32_t err_before = L.err;
     apply_decision_v1(L, act);  // regrouped: the branch form, as k_rollout_sorted
     L.move += 1u;
     resolve_chance(L, rng);
     errs += (L.err && !err_before) ? 1u : 0u;
+    COUP_TRAJ_STAMP(4);
     const bool term = is_terminal(L);
     put_act((int8_t)act);
     put_rew((uint16_t)((uint8_t)L.r0 | ((uint8_t)(-L.r0) << 8)));
@@ -1889,11 +1984,13 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
         put_legal(legal);
         put_cp((int8_t)L.M);
         put_rec(L);
-        key = s + 1 < steps ? regroup_key(L, sample_action(legal, rng.draw(L.episode, L.move))) : kKeyDead;
+        key = s + 1 < steps ? draw_decision(legal) : kKeyDead;
         continue;
       }
       if (ar) {
         key = kKeyReset;  // legal mask and player once the next episode is dealt
+        rw = pack(L);
+        if constexpr (STAGE == 2) s_st.cp[lane] = kCpDeferred;
         continue;
       }
       key = kKeyFirst;
@@ -1906,9 +2003,10 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
     put_legal(legal);
     put_cp((int8_t)L.M);
     put_rec(L);
-    if (s + 1 < steps) key = regroup_key(L, sample_action(legal, rng.draw(L.episode, L.move)));
+    if (s + 1 < steps) key = draw_decision(legal);
     } while (false);
-    if constexpr (STAGE) {  // the staged outputs from each lane's home thread, coalesced
+    COUP_TRAJ_STAMP(5);
+    if constexpr (STAGE == 1) {  // the staged outputs from each lane's home thread, coalesced
       __syncthreads();
       const int64_t i = base + t;
       if (i < a.n) {
@@ -1960,15 +2058,21 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
       }
     }
   }
+  if constexpr (STAGE == 2) {
+    __syncthreads();  // the last step's staged outputs are complete
+    if (steps > 0) store_staged(steps - 1);
+    __syncthreads();  // ... and stored before the finished lanes' direct stores below
+  }
   if (!kNow && key == kKeyReset && base + lane < a.n) {  // finished on the last step
-    L = new_episode(L.episode + 1u, rng, none);
+    L = new_episode(unpack(rw).episode + 1u, rng, none);
     const int64_t o = (steps - 1) * x.stride + base + lane;
     if (FULL || a.legal) a.legal[o] = decision_mask(L);
     if (FULL || a.cur_player) a.cur_player[o] = (int8_t)L.M;
-    if (REC) x.rec[(steps - 1) * a.n + base + lane] = pack(L);
+    rw = pack(L);
+    if (REC) x.rec[(steps - 1) * a.n + base + lane] = rw;
   }
   __syncthreads();
-  s_rec[lane] = pack(L);
+  s_rec[lane] = rw;
   __syncthreads();
   if (base + t < a.n) {
     const int64_t i = base + t;
@@ -1976,6 +2080,7 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
     a.ep.add(i, s_eps[t], s_ret[t]);
   }
   if (errs) atomicAdd(a.err_count, errs);
+  COUP_TRAJ_STAMP_FLUSH(steps);
 }
 
 // NewInitialState / reset of selected lanes.  mode 0: fresh env (episode 0);
@@ -3751,7 +3856,7 @@ int step_many_fused(coup_env* env, int64_t steps, const coup_step_outputs* out, 
   const coup::TrajOut x{nullptr, slices ? n : 0, slices ? n * 2 * COUP_OBS_SIZE : 0};
   auto go = [&](auto tt, auto ww) {
     constexpr int T = decltype(tt)::value, W = decltype(ww)::value;
-    coup::note_launch("coup::k_trajectory_sorted<{}, false, true, {}, false>", T, W);
+    coup::note_launch("coup::k_trajectory_sorted<{}, false, true, {}, 0>", T, W);
     coup::k_trajectory_sorted<T, false, true, W><<<(unsigned)((n + T - 1) / T), T, 0, env->stream>>>(a, steps, x);
   };
   switch (env->knobs.fused_shape) {  // COUP_FUSED_SHAPE
@@ -3796,12 +3901,12 @@ int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, b
 #ifdef COUP_AB_VARIANTS
     auto shape = [&](auto tt, auto ww) {  // COUP_MANY_SHAPE: lanes per block, waves per SIMD budget
       constexpr int T = decltype(tt)::value, W = decltype(ww)::value;
-      coup::note_launch("coup::k_trajectory_sorted<{}, true, false, {}, false>", T, W);
-      coup::k_trajectory_sorted<T, true, false, W, false><<<(unsigned)((n + T - 1) / T), T, 0, R>>>(a, c, x);
+      coup::note_launch("coup::k_trajectory_sorted<{}, true, false, {}, 0>", T, W);
+      coup::k_trajectory_sorted<T, true, false, W, 0><<<(unsigned)((n + T - 1) / T), T, 0, R>>>(a, c, x);
     };
     if (env->knobs.many_stage)  // outputs staged by lane: 148.3 against 134.5 us per step (call r05m)
-      coup::note_launch("coup::k_trajectory_sorted<{}, true, false, 8, true>", TB),
-          coup::k_trajectory_sorted<TB, true, false, 8, true><<<grid, TB, 0, R>>>(a, c, x);
+      coup::note_launch("coup::k_trajectory_sorted<{}, true, false, 8, 1>", TB),
+          coup::k_trajectory_sorted<TB, true, false, 8, 1><<<grid, TB, 0, R>>>(a, c, x);
     else if (env->knobs.many_shape == 1)
       shape(std::integral_constant<int, 512>(), std::integral_constant<int, 8>());
     else if (env->knobs.many_shape == 2)
@@ -3811,8 +3916,8 @@ int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, b
     else if (env->knobs.many_shape == 4)
       shape(std::integral_constant<int, 1024>(), std::integral_constant<int, 4>());
     else if (overlap && env->knobs.overlap_lds > 0)  // COUP_OVERLAP_LDS: cap the rules' blocks per CU
-      coup::note_launch("coup::k_trajectory_sorted<{}, true, false, 8, false>", TB),
-          coup::k_trajectory_sorted<TB, true, false, 8, false><<<grid, TB, (unsigned)env->knobs.overlap_lds, R>>>(a, c, x);
+      coup::note_launch("coup::k_trajectory_sorted<{}, true, false, 8, 0>", TB),
+          coup::k_trajectory_sorted<TB, true, false, 8, 0><<<grid, TB, (unsigned)env->knobs.overlap_lds, R>>>(a, c, x);
     else
 #endif
 #ifndef COUP_TRAJ_NOFULL
@@ -3820,12 +3925,12 @@ int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, b
     // form, no pointer tests (c3 132.3 against 133.6-133.9 us per step, call
     // r06f; within the process-to-process spread, and fewer instructions)
     if (a.actions && a.rewards && a.step_type && a.legal && a.cur_player)
-      coup::note_launch("coup::k_trajectory_sorted<{}, true, false, 8, false, true>", TB),
-          coup::k_trajectory_sorted<TB, true, false, 8, false, true><<<grid, TB, 0, R>>>(a, c, x);
+      coup::note_launch("coup::k_trajectory_sorted<{}, true, false, 8, {}, true>", TB, coup::kTrajStage),
+          coup::k_trajectory_sorted<TB, true, false, 8, coup::kTrajStage, true><<<grid, TB, 0, R>>>(a, c, x);
     else
 #endif
-      coup::note_launch("coup::k_trajectory_sorted<{}, true, false, 8, false>", TB),
-          coup::k_trajectory_sorted<TB, true, false, 8, false><<<grid, TB, 0, R>>>(a, c, x);
+      coup::note_launch("coup::k_trajectory_sorted<{}, true, false, 8, {}>", TB, coup::kTrajStage),
+          coup::k_trajectory_sorted<TB, true, false, 8, coup::kTrajStage><<<grid, TB, 0, R>>>(a, c, x);
     COUP_HIP_TRY(hipGetLastError());
     if (overlap) {
       COUP_HIP_TRY(hipEventRecord(env->ev_rules[b], R));
@@ -3966,8 +4071,9 @@ int step_many_bare(coup_env* env, int64_t steps, const coup_step_outputs* out) {
   }
   if (coup::regroup_lanes(env->knobs, n)) {
     constexpr int TB = coup::kRolloutSortLanes;
-    coup::note_launch("coup::k_trajectory_sorted<{}, false, false, 8, false>", TB);
-    coup::k_trajectory_sorted<TB><<<(unsigned)((n + TB - 1) / TB), TB, 0, env->stream>>>(a, steps, {nullptr, 0});
+    coup::note_launch("coup::k_trajectory_sorted<{}, false, false, 8, {}>", TB, coup::kTrajStage);
+    coup::k_trajectory_sorted<TB, false, false, 8, coup::kTrajStage><<<(unsigned)((n + TB - 1) / TB), TB, 0, env->stream>>>(
+        a, steps, {nullptr, 0});
   } else {
     coup::note_launch("coup::k_step_trajectory");
     coup::k_step_trajectory<<<grid_for(n), coup::kThreads, 0, env->stream>>>(a, steps, 0);
@@ -4071,22 +4177,24 @@ int coup_step_trajectory(coup_env* env, int64_t steps, const coup_step_outputs* 
 #ifdef COUP_AB_VARIANTS
     switch (coup::sort_lanes(env->knobs.sort_lanes, coup::kRolloutSortLanes)) {
       case 256:
-        coup::note_launch("coup::k_trajectory_sorted<256, false, false, 8, false>");
+        coup::note_launch("coup::k_trajectory_sorted<256, false, false, 8, 0>");
         coup::k_trajectory_sorted<256><<<grid_for(n), 256, 0, env->stream>>>(a, steps, {nullptr, n});
         break;
       case 512:
-        coup::note_launch("coup::k_trajectory_sorted<512, false, false, 8, false>");
+        coup::note_launch("coup::k_trajectory_sorted<512, false, false, 8, 0>");
         coup::k_trajectory_sorted<512><<<(unsigned)((n + 511) / 512), 512, 0, env->stream>>>(a, steps, {nullptr, n});
         break;
       default:
-        coup::note_launch("coup::k_trajectory_sorted<1024, false, false, 8, false>");
-        coup::k_trajectory_sorted<1024><<<(unsigned)((n + 1023) / 1024), 1024, 0, env->stream>>>(a, steps, {nullptr, n});
+        coup::note_launch("coup::k_trajectory_sorted<1024, false, false, 8, {}>", coup::kTrajStage);
+        coup::k_trajectory_sorted<1024, false, false, 8, coup::kTrajStage>
+            <<<(unsigned)((n + 1023) / 1024), 1024, 0, env->stream>>>(a, steps, {nullptr, n});
         break;
     }
 #else
     constexpr int TB = coup::kRolloutSortLanes;
-    coup::note_launch("coup::k_trajectory_sorted<{}, false, false, 8, false>", TB);
-    coup::k_trajectory_sorted<TB><<<(unsigned)((n + TB - 1) / TB), TB, 0, env->stream>>>(a, steps, {nullptr, n});
+    coup::note_launch("coup::k_trajectory_sorted<{}, false, false, 8, {}>", TB, coup::kTrajStage);
+    coup::k_trajectory_sorted<TB, false, false, 8, coup::kTrajStage><<<(unsigned)((n + TB - 1) / TB), TB, 0, env->stream>>>(
+        a, steps, {nullptr, n});
 #endif
   } else {
     coup::note_launch("coup::k_step_trajectory");
@@ -4571,10 +4679,11 @@ int coup_launch_log(char* buf, int cap, int reset) {
 }
 
 int coup_build_flags(void) {
+  const int stage = coup::kTrajStage << COUP_BUILD_TRAJ_STAGE_SHIFT;
 #ifdef COUP_AB_VARIANTS
-  return COUP_BUILD_AB_VARIANTS;
+  return COUP_BUILD_AB_VARIANTS | stage;
 #else
-  return 0;
+  return stage;
 #endif
 }
 
@@ -4660,6 +4769,18 @@ int coup_measure_store_sweep(float* dst, int64_t n_float4, int threads, int pass
 
 }  // extern "C"
 
+#ifdef COUP_TRAJ_PHASES
+// Measurement builds (-DCOUP_TRAJ_PHASES): k_trajectory_sorted's per-phase
+// shader cycles summed over waves, then wave-steps (kTrajPhases + 1 values).
+extern "C" int coup_debug_traj_phases(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_traj_phases), sizeof(g_traj_phases)) != hipSuccess) return 2;
+  if (reset) {
+    const unsigned long long z[kTrajPhases + 1] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_traj_phases), z, sizeof(z)) != hipSuccess) return 2;
+  }
+  return 0;
+}
+#endif
 #ifdef COUP_COUNT_PHILOX
 extern "C" int coup_debug_philox_counts(unsigned long long* out, int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_philox_counts), sizeof(unsigned long long) * 2) != hipSuccess) return 2;

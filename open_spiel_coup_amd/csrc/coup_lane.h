@@ -983,8 +983,12 @@ struct Rng {
       blk = philox4x32_10(make_uint4(idx >> 2, ep, seed_hi, 0x436F7570u), env_id, seed_lo);
       blk_tag = tag;
     }
-    const uint32_t j = idx & 3u;
-    return j == 0 ? blk.x : (j == 1 ? blk.y : (j == 2 ? blk.z : blk.w));
+    // two levels of selects on the word index's bits: the equality chain can
+    // be folded into a variable extractelement, which the backend lowers
+    // through scratch memory (an indexed private load)
+    const bool odd = (idx & 1u) != 0u;
+    const uint32_t lo = odd ? blk.y : blk.x, hi = odd ? blk.w : blk.z;
+    return (idx & 2u) ? hi : lo;
   }
 };
 

@@ -593,9 +593,15 @@ __global__ __launch_bounds__(T, 8) void k_rollout_sorted(RolloutArgs a) {
     resolve_chance(L, rng);  // a lane left at a chance node
     key = draw_key(L, rng, errs);
   }
+  // two barriers per step (coup_kernels.hip k_trajectory_sorted: this step's
+  // bins were zeroed before the last step's slot barrier, and every thread
+  // reads its slot before it reaches this step's count barrier)
+  __syncthreads();  // the bins and by-lane counters above are initialised
   for (int64_t s = 0; s < a.steps; ++s) {
     uint32_t* bin = s_bin[s & 1];
-    __syncthreads();  // this step's bins are zero; last step's slots are read
+#ifdef COUP_TRAJ_TOP_BARRIER
+    __syncthreads();  // measurement builds: the third barrier of rounds 2-5
+#endif
     const uint32_t rank = atomicAdd(&bin[key], 1u);
     __syncthreads();
 #ifndef COUP_NP_BINS_LANE
@@ -713,24 +719,39 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
   s_ret[t] = 0;
   NRng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, base + t), 0u, make_uint4(0, 0, 0, 0)};
   NLane<N> L = initial_lane<N>(0u);
+  // ra, rb: the lane's packed record, the value that crosses the step
+  // loop's back edge (the regroup moves it through LDS); every exit of a
+  // lane's step packs its NLane into them, so the unpacked fields die inside
+  // the step and the exits' join copies 8 registers, not the NLane's
+  // (coup_kernels.hip k_trajectory_sorted: the 2-player form)
+  uint4 ra = make_uint4(0u, 0u, 0u, 0u), rb = ra;
   uint32_t lane = t, key = kKeyDead, errs = 0u;
   if (base + t < a.n) {
-    L = unpack<N>(a.sa[base + t], a.sb[base + t]);
+    ra = a.sa[base + t];
+    rb = a.sb[base + t];
+    L = unpack<N>(ra, rb);
     if (is_terminal(L)) {
       key = kKeyFirst;
     } else {
       resolve_chance(L, rng);  // a lane left at a chance node
       const uint32_t m = decision_mask(L);
       key = m ? ahead_key(L, sample_action(m, rng.draw(L.episode, L.move))) : kKeyDead;
+      pack(L, ra, rb);
     }
   }
   const uint32_t nvalid = base < a.n ? (uint32_t)(a.n - base < T ? a.n - base : T) : 0u;  // block-uniform
+  // two barriers per step (coup_kernels.hip k_trajectory_sorted); the last
+  // step's staged outputs are stored behind this step's count barrier, which
+  // every thread reaches after staging them
+  __syncthreads();  // the bins and by-lane counters above are initialised
   for (int64_t s = 0; s < steps; ++s) {
     uint32_t* bin = s_bin[s & 1];
-    __syncthreads();  // this step's bins are zero; last step's slots and outputs are complete
-    if (STAGE == 1 && s > 0 && t < nvalid) store_staged<N>(a, (s - 1) * a.ostride + base + t, s_out[t], s_olegal[t]);
+#ifdef COUP_TRAJ_TOP_BARRIER
+    __syncthreads();  // measurement builds: the third barrier of rounds 2-5
+#endif
     const uint32_t rank = atomicAdd(&bin[key], 1u);
     __syncthreads();
+    if (STAGE == 1 && s > 0 && t < nvalid) store_staged<N>(a, (s - 1) * a.ostride + base + t, s_out[t], s_olegal[t]);
     // (the shuffle form, wave_bins_below, spilled 38 VGPRs instead of 22 here
     // and measured 26.07 vs 24.12 us per step: profiles/r03/ab/
     // np_scan_forms_traj_rollout.jsonl; the DPP form below does not spill)
@@ -743,16 +764,16 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
     const uint32_t pos = bins_below<7>(bin, key) + rank;  // keys up to kKeyFirst = 26
 #endif
     if (t < 32u) s_bin[(s + 1) & 1][t] = 0u;  // read for the last time in step s - 1
-    uint4 wa, wb;
-    pack(L, wa, wb);
-    s_a[pos] = wa;
-    s_b[pos] = wb;
+    s_a[pos] = ra;
+    s_b[pos] = rb;
     s_meta[pos] = lane | (key << kO);
     __syncthreads();
     const uint32_t m = s_meta[t];
     lane = m & (T - 1u);
     key = (m >> kO) & 31u;
-    L = unpack<N>(s_a[t], s_b[t]);
+    ra = s_a[t];
+    rb = s_b[t];
+    L = unpack<N>(ra, rb);
     const int64_t li = base + lane;
     if (li >= a.n) continue;  // past the batch
     const int64_t o = s * a.ostride + li;
@@ -775,6 +796,7 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
       const uint32_t legal = decision_mask(L);
       out(stage_head(-1, 0u, 0u, 0u) | stage_player((int)L.M), legal);
       key = ahead_key(L, sample_action(legal, rng.draw(L.episode, L.move)));
+      pack(L, ra, rb);
       continue;
     }
     if (key == kKeyReset) {  // finished in step s - 1 with auto-reset (vector_env.py:62-65)
@@ -788,6 +810,7 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
     if (key == kKeyDead) {  // no legal decision: coup_step's rejected step
       errs += 1u;
       out(stage_head(-1, 1u, 0u, 0u) | stage_player(current_player(L)), legal_mask(L));
+      pack(L, ra, rb);
       continue;
     }
     const uint32_t x = key_action(key);
@@ -804,28 +827,30 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
       if (ar) {
         out(head, 0u);  // legal mask and player once the next episode is dealt
         key = kKeyReset;
+        pack(L, ra, rb);
         continue;
       }
       key = kKeyFirst;
       out(head | stage_player(-4), 0u);  // terminal: no legal actions, kTerminalPlayerId
+      pack(L, ra, rb);
       continue;
     }
     const uint32_t legal = decision_mask(L);
     out(head | stage_player((int)L.M), legal);
     if (s + 1 < steps) key = ahead_key(L, sample_action(legal, rng.draw(L.episode, L.move)));
+    pack(L, ra, rb);
   }
   __syncthreads();  // the last step's staged outputs are complete
   if (STAGE == 1 && steps > 0 && t < nvalid)
     store_staged<N>(a, (steps - 1) * a.ostride + base + t, s_out[t], s_olegal[t]);
   if (steps > 0 && key == kKeyReset && base + lane < a.n) {  // finished on the last step
-    L = new_episode<N>(L.episode + 1u, rng);
+    L = new_episode<N>(unpack<N>(ra, rb).episode + 1u, rng);
     store_legal_player(a, (steps - 1) * a.ostride + base + lane, decision_mask(L), (int)L.M);
+    pack(L, ra, rb);
   }
   __syncthreads();
-  uint4 wa, wb;
-  pack(L, wa, wb);
-  s_a[lane] = wa;
-  s_b[lane] = wb;
+  s_a[lane] = ra;
+  s_b[lane] = rb;
   __syncthreads();
   if (base + t < a.n) {
     const int64_t i = base + t;

@@ -187,9 +187,9 @@ void coup::k_step<true, 0, 256, 2, false> | void coup::k_step<true, 4, 256, 1, f
 void coup::k_step<true, 4, 256, 2, false> | void coup::k_step<true, 9, 256, 0, false> |
 void coup::k_step_group<1, false> | void coup::k_step_group<1, true> |
 void coup::k_step_sorted<false, 512> | void coup::k_step_sorted<true, 512> |
-void coup::k_trajectory_sorted<1024, false, false, 8, false, false> |
-void coup::k_trajectory_sorted<1024, true, false, 8, false, false> |
-void coup::k_trajectory_sorted<1024, true, false, 8, false, true> |
+void coup::k_trajectory_sorted<1024, false, false, 8, 2, false> |
+void coup::k_trajectory_sorted<1024, true, false, 8, 2, false> |
+void coup::k_trajectory_sorted<1024, true, false, 8, 2, true> |
 void coup::k_store_sweep<512, 2> | void coup::k_store_sweep<1024, 2>
 """
 
@@ -233,7 +233,8 @@ def test_product_library_ships_only_the_shipped_kernels():
     want = _shipped_kernels()
     assert got == want, {"unexpected": sorted(got - want), "missing": sorted(want - got)}
     lib = ctypes.CDLL(_native.LIB_PATH)
-    assert lib.coup_build_flags() == 0
+    # the product: no variants, the rules trajectories' outputs staged by lane (2)
+    assert lib.coup_build_flags() == 2 << _native.BUILD_TRAJ_STAGE_SHIFT
 
 
 def test_measurement_build_holds_the_variants():
@@ -245,11 +246,11 @@ def test_measurement_build_holds_the_variants():
     for k in ("void coup::k_obs_sweep<1>", "void coup::k_obs_sweep_rows<256, 2, 0, 0>", "void coup::k_step_group<4, true>",
               "void coup::k_step<true, 1, 256, 0, false>", "void coup::k_step_sorted<true, 1024>",
               "void coup::k_info_sweep<512, 2, 0>", "void coup::k_step_obs_pipe<512, 2>",
-              "void coup::k_trajectory_sorted<1024, false, true, 4, false, false>",
-              "void coup::k_trajectory_sorted<1024, true, false, 8, true, false>", "void coup::k_obs_sweep_nib<512, 2>",
+              "void coup::k_trajectory_sorted<1024, false, true, 4, 0, false>",
+              "void coup::k_trajectory_sorted<1024, true, false, 8, 1, false>", "void coup::k_obs_sweep_nib<512, 2>",
               "void coup::np::k_step_sorted<6, true, true, 1024, true, 4>",
               "void coup::np::k_rollout_sorted<6, 1024, false>", "void coup::np::k_trajectory_sorted<6, 1024, 0>"):
         assert k in got, k
     lib = ctypes.CDLL(build.VARIANTS_OUT)
     lib.coup_build_flags.restype = ctypes.c_int
-    assert lib.coup_build_flags() == _native.BUILD_AB_VARIANTS
+    assert lib.coup_build_flags() == _native.BUILD_AB_VARIANTS | (2 << _native.BUILD_TRAJ_STAGE_SHIFT)

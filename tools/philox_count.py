@@ -6,7 +6,9 @@
 Each wave-level evaluation of philox4x32_10 (one pass of the wave through
 it, whatever its active lanes) is counted with the lanes active in it.
 Prints evaluations per wave per env step and the mean active lanes, for the
-step kernel and the fused rollout.  Measurement tool only.
+step kernel, the fused rollout and (2 players) coup_step_many's c3 form --
+the rules trajectory with every step's records, from 2^20 lanes with
+observations (its writers draw nothing).  Measurement tool only.
 """
 import argparse
 import ctypes
@@ -50,6 +52,17 @@ def main():
         evals, lanes = buf[0], buf[1]
         out[kind] = {"evals_per_wave_step": round(evals / (waves * a.steps), 3),
                      "active_lanes_per_eval": round(lanes / max(evals, 1), 1)}
+    if a.players == 2:
+        envo = BatchedCoupEnv(a.batch, seed=1, auto_reset=True, obs=True, device="cuda:0")
+        envo.rollout(256)
+        torch.cuda.synchronize()
+        fn(buf, 1)
+        envo.step_many(a.steps)
+        torch.cuda.synchronize()
+        fn(buf, 1)
+        evals, lanes = buf[0], buf[1]
+        out["step_many_obs"] = {"evals_per_wave_step": round(evals / (waves * a.steps), 3),
+                                "active_lanes_per_eval": round(lanes / max(evals, 1), 1)}
     print(json.dumps(out), flush=True)
 
 
