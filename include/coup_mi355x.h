@@ -466,7 +466,7 @@ int coup_info_split_variant(int64_t batch);
 /* Bits 3:1: how the 2-player rules trajectories store each step's outputs
  * (their STAGE template argument): 0 from the thread
  * that played the lane, 2 staged by lane in LDS and stored by the lane's
- * home thread behind the next step's count barrier (the product). */
+ * home thread behind the next step's count barrier (a measurement build). */
 #define COUP_BUILD_TRAJ_STAGE_SHIFT 1
 #define COUP_BUILD_TRAJ_STAGE_MASK 0x7
 int coup_build_flags(void);

@@ -1776,10 +1776,13 @@ struct TrajObsLds {
 template <int T>
 struct TrajNoLds {};
 // STAGE: a step's outputs by lane, stored by each lane's home thread
-// The output staging the shipped rules trajectories use (STAGE above;
-// -DCOUP_TRAJ_OUT_STAGE=0 measurement builds store from the playing thread)
+// The output staging the shipped rules trajectories use (STAGE above): 0,
+// the playing thread stores.  -DCOUP_TRAJ_OUT_STAGE=2 measurement builds
+// stage by lane: equal within noise (c3 132.5 against 132.4 us per step, the
+// bare trajectory at 2^20 lanes 17.54 against 17.34, call r06l), so the
+// simpler form ships.
 #ifndef COUP_TRAJ_OUT_STAGE
-#define COUP_TRAJ_OUT_STAGE 2
+#define COUP_TRAJ_OUT_STAGE 0
 #endif
 constexpr int kTrajStage = COUP_TRAJ_OUT_STAGE;
 constexpr int8_t kCpDeferred = -128;  // STAGE 2: legal mask, player and record stored by the reset group
@@ -1834,8 +1837,15 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
   // once, not again at the next step's top).
   uint4 rw = make_uint4(0u, 0u, 0u, 0u);
   uint32_t lane = t, key = kKeyDead, errs = 0u;
-  // a drawn decision's sort key
-  auto draw_decision = [&](uint32_t legal) { return regroup_key(L, sample_action(legal, rng.draw(L.episode, L.move))); };
+  // a drawn decision's sort key (-DCOUP_TRAJ_SELECT_DRAW measurement builds:
+  // the loop-free policy draw)
+  auto draw_decision = [&](uint32_t legal) {
+#ifdef COUP_TRAJ_SELECT_DRAW
+    return regroup_key(L, sample_action_select(legal, rng.draw(L.episode, L.move)));
+#else
+    return regroup_key(L, sample_action(legal, rng.draw(L.episode, L.move)));
+#endif
+  };
   // STAGE 2: step sp's staged outputs of lane base + t, from its home thread
   auto store_staged = [&](int64_t sp) {
     if constexpr (STAGE == 2) {
@@ -1903,28 +1913,41 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
     const int64_t o = s * x.stride + li;
     uint4* const rec_s = REC ? x.rec + s * a.n + li : nullptr;  // step s's record of the lane
     // the lane's step-s outputs: to the buffers, or (STAGE) to LDS by lane
+#if defined(COUP_ABLATE_TRAJ_STORES) && COUP_ABLATE_TRAJ_STORES >= 1
+    // measurement builds: the small outputs not stored (1), nor the records
+    // (2) -- wrong results, the stores' share of the rules trajectory
+    constexpr bool kSkipOut = true, kSkipRec = COUP_ABLATE_TRAJ_STORES >= 2;
+#else
+    constexpr bool kSkipOut = false, kSkipRec = false;
+#endif
     auto put_act = [&](int8_t v) {
+      if constexpr (kSkipOut) return;
       if constexpr (STAGE != 0) s_st.act[lane] = v;
       else if (FULL || a.actions) a.actions[o] = v;
     };
     auto put_rew = [&](uint16_t v) {
+      if constexpr (kSkipOut) return;
       if constexpr (STAGE != 0) s_st.rew[lane] = v;
       else if (FULL || a.rewards) reinterpret_cast<uint16_t*>(a.rewards)[o] = v;
     };
     auto put_st = [&](uint8_t v) {
+      if constexpr (kSkipOut) return;
       if constexpr (STAGE != 0) s_st.st[lane] = v;
       else if (FULL || a.step_type) a.step_type[o] = v;
     };
     auto put_legal = [&](uint32_t v) {
+      if constexpr (kSkipOut) return;
       if constexpr (STAGE != 0) s_st.legal[lane] = v;
       else if (FULL || a.legal) a.legal[o] = v;
     };
     auto put_cp = [&](int8_t v) {
+      if constexpr (kSkipOut) return;
       if constexpr (STAGE != 0) s_st.cp[lane] = v;
       else if (FULL || a.cur_player) a.cur_player[o] = v;
     };
     auto put_rec = [&](const Lane& R) {  // also the lane's rw
       rw = pack(R);
+      if constexpr (kSkipRec) return;
       if constexpr (STAGE != 0) s_st.rec[lane] = rw;
       else if (REC) *rec_s = rw;
     };

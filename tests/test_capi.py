@@ -187,9 +187,9 @@ void coup::k_step<true, 0, 256, 2, false> | void coup::k_step<true, 4, 256, 1, f
 void coup::k_step<true, 4, 256, 2, false> | void coup::k_step<true, 9, 256, 0, false> |
 void coup::k_step_group<1, false> | void coup::k_step_group<1, true> |
 void coup::k_step_sorted<false, 512> | void coup::k_step_sorted<true, 512> |
-void coup::k_trajectory_sorted<1024, false, false, 8, 2, false> |
-void coup::k_trajectory_sorted<1024, true, false, 8, 2, false> |
-void coup::k_trajectory_sorted<1024, true, false, 8, 2, true> |
+void coup::k_trajectory_sorted<1024, false, false, 8, 0, false> |
+void coup::k_trajectory_sorted<1024, true, false, 8, 0, false> |
+void coup::k_trajectory_sorted<1024, true, false, 8, 0, true> |
 void coup::k_store_sweep<512, 2> | void coup::k_store_sweep<1024, 2>
 """
 
@@ -233,8 +233,8 @@ def test_product_library_ships_only_the_shipped_kernels():
     want = _shipped_kernels()
     assert got == want, {"unexpected": sorted(got - want), "missing": sorted(want - got)}
     lib = ctypes.CDLL(_native.LIB_PATH)
-    # the product: no variants, the rules trajectories' outputs staged by lane (2)
-    assert lib.coup_build_flags() == 2 << _native.BUILD_TRAJ_STAGE_SHIFT
+    # the product: no variants, the rules trajectories' outputs stored by the playing thread (0)
+    assert lib.coup_build_flags() == 0
 
 
 def test_measurement_build_holds_the_variants():
@@ -253,4 +253,4 @@ def test_measurement_build_holds_the_variants():
         assert k in got, k
     lib = ctypes.CDLL(build.VARIANTS_OUT)
     lib.coup_build_flags.restype = ctypes.c_int
-    assert lib.coup_build_flags() == _native.BUILD_AB_VARIANTS | (2 << _native.BUILD_TRAJ_STAGE_SHIFT)
+    assert lib.coup_build_flags() == _native.BUILD_AB_VARIANTS
