@@ -32,36 +32,9 @@ __device__ __forceinline__ void count_philox_eval() {
 #define COUP_PHILOX_HOOK() count_philox_eval()
 #endif
 #ifdef COUP_TRAJ_PHASES
-// Measurement builds: where k_trajectory_sorted's waves spend their steps.
-// Each wave stamps s_memtime (the shader clock) at fixed points of every
-// step and accumulates the cycles between consecutive stamps per phase
-// (coup_debug_traj_phases): [0] the count atomic and the count barrier,
-// [1] the prefix and the slot writes, [2] the slot barrier, [3] the slot
-// read, unpack and the FIRST / reset / rejected paths, [4] the decision and
-// its deals, [5] the outputs, the legal mask and the next draw; [6] wave-steps.
-// A stamp in a branch no lane of the wave takes is skipped, and its cycles
-// go to the next stamp's phase.
-constexpr int kTrajPhases = 6;
-__device__ unsigned long long g_traj_phases[kTrajPhases + 1];
-#define COUP_TRAJ_STAMP(k)                                                    \
-  do {                                                                         \
-    const uint32_t now_ = (uint32_t)__builtin_amdgcn_s_memtime();             \
-    ph_[k] += now_ - ph_last_;                                                 \
-    ph_last_ = now_;                                                           \
-  } while (0)
-#define COUP_TRAJ_STAMP_DECL uint32_t ph_[kTrajPhases] = {}, ph_last_ = (uint32_t)__builtin_amdgcn_s_memtime();
-#define COUP_TRAJ_STAMP_FLUSH(steps)                                          \
-  do {                                                                         \
-    if ((threadIdx.x & 63u) == 0u) {                                           \
-      for (int k_ = 0; k_ < kTrajPhases; ++k_) atomicAdd(&g_traj_phases[k_], (unsigned long long)ph_[k_]); \
-      atomicAdd(&g_traj_phases[kTrajPhases], (unsigned long long)(steps));    \
-    }                                                                          \
-  } while (0)
-#else
-#define COUP_TRAJ_STAMP(k)
-#define COUP_TRAJ_STAMP_DECL
-#define COUP_TRAJ_STAMP_FLUSH(steps)
+__device__ unsigned long long g_traj_phases[7];  // coup_traj_phases.h
 #endif
+#include "coup_traj_phases.h"
 #include "coup_lane.h"
 #include "coup_launch_log.h"
 #include "coup_mi355x.h"
@@ -2103,7 +2076,7 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
     a.ep.add(i, s_eps[t], s_ret[t]);
   }
   if (errs) atomicAdd(a.err_count, errs);
-  COUP_TRAJ_STAMP_FLUSH(steps);
+  COUP_TRAJ_STAMP_FLUSH(g_traj_phases, steps);
 }
 
 // NewInitialState / reset of selected lanes.  mode 0: fresh env (episode 0);

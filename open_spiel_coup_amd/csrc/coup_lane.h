@@ -983,12 +983,18 @@ struct Rng {
       blk = philox4x32_10(make_uint4(idx >> 2, ep, seed_hi, 0x436F7570u), env_id, seed_lo);
       blk_tag = tag;
     }
+#ifdef COUP_RNG_SELECT_CHAIN
+    // measurement builds: rounds 1-5's equality chain
+    const uint32_t j = idx & 3u;
+    return j == 0 ? blk.x : (j == 1 ? blk.y : (j == 2 ? blk.z : blk.w));
+#else
     // two levels of selects on the word index's bits: the equality chain can
     // be folded into a variable extractelement, which the backend lowers
     // through scratch memory (an indexed private load)
     const bool odd = (idx & 1u) != 0u;
     const uint32_t lo = odd ? blk.y : blk.x, hi = odd ? blk.w : blk.z;
     return (idx & 2u) ? hi : lo;
+#endif
   }
 };
 

@@ -22,6 +22,10 @@ __device__ __forceinline__ void count_philox_eval() {
 }
 #define COUP_PHILOX_HOOK() count_philox_eval()
 #endif
+#ifdef COUP_TRAJ_PHASES
+__device__ unsigned long long g_np_traj_phases[7];  // coup_traj_phases.h
+#endif
+#include "coup_traj_phases.h"
 #include "coup_launch_log.h"
 #include "coup_nlane.h"
 #include "coup_np.h"
@@ -744,6 +748,7 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
   // step's staged outputs are stored behind this step's count barrier, which
   // every thread reaches after staging them
   __syncthreads();  // the bins and by-lane counters above are initialised
+  COUP_TRAJ_STAMP_DECL
   for (int64_t s = 0; s < steps; ++s) {
     uint32_t* bin = s_bin[s & 1];
 #ifdef COUP_TRAJ_TOP_BARRIER
@@ -751,6 +756,7 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
 #endif
     const uint32_t rank = atomicAdd(&bin[key], 1u);
     __syncthreads();
+    COUP_TRAJ_STAMP(0);
     if (STAGE == 1 && s > 0 && t < nvalid) store_staged<N>(a, (s - 1) * a.ostride + base + t, s_out[t], s_olegal[t]);
     // (the shuffle form, wave_bins_below, spilled 38 VGPRs instead of 22 here
     // and measured 26.07 vs 24.12 us per step: profiles/r03/ab/
@@ -767,7 +773,9 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
     s_a[pos] = ra;
     s_b[pos] = rb;
     s_meta[pos] = lane | (key << kO);
+    COUP_TRAJ_STAMP(1);
     __syncthreads();
+    COUP_TRAJ_STAMP(2);
     const uint32_t m = s_meta[t];
     lane = m & (T - 1u);
     key = (m >> kO) & 31u;
@@ -813,12 +821,14 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
       pack(L, ra, rb);
       continue;
     }
+    COUP_TRAJ_STAMP(3);
     const uint32_t x = key_action(key);
     const uint32_t err_before = L.err;
     apply_decision(L, x);
     L.move += 1u;
     resolve_chance(L, rng);
     errs += (L.err && !err_before) ? 1u : 0u;
+    COUP_TRAJ_STAMP(4);
     const bool term = is_terminal(L);
     const uint32_t head = stage_head((int)x, term ? 2u : 1u, L.rloser, L.rcount);
     if (term) {
@@ -839,6 +849,7 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
     out(head | stage_player((int)L.M), legal);
     if (s + 1 < steps) key = ahead_key(L, sample_action(legal, rng.draw(L.episode, L.move)));
     pack(L, ra, rb);
+    COUP_TRAJ_STAMP(5);
   }
   __syncthreads();  // the last step's staged outputs are complete
   if (STAGE == 1 && steps > 0 && t < nvalid)
@@ -859,6 +870,7 @@ __global__ __launch_bounds__(T, 8) void k_trajectory_sorted(StepArgs a, int64_t 
     a.ep.add(i, s_eps[t], s_ret[t]);
   }
   if (errs) atomicAdd(a.err_count, errs);
+  COUP_TRAJ_STAMP_FLUSH(g_np_traj_phases, steps);
 }
 
 template <int N>
@@ -1279,6 +1291,18 @@ hipError_t launch_import(const Env& e, const uint32_t* src) {
 }  // namespace np
 }  // namespace coup
 
+#ifdef COUP_TRAJ_PHASES
+// Measurement builds (-DCOUP_TRAJ_PHASES): np::k_trajectory_sorted's
+// per-phase shader cycles summed over waves, then wave-steps.
+extern "C" int coup_debug_np_traj_phases(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_np_traj_phases), sizeof(g_np_traj_phases)) != hipSuccess) return 2;
+  if (reset) {
+    const unsigned long long z[kTrajPhases + 1] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_np_traj_phases), z, sizeof(z)) != hipSuccess) return 2;
+  }
+  return 0;
+}
+#endif
 #ifdef COUP_COUNT_PHILOX
 extern "C" int coup_debug_philox_counts_np(unsigned long long* out, int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_philox_counts), sizeof(unsigned long long) * 2) != hipSuccess) return 2;

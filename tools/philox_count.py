@@ -6,7 +6,8 @@
 Each wave-level evaluation of philox4x32_10 (one pass of the wave through
 it, whatever its active lanes) is counted with the lanes active in it.
 Prints evaluations per wave per env step and the mean active lanes, for the
-step kernel, the fused rollout and (2 players) coup_step_many's c3 form --
+step kernel, the fused rollout, coup_step_many without tensors (one
+trajectory launch) and (2 players) coup_step_many's c3 form --
 the rules trajectory with every step's records, from 2^20 lanes with
 observations (its writers draw nothing).  Measurement tool only.
 """
@@ -52,6 +53,15 @@ def main():
         evals, lanes = buf[0], buf[1]
         out[kind] = {"evals_per_wave_step": round(evals / (waves * a.steps), 3),
                      "active_lanes_per_eval": round(lanes / max(evals, 1), 1)}
+    # coup_step_many without tensors: one trajectory launch (c2 / c4's form)
+    torch.cuda.synchronize()
+    fn(buf, 1)
+    env.step_many(a.steps)
+    torch.cuda.synchronize()
+    fn(buf, 1)
+    evals, lanes = buf[0], buf[1]
+    out["step_many"] = {"evals_per_wave_step": round(evals / (waves * a.steps), 3),
+                        "active_lanes_per_eval": round(lanes / max(evals, 1), 1)}
     if a.players == 2:
         envo = BatchedCoupEnv(a.batch, seed=1, auto_reset=True, obs=True, device="cuda:0")
         envo.rollout(256)

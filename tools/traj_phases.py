@@ -6,8 +6,9 @@ build only).
 
 k_trajectory_sorted stamps the shader clock (s_memtime) at fixed points of
 every step; coup_debug_traj_phases returns the cycles each phase took,
-summed over waves, and the wave-steps.  Prints, per form (c3's rules
-trajectory with records; the bare trajectory of tensor-free steps), the
+summed over waves, and the wave-steps (--players 6: np::k_trajectory_sorted,
+coup_debug_np_traj_phases).  Prints, per form (c3's rules trajectory with
+records; the bare trajectory of tensor-free steps), the
 cycles per wave-step of each phase and its share.  The stamps cost a few
 dozen cycles each, so the totals run above the product kernel's.
 Measurement tool only.
@@ -30,17 +31,20 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=1 << 20)
     ap.add_argument("--steps", type=int, default=16)
+    ap.add_argument("--players", type=int, default=2, help="6: np::k_trajectory_sorted (c4's form)")
     a = ap.parse_args()
     import torch
 
     from open_spiel_coup_amd import BatchedCoupEnv, _native
     lib = _native.load()
-    fn = getattr(lib, "coup_debug_traj_phases", None)
+    fn = getattr(lib, "coup_debug_traj_phases" if a.players == 2 else "coup_debug_np_traj_phases", None)
     if fn is None:
         raise SystemExit("not a COUP_TRAJ_PHASES build (set COUP_LIB_PATH)")
     buf = (ctypes.c_ulonglong * (len(PHASES) + 1))()
-    for form, obs in (("c3 rules trajectory (records)", True), ("bare trajectory", False)):
-        env = BatchedCoupEnv(a.batch, seed=1, auto_reset=True, obs=obs, device="cuda:0")
+    forms = ((("c3 rules trajectory (records)", True), ("bare trajectory", False)) if a.players == 2 else
+             (("bare trajectory (%d players)" % a.players, False),))
+    for form, obs in forms:
+        env = BatchedCoupEnv(a.batch, seed=1, auto_reset=True, obs=obs, device="cuda:0", num_players=a.players)
         env.rollout(256)
         env.step_many(a.steps)  # warm
         torch.cuda.synchronize()
