@@ -1861,6 +1861,9 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
 #ifdef COUP_TRAJ_TOP_BARRIER
     __syncthreads();  // measurement builds: the third barrier of rounds 2-5
 #endif
+#ifdef COUP_TRAJ_PRIO
+    __builtin_amdgcn_s_setprio(0);  // measurement builds: the step's slow waves raised below
+#endif
     const uint32_t rank = atomicAdd(&bin[key], 1u);
     __syncthreads();
     COUP_TRAJ_STAMP(0);
@@ -1941,7 +1944,26 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
       continue;
     }
     if (!kNow && key == kKeyReset) {  // finished in step s - 1 with auto-reset (vector_env.py:62-65)
+#ifdef COUP_TRAJ_PRIO
+      __builtin_amdgcn_s_setprio(COUP_TRAJ_PRIO);  // a wave of the reset group: the block's slowest
+#endif
+#ifdef COUP_ABLATE_TRAJ_RESET
+      {  // measurement builds: the reset group's cost without its deals (wrong results): four distinct
+         // types from the lane's id and episode, no Philox block, then the decision drawn as usual
+        Lane R = initial_lane(L.episode + 1u);
+        const uint32_t b0 = (uint32_t)(li + L.episode) % 5u, b1 = (b0 + 1u) % 5u, b2 = (b0 + 2u) % 5u,
+                       b3 = (b0 + 3u) % 5u;
+        R.h0 = (2u * min(b0, b2)) | ((2u * max(b0, b2)) << 4) | 0xFF00u;
+        R.h1 = (2u * min(b1, b3)) | ((2u * max(b1, b3)) << 4) | 0xFF00u;
+        R.deck -= (1u << (4u * b0)) + (1u << (4u * b1)) + (1u << (4u * b2)) + (1u << (4u * b3));
+        R.qlen = 0u;
+        R.qids = 0u;
+        R.move = 4u;
+        L = R;
+      }
+#else
       L = new_episode(L.episode + 1u, rng, none);
+#endif
       const uint32_t legal = decision_mask(L);
       if (FULL || a.legal) a.legal[o - x.stride] = legal;
       if (FULL || a.cur_player) a.cur_player[o - x.stride] = (int8_t)L.M;
@@ -1964,6 +1986,9 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
     const uint32_t err_before = L.err;
     apply_decision_v1(L, act);  // regrouped: the branch form, as k_rollout_sorted
     L.move += 1u;
+#ifdef COUP_TRAJ_PRIO
+    if (L.qlen != 0u) __builtin_amdgcn_s_setprio(COUP_TRAJ_PRIO);  // a wave with deals
+#endif
     resolve_chance(L, rng);
     errs += (L.err && !err_before) ? 1u : 0u;
     COUP_TRAJ_STAMP(4);
@@ -4066,6 +4091,19 @@ int step_many_bare(coup_env* env, int64_t steps, const coup_step_outputs* out) {
     a.cur_player = out->cur_player;
   }
   if (coup::regroup_lanes(env->knobs, n)) {
+#ifdef COUP_AB_VARIANTS
+    // measurement builds: COUP_SORT_THREADS=256 / 512 lanes per regrouping block
+    if (env->knobs.sort_lanes == 256 || env->knobs.sort_lanes == 512) {
+      if (env->knobs.sort_lanes == 256)
+        coup::note_launch("coup::k_trajectory_sorted<256, false, false, 8, 0>"),
+            coup::k_trajectory_sorted<256><<<(unsigned)((n + 255) / 256), 256, 0, env->stream>>>(a, steps, {nullptr, 0});
+      else
+        coup::note_launch("coup::k_trajectory_sorted<512, false, false, 8, 0>"),
+            coup::k_trajectory_sorted<512><<<(unsigned)((n + 511) / 512), 512, 0, env->stream>>>(a, steps, {nullptr, 0});
+      COUP_HIP_TRY(hipGetLastError());
+      return COUP_OK;
+    }
+#endif
     constexpr int TB = coup::kRolloutSortLanes;
     coup::note_launch("coup::k_trajectory_sorted<{}, false, false, 8, {}>", TB, coup::kTrajStage);
     coup::k_trajectory_sorted<TB, false, false, 8, coup::kTrajStage><<<(unsigned)((n + TB - 1) / TB), TB, 0, env->stream>>>(

@@ -3,7 +3,10 @@ round, one bench.py process per library (COUP_LIB_PATH), in turn, so the
 box's drift cancels.  Prints one JSON line per run and a summary line per
 library (median / min of ms_per_step and kernel_ms).  Measurement tool only.
 
-    python tools/bench_ab.py --rounds 5 LIB1.so LIB2.so [...] -- --config c3 --steps 20 --warmup 5
+    python tools/bench_ab.py --rounds 5 LIB1.so LIB2.so[:VAR=VAL,...] [...] -- --config c3 --steps 20 --warmup 5
+
+A library may carry environment settings after a colon (knobs read at
+coup_create, e.g. COUP_REGROUP=1), so one library can run in two forms.
 """
 import json
 import os
@@ -23,7 +26,11 @@ def main():
     res = {lib: [] for lib in libs}
     for r in range(rounds):
         for lib in libs:
-            env = dict(os.environ, COUP_LIB_PATH=os.path.abspath(lib))
+            path, _, kvs = lib.partition(":")
+            env = dict(os.environ, COUP_LIB_PATH=os.path.abspath(path))
+            for kv in filter(None, kvs.split(",")):
+                k, v = kv.split("=", 1)
+                env[k] = v
             p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--no-cpu-baseline"] + args, env=env,
                                capture_output=True, text=True, timeout=240)
             if p.returncode != 0:
