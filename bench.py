@@ -199,7 +199,7 @@ def obs_split_active(batch):
     return int(_native.load().coup_obs_split_variant(int(batch)))
 
 
-TRAJ_CHUNK_DEFAULT, TRAJ_CHUNK_MAX = 8, 32  # coup::kTrajChunkDefault, kTrajChunkMax
+TRAJ_CHUNK_DEFAULT, TRAJ_CHUNK_MAX = 10, 32  # coup::kTrajChunkDefault, kTrajChunkMax
 
 
 def step_many_form(batch, players, graph):

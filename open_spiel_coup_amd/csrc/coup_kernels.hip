@@ -1790,6 +1790,7 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
   __shared__ uint32_t s_meta[T];          // slot -> lane | key << kO
   __shared__ int32_t s_eps[T], s_ret[T];  // by lane
   __shared__ __attribute__((aligned(16))) uint32_t s_bin[2][32];
+  __shared__ uint32_t s_fin;  // lanes that finished on the last step (gathered after the loop)
   __shared__ typename std::conditional<OBS, TrajObsLds<T>, TrajNoLds<T>>::type s_obs;
   __shared__ typename std::conditional<STAGE != 0, TrajStageLds<T>, TrajNoLds<T>>::type s_st;
   constexpr bool kNow = OBS || STAGE == 1;  // a finished lane's next episode dealt in the same step
@@ -1797,6 +1798,7 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
   const int64_t base = (int64_t)blockIdx.x * T;
   const bool ar = a.auto_reset != 0;
   if (t < 64u) s_bin[t >> 5][t & 31u] = 0u;
+  if (t == 0u) s_fin = 0u;
   s_eps[t] = 0;
   s_ret[t] = 0;
   Rng rng{a.seed_lo, a.seed_hi, lane_stream_id(a.env_id_base, base + t), 0u, make_uint4(0, 0, 0, 0)};
@@ -2084,16 +2086,41 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
     if (steps > 0) store_staged(steps - 1);
     __syncthreads();  // ... and stored before the finished lanes' direct stores below
   }
-  if (!kNow && key == kKeyReset && base + lane < a.n) {  // finished on the last step
-    L = new_episode(unpack(rw).episode + 1u, rng, none);
-    const int64_t o = (steps - 1) * x.stride + base + lane;
-    if (FULL || a.legal) a.legal[o] = decision_mask(L);
-    if (FULL || a.cur_player) a.cur_player[o] = (int8_t)L.M;
-    rw = pack(L);
-    if (REC) x.rec[(steps - 1) * a.n + base + lane] = rw;
-  }
-  __syncthreads();
+  // The lanes that finished on the last step are dealt their next episode
+  // here, in place: after the last step's regroup they sit a few to a wave.
+  // -DCOUP_TRAJ_FIN_GATHER measurement builds gather them into the block's
+  // first slots through LDS so one or two waves deal them: no faster (c3
+  // 132.8 against 132.5 us per step, the bare trajectory 17.00 against 16.86,
+  // call r06y), the extra barrier costing what the waves save.
+  auto deal_finished = [&](uint32_t fl, uint4 w) {  // lane fl finished the last step; returns its record
+    const int64_t li = base + fl;
+    rng.env_id = lane_stream_id(a.env_id_base, li);
+    rng.blk_tag = 0u;
+    const Lane R = new_episode(unpack(w).episode + 1u, rng, none);
+    const int64_t o = (steps - 1) * x.stride + li;
+    if (FULL || a.legal) a.legal[o] = decision_mask(R);
+    if (FULL || a.cur_player) a.cur_player[o] = (int8_t)R.M;
+    const uint4 rr = pack(R);
+    if (REC) x.rec[(steps - 1) * a.n + li] = rr;
+    return rr;
+  };
+#ifdef COUP_TRAJ_FIN_GATHER
+  constexpr bool kFinSorted = !kNow;
+#else
+  constexpr bool kFinSorted = false;
+#endif
+  const bool fin = !kNow && key == kKeyReset && base + lane < a.n;
+  if (!kFinSorted && fin) rw = deal_finished(lane, rw);
+  __syncthreads();  // every thread has read its last slot
   s_rec[lane] = rw;
+  if constexpr (kFinSorted) {
+    if (fin) s_meta[atomicAdd(&s_fin, 1u)] = lane;
+    __syncthreads();
+    if (t < s_fin) {
+      const uint32_t fl = s_meta[t];
+      s_rec[fl] = deal_finished(fl, s_rec[fl]);
+    }
+  }
   __syncthreads();
   if (base + t < a.n) {
     const int64_t i = base + t;
@@ -3904,9 +3931,14 @@ int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, b
     COUP_HIP_TRY(hipStreamWaitEvent(R, env->ev_fork, 0));
     if (S != env->stream) COUP_HIP_TRY(hipStreamWaitEvent(S, env->ev_fork, 0));
   }
+  // the fewest chunks of at most `chunk` steps, balanced (K = 20 at the
+  // default 10: 10 + 10; at 8: 7 + 7 + 6, not 8 + 8 + 4): each launch costs a
+  // fixed ~14 us beside its ~14.5 us per step (the c3 trace, call r06q), and
+  // a short last chunk pays it for few steps (call r06w)
+  const int64_t nchunks = (steps + chunk - 1) / chunk;
   int64_t k = 0;  // chunk index
-  for (int64_t t0 = 0; t0 < steps; t0 += chunk, ++k) {
-    const int64_t c = std::min(chunk, steps - t0);
+  for (int64_t t0 = 0, c = 0; t0 < steps; t0 += c, ++k) {
+    c = (steps - t0 + (nchunks - k) - 1) / (nchunks - k);
     const int b = (int)(k & 1);
     uint4* const rec = env->traj_rec + (overlap ? b * env->traj_cap * n : 0);
     const coup_step_outputs o = slices ? slice_outputs(*out, n, 2, t0) : *out;

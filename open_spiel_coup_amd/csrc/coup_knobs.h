@@ -34,7 +34,7 @@ constexpr int kInfoSplitDefault = 3;
 // block in address order (kManyFused) -- all measured slower, DESIGN.md
 // section 5.
 constexpr int kManySerial = 0, kManyTraj = 1, kManyPipe = 2, kManyOverlap = 3, kManyFused = 4;
-constexpr int kTrajChunkDefault = 8, kTrajChunkMax = 32;
+constexpr int kTrajChunkDefault = 10, kTrajChunkMax = 32;  // 10: c3 131.8 against 132.8 us per step at 8 (call r06w)
 // rules blocks spread over the first kPipeSpanDefault of a pipelined
 // launch's block positions (COUP_PIPE_SPAN)
 constexpr double kPipeSpanDefault = 0.85;
