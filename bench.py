@@ -233,19 +233,6 @@ def traj_stage():
     return (_native.load().coup_build_flags() >> _native.BUILD_TRAJ_STAGE_SHIFT) & _native.BUILD_TRAJ_STAGE_MASK
 
 
-def _traj_rec16():
-    """The measurement build's knobs that keep step_many_traj on 16-byte
-    records (the writer variants read them; mirrors its `words` test)."""
-    from open_spiel_coup_amd import _native
-    if not _native.load().coup_build_flags() & _native.BUILD_AB_VARIANTS:
-        return False
-    def on(k, off="0"):
-        return os.environ.get(k, off).strip() not in (off, "")
-    return (on("COUP_TRAJ_REC16") or on("COUP_MANY_STAGE") or on("COUP_MANY_SHAPE") or on("COUP_WRITER_FORM") or
-            on("COUP_WRITER_DYN_LDS") or on("COUP_WRITER_PRIO") or os.environ.get("COUP_WRITER_POL", "-1").strip() not in
-            ("-1", "0", "") or os.environ.get("COUP_PIPE", "1").strip() == "3")
-
-
 def traj_chunk():
     """COUP_TRAJ_CHUNK as coup::read_knobs clamps it."""
     try:
@@ -314,14 +301,9 @@ def expected_kernel(cfg, batch, graph):
         if form:
             # one rules-trajectory launch per chunk of steps + the writer per step
             stage = os.environ.get("COUP_MANY_STAGE", "0").strip() not in ("0", "")
-            if form == "fused-trajectory":
-                return "coup::k_trajectory_sorted<1024, false, true, 4, 0>"
-            if stage:
-                return "coup::k_trajectory_sorted<1024, true, false, 8, 1> + " + _SPLIT_WRITERS.get(split, "coup::k_obs_sweep")
-            if traj_stage() == 0 and split == 11 and not _traj_rec16():
-                # each step's records as 8-byte obs_word (coup_kernels.hip step_many_traj)
-                return "coup::k_trajectory_sorted<1024, true, false, 8, 0, true, true> + coup::k_obs_sweep_words<512, 2>"
-            return ("coup::k_trajectory_sorted<1024, true, false, 8, %d, true> + " % traj_stage() +
+            return ("coup::k_trajectory_sorted<1024, false, true, 4, 0>" if form == "fused-trajectory" else
+                    ("coup::k_trajectory_sorted<1024, true, false, 8, 1> + " if stage else
+                     "coup::k_trajectory_sorted<1024, true, false, 8, %d, true> + " % traj_stage()) +
                     _SPLIT_WRITERS.get(split, "coup::k_obs_sweep"))
         if split:
             # the rules step without tensors (regrouped from 2^18 lanes) + the writer

@@ -1029,10 +1029,9 @@ struct ObsSweepLds {
 };
 
 // Block `blk` of the writer (T threads): float4s [blk T S, (blk + 1) T S) of
-// the [n][2][98] buffer from the records `state` (16-byte records, or the
-// rules trajectory's 8-byte obs_word records).
-template <int T, int S, int POL = 0, class Rec = uint4>
-__device__ __forceinline__ void obs_sweep_rows_block(const Rec* __restrict__ state, float* __restrict__ obs,
+// the [n][2][98] buffer from the records `state`.
+template <int T, int S, int POL = 0>
+__device__ __forceinline__ void obs_sweep_rows_block(const uint4* __restrict__ state, float* __restrict__ obs,
                                                      int64_t n, uint32_t blk, ObsSweepLds<T, S>& lds) {
   typedef float v4f __attribute__((ext_vector_type(4)));
   constexpr uint32_t kLanes = ObsSweepLds<T, S>::kLanes;
@@ -1043,12 +1042,12 @@ __device__ __forceinline__ void obs_sweep_rows_block(const Rec* __restrict__ sta
   const int64_t x0 = (int64_t)blk * (T * S);
   const int64_t o0 = x0 / kRowF4;
   if (t < 2u * kLanes && o0 + (t >> 1) < n) {
-    const ObsIn in = obs_in(state[o0 + (t >> 1)]);
+    const Lane L = unpack(state[o0 + (t >> 1)]);
     uint64_t lo, hi;
-    obs_row_bits_rt(in.L, in.term, t & 1u, lo, hi);
+    obs_row_bits_rt(L, is_terminal(L), t & 1u, lo, hi);
     reinterpret_cast<uint4*>(rows)[t] = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi,
                                                    (uint32_t)(hi >> 32));
-    if ((t & 1u) == 0u) coins[t >> 1] = in.L.c0 | (in.L.c1 << 8);
+    if ((t & 1u) == 0u) coins[t >> 1] = L.c0 | (L.c1 << 8);
   }
   __syncthreads();
   const int64_t nf4 = n * kRowF4;
@@ -1174,15 +1173,6 @@ __global__ __launch_bounds__(T) void k_obs_sweep_rows(const uint4* __restrict__ 
   if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO);
   __shared__ ObsSweepLds<T, S> lds;
   obs_sweep_rows_block<T, S, POL>(state, obs, n, blockIdx.x, lds);
-}
-
-// The same writer from the rules trajectory's 8-byte obs_word records
-// (coup_step_many's c3 form, round 6)
-template <int T, int S>
-__global__ __launch_bounds__(T) void k_obs_sweep_words(const uint64_t* __restrict__ words, float* __restrict__ obs,
-                                                       int64_t n) {
-  __shared__ ObsSweepLds<T, S> lds;
-  obs_sweep_rows_block<T, S, 0, uint64_t>(words, obs, n, blockIdx.x, lds);
 }
 
 // coup_measure_step_traffic: the bytes of k_step<*, kObsWaveBitsSc1, 256,
@@ -1746,10 +1736,9 @@ __global__ __launch_bounds__(T, 8) void k_rollout_sorted(RolloutArgs a) {
 // finished lane is dealt its next episode in the same step (the post-reset
 // record is the observed one), not at the next.
 struct TrajOut {
-  uint4* rec;          // REC: [steps][B] post-step records (as obs_word into `words` with WORDS)
+  uint4* rec;          // REC: [steps][B] post-step records
   int64_t stride;      // output offset per step: B or 0
   int64_t obs_stride;  // OBS: floats per step (B * 196) or 0
-  uint64_t* words = nullptr;  // REC && WORDS: [steps][B] post-step obs_word records
 };
 
 template <int T>
@@ -1793,10 +1782,9 @@ struct TrajStageLds {
 // follow the staged ones (the slot barrier orders them).
 // FULL: every per-step output buffer (actions, rewards, step types, legal
 // masks, players) is present, so no store tests its pointer.
-template <int T, bool REC = false, bool OBS = false, int W = 8, int STAGE = 0, bool FULL = false, bool WORDS = false>
+template <int T, bool REC = false, bool OBS = false, int W = 8, int STAGE = 0, bool FULL = false>
 __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t steps, TrajOut x) {
   static_assert((T & (T - 1)) == 0 && T >= 64 && T <= 1024, "power-of-two block of whole waves");
-  static_assert(!WORDS || (REC && STAGE == 0), "obs_word records: the playing thread's stores");
   constexpr uint32_t kO = T <= 256 ? 8u : 10u;  // lane bits of s_meta
   __shared__ uint4 s_rec[T];
   __shared__ uint32_t s_meta[T];          // slot -> lane | key << kO
@@ -1901,8 +1889,7 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
     const int64_t li = base + lane;
     if (li >= a.n) continue;  // past the batch
     const int64_t o = s * x.stride + li;
-    uint4* const rec_s = REC && !WORDS ? x.rec + s * a.n + li : nullptr;  // step s's record of the lane
-    uint64_t* const word_s = REC && WORDS ? x.words + s * a.n + li : nullptr;  // ... as obs_word
+    uint4* const rec_s = REC ? x.rec + s * a.n + li : nullptr;  // step s's record of the lane
     // the lane's step-s outputs: to the buffers, or (STAGE) to LDS by lane
 #if defined(COUP_ABLATE_TRAJ_STORES) && COUP_ABLATE_TRAJ_STORES >= 1
     // measurement builds: the small outputs not stored (1), nor the records
@@ -1940,7 +1927,6 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
       rw = pack(R);
       if constexpr (kSkipRec) return;
       if constexpr (STAGE != 0) s_st.rec[lane] = rw;
-      else if constexpr (WORDS) *word_s = obs_word(R);
       else if (REC) *rec_s = rw;
     };
     rng.env_id = lane_stream_id(a.env_id_base, li);
@@ -1984,8 +1970,7 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
       if (FULL || a.legal) a.legal[o - x.stride] = legal;
       if (FULL || a.cur_player) a.cur_player[o - x.stride] = (int8_t)L.M;
       rw = pack(L);
-      if constexpr (WORDS) *(word_s - a.n) = obs_word(L);  // step s - 1's record, after its auto-reset
-      else if (REC) *(rec_s - a.n) = rw;
+      if (REC) *(rec_s - a.n) = rw;  // step s - 1's record, after its auto-reset
       key = regroup_key(L, sample_action(legal, rng.draw(L.episode, L.move)));
     }
     if (key == kKeyDead) {  // no legal decision: coup_step's rejected step
@@ -2116,8 +2101,7 @@ __global__ __launch_bounds__(T, W) void k_trajectory_sorted(StepArgs a, int64_t 
     if (FULL || a.legal) a.legal[o] = decision_mask(R);
     if (FULL || a.cur_player) a.cur_player[o] = (int8_t)R.M;
     const uint4 rr = pack(R);
-    if constexpr (WORDS) x.words[(steps - 1) * a.n + li] = obs_word(R);
-    else if (REC) x.rec[(steps - 1) * a.n + li] = rr;
+    if (REC) x.rec[(steps - 1) * a.n + li] = rr;
     return rr;
   };
 #ifdef COUP_TRAJ_FIN_GATHER
@@ -2867,8 +2851,7 @@ struct coup_env {
   coup_server* server;        // coup_attach_server: coup_slot_op goes through this resident wave
   bool dirty;                 // work enqueued on `stream` since its last synchronisation
   hipEvent_t stream_event;    // coup_set_stream: orders a new stream after the old one's pending work
-  uint4* traj_rec;            // 2 players: [traj_cap][B] obs_word records of coup_step_many's rules trajectories
-                              // (16-byte records in the measurement build's variants)
+  uint4* traj_rec;            // 2 players: [traj_cap][B] records of coup_step_many's rules trajectories
                               // ([2][traj_cap][B] once the overlapped form's resources exist)
   int64_t traj_cap;           // steps per rules-trajectory launch the buffer holds (COUP_TRAJ_CHUNK at create)
   uint4* state2;              // = traj_rec: the second record buffer of the merged pipelined step
@@ -3320,12 +3303,7 @@ int coup_create_ex(int64_t batch, uint64_t seed, uint32_t env_id_base, int flags
   if (e == hipSuccess && !generic && !(flags & COUP_FLAG_HISTORY) && env->knobs.pipe != coup::kManySerial &&
       obs_split(env->knobs, batch) != 0) {
     env->traj_cap = env->knobs.traj_chunk;
-#ifdef COUP_AB_VARIANTS
-    const size_t per_lane_step = sizeof(uint4);  // the measurement build's writer variants read 16-byte records
-#else
-    const size_t per_lane_step = sizeof(uint64_t);  // obs_word records (step_many_traj)
-#endif
-    e = hipMalloc(&env->traj_rec, lanes * per_lane_step * env->traj_cap);
+    e = hipMalloc(&env->traj_rec, lanes * sizeof(uint4) * env->traj_cap);
     env->state2 = env->traj_rec;
   }
   if (e == hipSuccess) e = hipMalloc(&env->err_count, sizeof(uint32_t));
@@ -3958,21 +3936,11 @@ int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, b
   // fixed ~14 us beside its ~14.5 us per step (the c3 trace, call r06q), and
   // a short last chunk pays it for few steps (call r06w)
   const int64_t nchunks = (steps + chunk - 1) / chunk;
-  // each step's records as 8-byte obs_word (k_obs_sweep_words), or -- the
-  // measurement build's variants, COUP_TRAJ_REC16 -- as 16-byte records
-#ifdef COUP_AB_VARIANTS
-  const bool words = coup::kTrajStage == 0 && !overlap && !env->knobs.many_stage && env->knobs.many_shape == 0 &&
-                     env->knobs.writer_form == 0 && env->knobs.writer_pol <= 0 && env->knobs.writer_dyn_lds == 0 &&
-                     env->knobs.writer_prio == 0 && !env->knobs.traj_rec16;
-#else
-  constexpr bool words = coup::kTrajStage == 0;
-#endif
   int64_t k = 0;  // chunk index
   for (int64_t t0 = 0, c = 0; t0 < steps; t0 += c, ++k) {
     c = (steps - t0 + (nchunks - k) - 1) / (nchunks - k);
     const int b = (int)(k & 1);
     uint4* const rec = env->traj_rec + (overlap ? b * env->traj_cap * n : 0);
-    uint64_t* const wrec = reinterpret_cast<uint64_t*>(env->traj_rec);
     const coup_step_outputs o = slices ? slice_outputs(*out, n, 2, t0) : *out;
     coup::StepArgs a = uniform_args(env, out);
     a.actions = o.actions;
@@ -3981,7 +3949,7 @@ int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, b
     a.legal = o.legal_mask;
     a.cur_player = o.cur_player;
     if (overlap && k >= 2) COUP_HIP_TRY(hipStreamWaitEvent(R, env->ev_writers[b], 0));
-    const coup::TrajOut x{rec, slices ? n : 0, 0, wrec};
+    const coup::TrajOut x{rec, slices ? n : 0, 0};
     const unsigned grid = (unsigned)((n + TB - 1) / TB);
 #ifdef COUP_AB_VARIANTS
     auto shape = [&](auto tt, auto ww) {  // COUP_MANY_SHAPE: lanes per block, waves per SIMD budget
@@ -4005,25 +3973,17 @@ int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, b
           coup::k_trajectory_sorted<TB, true, false, 8, 0><<<grid, TB, (unsigned)env->knobs.overlap_lds, R>>>(a, c, x);
     else
 #endif
+#ifndef COUP_TRAJ_NOFULL
     // every output present (the env's own buffers, bench.py's c3): the FULL
     // form, no pointer tests (c3 132.3 against 133.6-133.9 us per step, call
     // r06f; within the process-to-process spread, and fewer instructions)
-    if (words) {
-      if (a.actions && a.rewards && a.step_type && a.legal && a.cur_player)
-        coup::note_launch("coup::k_trajectory_sorted<{}, true, false, 8, 0, true, true>", TB),
-            coup::k_trajectory_sorted<TB, true, false, 8, 0, true, true><<<grid, TB, 0, R>>>(a, c, x);
-      else
-        coup::note_launch("coup::k_trajectory_sorted<{}, true, false, 8, 0, false, true>", TB),
-            coup::k_trajectory_sorted<TB, true, false, 8, 0, false, true><<<grid, TB, 0, R>>>(a, c, x);
-    }
-#ifdef COUP_AB_VARIANTS
-    else if (a.actions && a.rewards && a.step_type && a.legal && a.cur_player)  // 16-byte records
+    if (a.actions && a.rewards && a.step_type && a.legal && a.cur_player)
       coup::note_launch("coup::k_trajectory_sorted<{}, true, false, 8, {}, true>", TB, coup::kTrajStage),
           coup::k_trajectory_sorted<TB, true, false, 8, coup::kTrajStage, true><<<grid, TB, 0, R>>>(a, c, x);
     else
+#endif
       coup::note_launch("coup::k_trajectory_sorted<{}, true, false, 8, {}>", TB, coup::kTrajStage),
           coup::k_trajectory_sorted<TB, true, false, 8, coup::kTrajStage><<<grid, TB, 0, R>>>(a, c, x);
-#endif
     COUP_HIP_TRY(hipGetLastError());
     if (overlap) {
       COUP_HIP_TRY(hipEventRecord(env->ev_rules[b], R));
@@ -4060,13 +4020,7 @@ int step_many_traj(coup_env* env, int64_t steps, const coup_step_outputs* out, b
         coup::note_launch("coup::k_obs_sweep_rows<512, 2, 0, 3>"), coup::k_obs_sweep_rows<512, 2, 0, 3><<<wgrid, 512, 0, S>>>(rec + s * n, obs, n);
       else
 #endif
-      if (words)
-        coup::note_launch("coup::k_obs_sweep_words<512, 2>"),
-            coup::k_obs_sweep_words<512, 2><<<wgrid, 512, 0, S>>>(wrec + s * n, obs, n);
-#ifdef COUP_AB_VARIANTS
-      else
         coup::note_launch("coup::k_obs_sweep_rows<512, 2>"), coup::k_obs_sweep_rows<512, 2><<<wgrid, 512, 0, S>>>(rec + s * n, obs, n);
-#endif
       COUP_HIP_TRY(hipGetLastError());
     }
     if (overlap) COUP_HIP_TRY(hipEventRecord(env->ev_writers[b], S));

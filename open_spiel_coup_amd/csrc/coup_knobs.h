@@ -64,7 +64,6 @@ struct Knobs {
   int writer_pol = -1;  // COUP_WRITER_POL: the split writers' stores (-1 shipped, 0 nt, 1 plain, 2 sc1, 3 sc1 nt)
   int writer_prio = 0;  // COUP_WRITER_PRIO: the split writer's waves at s_setprio 1 (1) or 3 (2)
   int writer_dyn_lds = 0;  // COUP_WRITER_DYN_LDS: extra dynamic LDS per block of the rules-trajectory form's writer
-  bool traj_rec16 = false;  // COUP_TRAJ_REC16: the rules trajectory's per-step records as 16-byte records, not obs_word
   int writer_form = 0;  // COUP_WRITER_FORM: 0 the rows writer, 1..4 the nibble writer <512,2> <512,4> <1024,2> <256,4>
   int overlap_lds = 0;  // COUP_OVERLAP_LDS: extra dynamic LDS per rules block of kManyOverlap (fewer per CU)
   int many_shape = 0;   // COUP_MANY_SHAPE: its block / register budget (1: 512 x 8, 2: 512 x 6, 3: 256 x 8, 4: 1024 x 4)
@@ -111,7 +110,6 @@ inline Knobs read_knobs() {
   k.writer_prio = knob_int("COUP_WRITER_PRIO", 0);
   k.writer_form = knob_int("COUP_WRITER_FORM", 0);
   k.writer_dyn_lds = knob_int("COUP_WRITER_DYN_LDS", 0);
-  k.traj_rec16 = knob_int("COUP_TRAJ_REC16", 0) != 0;
   k.overlap_lds = knob_int("COUP_OVERLAP_LDS", 0);
 #else
   // the merged launch, the two-stream overlap and the fused trajectory ship

@@ -97,39 +97,6 @@ __device__ __forceinline__ void obs_row_bits_rt(const Lane& L, bool term, uint32
   }
 }
 
-// The ObservationTensor's inputs of a lane as one 64-bit word -- the rules
-// trajectory's per-step record for the split writer (coup_step_many's c3
-// form; half the 16-byte record, so a chunk's slices take half the Infinity
-// Cache): hands [31:0], coins [39:32], last actions [49:40], the mover [50],
-// terminal [51].  A 64-bit integer, not a two-word vector (DESIGN.md section
-// 12).
-__device__ __forceinline__ uint64_t obs_word(const Lane& L) {
-  const uint32_t hi = L.c0 | (L.c1 << 4) | (L.l0 << 8) | (L.l1 << 13) | (L.M << 18) | ((is_terminal(L) ? 1u : 0u) << 19);
-  return (uint64_t)(L.h0 | (L.h1 << 16)) | ((uint64_t)hi << 32);
-}
-
-// The fields obs_row_bits_rt and the coins read, from a record or a word.
-struct ObsIn {
-  Lane L;
-  bool term;
-};
-__device__ __forceinline__ ObsIn obs_in(const uint4& r) {
-  const Lane L = unpack(r);
-  return {L, is_terminal(L)};
-}
-__device__ __forceinline__ ObsIn obs_in(const uint64_t& w) {
-  Lane L = initial_lane(0u);
-  const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
-  L.h0 = lo & 0xFFFFu;
-  L.h1 = lo >> 16;
-  L.c0 = hi & 0xFu;
-  L.c1 = (hi >> 4) & 0xFu;
-  L.l0 = (hi >> 8) & 0x1Fu;
-  L.l1 = (hi >> 13) & 0x1Fu;
-  L.M = (hi >> 18) & 1u;
-  return {L, ((hi >> 19) & 1u) != 0u};
-}
-
 // InformationStateTensor layout (see coup_kernels.hip's write_info_wave):
 constexpr int kInfoSize = COUP_INFO_STATE_SIZE;  // 2492
 constexpr int kInfoHalfF4 = kInfoSize / 4;       // 623 float4 per player

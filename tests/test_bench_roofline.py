@@ -55,7 +55,7 @@ def test_traffic_table_carries_valu_for_the_trajectory_forms():
 
 
 @pytest.mark.parametrize("cfg,want", [
-    ("c3", "coup::k_trajectory_sorted<1024, true, false, 8, 0, true, true> + coup::k_obs_sweep_words<512, 2>"),
+    ("c3", "coup::k_trajectory_sorted<1024, true, false, 8, 0, true> + coup::k_obs_sweep_rows<512, 2>"),
     ("c2", "coup::k_step_trajectory"),
     ("c4", "coup::np::k_trajectory_sorted<6, 1024>"),
     ("c2r", "coup::k_rollout"),

@@ -187,9 +187,9 @@ void coup::k_step<true, 0, 256, 2, false> | void coup::k_step<true, 4, 256, 1, f
 void coup::k_step<true, 4, 256, 2, false> | void coup::k_step<true, 9, 256, 0, false> |
 void coup::k_step_group<1, false> | void coup::k_step_group<1, true> |
 void coup::k_step_sorted<false, 512> | void coup::k_step_sorted<true, 512> |
-void coup::k_trajectory_sorted<1024, false, false, 8, 0, false, false> |
-void coup::k_trajectory_sorted<1024, true, false, 8, 0, false, true> |
-void coup::k_trajectory_sorted<1024, true, false, 8, 0, true, true> | void coup::k_obs_sweep_words<512, 2> |
+void coup::k_trajectory_sorted<1024, false, false, 8, 0, false> |
+void coup::k_trajectory_sorted<1024, true, false, 8, 0, false> |
+void coup::k_trajectory_sorted<1024, true, false, 8, 0, true> |
 void coup::k_store_sweep<512, 2> | void coup::k_store_sweep<1024, 2>
 """
 
@@ -246,9 +246,8 @@ def test_measurement_build_holds_the_variants():
     for k in ("void coup::k_obs_sweep<1>", "void coup::k_obs_sweep_rows<256, 2, 0, 0>", "void coup::k_step_group<4, true>",
               "void coup::k_step<true, 1, 256, 0, false>", "void coup::k_step_sorted<true, 1024>",
               "void coup::k_info_sweep<512, 2, 0>", "void coup::k_step_obs_pipe<512, 2>",
-              "void coup::k_trajectory_sorted<1024, false, true, 4, 0, false, false>",
-              "void coup::k_trajectory_sorted<1024, true, false, 8, 1, false, false>", "void coup::k_obs_sweep_nib<512, 2>",
-              "void coup::k_trajectory_sorted<1024, true, false, 8, 0, true, false>",
+              "void coup::k_trajectory_sorted<1024, false, true, 4, 0, false>",
+              "void coup::k_trajectory_sorted<1024, true, false, 8, 1, false>", "void coup::k_obs_sweep_nib<512, 2>",
               "void coup::np::k_step_sorted<6, true, true, 1024, true, 4>",
               "void coup::np::k_rollout_sorted<6, 1024, false>", "void coup::np::k_trajectory_sorted<6, 1024, 0>"):
         assert k in got, k

@@ -7,7 +7,7 @@ bench.py's lines run these forms (the driver's command is `bench.py --gpus 1
        rollout, 5 eager warm-up steps, then K = 20 steps replayed from one
        HIP graph of coup_step_many -- the rules-trajectory form
        (k_trajectory_sorted<1024, true, false, 8, 0, true>, balanced chunks of up to 10 steps,
-       then k_obs_sweep_words<512, 2> once per step, from 8-byte obs_word records);
+       then k_obs_sweep_rows<512, 2> once per step);
   c2   65,536 lanes, no tensors: the same settle and warm-up, then the K = 20
        steps as ONE coup_step_many launch (k_step_trajectory, outputs stored
        with stride 0) replayed from a graph;

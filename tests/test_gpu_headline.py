@@ -3,11 +3,11 @@
 bench.py's c3 line (the BASELINE metric) runs the split observation step
 over 2^20 lanes: settle through the fused rollout, W warm-up steps, then K
 steps replayed from one HIP graph (BatchedCoupEnv.capture_steps), which
-records coup_step_many -- the rules-trajectory form: balanced chunks of up
-to 10 steps as one regrouped rules-trajectory launch (k_trajectory_sorted<1024,
+records coup_step_many -- the rules-trajectory form: chunks of up to 8
+steps as one regrouped rules-trajectory launch (k_trajectory_sorted<1024,
 true>, the branch-form transition apply_decision_v1) storing every step's
-records as 8-byte obs_word, then the address-order observation writer
-k_obs_sweep_words<512, 2> once per step.  Its timed region keeps only the last
+records, then the address-order observation writer k_obs_sweep_rows<512, 2>
+once per step.  Its timed region keeps only the last
 step's tensors, so the same launches also run as a trajectory whose every
 step lands in its own [T][B][2][98] slice, checked step by step.  c3i runs
 the history-keeping rules step and k_info_sweep<1024, 2> over 2^18 lanes

@@ -2,8 +2,8 @@
 rules-trajectory form (COUP_PIPE=1, the default):
 chunks of up to COUP_TRAJ_CHUNK steps run as ONE regrouped rules-trajectory
 launch (k_trajectory_sorted<1024, true>) that also stores every step's
-post-step records (as 8-byte obs_word), then one k_obs_sweep_words<512, 2>
-launch per step reading them.  It must equal coup_step launched once per step (COUP_PIPE=0: the
+post-step records, then one k_obs_sweep_rows<512, 2> launch per step reading
+them.  It must equal coup_step launched once per step (COUP_PIPE=0: the
 split step's two kernels per step) bit for bit -- the last step's outputs,
 the records, the episode accumulators and the error count -- for every
 chunk length (a chunk ending mid-call, episodes ending on a chunk's last
